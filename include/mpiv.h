@@ -1,0 +1,139 @@
+/*
+ * mpiv.h -- C ABI of libmpiv.so, the MI355X (gfx950) kernels behind the
+ * mpi-vision hot path.
+ *
+ * The reference (Findeton/mpi-vision) has no FFI layer: its hot path is the
+ * Python module functions of utils.py.  Each entry point below replaces the
+ * per-pixel work of the reference function cited next to it; the Python
+ * drop-in (mpi_vision_amd/utils.py) binds them with ctypes.
+ *
+ * Conventions
+ *  - Every pointer is DEVICE memory owned by the caller (e.g. a torch tensor);
+ *    the library never allocates or frees on these paths.
+ *  - Strides are in ELEMENTS (floats), int64.  A stride may be 0 (broadcast).
+ *  - `stream` is a hipStream_t (NULL = default stream).  Calls are
+ *    stream-ordered and asynchronous; the library keeps no mutable global state
+ *    (re-entrant, safe from several streams / threads).
+ *  - Return 0 on success, a negative MPIV_ERR_* code otherwise; the message is
+ *    available from mpiv_last_error() on the calling thread.  Never aborts.
+ *  - All arithmetic is fp32 and rounds exactly like the reference's ATen CPU
+ *    ops; matrices (homographies, Ki, proj) are computed by the
+ *    caller on the host and passed as device buffers.
+ */
+#ifndef MPIV_H
+#define MPIV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPIV_ABI_VERSION 1
+
+enum {
+    MPIV_OK = 0,
+    MPIV_ERR_ARG = -1,   /* bad shape / stride / alignment / null pointer */
+    MPIV_ERR_HIP = -2,   /* a HIP runtime call or kernel launch failed */
+};
+
+int mpiv_abi_version(void);
+const char *mpiv_last_error(void);
+
+/* ---- MPI render -------------------------------------------------------- */
+
+/* mpi_render_view_torch (utils.py:267-294), fused warp + over-composite.
+ * mpi:   [B,H,W,P,4] with element strides mpi_strides[5] (B may be stride 0)
+ * homs:  [B][P][9] row-major target->source homographies
+ *        (inv_homography_torch, utils.py:44-67, evaluated by the caller)
+ * out:   [B,H,W,3] contiguous */
+int mpiv_render(const float *mpi, const int64_t mpi_strides[5], int B, int H, int W, int P,
+                const float *homs, float *out, void *stream);
+
+/* Layout pack for repeated rendering of one MPI: one view [H,W,P,4] (element
+ * strides strides[4] = H,W,P,C) -> plane-major packed [P][H][W][4] (16-B aligned,
+ * contiguous).  No reference counterpart (the reference re-materialises the
+ * plane-major copy on every call, utils.py:121). */
+int mpiv_pack_planes(const float *mpi_view, const int64_t strides[4], int H, int W, int P,
+                     float *packed, void *stream);
+
+/* mpi_render_view_torch on a packed MPI for V views at once.
+ * homs [V][P][9]; out [V,H,W,3] contiguous. */
+int mpiv_render_packed(const float *packed, int H, int W, int P, const float *homs, int V,
+                       float *out, void *stream);
+
+/* Plane-range partial for plane sharding: planes [p_begin, p_end)
+ * of a packed MPI -> ct [V,H,W,4] = (C rgb, T).  back != 0: the range holds the
+ * reference's plane 0 (its alpha ignored, utils.py:152-153) -> T = 0. */
+int mpiv_render_packed_ct(const float *packed, int H, int W, int P, int p_begin, int p_end, int back,
+                          const float *homs, int V, float *ct, void *stream);
+
+/* Ordered over-operator combine: parts [G][n][4] (C,T), index 0 = back-most range
+ * -> out [n][3].  (Cf,Tf) o (Cb,Tb) = (Cf + Tf*Cb, Tf*Tb). */
+int mpiv_combine_ct(const float *parts, int G, int64_t n, float *out, void *stream);
+
+/* ---- plane sweep -------------------------------------------------------- */
+
+/* plane_sweep_torch / plane_sweep_torch_one / plane_sweep_torch_one2
+ * (utils.py:452-471, 513-533, 771-799).
+ * img:    [B,Hs,Ws,C] element strides img_strides[4]
+ * ki:     [B][9]  inverse(tgt intrinsics)         (utils.py:370 / :747)
+ * proj:   [B][16] [[K_src,0],[0,0,0,1]] @ pose     (utils.py:431-438 / :750-757)
+ * depths: [D] fp32
+ * out:    [B,Ht,Wt,D*C] contiguous, channel d*C + c (torch.cat order, utils.py:470) */
+int mpiv_plane_sweep(const float *img, const int64_t img_strides[4], int B, int Hs, int Ws, int C,
+                     const float *ki, const float *proj, const float *depths, int D, int Ht, int Wt,
+                     float *out, void *stream);
+
+/* projective_inverse_warp_torch / projective_inverse_warp_torch2 with a per-pixel
+ * depth map (utils.py:409-450, 725-769).
+ * depth: [B,Ht,Wt] element strides depth_strides[3]; out [B,Ht,Wt,C] contiguous. */
+int mpiv_inverse_warp(const float *img, const int64_t img_strides[4], int B, int Hs, int Ws, int C,
+                      const float *ki, const float *proj, const float *depth, const int64_t depth_strides[3],
+                      int Ht, int Wt, float *out, void *stream);
+
+/* ---- sampling / compositing primitives ---------------------------------- */
+
+/* bilinear_wrapper_torch (utils.py:104-134) / resampler_wrapper_torch
+ * (utils.py:395-407): grid_sample(bilinear, zeros, align_corners=False) at
+ * -1 + 2*coords.
+ * in:     [N,C,Hi,Wi] element strides in_strides[4]
+ * coords: [N,Ho,Wo,2] element strides coord_strides[4] (last = component stride)
+ * out:    element strides out_strides[4] in (N,C,H,W) order (NCHW or NHWC memory) */
+int mpiv_grid_sample(const float *in, const int64_t in_strides[4], int N, int C, int Hi, int Wi,
+                     const float *coords, const int64_t coord_strides[4], int Ho, int Wo, float *out,
+                     const int64_t out_strides[4], void *stream);
+
+/* over_composite (utils.py:136-157).
+ * layers: DEVICE array of P pointers, each to n RGBA pixels with element strides
+ *         (pixel_stride, channel_stride); layer 0 is the back.  out [n][3]. */
+int mpiv_over_composite(const float *const *layers, int P, int64_t n, int64_t pixel_stride,
+                        int64_t channel_stride, float *out, void *stream);
+
+/* ---- geometry helpers ---------------------------------------------------- */
+
+/* transform_points_torch (utils.py:69-88): pts [M][n][3], homs [M][9] -> out [M][n][3] */
+int mpiv_transform_points(const float *pts, int M, int64_t n, const float *homs, float *out, void *stream);
+
+/* normalize_homogeneous_torch (utils.py:90-101): pts [n][k+1] -> out [n][k];
+ * w == 0 is replaced by 1e-8 IN pts, as the reference's in-place `+=` does. */
+int mpiv_normalize_homogeneous(float *pts, int64_t n, int k, float *out, void *stream);
+
+/* pixel2cam_torch (utils.py:356-375): depth [B][n], pix [B][3][n], ki [B][9]
+ * -> cam [B][3 or 4][n] */
+int mpiv_pixel2cam(const float *depth, const float *pix, const float *ki, int B, int64_t n, int homogeneous,
+                   float *cam, void *stream);
+
+/* cam2pixel_torch (utils.py:377-393): cam [B][4][n], proj [B][16] -> out [B][n][2] */
+int mpiv_cam2pixel(const float *cam, const float *proj, int B, int64_t n, float *out, void *stream);
+
+/* transform_plane_imgs_torch coordinates (utils.py:176-188): pts [M][n][3],
+ * homs [M][9] -> coords [M][n][2] = (u/w/(Ht-1), v/w/(Wt-1)) */
+int mpiv_plane_coords(const float *pts, int M, int64_t n, const float *homs, int Ht, int Wt, float *coords,
+                      void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPIV_H */

@@ -1,0 +1,77 @@
+"""Host-side 3x3 / 4x4 setup for the render and plane-sweep kernels.
+
+These matrices are tiny (P*B 3x3 homographies, B 3x3 + 4x4 PSV matrices) but
+their exact fp32 bits decide whether the kernels land within 1e-5 of the
+reference (a float64-derived H breaks 1e-5 on ~1.4% of pixels).
+So they are computed with torch-CPU fp32 ops in the reference's association
+order -- the same ATen kernels the reference itself calls -- and then uploaded
+once per call (P*B*36 bytes).
+"""
+from __future__ import annotations
+
+import torch
+
+_CPU = torch.device("cpu")
+_F32 = torch.float32
+
+
+def _cpu32(x: torch.Tensor) -> torch.Tensor:
+    return x.detach().to(device=_CPU, dtype=_F32)
+
+
+def divide_safe(num: torch.Tensor, den: torch.Tensor) -> torch.Tensor:
+    """utils.py:35-39: den == 0 -> den + 1e-8 (fp32), then num / den."""
+    den = den.to(_F32)
+    den = den + 1e-8 * (den == 0)
+    return num.to(_F32) / den
+
+
+def inv_homography(k_s, k_t, rot, t, n_hat, a):
+    """utils.py:44-67, same op order:
+        denom     = a - (n_hat @ R^T) @ t
+        numerator = ((R^T @ t) @ n_hat) @ R^T
+        H         = (k_s @ (R^T + numerator / denom)) @ inverse(k_t)
+    Runs on the inputs' device (the render path calls it with CPU tensors)."""
+    rot_t = rot.transpose(-2, -1)
+    k_t_inv = torch.inverse(k_t)
+    denom = a - torch.matmul(torch.matmul(n_hat, rot_t), t)
+    numerator = torch.matmul(torch.matmul(torch.matmul(rot_t, t), n_hat), rot_t)
+    return torch.matmul(torch.matmul(k_s, rot_t + divide_safe(numerator, denom)), k_t_inv)
+
+
+def render_homographies(pose: torch.Tensor, depths: torch.Tensor, intrinsics: torch.Tensor,
+                        batch: int) -> torch.Tensor:
+    """Per-(view, plane) target->source homographies for mpi_render_view_torch
+    (utils.py:278-285 -> 255-262 -> 225-229 -> 44-67), as a [B, P, 9] fp32 CPU tensor.
+
+    The reference materialises every camera tensor as a contiguous [P, B, ...]
+    repeat before the matmul chain (utils.py:225-228, 258).  That matters: on
+    stride-0 (expanded) operands torch.matmul folds the batch into one MKL sgemm
+    whose FMA rounding differs by up to ~4e-6 in H, so the repeats are kept."""
+    pose = _cpu32(pose)
+    K = _cpu32(intrinsics)
+    P = depths.shape[0]
+    d = _cpu32(depths).reshape(P, 1).repeat(1, batch)
+    rot = pose[:, :3, :3].unsqueeze(0).repeat(P, 1, 1, 1)
+    t = pose[:, :3, 3:].unsqueeze(0).repeat(P, 1, 1, 1)
+    n_hat = torch.tensor([0.0, 0.0, 1.0], dtype=_F32).reshape(1, 1, 1, 3).repeat(P, batch, 1, 1)
+    a = -d.reshape(P, batch, 1, 1)
+    k = K.unsqueeze(0).repeat(P, 1, 1, 1)
+    H = inv_homography(k, k, rot, t, n_hat, a)  # [P, B, 3, 3]
+    return H.permute(1, 0, 2, 3).reshape(batch, P, 9).contiguous()
+
+
+def psv_matrices(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pose: torch.Tensor):
+    """Matrices for projective_inverse_warp_torch[2] (utils.py:428-438, 747-757):
+        Ki   = inverse(K_tgt)                       [B, 9]
+        proj = [[K_src, 0], [0, 0, 0, 1]] @ pose    [B, 16]
+    computed on CPU in fp32 with the reference's ops."""
+    Ks = _cpu32(src_intrinsics)
+    Kt = _cpu32(tgt_intrinsics)
+    pose = _cpu32(pose)
+    B = pose.shape[0]
+    ki = torch.inverse(Kt)
+    k4 = torch.cat([Ks, torch.zeros(B, 3, 1)], dim=2)
+    k4 = torch.cat([k4, torch.tensor([[[0.0, 0.0, 0.0, 1.0]]]).repeat(B, 1, 1)], dim=1)
+    proj = torch.matmul(k4, pose)
+    return ki.reshape(B, 9).contiguous(), proj.reshape(B, 16).contiguous()

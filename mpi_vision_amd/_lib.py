@@ -1,0 +1,351 @@
+"""ctypes binding to libmpiv.so (C ABI: include/mpiv.h) + tensor plumbing.
+
+Every function here launches a hand-written gfx950 kernel on the caller's
+current torch stream.  There is no CPU fallback: without a ROCm device or
+without the built library these functions raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmpiv.so")
+
+_c_i64p = ctypes.POINTER(ctypes.c_int64)
+_vp = ctypes.c_void_p
+_int = ctypes.c_int
+_i64 = ctypes.c_int64
+
+# name -> argtypes (mirrors include/mpiv.h)
+_SIGS = {
+    "mpiv_render": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp],
+    "mpiv_pack_planes": [_vp, _c_i64p, _int, _int, _int, _vp, _vp],
+    "mpiv_render_packed": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
+    "mpiv_render_packed_ct": [_vp, _int, _int, _int, _int, _int, _int, _vp, _int, _vp, _vp],
+    "mpiv_combine_ct": [_vp, _int, _i64, _vp, _vp],
+    "mpiv_plane_sweep": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
+    "mpiv_inverse_warp": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _c_i64p, _int, _int, _vp, _vp],
+    "mpiv_grid_sample": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _c_i64p, _int, _int, _vp, _c_i64p, _vp],
+    "mpiv_over_composite": [_vp, _int, _i64, _i64, _i64, _vp, _vp],
+    "mpiv_transform_points": [_vp, _int, _i64, _vp, _vp, _vp],
+    "mpiv_normalize_homogeneous": [_vp, _i64, _int, _vp, _vp],
+    "mpiv_pixel2cam": [_vp, _vp, _vp, _int, _i64, _int, _vp, _vp],
+    "mpiv_cam2pixel": [_vp, _vp, _int, _i64, _vp, _vp],
+    "mpiv_plane_coords": [_vp, _int, _i64, _vp, _int, _int, _vp, _vp],
+}
+EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error")
+ABI_VERSION = 1
+
+_lib = None
+
+
+def load():
+    """Load libmpiv.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"mpi_vision_amd: {LIB_PATH} is missing -- build it first "
+                               "(python -c 'import __graft_entry__ as g; g.build()')")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        L.mpiv_abi_version.restype = ctypes.c_int
+        L.mpiv_last_error.restype = ctypes.c_char_p
+        if L.mpiv_abi_version() != ABI_VERSION:
+            raise RuntimeError("mpi_vision_amd: libmpiv.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def _call(name, *args):
+    L = load()
+    rc = getattr(L, name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed ({rc}): {L.mpiv_last_error().decode()}")
+
+
+def _strides(t: torch.Tensor, dims=None):
+    st = t.stride() if dims is None else [t.stride(d) for d in dims]
+    return (ctypes.c_int64 * len(st))(*st)
+
+
+def _dev(*tensors):
+    """All tensors must be fp32 on one ROCm device; returns that device."""
+    dev = None
+    for t in tensors:
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"expected a torch.Tensor, got {type(t).__name__}")
+        if t.device.type != "cuda":
+            raise RuntimeError("mpi_vision_amd kernels need ROCm device tensors "
+                               f"(got a tensor on {t.device}); there is no CPU path")
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"expected scalar type Float but found {t.dtype}")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"tensors on different devices: {dev} and {t.device}")
+    return dev
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _up(x: torch.Tensor, dev) -> torch.Tensor:
+    """Upload a small host-computed matrix buffer (contiguous fp32)."""
+    return x.to(device=dev, dtype=torch.float32).contiguous()
+
+
+def _p(t: torch.Tensor):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+# ---------------------------------------------------------------------------
+# render
+# ---------------------------------------------------------------------------
+
+def pack_planes(view: torch.Tensor) -> torch.Tensor:
+    """One MPI view [H, W, P, 4] (any strides) -> packed plane-major [P, H, W, 4]."""
+    dev = _dev(view)
+    H, W, P, C = view.shape
+    if C != 4:
+        raise RuntimeError(f"MPI texels must have 4 channels (RGBA), got {C}")
+    packed = torch.empty((P, H, W, 4), device=dev, dtype=torch.float32)
+    _call("mpiv_pack_planes", _p(view), _strides(view), H, W, P, _p(packed), _stream(dev))
+    return packed
+
+
+def render_packed(packed: torch.Tensor, homs: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """packed [P,H,W,4] + homs [V,P,9] (host or device) -> [V,H,W,3]."""
+    dev = _dev(packed)
+    P, H, W, _ = packed.shape
+    V = homs.shape[0]
+    h = _up(homs.reshape(V, P, 9), dev)
+    if out is None:
+        out = torch.empty((V, H, W, 3), device=dev, dtype=torch.float32)
+    _call("mpiv_render_packed", _p(packed), H, W, P, _p(h), V, _p(out), _stream(dev))
+    return out
+
+
+def render_packed_ct(packed: torch.Tensor, homs: torch.Tensor, back: bool, p_begin: int = 0,
+                     p_end: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Plane-range partial (C, T) [V,H,W,4] for plane sharding."""
+    dev = _dev(packed)
+    P, H, W, _ = packed.shape
+    p_end = P if p_end is None else p_end
+    V = homs.shape[0]
+    h = _up(homs.reshape(V, P, 9), dev)
+    if out is None:
+        out = torch.empty((V, H, W, 4), device=dev, dtype=torch.float32)
+    _call("mpiv_render_packed_ct", _p(packed), H, W, P, p_begin, p_end, int(back), _p(h), V, _p(out),
+          _stream(dev))
+    return out
+
+
+def combine_ct(parts: torch.Tensor) -> torch.Tensor:
+    """parts [G, ..., 4] ordered back->front -> [..., 3]."""
+    dev = _dev(parts)
+    parts = parts.contiguous()
+    G = parts.shape[0]
+    n = parts[0].numel() // 4
+    out = torch.empty(tuple(parts.shape[1:-1]) + (3,), device=dev, dtype=torch.float32)
+    _call("mpiv_combine_ct", _p(parts), G, n, _p(out), _stream(dev))
+    return out
+
+
+def render(rgba_layers: torch.Tensor, homs: torch.Tensor) -> torch.Tensor:
+    """rgba_layers [B,H,W,P,4], homs [B,P,9] -> [B,H,W,3].
+
+    A stride-0 (broadcast) batch is packed once into the plane-major layout and
+    all B views render from it; otherwise the native-layout kernel reads the
+    reference's tensor in place."""
+    dev = _dev(rgba_layers)
+    if rgba_layers.dim() != 5 or rgba_layers.shape[-1] != 4:
+        raise RuntimeError(f"rgba_layers must be [B,H,W,P,4], got {tuple(rgba_layers.shape)}")
+    B, H, W, P, _ = rgba_layers.shape
+    if homs.shape[0] != B or homs.shape[1] != P:
+        raise RuntimeError(f"shape mismatch: MPI batch/planes {B}/{P} vs poses/planes {homs.shape[0]}/{homs.shape[1]}")
+    if B > 1 and rgba_layers.stride(0) == 0:
+        return render_packed(pack_planes(rgba_layers[0]), homs)
+    h = _up(homs, dev)
+    out = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32)
+    _call("mpiv_render", _p(rgba_layers), _strides(rgba_layers), B, H, W, P, _p(h), _p(out), _stream(dev))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# plane sweep / inverse warp
+# ---------------------------------------------------------------------------
+
+def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.Tensor, tgt_h: int,
+                tgt_w: int) -> torch.Tensor:
+    dev = _dev(img)
+    B, Hs, Ws, C = img.shape
+    d = torch.tensor([float(x) for x in depth_planes], dtype=torch.float32)
+    D = d.shape[0]
+    out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
+    _call("mpiv_plane_sweep", _p(img), _strides(img), B, Hs, Ws, C, _p(_up(ki, dev)), _p(_up(proj, dev)),
+          _p(_up(d, dev)), D, tgt_h, tgt_w, _p(out), _stream(dev))
+    return out
+
+
+def inverse_warp_depthmap(img, depth, ki, proj, tgt_h, tgt_w):
+    dev = _dev(img, depth)
+    B, Hs, Ws, C = img.shape
+    if tuple(depth.shape) != (B, tgt_h, tgt_w):
+        raise RuntimeError(f"depth must be [{B},{tgt_h},{tgt_w}], got {tuple(depth.shape)}")
+    out = torch.empty((B, tgt_h, tgt_w, C), device=dev, dtype=torch.float32)
+    _call("mpiv_inverse_warp", _p(img), _strides(img), B, Hs, Ws, C, _p(_up(ki, dev)), _p(_up(proj, dev)),
+          _p(depth), _strides(depth), tgt_h, tgt_w, _p(out), _stream(dev))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# sampler / compositor primitives
+# ---------------------------------------------------------------------------
+
+def bilinear_sample(imgs: torch.Tensor, coords: torch.Tensor, channels_last_out: bool) -> torch.Tensor:
+    """channels_last_out=False: bilinear_wrapper_torch semantics ([..., Hs, Ws, C] ->
+    [..., C, Ht, Wt]); True: resampler_wrapper_torch ([N,H,W,C] -> [N,H',W',C])."""
+    dev = _dev(imgs, coords)
+    if channels_last_out:
+        if imgs.dim() != 4 or coords.dim() != 4:
+            raise RuntimeError("resampler_wrapper_torch expects imgs [N,H,W,C] and coords [N,H,W,2]")
+        lead = [imgs.shape[0]]
+        im4 = imgs
+        co4 = coords
+    else:
+        lead = list(imgs.shape[:-3])
+        n = lead[0]  # IndexError for 3-d input, like the reference (utils.py:117)
+        for s in lead[1:]:
+            n *= s
+        im4 = imgs.reshape([n] + list(imgs.shape[-3:]))
+        co4 = coords.reshape([n] + list(coords.shape[-3:]))
+    N, Hi, Wi, C = im4.shape
+    if co4.shape[0] != N or co4.shape[-1] != 2:
+        raise RuntimeError(f"grid_sample: coords {tuple(coords.shape)} do not match images {tuple(imgs.shape)}")
+    Ho, Wo = co4.shape[1], co4.shape[2]
+    if channels_last_out:
+        out = torch.empty((N, Ho, Wo, C), device=dev, dtype=torch.float32)
+        ost = _strides(out, (0, 3, 1, 2))
+    else:
+        out = torch.empty((N, C, Ho, Wo), device=dev, dtype=torch.float32)
+        ost = _strides(out)
+    _call("mpiv_grid_sample", _p(im4), _strides(im4, (0, 3, 1, 2)), N, C, Hi, Wi, _p(co4), _strides(co4), Ho, Wo,
+          _p(out), ost, _stream(dev))
+    if channels_last_out:
+        return out
+    return out.reshape(lead + [C, Ho, Wo])
+
+
+def _flat_pixels(t: torch.Tensor):
+    """(pixel_stride, channel_stride) if the leading dims of t [..., 4] collapse to one
+    uniform pixel stride, else None."""
+    ps = t.stride(-2) if t.dim() >= 2 else 0
+    expect = ps
+    for d in range(t.dim() - 2, -1, -1):
+        if t.shape[d] != 1 and t.stride(d) != expect:
+            return None
+        expect *= t.shape[d]
+    return ps, t.stride(-1)
+
+
+def over_composite(rgbas) -> torch.Tensor:
+    rgbas = list(rgbas)
+    if not rgbas:
+        raise UnboundLocalError("over_composite: empty list")  # the reference fails the same way
+    dev = _dev(*rgbas)
+    shape = rgbas[0].shape
+    if shape[-1] != 4:
+        raise RuntimeError(f"over_composite expects RGBA layers, got {tuple(shape)}")
+    layers = []
+    for t in rgbas:
+        if t.shape != shape:
+            raise RuntimeError(f"over_composite: layer shapes differ {tuple(shape)} vs {tuple(t.shape)}")
+        layers.append(t)
+    # one (pixel stride, channel stride) pair must describe every layer; else copy
+    if None in {_flat_pixels(t) for t in layers} or len({_flat_pixels(t) for t in layers}) != 1:
+        layers = [t.contiguous() for t in layers]
+    ps, cs = _flat_pixels(layers[0])
+    n = layers[0].numel() // 4
+    ptrs = torch.tensor([t.data_ptr() for t in layers], dtype=torch.int64).to(dev)
+    out = torch.empty(tuple(shape[:-1]) + (3,), device=dev, dtype=torch.float32)
+    _call("mpiv_over_composite", _p(ptrs), len(layers), n, ps, cs, _p(out), _stream(dev))
+    # temporaries (pointer table, contiguous copies) may be freed now: the caching
+    # allocator only hands their memory to later work on this same stream
+    return out
+
+
+# ---------------------------------------------------------------------------
+# geometry helpers
+# ---------------------------------------------------------------------------
+
+def transform_points(points: torch.Tensor, homography: torch.Tensor) -> torch.Tensor:
+    dev = _dev(points, homography)
+    hshape = list(homography.shape)
+    M = 1
+    for s in hshape[:-2]:
+        M *= s
+    pts = points.reshape(hshape[:-2] + [-1, 3]).contiguous()
+    n = pts.shape[-2]
+    out = torch.empty_like(pts)
+    _call("mpiv_transform_points", _p(pts), M, n, _p(homography.reshape(M, 9).contiguous()), _p(out),
+          _stream(dev))
+    return out.reshape(points.shape)
+
+
+def normalize_homogeneous(points: torch.Tensor) -> torch.Tensor:
+    dev = _dev(points)
+    k = points.shape[-1] - 1
+    if k < 1:
+        raise RuntimeError("normalize_homogeneous_torch needs at least 2 coordinates")
+    work = points if points.is_contiguous() else points.contiguous()
+    out = torch.empty(tuple(points.shape[:-1]) + (k,), device=dev, dtype=torch.float32)
+    _call("mpiv_normalize_homogeneous", _p(work), work.numel() // (k + 1), k, _p(out), _stream(dev))
+    if work is not points:  # keep the reference's in-place w update visible
+        points.copy_(work)
+    return out
+
+
+def pixel2cam(depth, pixel_coords, intrinsics, is_homogeneous=True):
+    dev = _dev(depth, pixel_coords)
+    B, H, W = depth.shape
+    n = H * W
+    from ._host import _cpu32
+    ki = torch.inverse(_cpu32(intrinsics)).reshape(B, 9)
+    rows = 4 if is_homogeneous else 3
+    cam = torch.empty((B, rows, H, W), device=dev, dtype=torch.float32)
+    _call("mpiv_pixel2cam", _p(depth.contiguous()), _p(pixel_coords.reshape(B, 3, n).contiguous()),
+          _p(_up(ki, dev)), B, n, int(bool(is_homogeneous)), _p(cam), _stream(dev))
+    return cam
+
+
+def cam2pixel(cam_coords, proj):
+    dev = _dev(cam_coords, proj)
+    B, _, H, W = cam_coords.shape
+    n = H * W
+    out = torch.empty((B, H, W, 2), device=dev, dtype=torch.float32)
+    _call("mpiv_cam2pixel", _p(cam_coords.reshape(B, 4, n).contiguous()), _p(proj.reshape(B, 16).contiguous()), B,
+          n, _p(out), _stream(dev))
+    return out
+
+
+def warp_planes(imgs: torch.Tensor, pixel_coords_trg: torch.Tensor, hom: torch.Tensor) -> torch.Tensor:
+    """transform_plane_imgs_torch: imgs [..., Hs, Ws, C], target points [..., Ht, Wt, 3],
+    hom [..., 3, 3] -> [..., C, Ht, Wt]."""
+    dev = _dev(imgs, pixel_coords_trg)
+    hshape = list(hom.shape)
+    M = 1
+    for s in hshape[:-2]:
+        M *= s
+    Ht, Wt = pixel_coords_trg.shape[-3], pixel_coords_trg.shape[-2]
+    pts = pixel_coords_trg.reshape(M, Ht * Wt, 3).contiguous()
+    coords = torch.empty((M, Ht, Wt, 2), device=dev, dtype=torch.float32)
+    _call("mpiv_plane_coords", _p(pts), M, Ht * Wt, _p(_up(hom.reshape(M, 9), dev)), Ht, Wt, _p(coords),
+          _stream(dev))
+    return bilinear_sample(imgs, coords.reshape(list(pixel_coords_trg.shape[:-1]) + [2]), channels_last_out=False)

@@ -1,0 +1,214 @@
+// abi.hip -- extern "C" entry points of libmpiv.so (declared in include/mpiv.h).
+// Unity build: the kernel sources are included here so the library is one
+// code object.  Entry points validate shapes/alignment, launch on the caller's
+// stream, and report failures through a thread-local message; they never allocate,
+// synchronise or abort.
+#include <cstdio>
+#include <cstdarg>
+#include <cstring>
+
+#include "../../include/mpiv.h"
+#include "render.hip"
+#include "sweep.hip"
+#include "geometry.hip"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int launched(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MPIV_ERR_HIP, "%s: launch failed: %s", what, hipGetErrorString(e));
+    g_err[0] = '\0';
+    return MPIV_OK;
+}
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+constexpr int64_t kMaxGridYZ = 65535;
+constexpr int64_t kMaxGridX = 2147483647;
+
+}  // namespace
+
+using namespace mpiv;
+
+extern "C" {
+
+int mpiv_abi_version(void) { return MPIV_ABI_VERSION; }
+const char* mpiv_last_error(void) { return g_err; }
+
+int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int P, const float* homs,
+                float* out, void* stream) {
+    if (!mpi || !st || !homs || !out) return fail(MPIV_ERR_ARG, "mpiv_render: null pointer");
+    if (B <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "mpiv_render: bad shape");
+    if (B > kMaxGridYZ || (H + kTileY - 1) / kTileY > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_render: too large");
+    const NativeStrides s{st[0], st[1], st[2], st[3], st[4]};
+    dim3 grid(blocks(W, kTileX), blocks(H, kTileY), B);
+    render_native_kernel<<<grid, 256, 0, S(stream)>>>(mpi, s, make_geom(H, W, P), homs, out);
+    return launched("mpiv_render");
+}
+
+int mpiv_pack_planes(const float* mpi, const int64_t st[4], int H, int W, int P, float* packed, void* stream) {
+    if (!mpi || !st || !packed) return fail(MPIV_ERR_ARG, "mpiv_pack_planes: null pointer");
+    if (H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "mpiv_pack_planes: bad shape");
+    if (!aligned16(packed)) return fail(MPIV_ERR_ARG, "mpiv_pack_planes: packed must be 16-byte aligned");
+    const int64_t npix = (int64_t)H * W;
+    if (blocks(P, kPackPl) > kMaxGridYZ || (npix + kPackPix - 1) / kPackPix > kMaxGridX)
+        return fail(MPIV_ERR_ARG, "mpiv_pack_planes: too large");
+    const NativeStrides s{0, st[0], st[1], st[2], st[3]};
+    dim3 grid(blocks(npix, kPackPix), blocks(P, kPackPl), 1);
+    pack_planes_kernel<<<grid, 256, 0, S(stream)>>>(mpi, s, H, W, P, reinterpret_cast<float4*>(packed), npix);
+    return launched("mpiv_pack_planes");
+}
+
+static int render_packed_impl(const float* packed, int H, int W, int P, int p_begin, int p_end, int back,
+                              const float* homs, int V, float* out, bool ct, void* stream) {
+    const char* nm = ct ? "mpiv_render_packed_ct" : "mpiv_render_packed";
+    if (!packed || !homs || !out) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (V <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    if (p_begin < 0 || p_end > P || p_begin >= p_end) return fail(MPIV_ERR_ARG, "%s: bad plane range", nm);
+    if (!aligned16(packed) || (ct && !aligned16(out))) return fail(MPIV_ERR_ARG, "%s: 16-byte alignment", nm);
+    if (V > kMaxGridYZ || (H + kTileY - 1) / kTileY > kMaxGridYZ) return fail(MPIV_ERR_ARG, "%s: too large", nm);
+    dim3 grid(blocks(W, kTileX), blocks(H, kTileY), V);
+    const float4* pk = reinterpret_cast<const float4*>(packed);
+    const int64_t ps = (int64_t)H * W;
+    if (ct)
+        render_packed_kernel<true><<<grid, 256, 0, S(stream)>>>(pk, ps, make_geom(H, W, P), p_begin, p_end,
+                                                                back, homs, out);
+    else
+        render_packed_kernel<false><<<grid, 256, 0, S(stream)>>>(pk, ps, make_geom(H, W, P), p_begin, p_end,
+                                                                 1, homs, out);
+    return launched(nm);
+}
+
+int mpiv_render_packed(const float* packed, int H, int W, int P, const float* homs, int V, float* out,
+                       void* stream) {
+    return render_packed_impl(packed, H, W, P, 0, P, 1, homs, V, out, false, stream);
+}
+
+int mpiv_render_packed_ct(const float* packed, int H, int W, int P, int p_begin, int p_end, int back,
+                          const float* homs, int V, float* ct, void* stream) {
+    return render_packed_impl(packed, H, W, P, p_begin, p_end, back, homs, V, ct, true, stream);
+}
+
+int mpiv_combine_ct(const float* parts, int G, int64_t n, float* out, void* stream) {
+    if (!parts || !out) return fail(MPIV_ERR_ARG, "mpiv_combine_ct: null pointer");
+    if (G <= 0 || n <= 0) return fail(MPIV_ERR_ARG, "mpiv_combine_ct: bad shape");
+    if (!aligned16(parts)) return fail(MPIV_ERR_ARG, "mpiv_combine_ct: parts must be 16-byte aligned");
+    combine_ct_kernel<<<blocks(n, 256), 256, 0, S(stream)>>>(reinterpret_cast<const float4*>(parts), n, G, n, out);
+    return launched("mpiv_combine_ct");
+}
+
+static SweepParams sweep_params(int B, int Hs, int Ws, int C, int D, int Ht, int Wt) {
+    SweepParams sp;
+    sp.B = B; sp.Hs = Hs; sp.Ws = Ws; sp.C = C; sp.D = D; sp.Ht = Ht; sp.Wt = Wt;
+    sp.fhs = (float)Hs;
+    sp.fws = (float)Ws;
+    sp.half_ws = (float)Ws * 0.5f;
+    sp.half_hs = (float)Hs * 0.5f;
+    return sp;
+}
+
+int mpiv_plane_sweep(const float* img, const int64_t st[4], int B, int Hs, int Ws, int C, const float* ki,
+                     const float* proj, const float* depths, int D, int Ht, int Wt, float* out, void* stream) {
+    if (!img || !st || !ki || !proj || !depths || !out) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep: null pointer");
+    if (B <= 0 || Hs <= 0 || Ws <= 0 || C <= 0 || D <= 0 || Ht <= 0 || Wt <= 0)
+        return fail(MPIV_ERR_ARG, "mpiv_plane_sweep: bad shape");
+    const int64_t per_view = (int64_t)Ht * Wt * D;
+    if (B > kMaxGridYZ || blocks(per_view, 256) > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep: too large");
+    const ImgStrides s{st[0], st[1], st[2], st[3]};
+    dim3 grid(blocks(per_view, 256), B, 1);
+    plane_sweep_kernel<<<grid, 256, 0, S(stream)>>>(img, s, sweep_params(B, Hs, Ws, C, D, Ht, Wt), ki, proj, depths,
+                                                    out);
+    return launched("mpiv_plane_sweep");
+}
+
+int mpiv_inverse_warp(const float* img, const int64_t st[4], int B, int Hs, int Ws, int C, const float* ki,
+                      const float* proj, const float* depth, const int64_t dst[3], int Ht, int Wt, float* out,
+                      void* stream) {
+    if (!img || !st || !ki || !proj || !depth || !dst || !out)
+        return fail(MPIV_ERR_ARG, "mpiv_inverse_warp: null pointer");
+    if (B <= 0 || Hs <= 0 || Ws <= 0 || C <= 0 || Ht <= 0 || Wt <= 0)
+        return fail(MPIV_ERR_ARG, "mpiv_inverse_warp: bad shape");
+    if (B > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_inverse_warp: too large");
+    const ImgStrides s{st[0], st[1], st[2], st[3]};
+    dim3 grid(blocks((int64_t)Ht * Wt, 256), B, 1);
+    inverse_warp_kernel<<<grid, 256, 0, S(stream)>>>(img, s, sweep_params(B, Hs, Ws, C, 1, Ht, Wt), ki, proj, depth,
+                                                     dst[0], dst[1], dst[2], out);
+    return launched("mpiv_inverse_warp");
+}
+
+int mpiv_grid_sample(const float* in, const int64_t ist[4], int N, int C, int Hi, int Wi, const float* coords,
+                     const int64_t cst[4], int Ho, int Wo, float* out, const int64_t ost[4], void* stream) {
+    if (!in || !ist || !coords || !cst || !out || !ost) return fail(MPIV_ERR_ARG, "mpiv_grid_sample: null pointer");
+    if (N <= 0 || C <= 0 || Hi <= 0 || Wi <= 0 || Ho <= 0 || Wo <= 0)
+        return fail(MPIV_ERR_ARG, "mpiv_grid_sample: bad shape");
+    if (N > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_grid_sample: too large");
+    const Strides4 is{ist[0], ist[1], ist[2], ist[3]};
+    // coords strides arrive as (n, y, x, component); the kernel reads them as
+    // {n, c=component, y, x}
+    const Strides4 cs{cst[0], cst[3], cst[1], cst[2]};
+    const Strides4 os{ost[0], ost[1], ost[2], ost[3]};
+    dim3 grid(blocks((int64_t)Ho * Wo, 256), N, 1);
+    grid_sample_kernel<<<grid, 256, 0, S(stream)>>>(in, is, C, Hi, Wi, coords, cs, Ho, Wo, out, os);
+    return launched("mpiv_grid_sample");
+}
+
+int mpiv_over_composite(const float* const* layers, int P, int64_t n, int64_t ps, int64_t cs, float* out,
+                        void* stream) {
+    if (!layers || !out) return fail(MPIV_ERR_ARG, "mpiv_over_composite: null pointer");
+    if (P <= 0 || n <= 0) return fail(MPIV_ERR_ARG, "mpiv_over_composite: bad shape");
+    over_composite_kernel<<<blocks(n, 256), 256, 0, S(stream)>>>(layers, P, n, ps, cs, out);
+    return launched("mpiv_over_composite");
+}
+
+int mpiv_transform_points(const float* pts, int M, int64_t n, const float* homs, float* out, void* stream) {
+    if (!pts || !homs || !out) return fail(MPIV_ERR_ARG, "mpiv_transform_points: null pointer");
+    if (M <= 0 || n <= 0 || M > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_transform_points: bad shape");
+    transform_points_kernel<<<dim3(blocks(n, 256), M), 256, 0, S(stream)>>>(pts, n, homs, out);
+    return launched("mpiv_transform_points");
+}
+
+int mpiv_normalize_homogeneous(float* pts, int64_t n, int k, float* out, void* stream) {
+    if (!pts || !out) return fail(MPIV_ERR_ARG, "mpiv_normalize_homogeneous: null pointer");
+    if (n <= 0 || k <= 0) return fail(MPIV_ERR_ARG, "mpiv_normalize_homogeneous: bad shape");
+    normalize_homogeneous_kernel<<<blocks(n, 256), 256, 0, S(stream)>>>(pts, n, k, out);
+    return launched("mpiv_normalize_homogeneous");
+}
+
+int mpiv_pixel2cam(const float* depth, const float* pix, const float* ki, int B, int64_t n, int homogeneous,
+                   float* cam, void* stream) {
+    if (!depth || !pix || !ki || !cam) return fail(MPIV_ERR_ARG, "mpiv_pixel2cam: null pointer");
+    if (B <= 0 || n <= 0 || B > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_pixel2cam: bad shape");
+    pixel2cam_kernel<<<dim3(blocks(n, 256), B), 256, 0, S(stream)>>>(depth, pix, ki, n, homogeneous, cam);
+    return launched("mpiv_pixel2cam");
+}
+
+int mpiv_cam2pixel(const float* cam, const float* proj, int B, int64_t n, float* out, void* stream) {
+    if (!cam || !proj || !out) return fail(MPIV_ERR_ARG, "mpiv_cam2pixel: null pointer");
+    if (B <= 0 || n <= 0 || B > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_cam2pixel: bad shape");
+    cam2pixel_kernel<<<dim3(blocks(n, 256), B), 256, 0, S(stream)>>>(cam, proj, n, out);
+    return launched("mpiv_cam2pixel");
+}
+
+int mpiv_plane_coords(const float* pts, int M, int64_t n, const float* homs, int Ht, int Wt, float* coords,
+                      void* stream) {
+    if (!pts || !homs || !coords) return fail(MPIV_ERR_ARG, "mpiv_plane_coords: null pointer");
+    if (M <= 0 || n <= 0 || M > kMaxGridYZ || Ht <= 0 || Wt <= 0)
+        return fail(MPIV_ERR_ARG, "mpiv_plane_coords: bad shape");
+    plane_coords_kernel<<<dim3(blocks(n, 256), M), 256, 0, S(stream)>>>(pts, n, homs, (float)(Ht - 1),
+                                                                        (float)(Wt - 1), coords);
+    return launched("mpiv_plane_coords");
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// geometry.hip -- per-point projective-geometry helpers of the reference, for callers
+// that use them directly (the render / PSV kernels fuse the same arithmetic):
+//   transform_points_torch      utils.py:69-88    points @ H^T   (MKL sgemm FMA order)
+//   normalize_homogeneous_torch utils.py:90-101   uv / w, w == 0 -> 1e-8 (written back,
+//                                                 like the reference's in-place `+=`)
+//   pixel2cam_torch             utils.py:356-375  (Ki @ pix) * depth [, 1]
+//   cam2pixel_torch             utils.py:377-393  (proj @ cam)[:2] / (z + 1e-10)
+#include "mpiv_common.hpp"
+
+namespace mpiv {
+
+// points [M][n][3] contiguous, homs [M][9] -> out [M][n][3]
+__global__ __launch_bounds__(256) void transform_points_kernel(const float* __restrict__ pts, int64_t n,
+                                                               const float* __restrict__ homs,
+                                                               float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = blockIdx.y;
+    if (i >= n) return;
+    const float* h = homs + (int64_t)m * 9;
+    const float* p = pts + ((int64_t)m * n + i) * 3;
+    float* o = out + ((int64_t)m * n + i) * 3;
+    const float x = p[0], y = p[1], z = p[2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) o[r] = __builtin_fmaf(h[3 * r + 2], z, __builtin_fmaf(h[3 * r + 1], y, h[3 * r] * x));
+}
+
+// pts [n][k+1] contiguous (k = 1..3) -> out [n][k]; w == 0 is replaced in pts
+__global__ __launch_bounds__(256) void normalize_homogeneous_kernel(float* __restrict__ pts, int64_t n, int k,
+                                                                    float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float* p = pts + i * (k + 1);
+    float w = p[k];
+    if (w == 0.0f) {
+        w = w + 1e-8f;
+        p[k] = w;
+    }
+    for (int j = 0; j < k; ++j) out[i * k + j] = div_rn(p[j], w);
+}
+
+// depth [B][n], pix [B][3][n], ki [B][9] -> cam [B][3 or 4][n]
+__global__ __launch_bounds__(256) void pixel2cam_kernel(const float* __restrict__ depth,
+                                                        const float* __restrict__ pix, const float* __restrict__ ki,
+                                                        int64_t n, int homogeneous, float* __restrict__ cam) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (i >= n) return;
+    const float* k = ki + (int64_t)b * 9;
+    const float* pp = pix + (int64_t)b * 3 * n + i;
+    const float x = pp[0], y = pp[n], z = pp[2 * n];
+    const float d = depth[(int64_t)b * n + i];
+    const int rows = homogeneous ? 4 : 3;
+    float* c = cam + (int64_t)b * rows * n + i;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        c[r * n] = __builtin_fmaf(k[3 * r + 2], z, __builtin_fmaf(k[3 * r + 1], y, k[3 * r] * x)) * d;
+    if (homogeneous) c[3 * n] = 1.0f;
+}
+
+// cam [B][4][n], proj [B][16] -> out [B][n][2]
+__global__ __launch_bounds__(256) void cam2pixel_kernel(const float* __restrict__ cam,
+                                                        const float* __restrict__ proj, int64_t n,
+                                                        float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (i >= n) return;
+    const float* m = proj + (int64_t)b * 16;
+    const float* c = cam + (int64_t)b * 4 * n + i;
+    const float X = c[0], Y = c[n], Z = c[2 * n], Wc = c[3 * n];
+    float r[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+        r[j] = __builtin_fmaf(m[4 * j + 3], Wc,
+                              __builtin_fmaf(m[4 * j + 2], Z, __builtin_fmaf(m[4 * j + 1], Y, m[4 * j] * X)));
+    const float den = r[2] + 1e-10f;
+    float* o = out + ((int64_t)b * n + i) * 2;
+    o[0] = div_rn(r[0], den);
+    o[1] = div_rn(r[1], den);
+}
+
+// transform_plane_imgs_torch (utils.py:160-195) for arbitrary target points:
+// points [M][Ht*Wt][3], homs [M][9] -> normalised [0,1] sample coords [M][Ht*Wt][2]
+// (x / (Ht-1), y / (Wt-1) -- the reference's swap), ready for grid_sample_kernel.
+__global__ __launch_bounds__(256) void plane_coords_kernel(const float* __restrict__ pts, int64_t n,
+                                                           const float* __restrict__ homs, float hm1, float wm1,
+                                                           float* __restrict__ coords) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = blockIdx.y;
+    if (i >= n) return;
+    const float* h = homs + (int64_t)m * 9;
+    const float* p = pts + ((int64_t)m * n + i) * 3;
+    const float x = p[0], y = p[1], z = p[2];
+    const float u = __builtin_fmaf(h[2], z, __builtin_fmaf(h[1], y, h[0] * x));
+    const float v = __builtin_fmaf(h[5], z, __builtin_fmaf(h[4], y, h[3] * x));
+    float w = __builtin_fmaf(h[8], z, __builtin_fmaf(h[7], y, h[6] * x));
+    w = (w == 0.0f) ? w + 1e-8f : w;
+    float* o = coords + ((int64_t)m * n + i) * 2;
+    o[0] = div_rn(div_rn(u, w), hm1);
+    o[1] = div_rn(div_rn(v, w), wm1);
+}
+
+}  // namespace mpiv

@@ -1,0 +1,93 @@
+// mpiv_common.hpp -- device-side arithmetic shared by the MPI render / plane-sweep
+// kernels (gfx950, wave64).
+//
+// Every helper rounds exactly like the ATen CPU ops the reference utils.py runs
+// (SURVEY.md §8a recipe; pinned bit-exact by tests/test_oracle.py against the
+// reference's own outputs).  The library is compiled with -ffp-contract=off, so an
+// FMA appears only where it is written as __builtin_fmaf.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mpiv {
+
+constexpr int kWave = 64;
+
+// Correctly rounded fp32 division.  hipcc's default expansion of `a / b` is the
+// IEEE-exact v_div_scale / v_rcp / fma / v_div_fmas / v_div_fixup sequence; it is
+// kept verbatim (a reciprocal-multiply shifts coordinates by 1 ulp -> ~1e-4 output
+// error on sharp texels, measured in the survey).
+__device__ __forceinline__ float div_rn(float a, float b) { return a / b; }
+
+// grid value g in [-1, 1] -> source pixel, align_corners=False (ATen CPU vectorised
+// grid sampler: (g + 1) * (size / 2) - 0.5, contracted to one FMA).
+__device__ __forceinline__ float unnormalize(float g, float half_size) {
+    return __builtin_fmaf(g + 1.0f, half_size, -0.5f);
+}
+
+// -1 + 2*c (utils.py:127, :406).  2*c is exact, so one FMA rounds identically.
+__device__ __forceinline__ float to_grid(float c) { return __builtin_fmaf(2.0f, c, -1.0f); }
+
+// Bilinear weights + per-tap in-bounds flags for one sample point.
+struct Bilinear {
+    float nw, ne, sw, se;
+    int ix, iy;                  // floor(px), floor(py) as ints (valid where the flags say)
+    bool x0, x1, y0, y1;         // tap column/row inside the image
+};
+
+__device__ __forceinline__ Bilinear bilinear_setup(float px, float py, int Wi, int Hi) {
+    Bilinear b;
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float w = px - fx0, e = 1.0f - w;
+    const float n = py - fy0, s = 1.0f - n;
+    b.nw = s * e;
+    b.ne = s * w;
+    b.sw = n * e;
+    b.se = n * w;
+    // float compares: NaN / huge coordinates are simply out of bounds (== ATen's int
+    // compares for every finite coordinate)
+    b.x0 = (fx0 >= 0.0f) & (fx0 < (float)Wi);
+    b.x1 = (fx0 >= -1.0f) & (fx0 < (float)(Wi - 1));
+    b.y0 = (fy0 >= 0.0f) & (fy0 < (float)Hi);
+    b.y1 = (fy0 >= -1.0f) & (fy0 < (float)(Hi - 1));
+    // clamp before the int conversion so the index is always defined
+    b.ix = (int)fminf(fmaxf(fx0, -1.0f), (float)Wi);
+    b.iy = (int)fminf(fmaxf(fy0, -1.0f), (float)Hi);
+    return b;
+}
+
+// v = nw_v*nw; v = fma(ne_v, ne, v); v = fma(sw_v, sw, v); v = fma(se_v, se, v)
+__device__ __forceinline__ float blend4(const Bilinear& b, float v_nw, float v_ne, float v_sw, float v_se) {
+    float acc = v_nw * b.nw;
+    acc = __builtin_fmaf(v_ne, b.ne, acc);
+    acc = __builtin_fmaf(v_sw, b.sw, acc);
+    acc = __builtin_fmaf(v_se, b.se, acc);
+    return acc;
+}
+
+// Over operator, back-to-front, unfused like the reference's separate tensor ops
+// (utils.py:155-156): out = rgb*a + out*(1-a).
+__device__ __forceinline__ float over(float rgb, float a, float one_minus_a, float out) {
+    const float t0 = rgb * a;
+    const float t2 = out * one_minus_a;
+    return t0 + t2;
+}
+
+// Target pixel (x, y) through a row-major 3x3 homography -> normalised sample
+// position (px, py) in source pixels, the render's recipe (utils.py:178-188, 127;
+// grid_sample unnormalise).  inv_hm1 / inv_wm1 are NOT reciprocals: the reference
+// divides by (H-1) and (W-1), so those stay true divisions.
+__device__ __forceinline__ void hom_sample_pos(const float* __restrict__ h, float fx, float fy,
+                                               float hm1, float wm1, float half_w, float half_h,
+                                               float& px, float& py) {
+    const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
+    const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
+    float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+    w = (w == 0.0f) ? w + 1e-8f : w;  // divide_safe_torch, utils.py:38
+    const float cx = div_rn(div_rn(u, w), hm1);  // SWAPPED: x / (H-1), utils.py:188
+    const float cy = div_rn(div_rn(v, w), wm1);  //          y / (W-1)
+    px = unnormalize(to_grid(cx), half_w);
+    py = unnormalize(to_grid(cy), half_h);
+}
+
+}  // namespace mpiv

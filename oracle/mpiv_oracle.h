@@ -1,0 +1,26 @@
+/* mpiv_oracle.h -- CPU restatement of the reference arithmetic (TEST INFRASTRUCTURE ONLY).
+ * See mpiv_oracle.c for the per-step citations into the reference utils.py.
+ * All strides are in ELEMENTS (floats). */
+#ifndef MPIV_ORACLE_H
+#define MPIV_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* mpi [B,H,W,P,4] with strides st[5]; homs [B][P][9] row-major; out [B,H,W,3] contiguous */
+void oracle_render(const float *mpi, const int64_t st[5], int B, int H, int W, int P,
+                   const float *homs, float *out, int nthreads);
+/* img [B,Hs,Ws,C] strides st[4]; ki [B][9]; proj [B][16]; depths [D] fp32; out [B,Ht,Wt,D*C] */
+void oracle_plane_sweep(const float *img, const int64_t st[4], int B, int Hs, int Ws, int C,
+                        const float *ki, const float *proj, const float *depths, int D,
+                        int Ht, int Wt, float *out, int nthreads);
+/* in [N,C,Hi,Wi] strides ist; coords [N,Ho,Wo,2] contiguous (in [0,1] units); out strides ost (N,C,H,W) */
+void oracle_grid_sample(const float *in, const int64_t ist[4], int N, int C, int Hi, int Wi,
+                        const float *coords, int Ho, int Wo, float *out, const int64_t ost[4],
+                        int nthreads);
+/* layers [P][n][4] contiguous; out [n][3] */
+void oracle_over_composite(const float *layers, int P, int64_t n, float *out);
+#ifdef __cplusplus
+}
+#endif
+#endif

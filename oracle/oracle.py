@@ -1,0 +1,104 @@
+"""ctypes wrapper around oracle/libmpiv_oracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+as the checker; the product package (mpi_vision_amd) never imports it.
+Pinned against the reference's outputs in tests/golden/ (tests/test_oracle.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "libmpiv_oracle.so")
+_lib = None
+
+_f = ctypes.POINTER(ctypes.c_float)
+_i64 = ctypes.POINTER(ctypes.c_int64)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        L.oracle_render.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, _f, ctypes.c_int]
+        L.oracle_plane_sweep.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, _f, _f] + \
+            [ctypes.c_int] * 3 + [_f, ctypes.c_int]
+        L.oracle_grid_sample.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, ctypes.c_int, ctypes.c_int,
+                                                                          _f, _i64, ctypes.c_int]
+        L.oracle_over_composite.argtypes = [_f, ctypes.c_int, ctypes.c_int64, _f]
+        _lib = L
+    return _lib
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(_f)
+
+
+def _strides(a: np.ndarray):
+    return (ctypes.c_int64 * a.ndim)(*[s // a.itemsize for s in a.strides])
+
+
+def _threads(n):
+    return int(n if n else os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def render(mpi: np.ndarray, homs: np.ndarray, nthreads: int = 0) -> np.ndarray:
+    """mpi [B,H,W,P,4] float32 (any strides, e.g. a broadcast view), homs [B,P,9] -> [B,H,W,3]."""
+    assert mpi.dtype == np.float32 and mpi.ndim == 5 and mpi.shape[-1] == 4
+    B, H, W, P, _ = mpi.shape
+    homs = np.ascontiguousarray(homs, dtype=np.float32).reshape(B, P, 9)
+    out = np.empty((B, H, W, 3), np.float32)
+    lib().oracle_render(_fp(mpi), _strides(mpi), B, H, W, P, _fp(homs), _fp(out), _threads(nthreads))
+    return out
+
+
+def plane_sweep(img: np.ndarray, ki: np.ndarray, proj: np.ndarray, depths, tgt_h: int, tgt_w: int,
+                nthreads: int = 0) -> np.ndarray:
+    """img [B,Hs,Ws,C]; ki [B,9]; proj [B,16]; depths (python floats -> fp32) -> [B,Ht,Wt,D*C]."""
+    assert img.dtype == np.float32 and img.ndim == 4
+    B, Hs, Ws, C = img.shape
+    ki = np.ascontiguousarray(ki, np.float32).reshape(B, 9)
+    proj = np.ascontiguousarray(proj, np.float32).reshape(B, 16)
+    d = np.asarray(depths, dtype=np.float64).astype(np.float32)
+    D = d.shape[0]
+    out = np.empty((B, tgt_h, tgt_w, D * C), np.float32)
+    lib().oracle_plane_sweep(_fp(img), _strides(img), B, Hs, Ws, C, _fp(ki), _fp(proj), _fp(d), D,
+                             tgt_h, tgt_w, _fp(out), _threads(nthreads))
+    return out
+
+
+def grid_sample_nchw(inp: np.ndarray, coords: np.ndarray, out_channels_last: bool,
+                     nthreads: int = 0) -> np.ndarray:
+    """inp [N,C,Hi,Wi] (any strides), coords [N,Ho,Wo,2] in [0,1] units -> NCHW or NHWC."""
+    N, C, Hi, Wi = inp.shape
+    coords = np.ascontiguousarray(coords, np.float32)
+    _, Ho, Wo, _ = coords.shape
+    if out_channels_last:
+        out = np.empty((N, Ho, Wo, C), np.float32)
+        view = out.transpose(0, 3, 1, 2)
+    else:
+        out = np.empty((N, C, Ho, Wo), np.float32)
+        view = out
+    lib().oracle_grid_sample(_fp(inp), _strides(inp), N, C, Hi, Wi, _fp(coords), Ho, Wo, _fp(out),
+                             _strides(view), _threads(nthreads))
+    return out
+
+
+def over_composite(layers: np.ndarray) -> np.ndarray:
+    """layers [P, ..., 4] -> [..., 3]."""
+    layers = np.ascontiguousarray(layers, np.float32)
+    P = layers.shape[0]
+    n = int(np.prod(layers.shape[1:-1]))
+    out = np.empty(layers.shape[1:-1] + (3,), np.float32)
+    lib().oracle_over_composite(_fp(layers), P, n, _fp(out))
+    return out

@@ -1,0 +1,91 @@
+"""Shared fixtures.  `gpu`-marked tests need a ROCm device (run on the MI355X box);
+everything else runs on CPU (oracle vs reference goldens, host logic, ABI surface)."""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(REPO, "tests", "golden")
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X)")
+    config.addinivalue_line("markers", "slow: multi-second CPU case")
+
+
+@pytest.fixture(scope="session")
+def small():
+    return np.load(os.path.join(GOLD, "small.npz"))
+
+
+@pytest.fixture(scope="session")
+def large():
+    return np.load(os.path.join(GOLD, "large.npz"))
+
+
+@pytest.fixture(scope="session")
+def meta():
+    with open(os.path.join(GOLD, "meta.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")
+
+
+def sha256(a) -> str:
+    if isinstance(a, torch.Tensor):
+        a = a.detach().cpu().contiguous().numpy()
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def bits_equal(a, b) -> bool:
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def render_case_inputs(meta_small, name):
+    """Regenerate the seeded MPI of a golden render case (sha-checked)."""
+    from mpi_vision_amd import configs
+    m = meta_small[name]
+    mpi = configs.synthetic_mpi(1 if m["broadcast"] else m["B"], m["H"], m["W"], m["P"], m["seed"])
+    if m.get("alpha_fn") == "binary_alpha":
+        mpi[..., 3] = (mpi[..., 3] > 0.5).float()
+        mpi[:, :, :, 0, 3] = 1.0
+    assert sha256(mpi) == m["mpi_sha"], f"{name}: regenerated MPI does not match the golden input"
+    if m["broadcast"]:
+        mpi = mpi.expand(m["B"], *mpi.shape[1:])
+    return mpi
+
+
+def psv_case_input(meta_small, name):
+    m = meta_small[name]
+    g = torch.Generator().manual_seed(m["seed"])
+    img = torch.rand((m.get("B", 1), m["H"], m["W"], m["C"]), generator=g, dtype=torch.float32)
+    if "B" not in m:
+        img = img[0]
+    assert sha256(img) == m["img_sha"], f"{name}: regenerated image does not match the golden input"
+    return img
+
+
+def load_test_mpi():
+    """The repo's 10-plane test MPI (reference test/rgba_00..09.png) as [1,400,640,10,4]."""
+    from PIL import Image
+    planes = [np.array(Image.open(os.path.join(GOLD, "test_mpi", f"rgba_{i:02d}.png"))) for i in range(10)]
+    return (torch.tensor(np.stack(planes, axis=2)).float() / 255).unsqueeze(0)
+
+
+RENDER_CASES = ["render_a", "render_big", "render_odd", "render_bin", "render_p1"]

@@ -1,0 +1,139 @@
+"""GPU parity of the fused warp + over-composite kernels against the reference
+goldens (bit-exact) and the CPU oracle (tests/golden/, tools/gen_goldens.py).
+
+Tolerance: the bar is bit-exact (0 ulp) for every single-GPU render path; the
+plane-sharded (C,T) reassociation is checked at 1e-5 absolute (BASELINE.json
+north_star), with ~3e-7 expected."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import RENDER_CASES, bits_equal, load_test_mpi, render_case_inputs, sha256
+
+pytestmark = pytest.mark.gpu
+
+import mpi_vision_amd as mv  # noqa: E402
+from mpi_vision_amd import _lib, configs  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+
+def _t(small, key, dev):
+    return torch.tensor(small[key]).to(dev)
+
+
+@pytest.mark.parametrize("name", RENDER_CASES)
+def test_render_matches_reference(name, small, meta, dev):
+    mpi = render_case_inputs(meta["small"], name)
+    out = mv.mpi_render_view_torch(mpi.to(dev) if mpi.stride(0) else mpi[:1].to(dev).expand(*mpi.shape),
+                                   _t(small, f"{name}_pose", dev), _t(small, f"{name}_depths", dev),
+                                   _t(small, f"{name}_K", dev))
+    assert bits_equal(out.cpu().numpy(), small[f"{name}_out"])
+
+
+@pytest.mark.parametrize("name", RENDER_CASES)
+def test_native_and_packed_kernels_agree_with_oracle(name, small, meta, dev):
+    """Both texel layouts, driven with the reference's own H bits."""
+    mpi = render_case_inputs(meta["small"], name)
+    B, H, W, P, _ = mpi.shape
+    homs = torch.tensor(small[f"{name}_H"]).permute(1, 0, 2, 3).reshape(B, P, 9)
+    want = oracle.render(mpi.numpy(), homs.numpy())
+    dmpi = mpi.contiguous().to(dev)
+    nat = torch.empty((B, H, W, 3), device=dev)
+    _lib._call("mpiv_render", _lib._p(dmpi), _lib._strides(dmpi), B, H, W, P, _lib._p(homs.to(dev)),
+               _lib._p(nat), _lib._stream(dev))
+    assert bits_equal(nat.cpu().numpy(), want)
+    for b in range(B):
+        packed = _lib.pack_planes(dmpi[b])
+        assert torch.equal(packed.cpu(), mpi[b].permute(2, 0, 1, 3).contiguous())
+        pk = _lib.render_packed(packed, homs[b:b + 1])
+        assert bits_equal(pk.cpu().numpy(), want[b:b + 1])
+
+
+def test_render_strided_views(small, meta, dev):
+    """Non-contiguous MPI (a channel-sliced / permuted view) is read in place."""
+    mpi = render_case_inputs(meta["small"], "render_a")
+    big = torch.zeros((2, 72, 128, 8, 6))
+    big[..., 1:5] = mpi
+    dbig = big.to(dev)
+    view = dbig[..., 1:5]
+    out = mv.mpi_render_view_torch(view, _t(small, "render_a_pose", dev), _t(small, "render_a_depths", dev),
+                                   _t(small, "render_a_K", dev))
+    assert bits_equal(out.cpu().numpy(), small["render_a_out"])
+
+
+def test_render_c1_test_mpi(large, meta, dev):
+    """Config 1: the repo's 10-plane test MPI, two novel poses, full 400x640."""
+    mpi = load_test_mpi()
+    assert sha256(mpi) == meta["large"]["c1"]["mpi_sha"]
+    dmpi = mpi.to(dev).expand(2, *mpi.shape[1:])
+    out = mv.mpi_render_view_torch(dmpi, _t(large, "c1_pose", dev), _t(large, "c1_depths", dev),
+                                   _t(large, "c1_K", dev))
+    got = out.cpu().numpy()
+    assert bits_equal(got, large["c1_out"])
+    assert sha256(got) == meta["large"]["c1"]["out_sha"]
+    # also the native (non-broadcast) kernel on each pose
+    for b in range(2):
+        o1 = mv.mpi_render_view_torch(mpi.to(dev), _t(large, "c1_pose", dev)[b:b + 1],
+                                      _t(large, "c1_depths", dev), _t(large, "c1_K", dev)[b:b + 1])
+        assert bits_equal(o1.cpu().numpy(), large["c1_out"][b:b + 1])
+
+
+def test_render_c2_broadcast_batch(large, meta, dev):
+    """Config 2 shapes (576x1024x32, MPI broadcast over the view batch)."""
+    c2 = configs.config2()
+    mpi = configs.synthetic_mpi(1, c2["H"], c2["W"], c2["P"], c2["seed"])
+    assert sha256(mpi) == meta["large"]["c2"]["mpi_sha"]
+    poses = _t(large, "c2_pose", dev)
+    dmpi = mpi.to(dev).expand(poses.shape[0], *mpi.shape[1:])
+    out = mv.mpi_render_view_torch(dmpi, poses, _t(large, "c2_depths", dev), _t(large, "c2_K", dev))
+    assert sha256(out) == meta["large"]["c2"]["out_sha"]
+
+
+@pytest.mark.parametrize("pose_index", [0, 500])
+def test_render_c4_headline_config(pose_index, large, meta, dev):
+    """Config 4 (the bench workload): 1024x1024x128 MPI, poses 0 and 500 of the path."""
+    c4 = configs.config4()
+    mpi = configs.synthetic_mpi(1, c4["H"], c4["W"], c4["P"], c4["seed"])
+    assert sha256(mpi) == meta["large"]["c4"]["mpi_sha"]
+    j = meta["large"]["c4"]["sel"].index(pose_index)
+    out = mv.mpi_render_view_torch(mpi.to(dev), _t(large, f"c4_{pose_index}_pose", dev), _t(large, "c4_depths", dev),
+                                   _t(large, "c4_K", dev))
+    got = out.cpu().numpy().reshape(-1)
+    np.testing.assert_array_equal(got[large[f"c4_{pose_index}_idx"]], large[f"c4_{pose_index}_val"])
+    assert sha256(out) == meta["large"]["c4"]["out_sha"][j]
+
+
+def test_plane_range_partials_combine(small, meta, dev):
+    """(C,T) partials over plane ranges + ordered combine == sequential render (1e-5)."""
+    mpi = render_case_inputs(meta["small"], "render_a")[0:1]
+    P = mpi.shape[3]
+    homs = torch.tensor(small["render_a_H"]).permute(1, 0, 2, 3)[0:1].reshape(1, P, 9)
+    packed = _lib.pack_planes(mpi[0].to(dev))
+    want = small["render_a_out"][0:1]
+    for cuts in ([0, 8], [0, 3, 8], [0, 1, 2, 5, 8], list(range(9))):
+        parts = torch.stack([_lib.render_packed_ct(packed, homs, back=(a == 0), p_begin=a, p_end=b)
+                             for a, b in zip(cuts[:-1], cuts[1:])])
+        got = _lib.combine_ct(parts).cpu().numpy()
+        np.testing.assert_allclose(got, want, rtol=0, atol=1e-5)
+        if len(cuts) == 2:
+            assert bits_equal(got, want)  # a single range is the sequential order
+
+
+def test_render_deterministic(small, meta, dev):
+    mpi = render_case_inputs(meta["small"], "render_big").to(dev)
+    args = (_t(small, "render_big_pose", dev), _t(small, "render_big_depths", dev), _t(small, "render_big_K", dev))
+    a = mv.mpi_render_view_torch(mpi, *args)
+    b = mv.mpi_render_view_torch(mpi, *args)
+    assert torch.equal(a, b)
+
+
+def test_render_errors(dev):
+    mpi = torch.zeros((1, 8, 8, 2, 4), device=dev)
+    pose = torch.eye(4, device=dev)[None]
+    K = torch.eye(3, device=dev)[None]
+    with pytest.raises(AttributeError):  # planes must be a tensor, like the reference
+        mv.mpi_render_view_torch(mpi, pose, [2.0, 1.0], K)
+    with pytest.raises(RuntimeError):
+        mv.mpi_render_view_torch(mpi.double(), pose, torch.tensor([2.0, 1.0], device=dev), K)
+    with pytest.raises(RuntimeError):  # batch mismatch
+        mv.mpi_render_view_torch(mpi, pose.expand(2, 4, 4), torch.tensor([2.0, 1.0], device=dev), K.expand(2, 3, 3))
