@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Headline benchmark: rendered Mpix/s of the fused MPI warp + over-composite on
+BASELINE.json config 4 (128-plane 1024x1024 MPI, 1000-pose camera path,
+view-sharded), plus the dominant kernel's HBM roofline fraction and the CPU
+restatement timed on the same host.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--views V]
+
+One process per GPU (torchrun for N > 1).  Each rank holds a full MPI replica in
+HBM (packed plane-major once, outside the timed region) and every step renders
+V views of the camera path (rank r renders path poses r*V .. r*V+V-1 modulo the
+path), so per-GPU work is fixed as N grows ("weak"); at N = 8 and V = 125 one step
+is exactly the 1000-pose path.  There is no collective on the data path.
+
+Per step (inside the timed region): host-side homographies for the NEXT step
+(torch-CPU fp32, the reference's op order) overlap the current launch; then one
+render launch writes V frames [V,1024,1024,3] fp32 that stay in HBM.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from mpi_vision_amd import _host, _lib, configs  # noqa: E402
+
+METRIC = "rendered Mpix/sec (node) + achieved HBM GB/s fraction, 1024²×128-plane MPI"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--views", type=int, default=125, help="views rendered per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
+    ap.add_argument("--kernel", choices=["packed", "native"], default="packed")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local)
+
+
+def max_over_ranks(x: float, world: int, dev) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def load_traffic(profile_dir: str):
+    """Per-launch HBM bytes of the render kernel from the committed rocprofv3 PMC
+    summary (tools/profile.sh), corrected as MI355X_MICROARCH.md §HBM prescribes."""
+    path = os.path.join(profile_dir, "render_pmc.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(mpi_dev: torch.Tensor, homs_all: torch.Tensor, budget_s: float, check_frames):
+    """The oracle's C restatement (bit-exact to the reference) on this host's cores,
+    on a bounded sample: whole views of the same MPI, as many as fit ~budget_s."""
+    from oracle import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    mpi = mpi_dev.cpu().numpy()[None]          # [1,H,W,P,4]
+    H, W = mpi.shape[1], mpi.shape[2]
+    views, t_total, outs = 0, 0.0, []
+    while views == 0 or (t_total < budget_s and views < homs_all.shape[0]):
+        h = homs_all[views:views + 1].numpy()
+        t0 = time.perf_counter()
+        o = oracle.render(mpi, h, threads)
+        t_total += time.perf_counter() - t0
+        outs.append(o)
+        views += 1
+    mism = 0
+    for i, o in enumerate(outs[:len(check_frames)]):
+        if not np.array_equal(o, check_frames[i]):
+            mism += 1
+    return {"value": views * H * W / 1e6 / t_total, "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"{views} full view(s) of the 1024x1024x128 MPI with the oracle's C restatement "
+                      f"(oracle/mpiv_oracle.c, {threads} OpenMP threads), {t_total:.1f} s",
+            "gpu_frames_bit_exact_vs_cpu": mism == 0}
+
+
+def main():
+    args = parse()
+    world, rank, dev = dist_setup(args)
+    torch.cuda.set_device(dev)
+    c4 = configs.config4()
+    H, W, P = c4["H"], c4["W"], c4["P"]
+    V = args.views
+    n_path = len(c4["poses"])
+
+    # --- resident inputs: one MPI replica per GPU (generated on device), packed once
+    gen = torch.Generator(device=dev).manual_seed(c4["seed"])
+    view = torch.rand((H, W, P, 4), generator=gen, device=dev, dtype=torch.float32)
+    view[..., :3].mul_(2.0).sub_(1.0)
+    view[:, :, 0, 3] = 1.0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    packed = _lib.pack_planes(view) if args.kernel == "packed" else None
+    torch.cuda.synchronize()
+    pack_ms = (time.perf_counter() - t0) * 1e3
+    mpi5 = view.unsqueeze(0).expand(V, H, W, P, 4)
+
+    poses = configs.f32(c4["poses"])
+    K = configs.f32(c4["K"])
+    depths = configs.f32(c4["depths"])
+
+    def step_indices(s):
+        base = (rank * V + s * world * V) % n_path
+        return [(base + j) % n_path for j in range(V)]
+
+    def host_homs(s):
+        idx = step_indices(s)
+        return _host.render_homographies(poses[idx], depths, K.expand(V, 3, 3), V)
+
+    out = torch.empty((V, H, W, 3), device=dev, dtype=torch.float32)
+    hbuf = [torch.empty((V, P, 9), dtype=torch.float32).pin_memory() for _ in range(2)]
+    dbuf = [torch.empty((V, P, 9), device=dev, dtype=torch.float32) for _ in range(2)]
+    stream = torch.cuda.current_stream(dev)
+
+    def launch(s, h_dev):
+        if args.kernel == "packed":
+            _lib._call("mpiv_render_packed", _lib._p(packed), H, W, P, _lib._p(h_dev), V, _lib._p(out),
+                       _lib._stream(dev))
+        else:
+            _lib._call("mpiv_render", _lib._p(mpi5), _lib._strides(mpi5), V, H, W, P, _lib._p(h_dev),
+                       _lib._p(out), _lib._stream(dev))
+
+    copied = [None, None]  # event recorded after the last H2D copy out of each pinned slot
+
+    def upload(s):
+        slot = s % 2
+        if copied[slot] is not None:
+            copied[slot].synchronize()  # the DMA has read this pinned buffer; safe to refill
+        hbuf[slot].copy_(host_homs(s))
+        dbuf[slot].copy_(hbuf[slot], non_blocking=True)  # stream-ordered after earlier launches
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        copied[slot] = ev
+
+    def run(n_steps, first, events=None):
+        upload(first)
+        for s in range(first, first + n_steps):
+            if events is not None:
+                events[s - first][0].record(stream)
+            launch(s, dbuf[s % 2])
+            if events is not None:
+                events[s - first][1].record(stream)
+            if s + 1 < first + n_steps:
+                upload(s + 1)  # host-side homographies of the next step overlap this launch
+
+    run(args.warmup, 0)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    run(args.steps, args.warmup, events)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(elapsed, world, dev)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+
+    mpix_total = world * args.steps * V * H * W / 1e6
+    value = mpix_total / elapsed
+    alg_bytes = V * (P * H * W * 16 + H * W * 12)
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = load_traffic(os.path.join(REPO, "profiles"))
+
+    if rank == 0:
+        res = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Mpix/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded U[-1,1) rgb / U[0,1) alpha MPI generated on device; viewer-style 1000-pose sway path)",
+            "config": {"workload": "BASELINE config 4: 128-plane 1024x1024 MPI, 1000-pose camera path, view-sharded",
+                       "H": H, "W": W, "planes": P, "views_per_gpu_per_step": V, "kernel": args.kernel,
+                       "parallelism": f"view-sharded x{world} (replicas, no data-path collective)",
+                       "views_per_s": round(value / (H * W / 1e6), 2), "pack_ms_once": round(pack_ms, 2)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "render_packed_kernel" if args.kernel == "packed" else "render_native_kernel",
+                         "kernel_ms_per_launch": round(kern_ms, 3),
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": None,
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            # the GPU frames of the first views of step 0, to cross-check the CPU sample bit-exactly
+            hs = host_homs(0)
+            _lib._call("mpiv_render_packed" if args.kernel == "packed" else "mpiv_render",
+                       *([_lib._p(packed), H, W, P, _lib._p(hs[:1].to(dev)), 1, _lib._p(out), _lib._stream(dev)]
+                         if args.kernel == "packed" else
+                         [_lib._p(mpi5[:1]), _lib._strides(mpi5[:1]), 1, H, W, P, _lib._p(hs[:1].to(dev)),
+                          _lib._p(out), _lib._stream(dev)]))
+            torch.cuda.synchronize()
+            frames = [out[:1].cpu().numpy()]
+            res["cpu_baseline"] = cpu_baseline(view, hs, args.cpu_seconds, frames)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

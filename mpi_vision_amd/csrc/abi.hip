@@ -53,8 +53,16 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
     if (B <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "mpiv_render: bad shape");
     if (B > kMaxGridYZ || (H + kTileY - 1) / kTileY > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_render: too large");
     const NativeStrides s{st[0], st[1], st[2], st[3], st[4]};
-    dim3 grid(blocks(W, kTileX), blocks(H, kTileY), B);
-    render_native_kernel<<<grid, 256, 0, S(stream)>>>(mpi, s, make_geom(H, W, P), homs, out);
+    const dim3 grid(blocks(W, kTileX), blocks(H, kTileY), B);
+    const RenderGeom g = make_geom(H, W, P);
+    // 16-B vector texel loads when channels are contiguous and every texel is aligned
+    const bool vec = s.c == 1 && aligned16(mpi) && s.b % 4 == 0 && s.y % 4 == 0 && s.x % 4 == 0 && s.p % 4 == 0;
+    const bool fast = H >= 2 && W >= 2;
+    hipStream_t q = S(stream);
+    if (vec && fast) render_native_kernel<true, true><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
+    else if (vec) render_native_kernel<true, false><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
+    else if (fast) render_native_kernel<false, true><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
+    else render_native_kernel<false, false><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
     return launched("mpiv_render");
 }
 
@@ -78,16 +86,23 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     if (V <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
     if (p_begin < 0 || p_end > P || p_begin >= p_end) return fail(MPIV_ERR_ARG, "%s: bad plane range", nm);
     if (!aligned16(packed) || (ct && !aligned16(out))) return fail(MPIV_ERR_ARG, "%s: 16-byte alignment", nm);
-    if (V > kMaxGridYZ || (H + kTileY - 1) / kTileY > kMaxGridYZ) return fail(MPIV_ERR_ARG, "%s: too large", nm);
-    dim3 grid(blocks(W, kTileX), blocks(H, kTileY), V);
+    if ((int64_t)H * W * 16 >= (int64_t)kOOB) return fail(MPIV_ERR_ARG, "%s: plane larger than 2 GiB", nm);
+    const int64_t nblocks = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;
+    if (nblocks > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const float4* pk = reinterpret_cast<const float4*>(packed);
     const int64_t ps = (int64_t)H * W;
-    if (ct)
-        render_packed_kernel<true><<<grid, 256, 0, S(stream)>>>(pk, ps, make_geom(H, W, P), p_begin, p_end,
-                                                                back, homs, out);
+    const RenderGeom g = make_geom(H, W, P);
+    const bool fast = H >= 2 && W >= 2;  // div_const needs divisors >= 1
+    const dim3 grid((unsigned)nblocks), blk(256);
+    hipStream_t st = S(stream);
+    if (ct && fast)
+        render_packed_kernel<true, true><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
+    else if (ct)
+        render_packed_kernel<true, false><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
+    else if (fast)
+        render_packed_kernel<false, true><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
     else
-        render_packed_kernel<false><<<grid, 256, 0, S(stream)>>>(pk, ps, make_geom(H, W, P), p_begin, p_end,
-                                                                 1, homs, out);
+        render_packed_kernel<false, false><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
     return launched(nm);
 }
 

@@ -13,11 +13,45 @@ namespace mpiv {
 
 constexpr int kWave = 64;
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte raw buffer load.  ROCm 7.2's __builtin_amdgcn_raw_buffer_load_b128 lowers to
+// a 4-byte buffer_load_dword (observed in the .s; the other 12 bytes are garbage), so
+// the LLVM intrinsic is bound directly, as composable_kernel does.
+__device__ f32x4 llvm_raw_buffer_load_v4f32(__amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset,
+                                            int aux) __asm("llvm.amdgcn.raw.ptr.buffer.load.v4f32");
+__device__ float llvm_raw_buffer_load_f32(__amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset,
+                                          int aux) __asm("llvm.amdgcn.raw.ptr.buffer.load.f32");
+
+// Out-of-range buffer offset: the buffer unit's range check returns 0 for it without
+// touching memory -- exactly grid_sample's per-tap zero padding.
+constexpr int kOOB = 0x7FFFFF00;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+
 // Correctly rounded fp32 division.  hipcc's default expansion of `a / b` is the
 // IEEE-exact v_div_scale / v_rcp / fma / v_div_fmas / v_div_fixup sequence; it is
 // kept verbatim (a reciprocal-multiply shifts coordinates by 1 ulp -> ~1e-4 output
 // error on sharp texels, measured in the survey).
 __device__ __forceinline__ float div_rn(float a, float b) { return a / b; }
+
+// Correctly rounded x / c for a launch-uniform divisor c >= 1, given rc = RN(1/c)
+// (computed on the host as 1.0f / c).  This is the core of the hardware IEEE division
+// sequence (q = a*y; two residual corrections r = fma(-b, q, a), q = fma(r, y, q)) with
+// the per-element v_rcp + Newton step replaced by the exactly rounded reciprocal and
+// v_div_scale / v_div_fixup dropped: those only act when |x| or the quotient leaves
+// the normal range, and there (|x / c| < 2^-26, or x = +-inf) the quotient cannot
+// change the sample position: -1 + 2*cx rounds to -1 for any |cx| < 2^-26, and an
+// infinite coordinate yields NaN weights either way.  5 VALU instead of 11.
+__device__ __forceinline__ float div_const(float x, float c, float rc) {
+    float q = x * rc;
+    float r = __builtin_fmaf(-c, q, x);
+    q = __builtin_fmaf(r, rc, q);
+    r = __builtin_fmaf(-c, q, x);
+    return __builtin_fmaf(r, rc, q);
+}
 
 // grid value g in [-1, 1] -> source pixel, align_corners=False (ATen CPU vectorised
 // grid sampler: (g + 1) * (size / 2) - 0.5, contracted to one FMA).

@@ -24,89 +24,179 @@ constexpr int kTileY = 4;   // 4 waves per 256-thread block
 
 struct RenderGeom {
     int H, W, P;
-    float hm1, wm1, half_w, half_h;
+    int plane_bytes;            // H*W*16 (< 2 GiB, checked on the host)
+    float hm1, wm1;             // H-1, W-1: the reference's (swapped) normalisers
+    float rc_hm1, rc_wm1;       // RN(1/(H-1)), RN(1/(W-1)) for div_const
+    float half_w, half_h;       // grid_sample unnormalise scales W/2, H/2
 };
 
-__host__ __device__ inline RenderGeom make_geom(int H, int W, int P) {
+inline RenderGeom make_geom(int H, int W, int P) {
     RenderGeom g;
     g.H = H; g.W = W; g.P = P;
+    g.plane_bytes = (int)((int64_t)H * W * 16);
     g.hm1 = (float)(H - 1);
     g.wm1 = (float)(W - 1);
+    g.rc_hm1 = 1.0f / g.hm1;
+    g.rc_wm1 = 1.0f / g.wm1;
     g.half_w = (float)W * 0.5f;
     g.half_h = (float)H * 0.5f;
     return g;
+}
+
+// Target pixel through the plane's homography -> source sample position.
+// FAST: the two launch-constant divisions use div_const (valid for H, W >= 2).
+template <bool FAST>
+__device__ __forceinline__ void render_pos(const float* __restrict__ h, float fx, float fy, const RenderGeom& g,
+                                           float& px, float& py) {
+    if (FAST) {
+        const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
+        const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
+        float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+        w = (w == 0.0f) ? w + 1e-8f : w;  // divide_safe_torch, utils.py:38
+        const float cx = div_const(div_rn(u, w), g.hm1, g.rc_hm1);  // SWAPPED x / (H-1), utils.py:188
+        const float cy = div_const(div_rn(v, w), g.wm1, g.rc_wm1);  //         y / (W-1)
+        px = unnormalize(to_grid(cx), g.half_w);
+        py = unnormalize(to_grid(cy), g.half_h);
+    } else {
+        hom_sample_pos(h, fx, fy, g.hm1, g.wm1, g.half_w, g.half_h, px, py);
+    }
 }
 
 // ---------------------------------------------------------------------------
 // packed plane-major layout
 // ---------------------------------------------------------------------------
 
-__device__ __forceinline__ float4 ld_tap(const float4* __restrict__ plane, int W, int ix, int iy, bool ok) {
-    float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    return ok ? plane[(int64_t)iy * W + ix] : z;
+// One bilinear sample in flight: the four 16-B taps (already issued) + weights.
+struct TapSet {
+    f32x4 a, b, c, d;           // NW, NE, SW, SE texels (0 where outside the plane)
+    float nw, ne, sw, se;
+};
+
+// Issue the four tap loads of one sample of one packed plane.  Taps outside the
+// plane (and every tap when `live` is false) get the out-of-range offset, so the
+// buffer unit returns 0 for them without a memory access: grid_sample's zeros
+// padding, per tap.
+__device__ __forceinline__ void issue_taps(__amdgpu_buffer_rsrc_t r, const RenderGeom& g, float px, float py,
+                                           bool live, TapSet& t) {
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
+    // clamp to [-2, W] / [-2, H] so the int conversion is defined and every tap index
+    // outside [0, W) / [0, H) stays outside; unsigned compares then test the range
+    const unsigned ux = (unsigned)(int)__builtin_fminf(__builtin_fmaxf(fx0, -2.0f), (float)g.W);
+    const unsigned uy = (unsigned)(int)__builtin_fminf(__builtin_fmaxf(fy0, -2.0f), (float)g.H);
+    const unsigned uw = (unsigned)g.W, uh = (unsigned)g.H;
+    const int off = ((int)uy * g.W + (int)ux) * 16;
+    const int row = g.W * 16;
+    t.a = llvm_raw_buffer_load_v4f32(r, (live && ux < uw && uy < uh) ? off : kOOB, 0, 0);
+    t.b = llvm_raw_buffer_load_v4f32(r, (live && ux + 1 < uw && uy < uh) ? off + 16 : kOOB, 0, 0);
+    t.c = llvm_raw_buffer_load_v4f32(r, (live && ux < uw && uy + 1 < uh) ? off + row : kOOB, 0, 0);
+    t.d = llvm_raw_buffer_load_v4f32(r, (live && ux + 1 < uw && uy + 1 < uh) ? off + row + 16 : kOOB, 0, 0);
 }
 
-__device__ __forceinline__ float4 sample_packed(const float4* __restrict__ plane, const RenderGeom& g,
-                                                float px, float py) {
-    const Bilinear b = bilinear_setup(px, py, g.W, g.H);
-    const float4 a = ld_tap(plane, g.W, b.ix, b.iy, b.x0 & b.y0);
-    const float4 c = ld_tap(plane, g.W, b.ix + 1, b.iy, b.x1 & b.y0);
-    const float4 d = ld_tap(plane, g.W, b.ix, b.iy + 1, b.x0 & b.y1);
-    const float4 e = ld_tap(plane, g.W, b.ix + 1, b.iy + 1, b.x1 & b.y1);
-    float4 r;
-    r.x = blend4(b, a.x, c.x, d.x, e.x);
-    r.y = blend4(b, a.y, c.y, d.y, e.y);
-    r.z = blend4(b, a.z, c.z, d.z, e.z);
-    r.w = blend4(b, a.w, c.w, d.w, e.w);
-    return r;
+__device__ __forceinline__ f32x4 blend_taps(const TapSet& t) {
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float acc = t.a[k] * t.nw;
+        acc = __builtin_fmaf(t.b[k], t.ne, acc);
+        acc = __builtin_fmaf(t.c[k], t.sw, acc);
+        acc = __builtin_fmaf(t.d[k], t.se, acc);
+        o[k] = acc;
+    }
+    return o;
 }
 
-// CT = false: final colour [V,H,W,3] (plane p_begin is the back plane; its alpha is
-//             ignored, utils.py:152-153).
+// Bijective XCD-aware block order: the dispatcher deals blocks round-robin over the
+// 8 XCDs (MI355X_MICROARCH.md §Workgroup dispatch), so hardware block b is given the
+// logical id  start(b % 8) + b / 8, i.e. each XCD walks one contiguous range of
+// logical ids.  Logical ids enumerate (tile, view) with the VIEW fastest, so the
+// views of one output tile -- whose source footprints overlap almost entirely along a
+// camera path -- run together on one XCD and share its L2.  Placement only affects
+// speed, never correctness.
+__device__ __forceinline__ int xcd_logical_block(int b, int nblocks) {
+    const int q = nblocks >> 3, r = nblocks & 7;
+    const int xcd = b & 7, k = b >> 3;
+    return xcd * q + (xcd < r ? xcd : r) + k;
+}
+
+// CT = false: final colour [V,H,W,3]; plane p_begin is the back plane, whose alpha is
+//             ignored (utils.py:152-153).
 // CT = true : partial (C, T) for planes [p_begin, p_end) as [V,H,W,4]:
 //             C = over-composite of the range onto black, T = prod(1 - a);
-//             when `back` is set the range holds plane 0, whose rgb replaces the
+//             with `back` set the range holds plane 0, whose rgb replaces the
 //             background (C = rgb0, T = 0).  Ranges combine front-to-back with
 //             (Cf, Tf) o (Cb, Tb) = (Cf + Tf*Cb, Tf*Tb)  (SURVEY.md §8e).
-template <bool CT>
+// One work-item = one output pixel of one view.  Plane p+1's four tap loads are
+// issued before plane p is blended, so every wave keeps 8 x 16 B in flight.
+template <bool CT, bool FAST>
 __global__ __launch_bounds__(256) void render_packed_kernel(const float4* __restrict__ planes,
-                                                            int64_t plane_stride, RenderGeom g,
+                                                            int64_t plane_stride, RenderGeom g, int V,
                                                             int p_begin, int p_end, int back,
                                                             const float* __restrict__ homs,
                                                             float* __restrict__ out) {
-    const int v = blockIdx.z;
-    const int x = blockIdx.x * kTileX + (threadIdx.x & (kWave - 1));
-    const int y = blockIdx.y * kTileY + (threadIdx.x >> 6);
+    const int tiles_x = (g.W + kTileX - 1) / kTileX;
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int v = lb % V;
+    const int tile = lb / V;
+    const int x = (tile % tiles_x) * kTileX + (threadIdx.x & (kWave - 1));
+    const int y = (tile / tiles_x) * kTileY + (threadIdx.x >> 6);
     if (x >= g.W || y >= g.H) return;
     const float fx = (float)x, fy = (float)y;
     const float* hv = homs + (int64_t)v * g.P * 9;
 
-    float r = 0.f, gg = 0.f, bb = 0.f, t = 1.f;
-    int p = p_begin;
-    if (!CT || back) {
+    // The reference's plane 0 replaces the background: with alpha forced to 1 and the
+    // colour started at -0.0, `out = rgb*1 + (-0)*(1-1)` returns rgb bit for bit (x + -0
+    // == x for every x, signed zeros included), so every plane runs the same code.
+    float cr = -0.0f, cg = -0.0f, cb = -0.0f, t = 1.0f;
+    const bool replace_first = !CT || back;
+    const int last = p_end - 1;
+    // plane p's taps; past the range the loads are issued with OOB offsets (no memory
+    // traffic, result unused) so every iteration issues unconditionally and the
+    // compiler can count vmcnt exactly
+    auto issue = [&](int p, TapSet& ts) {
+        const int q = p < last ? p : last;
         float px, py;
-        hom_sample_pos(hv + (int64_t)p * 9, fx, fy, g.hm1, g.wm1, g.half_w, g.half_h, px, py);
-        const float4 s = sample_packed(planes + (int64_t)p * plane_stride, g, px, py);
-        r = s.x; gg = s.y; bb = s.z; t = 0.f;
-        ++p;
-    }
-    for (; p < p_end; ++p) {
-        float px, py;
-        hom_sample_pos(hv + (int64_t)p * 9, fx, fy, g.hm1, g.wm1, g.half_w, g.half_h, px, py);
-        const float4 s = sample_packed(planes + (int64_t)p * plane_stride, g, px, py);
-        const float om = 1.0f - s.w;
-        r = over(s.x, s.w, om, r);
-        gg = over(s.y, s.w, om, gg);
-        bb = over(s.z, s.w, om, bb);
+        render_pos<FAST>(hv + (int64_t)q * 9, fx, fy, g, px, py);
+        issue_taps(make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes), g, px, py, p <= last, ts);
+    };
+    auto consume = [&](const TapSet& ts, bool first) {
+        const f32x4 s = blend_taps(ts);
+        const float a = first ? 1.0f : s[3];
+        const float om = 1.0f - a;
+        cr = over(s[0], a, om, cr);
+        cg = over(s[1], a, om, cg);
+        cb = over(s[2], a, om, cb);
         if (CT) t = t * om;
+    };
+    // ping-pong between two tap sets (no register rotation): the next plane's loads
+    // are in flight while the current one is blended.  sched_barrier keeps each issue
+    // block ahead of the previous plane's blend.
+    // Loop invariant: at the top of every iteration exactly A's four loads are in
+    // flight (no mid-loop exits), so the compiler's vmcnt bookkeeping stays exact.
+    TapSet A, B;
+    issue(p_begin, A);
+    int p = p_begin;
+    for (; p + 1 < p_end; p += 2) {  // A holds plane p, B will hold p + 1
+        issue(p + 1, B);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(A, replace_first && p == p_begin);
+        issue(p + 2, A);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(B, false);
     }
+    if (p < p_end) consume(A, replace_first && p == p_begin);
     const int64_t o = ((int64_t)v * g.H + y) * g.W + x;
     if (CT) {
-        reinterpret_cast<float4*>(out)[o] = make_float4(r, gg, bb, t);
+        reinterpret_cast<float4*>(out)[o] = make_float4(cr, cg, cb, t);
     } else {
-        out[o * 3 + 0] = r;
-        out[o * 3 + 1] = gg;
-        out[o * 3 + 2] = bb;
+        out[o * 3 + 0] = cr;
+        out[o * 3 + 1] = cg;
+        out[o * 3 + 2] = cb;
     }
 }
 
@@ -118,11 +208,28 @@ struct NativeStrides {
     int64_t b, y, x, p, c;
 };
 
-__device__ __forceinline__ float ld_nat(const float* __restrict__ base, const NativeStrides& s, int ix, int iy,
-                                        int c, bool ok) {
-    return ok ? base[(int64_t)iy * s.y + (int64_t)ix * s.x + (int64_t)c * s.c] : 0.0f;
+// One RGBA texel of the native layout.  The address is always clamped into the image
+// (so it is valid memory) and the value is zeroed when the tap is outside it --
+// grid_sample's zeros padding.  VEC: channels contiguous and 16-B aligned texels.
+template <bool VEC>
+__device__ __forceinline__ f32x4 ld_texel(const float* __restrict__ plane, const NativeStrides& s, int W, int H,
+                                          int ix, int iy, bool ok) {
+    const int cx = ix < 0 ? 0 : (ix >= W ? W - 1 : ix);
+    const int cy = iy < 0 ? 0 : (iy >= H ? H - 1 : iy);
+    const float* t = plane + (int64_t)cy * s.y + (int64_t)cx * s.x;
+    f32x4 v;
+    if (VEC) {
+        v = *reinterpret_cast<const f32x4*>(t);
+    } else {
+        v[0] = t[0]; v[1] = t[s.c]; v[2] = t[2 * s.c]; v[3] = t[3 * s.c];
+    }
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    return ok ? v : z;
 }
 
+// The reference's own [B,H,W,P,4] tensor, read in place (no pack).  Same per-plane
+// arithmetic as the packed kernel; texel gathers stride over the P*16-B pixel rows.
+template <bool VEC, bool FAST>
 __global__ __launch_bounds__(256) void render_native_kernel(const float* __restrict__ mpi, NativeStrides s,
                                                             RenderGeom g, const float* __restrict__ homs,
                                                             float* __restrict__ out) {
@@ -133,31 +240,29 @@ __global__ __launch_bounds__(256) void render_native_kernel(const float* __restr
     const float fx = (float)x, fy = (float)y;
     const float* hv = homs + (int64_t)v * g.P * 9;
     const float* img = mpi + (int64_t)v * s.b;
-    float acc[3] = {0.f, 0.f, 0.f};
+    float cr = -0.0f, cg = -0.0f, cb = -0.0f;  // see render_packed_kernel: plane 0 replaces
     for (int p = 0; p < g.P; ++p) {
         float px, py;
-        hom_sample_pos(hv + (int64_t)p * 9, fx, fy, g.hm1, g.wm1, g.half_w, g.half_h, px, py);
+        render_pos<FAST>(hv + (int64_t)p * 9, fx, fy, g, px, py);
         const Bilinear b = bilinear_setup(px, py, g.W, g.H);
         const float* pl = img + (int64_t)p * s.p;
-        const bool m00 = b.x0 & b.y0, m10 = b.x1 & b.y0, m01 = b.x0 & b.y1, m11 = b.x1 & b.y1;
-        float ch[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            ch[c] = blend4(b, ld_nat(pl, s, b.ix, b.iy, c, m00), ld_nat(pl, s, b.ix + 1, b.iy, c, m10),
-                           ld_nat(pl, s, b.ix, b.iy + 1, c, m01), ld_nat(pl, s, b.ix + 1, b.iy + 1, c, m11));
-        }
-        if (p == 0) {
-            acc[0] = ch[0]; acc[1] = ch[1]; acc[2] = ch[2];
-        } else {
-            const float om = 1.0f - ch[3];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) acc[c] = over(ch[c], ch[3], om, acc[c]);
-        }
+        TapSet t;
+        t.nw = b.nw; t.ne = b.ne; t.sw = b.sw; t.se = b.se;
+        t.a = ld_texel<VEC>(pl, s, g.W, g.H, b.ix, b.iy, b.x0 && b.y0);
+        t.b = ld_texel<VEC>(pl, s, g.W, g.H, b.ix + 1, b.iy, b.x1 && b.y0);
+        t.c = ld_texel<VEC>(pl, s, g.W, g.H, b.ix, b.iy + 1, b.x0 && b.y1);
+        t.d = ld_texel<VEC>(pl, s, g.W, g.H, b.ix + 1, b.iy + 1, b.x1 && b.y1);
+        const f32x4 c = blend_taps(t);
+        const float a = p == 0 ? 1.0f : c[3];
+        const float om = 1.0f - a;
+        cr = over(c[0], a, om, cr);
+        cg = over(c[1], a, om, cg);
+        cb = over(c[2], a, om, cb);
     }
     const int64_t o = (((int64_t)v * g.H + y) * g.W + x) * 3;
-    out[o + 0] = acc[0];
-    out[o + 1] = acc[1];
-    out[o + 2] = acc[2];
+    out[o + 0] = cr;
+    out[o + 1] = cg;
+    out[o + 2] = cb;
 }
 
 // ---------------------------------------------------------------------------

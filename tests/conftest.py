@@ -57,6 +57,20 @@ def bits_equal(a, b) -> bool:
     return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+def assert_bits(got, want, what=""):
+    """Bit-exact comparison with a short failure message (no giant array reprs)."""
+    got = np.ascontiguousarray(got.detach().cpu().numpy() if isinstance(got, torch.Tensor) else got, np.float32)
+    want = np.ascontiguousarray(want, np.float32)
+    if got.shape != want.shape:
+        raise AssertionError(f"{what}: shape {got.shape} != {want.shape}")
+    diff = got.view(np.uint32) != want.view(np.uint32)
+    if diff.any():
+        d = np.abs(got.astype(np.float64) - want)
+        i = np.unravel_index(int(np.argmax(np.where(diff, d, -1))), got.shape)
+        raise AssertionError(f"{what}: {int(diff.sum())}/{diff.size} values differ, max |diff| "
+                             f"{np.nanmax(np.where(diff, d, 0)):.3g} at {i} (got {got[i]}, want {want[i]})")
+
+
 def render_case_inputs(meta_small, name):
     """Regenerate the seeded MPI of a golden render case (sha-checked)."""
     from mpi_vision_amd import configs

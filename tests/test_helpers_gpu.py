@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import bits_equal, render_case_inputs
+from conftest import assert_bits, render_case_inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -17,17 +17,17 @@ def _t(small, key, dev):
 
 def test_bilinear_wrapper(small, dev):
     out = mv.bilinear_wrapper_torch(_t(small, "bil_imgs", dev), _t(small, "bil_coords", dev))
-    assert bits_equal(out.cpu().numpy(), small["bil_out"])
+    assert_bits(out.cpu().numpy(), small["bil_out"])
 
 
 def test_resampler_wrapper(small, dev):
     out = mv.resampler_wrapper_torch(_t(small, "res_imgs", dev), _t(small, "res_coords", dev))
-    assert bits_equal(out.cpu().numpy(), small["res_out"])
+    assert_bits(out.cpu().numpy(), small["res_out"])
 
 
 def test_over_composite_list(small, dev):
     layers = [t for t in _t(small, "over_in", dev)]
-    assert bits_equal(mv.over_composite(layers).cpu().numpy(), small["over_out"])
+    assert_bits(mv.over_composite(layers).cpu().numpy(), small["over_out"])
 
 
 def test_over_composite_strided_layers(small, dev):
@@ -35,30 +35,30 @@ def test_over_composite_strided_layers(small, dev):
     stack = _t(small, "over_in", dev)                     # [P,B,H,W,4]
     perm = stack.permute(1, 2, 3, 0, 4).contiguous()      # [B,H,W,P,4]
     layers = [perm[:, :, :, i] for i in range(stack.shape[0])]
-    assert bits_equal(mv.over_composite(layers).cpu().numpy(), small["over_out"])
+    assert_bits(mv.over_composite(layers).cpu().numpy(), small["over_out"])
     mixed = [layers[0].contiguous()] + layers[1:]
-    assert bits_equal(mv.over_composite(mixed).cpu().numpy(), small["over_out"])
+    assert_bits(mv.over_composite(mixed).cpu().numpy(), small["over_out"])
 
 
 def test_transform_points(small, dev):
     out = mv.transform_points_torch(_t(small, "tp_pts", dev), _t(small, "tp_H", dev))
-    assert bits_equal(out.cpu().numpy(), small["tp_out"])
+    assert_bits(out.cpu().numpy(), small["tp_out"])
 
 
 def test_normalize_homogeneous_mutates_w_like_reference(small, dev):
     pts = _t(small, "nh_in", dev)
     out = mv.normalize_homogeneous_torch(pts)
-    assert bits_equal(out.cpu().numpy(), small["nh_out"])
-    assert bits_equal(pts.cpu().numpy(), small["nh_in_after"])
+    assert_bits(out.cpu().numpy(), small["nh_out"])
+    assert_bits(pts.cpu().numpy(), small["nh_in_after"])
 
 
 def test_pixel2cam_cam2pixel(small, dev):
     depth = _t(small, "p2c_depth", dev)
     pix = mv.meshgrid_abs_torch(2, 6, 7)
     cam = mv.pixel2cam_torch(depth, pix, _t(small, "p2c_K", dev))
-    assert bits_equal(cam.cpu().numpy(), small["p2c_out"])
+    assert_bits(cam.cpu().numpy(), small["p2c_out"])
     c2p = mv.cam2pixel_torch(cam, _t(small, "c2p_proj", dev))
-    assert bits_equal(c2p.cpu().numpy(), small["c2p_out"])
+    assert_bits(c2p.cpu().numpy(), small["c2p_out"])
 
 
 def test_layer_pipeline_helpers_match_render(small, meta, dev):
@@ -71,7 +71,7 @@ def test_layer_pipeline_helpers_match_render(small, meta, dev):
     proj = mv.projective_forward_homography_torch(layers, K, pose, depths)   # [P,B,4,H,W]
     proj = proj.permute(0, 1, 3, 4, 2)
     out = mv.over_composite([proj[i] for i in range(proj.shape[0])])
-    assert bits_equal(out.cpu().numpy(), small["render_a_out"])
+    assert_bits(out.cpu().numpy(), small["render_a_out"])
 
 
 def test_meshgrid(dev):

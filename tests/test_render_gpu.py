@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import RENDER_CASES, bits_equal, load_test_mpi, render_case_inputs, sha256
+from conftest import RENDER_CASES, assert_bits, load_test_mpi, render_case_inputs, sha256
 
 pytestmark = pytest.mark.gpu
 
@@ -27,7 +27,7 @@ def test_render_matches_reference(name, small, meta, dev):
     out = mv.mpi_render_view_torch(mpi.to(dev) if mpi.stride(0) else mpi[:1].to(dev).expand(*mpi.shape),
                                    _t(small, f"{name}_pose", dev), _t(small, f"{name}_depths", dev),
                                    _t(small, f"{name}_K", dev))
-    assert bits_equal(out.cpu().numpy(), small[f"{name}_out"])
+    assert_bits(out.cpu().numpy(), small[f"{name}_out"])
 
 
 @pytest.mark.parametrize("name", RENDER_CASES)
@@ -35,18 +35,18 @@ def test_native_and_packed_kernels_agree_with_oracle(name, small, meta, dev):
     """Both texel layouts, driven with the reference's own H bits."""
     mpi = render_case_inputs(meta["small"], name)
     B, H, W, P, _ = mpi.shape
-    homs = torch.tensor(small[f"{name}_H"]).permute(1, 0, 2, 3).reshape(B, P, 9)
+    homs = torch.tensor(small[f"{name}_H"]).permute(1, 0, 2, 3).reshape(B, P, 9).contiguous()
     want = oracle.render(mpi.numpy(), homs.numpy())
     dmpi = mpi.contiguous().to(dev)
     nat = torch.empty((B, H, W, 3), device=dev)
     _lib._call("mpiv_render", _lib._p(dmpi), _lib._strides(dmpi), B, H, W, P, _lib._p(homs.to(dev)),
                _lib._p(nat), _lib._stream(dev))
-    assert bits_equal(nat.cpu().numpy(), want)
+    assert_bits(nat.cpu().numpy(), want)
     for b in range(B):
         packed = _lib.pack_planes(dmpi[b])
         assert torch.equal(packed.cpu(), mpi[b].permute(2, 0, 1, 3).contiguous())
         pk = _lib.render_packed(packed, homs[b:b + 1])
-        assert bits_equal(pk.cpu().numpy(), want[b:b + 1])
+        assert_bits(pk.cpu().numpy(), want[b:b + 1])
 
 
 def test_render_strided_views(small, meta, dev):
@@ -58,7 +58,7 @@ def test_render_strided_views(small, meta, dev):
     view = dbig[..., 1:5]
     out = mv.mpi_render_view_torch(view, _t(small, "render_a_pose", dev), _t(small, "render_a_depths", dev),
                                    _t(small, "render_a_K", dev))
-    assert bits_equal(out.cpu().numpy(), small["render_a_out"])
+    assert_bits(out.cpu().numpy(), small["render_a_out"])
 
 
 def test_render_c1_test_mpi(large, meta, dev):
@@ -69,13 +69,13 @@ def test_render_c1_test_mpi(large, meta, dev):
     out = mv.mpi_render_view_torch(dmpi, _t(large, "c1_pose", dev), _t(large, "c1_depths", dev),
                                    _t(large, "c1_K", dev))
     got = out.cpu().numpy()
-    assert bits_equal(got, large["c1_out"])
+    assert_bits(got, large["c1_out"])
     assert sha256(got) == meta["large"]["c1"]["out_sha"]
     # also the native (non-broadcast) kernel on each pose
     for b in range(2):
         o1 = mv.mpi_render_view_torch(mpi.to(dev), _t(large, "c1_pose", dev)[b:b + 1],
                                       _t(large, "c1_depths", dev), _t(large, "c1_K", dev)[b:b + 1])
-        assert bits_equal(o1.cpu().numpy(), large["c1_out"][b:b + 1])
+        assert_bits(o1.cpu().numpy(), large["c1_out"][b:b + 1])
 
 
 def test_render_c2_broadcast_batch(large, meta, dev):
@@ -107,7 +107,7 @@ def test_plane_range_partials_combine(small, meta, dev):
     """(C,T) partials over plane ranges + ordered combine == sequential render (1e-5)."""
     mpi = render_case_inputs(meta["small"], "render_a")[0:1]
     P = mpi.shape[3]
-    homs = torch.tensor(small["render_a_H"]).permute(1, 0, 2, 3)[0:1].reshape(1, P, 9)
+    homs = torch.tensor(small["render_a_H"]).permute(1, 0, 2, 3)[0:1].reshape(1, P, 9).contiguous()
     packed = _lib.pack_planes(mpi[0].to(dev))
     want = small["render_a_out"][0:1]
     for cuts in ([0, 8], [0, 3, 8], [0, 1, 2, 5, 8], list(range(9))):
@@ -116,7 +116,7 @@ def test_plane_range_partials_combine(small, meta, dev):
         got = _lib.combine_ct(parts).cpu().numpy()
         np.testing.assert_allclose(got, want, rtol=0, atol=1e-5)
         if len(cuts) == 2:
-            assert bits_equal(got, want)  # a single range is the sequential order
+            assert_bits(got, want)  # a single range is the sequential order
 
 
 def test_render_deterministic(small, meta, dev):

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import bits_equal, psv_case_input, sha256
+from conftest import assert_bits, psv_case_input, sha256
 
 pytestmark = pytest.mark.gpu
 
@@ -20,7 +20,7 @@ def test_plane_sweep_batched(small, meta, dev):
     img = psv_case_input(meta["small"], "psv_a")
     out = mv.plane_sweep_torch(img.to(dev), list(small["psv_a_depths"]), _t(small, "psv_a_pose", dev),
                                _t(small, "psv_a_K", dev))
-    assert bits_equal(out.cpu().numpy(), small["psv_a_out"])
+    assert_bits(out.cpu().numpy(), small["psv_a_out"])
 
 
 def test_plane_sweep_one(small, meta, dev):
@@ -28,7 +28,7 @@ def test_plane_sweep_one(small, meta, dev):
     out = mv.plane_sweep_torch_one(img.to(dev), list(small["psv_one_depths"]), _t(small, "psv_one_pose", dev),
                                    _t(small, "psv_one_K", dev))
     assert out.shape == small["psv_one_out"].shape
-    assert bits_equal(out.cpu().numpy(), small["psv_one_out"])
+    assert_bits(out.cpu().numpy(), small["psv_one_out"])
 
 
 def test_plane_sweep_one2_separate_intrinsics(small, meta, dev):
@@ -36,7 +36,7 @@ def test_plane_sweep_one2_separate_intrinsics(small, meta, dev):
     m = meta["small"]["psv_two"]
     out = mv.plane_sweep_torch_one2(img.to(dev), list(small["psv_two_depths"]), _t(small, "psv_two_pose", dev),
                                     _t(small, "psv_two_Ks", dev), _t(small, "psv_two_Kt", dev), m["tgt_h"], m["tgt_w"])
-    assert bits_equal(out.cpu().numpy(), small["psv_two_out"])
+    assert_bits(out.cpu().numpy(), small["psv_two_out"])
 
 
 def test_plane_sweep_strided_input(small, meta, dev):
@@ -46,7 +46,7 @@ def test_plane_sweep_strided_input(small, meta, dev):
     view = wide.to(dev)[..., 1:4]
     out = mv.plane_sweep_torch(view, list(small["psv_a_depths"]), _t(small, "psv_a_pose", dev),
                                _t(small, "psv_a_K", dev))
-    assert bits_equal(out.cpu().numpy(), small["psv_a_out"])
+    assert_bits(out.cpu().numpy(), small["psv_a_out"])
 
 
 def test_inverse_warp_single_depth(small, meta, dev):
@@ -55,7 +55,7 @@ def test_inverse_warp_single_depth(small, meta, dev):
     d = float(small["psv_a_depths"][2])
     depth = torch.full((2, 48, 64), d, device=dev)
     out = mv.projective_inverse_warp_torch(img, depth, _t(small, "psv_a_pose", dev), _t(small, "psv_a_K", dev))
-    assert bits_equal(out.cpu().numpy(), small["psv_a_out"][..., 6:9])
+    assert_bits(out.cpu().numpy(), small["psv_a_out"][..., 6:9])
 
 
 def test_plane_sweep_c3(large, meta, dev):
