@@ -149,11 +149,11 @@ def main():
 
     def launch(s, h_dev):
         if args.kernel == "packed":
-            _lib._call("mpiv_render_packed", _lib._p(packed), H, W, P, _lib._p(h_dev), V, _lib._p(out),
+            _lib._call("mpiv_render_packed", packed, H, W, P, h_dev, V, out,
                        _lib._stream(dev))
         else:
-            _lib._call("mpiv_render", _lib._p(mpi5), _lib._strides(mpi5), V, H, W, P, _lib._p(h_dev),
-                       _lib._p(out), _lib._stream(dev))
+            _lib._call("mpiv_render", mpi5, _lib._strides(mpi5), V, H, W, P, h_dev,
+                       out, _lib._stream(dev))
 
     copied = [None, None]  # event recorded after the last H2D copy out of each pinned slot
 
@@ -219,10 +219,10 @@ def main():
             # the GPU frames of the first views of step 0, to cross-check the CPU sample bit-exactly
             hs = host_homs(0)
             _lib._call("mpiv_render_packed" if args.kernel == "packed" else "mpiv_render",
-                       *([_lib._p(packed), H, W, P, _lib._p(hs[:1].to(dev)), 1, _lib._p(out), _lib._stream(dev)]
+                       *([packed, H, W, P, hs[:1].to(dev), 1, out, _lib._stream(dev)]
                          if args.kernel == "packed" else
-                         [_lib._p(mpi5[:1]), _lib._strides(mpi5[:1]), 1, H, W, P, _lib._p(hs[:1].to(dev)),
-                          _lib._p(out), _lib._stream(dev)]))
+                         [mpi5[:1], _lib._strides(mpi5[:1]), 1, H, W, P, hs[:1].to(dev),
+                          out, _lib._stream(dev)]))
             torch.cuda.synchronize()
             frames = [out[:1].cpu().numpy()]
             res["cpu_baseline"] = cpu_baseline(view, hs, args.cpu_seconds, frames)

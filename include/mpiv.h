@@ -132,6 +132,14 @@ int mpiv_cam2pixel(const float *cam, const float *proj, int B, int64_t n, float 
 int mpiv_plane_coords(const float *pts, int M, int64_t n, const float *homs, int Ht, int Wt, float *coords,
                       void *stream);
 
+/* ---- diagnostics ------------------------------------------------------------ */
+
+/* Exhaustive self-check of the render's launch-constant division (x / (H-1),
+ * x / (W-1) via a precomputed reciprocal + two residual corrections) against IEEE
+ * division for all 2^32 fp32 inputs and the given integer divisor; adds the number
+ * of relevant mismatches to *mismatches (device counter, caller-zeroed). */
+int mpiv_selftest_div_const(int divisor, unsigned long long *mismatches, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

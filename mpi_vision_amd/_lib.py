@@ -35,6 +35,7 @@ _SIGS = {
     "mpiv_pixel2cam": [_vp, _vp, _vp, _int, _i64, _int, _vp, _vp],
     "mpiv_cam2pixel": [_vp, _vp, _int, _i64, _vp, _vp],
     "mpiv_plane_coords": [_vp, _int, _i64, _vp, _int, _int, _vp, _vp],
+    "mpiv_selftest_div_const": [_int, _vp, _vp],
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error")
 ABI_VERSION = 1
@@ -63,8 +64,12 @@ def load():
 
 
 def _call(name, *args):
+    """Call an entry point.  Tensor arguments are passed as their device pointers and
+    stay referenced (alive) for the duration of the call, so temporaries built inline
+    cannot be freed and their memory reused by a later argument's allocation."""
     L = load()
-    rc = getattr(L, name)(*args)
+    cargs = [ctypes.c_void_p(a.data_ptr()) if isinstance(a, torch.Tensor) else a for a in args]
+    rc = getattr(L, name)(*cargs)
     if rc != 0:
         raise RuntimeError(f"{name} failed ({rc}): {L.mpiv_last_error().decode()}")
 
@@ -116,7 +121,7 @@ def pack_planes(view: torch.Tensor) -> torch.Tensor:
     if C != 4:
         raise RuntimeError(f"MPI texels must have 4 channels (RGBA), got {C}")
     packed = torch.empty((P, H, W, 4), device=dev, dtype=torch.float32)
-    _call("mpiv_pack_planes", _p(view), _strides(view), H, W, P, _p(packed), _stream(dev))
+    _call("mpiv_pack_planes", view, _strides(view), H, W, P, packed, _stream(dev))
     return packed
 
 
@@ -128,7 +133,7 @@ def render_packed(packed: torch.Tensor, homs: torch.Tensor, out: torch.Tensor | 
     h = _up(homs.reshape(V, P, 9), dev)
     if out is None:
         out = torch.empty((V, H, W, 3), device=dev, dtype=torch.float32)
-    _call("mpiv_render_packed", _p(packed), H, W, P, _p(h), V, _p(out), _stream(dev))
+    _call("mpiv_render_packed", packed, H, W, P, h, V, out, _stream(dev))
     return out
 
 
@@ -142,7 +147,7 @@ def render_packed_ct(packed: torch.Tensor, homs: torch.Tensor, back: bool, p_beg
     h = _up(homs.reshape(V, P, 9), dev)
     if out is None:
         out = torch.empty((V, H, W, 4), device=dev, dtype=torch.float32)
-    _call("mpiv_render_packed_ct", _p(packed), H, W, P, p_begin, p_end, int(back), _p(h), V, _p(out),
+    _call("mpiv_render_packed_ct", packed, H, W, P, p_begin, p_end, int(back), h, V, out,
           _stream(dev))
     return out
 
@@ -154,7 +159,7 @@ def combine_ct(parts: torch.Tensor) -> torch.Tensor:
     G = parts.shape[0]
     n = parts[0].numel() // 4
     out = torch.empty(tuple(parts.shape[1:-1]) + (3,), device=dev, dtype=torch.float32)
-    _call("mpiv_combine_ct", _p(parts), G, n, _p(out), _stream(dev))
+    _call("mpiv_combine_ct", parts, G, n, out, _stream(dev))
     return out
 
 
@@ -174,7 +179,7 @@ def render(rgba_layers: torch.Tensor, homs: torch.Tensor) -> torch.Tensor:
         return render_packed(pack_planes(rgba_layers[0]), homs)
     h = _up(homs, dev)
     out = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32)
-    _call("mpiv_render", _p(rgba_layers), _strides(rgba_layers), B, H, W, P, _p(h), _p(out), _stream(dev))
+    _call("mpiv_render", rgba_layers, _strides(rgba_layers), B, H, W, P, h, out, _stream(dev))
     return out
 
 
@@ -189,8 +194,8 @@ def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.T
     d = torch.tensor([float(x) for x in depth_planes], dtype=torch.float32)
     D = d.shape[0]
     out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
-    _call("mpiv_plane_sweep", _p(img), _strides(img), B, Hs, Ws, C, _p(_up(ki, dev)), _p(_up(proj, dev)),
-          _p(_up(d, dev)), D, tgt_h, tgt_w, _p(out), _stream(dev))
+    _call("mpiv_plane_sweep", img, _strides(img), B, Hs, Ws, C, _up(ki, dev), _up(proj, dev),
+          _up(d, dev), D, tgt_h, tgt_w, out, _stream(dev))
     return out
 
 
@@ -200,8 +205,8 @@ def inverse_warp_depthmap(img, depth, ki, proj, tgt_h, tgt_w):
     if tuple(depth.shape) != (B, tgt_h, tgt_w):
         raise RuntimeError(f"depth must be [{B},{tgt_h},{tgt_w}], got {tuple(depth.shape)}")
     out = torch.empty((B, tgt_h, tgt_w, C), device=dev, dtype=torch.float32)
-    _call("mpiv_inverse_warp", _p(img), _strides(img), B, Hs, Ws, C, _p(_up(ki, dev)), _p(_up(proj, dev)),
-          _p(depth), _strides(depth), tgt_h, tgt_w, _p(out), _stream(dev))
+    _call("mpiv_inverse_warp", img, _strides(img), B, Hs, Ws, C, _up(ki, dev), _up(proj, dev),
+          depth, _strides(depth), tgt_h, tgt_w, out, _stream(dev))
     return out
 
 
@@ -236,8 +241,8 @@ def bilinear_sample(imgs: torch.Tensor, coords: torch.Tensor, channels_last_out:
     else:
         out = torch.empty((N, C, Ho, Wo), device=dev, dtype=torch.float32)
         ost = _strides(out)
-    _call("mpiv_grid_sample", _p(im4), _strides(im4, (0, 3, 1, 2)), N, C, Hi, Wi, _p(co4), _strides(co4), Ho, Wo,
-          _p(out), ost, _stream(dev))
+    _call("mpiv_grid_sample", im4, _strides(im4, (0, 3, 1, 2)), N, C, Hi, Wi, co4, _strides(co4), Ho, Wo,
+          out, ost, _stream(dev))
     if channels_last_out:
         return out
     return out.reshape(lead + [C, Ho, Wo])
@@ -275,7 +280,7 @@ def over_composite(rgbas) -> torch.Tensor:
     n = layers[0].numel() // 4
     ptrs = torch.tensor([t.data_ptr() for t in layers], dtype=torch.int64).to(dev)
     out = torch.empty(tuple(shape[:-1]) + (3,), device=dev, dtype=torch.float32)
-    _call("mpiv_over_composite", _p(ptrs), len(layers), n, ps, cs, _p(out), _stream(dev))
+    _call("mpiv_over_composite", ptrs, len(layers), n, ps, cs, out, _stream(dev))
     # temporaries (pointer table, contiguous copies) may be freed now: the caching
     # allocator only hands their memory to later work on this same stream
     return out
@@ -294,7 +299,7 @@ def transform_points(points: torch.Tensor, homography: torch.Tensor) -> torch.Te
     pts = points.reshape(hshape[:-2] + [-1, 3]).contiguous()
     n = pts.shape[-2]
     out = torch.empty_like(pts)
-    _call("mpiv_transform_points", _p(pts), M, n, _p(homography.reshape(M, 9).contiguous()), _p(out),
+    _call("mpiv_transform_points", pts, M, n, homography.reshape(M, 9).contiguous(), out,
           _stream(dev))
     return out.reshape(points.shape)
 
@@ -306,7 +311,7 @@ def normalize_homogeneous(points: torch.Tensor) -> torch.Tensor:
         raise RuntimeError("normalize_homogeneous_torch needs at least 2 coordinates")
     work = points if points.is_contiguous() else points.contiguous()
     out = torch.empty(tuple(points.shape[:-1]) + (k,), device=dev, dtype=torch.float32)
-    _call("mpiv_normalize_homogeneous", _p(work), work.numel() // (k + 1), k, _p(out), _stream(dev))
+    _call("mpiv_normalize_homogeneous", work, work.numel() // (k + 1), k, out, _stream(dev))
     if work is not points:  # keep the reference's in-place w update visible
         points.copy_(work)
     return out
@@ -320,8 +325,8 @@ def pixel2cam(depth, pixel_coords, intrinsics, is_homogeneous=True):
     ki = torch.inverse(_cpu32(intrinsics)).reshape(B, 9)
     rows = 4 if is_homogeneous else 3
     cam = torch.empty((B, rows, H, W), device=dev, dtype=torch.float32)
-    _call("mpiv_pixel2cam", _p(depth.contiguous()), _p(pixel_coords.reshape(B, 3, n).contiguous()),
-          _p(_up(ki, dev)), B, n, int(bool(is_homogeneous)), _p(cam), _stream(dev))
+    _call("mpiv_pixel2cam", depth.contiguous(), pixel_coords.reshape(B, 3, n).contiguous(),
+          _up(ki, dev), B, n, int(bool(is_homogeneous)), cam, _stream(dev))
     return cam
 
 
@@ -330,8 +335,8 @@ def cam2pixel(cam_coords, proj):
     B, _, H, W = cam_coords.shape
     n = H * W
     out = torch.empty((B, H, W, 2), device=dev, dtype=torch.float32)
-    _call("mpiv_cam2pixel", _p(cam_coords.reshape(B, 4, n).contiguous()), _p(proj.reshape(B, 16).contiguous()), B,
-          n, _p(out), _stream(dev))
+    _call("mpiv_cam2pixel", cam_coords.reshape(B, 4, n).contiguous(), proj.reshape(B, 16).contiguous(), B,
+          n, out, _stream(dev))
     return out
 
 
@@ -346,6 +351,6 @@ def warp_planes(imgs: torch.Tensor, pixel_coords_trg: torch.Tensor, hom: torch.T
     Ht, Wt = pixel_coords_trg.shape[-3], pixel_coords_trg.shape[-2]
     pts = pixel_coords_trg.reshape(M, Ht * Wt, 3).contiguous()
     coords = torch.empty((M, Ht, Wt, 2), device=dev, dtype=torch.float32)
-    _call("mpiv_plane_coords", _p(pts), M, Ht * Wt, _p(_up(hom.reshape(M, 9), dev)), Ht, Wt, _p(coords),
+    _call("mpiv_plane_coords", pts, M, Ht * Wt, _up(hom.reshape(M, 9), dev), Ht, Wt, coords,
           _stream(dev))
     return bilinear_sample(imgs, coords.reshape(list(pixel_coords_trg.shape[:-1]) + [2]), channels_last_out=False)

@@ -226,4 +226,11 @@ int mpiv_plane_coords(const float* pts, int M, int64_t n, const float* homs, int
     return launched("mpiv_plane_coords");
 }
 
+int mpiv_selftest_div_const(int divisor, unsigned long long* mismatches, void* stream) {
+    if (!mismatches || divisor < 1) return fail(MPIV_ERR_ARG, "mpiv_selftest_div_const: bad args");
+    const float c = (float)divisor;
+    div_const_selftest_kernel<<<4096, 256, 0, S(stream)>>>(c, 1.0f / c, mismatches);
+    return launched("mpiv_selftest_div_const");
+}
+
 }  // extern "C"

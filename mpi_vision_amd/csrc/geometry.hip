@@ -99,4 +99,22 @@ __global__ __launch_bounds__(256) void plane_coords_kernel(const float* __restri
     o[1] = div_rn(div_rn(v, w), wm1);
 }
 
+// Self-check of div_const (mpiv_common.hpp): every fp32 bit pattern x (a grid-strided
+// sweep of all 2^32) against the IEEE quotient x / c.  Counts mismatches among finite,
+// non-NaN x whose exact quotient matters for a sample position (|x / c| >= 2^-26).
+__global__ __launch_bounds__(256) void div_const_selftest_kernel(float c, float rc,
+                                                                 unsigned long long* __restrict__ bad) {
+    unsigned long long local = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
+        const float x = __builtin_bit_cast(float, (unsigned)i);
+        if (!__builtin_isfinite(x)) continue;
+        const float exact = x / c;
+        if (__builtin_fabsf(exact) < 1.4901161e-08f) continue;  // 2^-26
+        const float fast = div_const(x, c, rc);
+        local += __builtin_bit_cast(unsigned, fast) != __builtin_bit_cast(unsigned, exact);
+    }
+    if (local) atomicAdd(bad, local);
+}
+
 }  // namespace mpiv

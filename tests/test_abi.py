@@ -1,0 +1,63 @@
+"""CPU: the C-ABI library loads, exports every symbol include/mpiv.h declares, and
+rejects bad arguments with error codes + messages (validated before any HIP call,
+so this runs without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+from mpi_vision_amd import _lib  # noqa: E402
+
+HEADER = os.path.join(REPO, "include", "mpiv.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(mpiv_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert "mpiv_render" in syms and "mpiv_plane_sweep" in syms and len(syms) >= 15
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.load()
+    missing = [s for s in declared_symbols() if not hasattr(L, s)]
+    assert not missing, missing
+    assert set(declared_symbols()) <= set(_lib.EXPORTS)
+
+
+def test_abi_version():
+    assert _lib.load().mpiv_abi_version() == _lib.ABI_VERSION
+
+
+@pytest.mark.parametrize("call", [
+    ("mpiv_render", [None, None, 1, 4, 4, 2, None, None, None]),
+    ("mpiv_render_packed", [None, 4, 4, 2, None, 1, None, None]),
+    ("mpiv_plane_sweep", [None, None, 1, 4, 4, 3, None, None, None, 2, 4, 4, None, None]),
+    ("mpiv_grid_sample", [None, None, 1, 1, 4, 4, None, None, 2, 2, None, None, None]),
+    ("mpiv_over_composite", [None, 2, 4, 4, 1, None, None]),
+    ("mpiv_combine_ct", [None, 2, 4, None, None]),
+])
+def test_null_pointers_rejected(call):
+    name, args = call
+    L = _lib.load()
+    rc = getattr(L, name)(*args)
+    assert rc == -1
+    assert b"null pointer" in L.mpiv_last_error()
+
+
+def test_bad_shapes_rejected():
+    L = _lib.load()
+    st = (ctypes.c_int64 * 5)(1, 1, 1, 1, 1)
+    p = ctypes.c_void_p(16)
+    assert L.mpiv_render(p, st, 0, 4, 4, 2, p, p, None) == -1
+    assert b"bad shape" in L.mpiv_last_error()
+    assert L.mpiv_render_packed_ct(p, 4, 4, 8, 5, 3, 0, p, 1, p, None) == -1
+    assert b"plane range" in L.mpiv_last_error()
+    assert L.mpiv_render_packed(ctypes.c_void_p(8), 4, 4, 2, p, 1, p, None) == -1
+    assert b"alignment" in L.mpiv_last_error()

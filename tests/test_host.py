@@ -1,0 +1,107 @@
+"""CPU: host-side logic of the drop-in -- plane depths, homography / PSV matrix
+setup (bit-exact vs the reference's H), API error behaviour, no CPU fallback."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import RENDER_CASES, assert_bits
+
+import mpi_vision_amd as mv  # noqa: E402
+from mpi_vision_amd import _host, configs  # noqa: E402
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 10, 32, 64, 128, 256])
+def test_inv_depths_exact(n, small):
+    got = np.array(mv.inv_depths(1, 100, n), dtype=np.float64)
+    assert np.array_equal(got, small[f"inv_depths_{n}"])
+
+
+def test_inv_depths_other_range(small):
+    assert np.array_equal(np.array(mv.inv_depths(0.5, 20.0, 7)), small["inv_depths_0.5_20_7"])
+
+
+@pytest.mark.parametrize("name", RENDER_CASES)
+def test_render_homographies_bit_exact(name, small):
+    B = small[f"{name}_pose"].shape[0]
+    H = _host.render_homographies(torch.tensor(small[f"{name}_pose"]), torch.tensor(small[f"{name}_depths"]),
+                                  torch.tensor(small[f"{name}_K"]), B)
+    P = small[f"{name}_depths"].shape[0]
+    assert_bits(H.numpy(), small[f"{name}_H"].transpose(1, 0, 2, 3).reshape(B, P, 9), name)
+
+
+def test_inv_homography_helper_bit_exact(small):
+    K, pose, d = (torch.tensor(small[k]) for k in ("hom_K", "hom_pose", "hom_depths"))
+    P, B = d.shape[0], K.shape[0]
+    rep = lambda x: x.unsqueeze(0).repeat((P,) + (1,) * x.dim())  # noqa: E731
+    n_hat = torch.tensor([0.0, 0.0, 1.0]).reshape(1, 1, 1, 3).repeat(P, B, 1, 1)
+    a = -d.reshape(P, 1).repeat(1, B).reshape(P, B, 1, 1)
+    H = mv.inv_homography_torch(rep(K), rep(K), rep(pose[:, :3, :3]), rep(pose[:, :3, 3:]), n_hat, a)
+    assert_bits(H.numpy(), small["hom_H"])
+    # expanded (stride-0) operands are materialised like the reference's repeats
+    exp = lambda x: x.unsqueeze(0).expand((P,) + tuple(x.shape))  # noqa: E731
+    H2 = mv.inv_homography_torch(exp(K), exp(K), exp(pose[:, :3, :3]), exp(pose[:, :3, 3:]), n_hat, a)
+    assert_bits(H2.numpy(), small["hom_H"])
+
+
+def test_c4_homographies_match_reference(large):
+    for pose_index in (0, 500):
+        H = _host.render_homographies(torch.tensor(large[f"c4_{pose_index}_pose"]), torch.tensor(large["c4_depths"]),
+                                      torch.tensor(large["c4_K"]), 1)
+        assert_bits(H.numpy(), large[f"c4_{pose_index}_H"].transpose(1, 0, 2, 3).reshape(1, 128, 9))
+
+
+def test_psv_matrices():
+    K = configs.f32([configs.intrinsics_matrix(100.0, 110.0, 30.0, 20.0)])
+    pose = configs.f32([configs.pose_from(configs.rot_y(2.0), (0.1, 0.0, 0.2))])
+    ki, proj = _host.psv_matrices(K, K, pose)
+    assert torch.equal(ki.reshape(1, 3, 3), torch.inverse(K))
+    k4 = torch.eye(4)[None].clone()
+    k4[:, :3, :3] = K
+    assert torch.equal(proj.reshape(1, 4, 4), torch.matmul(k4, pose))
+
+
+def test_divide_safe():
+    num = torch.tensor([1.0, 2.0, 3.0])
+    den = torch.tensor([0.0, -0.0, 4.0])
+    out = mv.divide_safe_torch(num, den)
+    assert torch.equal(out, num / torch.tensor([1e-8, 1e-8, 4.0]))
+
+
+def test_meshgrid_values():
+    mv.utils.device = torch.device("cpu")
+    try:
+        g = mv.meshgrid_abs_torch(2, 3, 4)
+    finally:
+        mv.utils.device = torch.device("cuda")
+    assert g.shape == (2, 3, 3, 4)
+    assert torch.equal(g[0, 0, 1], torch.arange(4.0)) and torch.equal(g[1, 1, :, 2], torch.arange(3.0))
+
+
+def test_no_cpu_fallback():
+    """The product path refuses CPU tensors instead of silently computing on the host."""
+    mpi = torch.zeros((1, 4, 4, 2, 4))
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        mv.mpi_render_view_torch(mpi, torch.eye(4)[None], torch.tensor([2.0, 1.0]), torch.eye(3)[None])
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        mv.plane_sweep_torch(torch.zeros((1, 4, 4, 3)), [1.0, 2.0], torch.eye(4)[None], torch.eye(3)[None])
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        mv.over_composite([torch.zeros((1, 2, 2, 4))] * 2)
+
+
+def test_planes_must_be_tensor():
+    with pytest.raises(AttributeError):  # utils.py:279 behaviour
+        mv.mpi_render_view_torch(torch.zeros((1, 4, 4, 2, 4)), torch.eye(4)[None], [2.0, 1.0], torch.eye(3)[None])
+
+
+def test_ret_flows_unsupported():
+    with pytest.raises(RuntimeError):
+        mv.projective_inverse_warp_torch(torch.zeros((1, 4, 4, 3)), torch.ones((1, 4, 4)), torch.eye(4)[None],
+                                         torch.eye(3)[None], ret_flows=True)
+
+
+def test_configs():
+    c4 = configs.config4()
+    assert len(c4["poses"]) == 1000 and len(c4["depths"]) == 128
+    assert c4["depths"][0] == 100 and c4["depths"][-1] == 1
+    c1 = configs.config1_camera()
+    assert abs(c1["K"][0][0] - 554.2562584220408) < 1e-9

@@ -39,8 +39,8 @@ def test_native_and_packed_kernels_agree_with_oracle(name, small, meta, dev):
     want = oracle.render(mpi.numpy(), homs.numpy())
     dmpi = mpi.contiguous().to(dev)
     nat = torch.empty((B, H, W, 3), device=dev)
-    _lib._call("mpiv_render", _lib._p(dmpi), _lib._strides(dmpi), B, H, W, P, _lib._p(homs.to(dev)),
-               _lib._p(nat), _lib._stream(dev))
+    _lib._call("mpiv_render", dmpi, _lib._strides(dmpi), B, H, W, P, homs.to(dev),
+               nat, _lib._stream(dev))
     assert_bits(nat.cpu().numpy(), want)
     for b in range(B):
         packed = _lib.pack_planes(dmpi[b])
@@ -137,3 +137,13 @@ def test_render_errors(dev):
         mv.mpi_render_view_torch(mpi.double(), pose, torch.tensor([2.0, 1.0], device=dev), K)
     with pytest.raises(RuntimeError):  # batch mismatch
         mv.mpi_render_view_torch(mpi, pose.expand(2, 4, 4), torch.tensor([2.0, 1.0], device=dev), K.expand(2, 3, 3))
+
+
+@pytest.mark.parametrize("divisor", [1, 2, 3, 7, 36, 39, 71, 127, 159, 255, 399, 575, 639, 767, 1023, 1079,
+                                     2159, 4095, 65535])
+def test_div_const_exhaustive(divisor, dev):
+    """The render's launch-constant division equals IEEE x / c for every fp32 x whose
+    quotient can affect a sample position (all 2^32 bit patterns)."""
+    bad = torch.zeros(1, dtype=torch.int64, device=dev)
+    _lib._call("mpiv_selftest_div_const", divisor, bad, _lib._stream(dev))
+    assert int(bad.item()) == 0
