@@ -19,4 +19,4 @@ for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
     timeout -s KILL 240 rocprofv3 --pmc $pass --output-format csv -d "$OUT/$name" -o run \
         -- python -u "$ROOT/bench.py" $ARGS > "$OUT/$name.log" 2>&1 || { echo "pmc pass $pass failed"; tail -5 "$OUT/$name.log"; exit 1; }
 done
-cd "$ROOT" && python tools/parse_pmc.py "$OUT" "$TAG"
+echo "profile passes done; summarise locally: python tools/parse_pmc.py gpurun_out/pmc $TAG"
