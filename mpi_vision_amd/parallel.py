@@ -1,0 +1,114 @@
+"""Multi-GPU sharding of the MPI render.  One process per GPU,
+torch.distributed over RCCL ("nccl") on the box, gloo in CPU tests.
+
+* View sharding (configs 2/4): the camera path is split into contiguous pose
+  ranges, every rank renders its views from its own MPI replica -- no collective on
+  the data path; frames stay in HBM unless `gather_frames` is asked for.
+
+* Plane sharding (config 5): rank g owns planes [g*P/G, (g+1)*P/G), back to front,
+  and renders the partial (C, T) of its range (`mpiv_render_packed_ct`).  The
+  over-operator (Cf, Tf) o (Cb, Tb) = (Cf + Tf*Cb, Tf*Tb) is associative but NOT
+  commutative and RCCL has no custom reduction op, so the combine is an ordered
+  exchange instead of an all-reduce:
+      1. the frame is cut into G row bands; one all_to_all (RCCL point-to-point
+         over xGMI: every GPU sends G-1 bands and receives G-1 bands at once, one
+         per link, instead of a ring that is bound by one link) leaves rank k with
+         band k of every shard's partial, in plane order (source rank order);
+      2. rank k combines them back-to-front with `mpiv_combine_ct`;
+      3. the RGB bands are gathered to the destination rank.
+  Parity: reassociating the over-operator across G ranges moves results by ~1e-7
+  (SURVEY.md §8e measured 2.4e-7 over 8 ranges of 256 planes); the tests hold it to
+  1e-5 against the single-GPU sequential render.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Balanced contiguous split of n items: rank's [begin, end)."""
+    q, r = divmod(n, world)
+    begin = rank * q + min(rank, r)
+    return begin, begin + q + (1 if rank < r else 0)
+
+
+def band_bounds(height: int, world: int) -> list[tuple[int, int]]:
+    return [shard_range(height, k, world) for k in range(world)]
+
+
+def _world(group):
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def exchange_bands(ct: torch.Tensor, group=None) -> torch.Tensor:
+    """all_to_all of row bands.
+
+    ct: this rank's partial [V, H, W, 4] (C, T) for its plane range.
+    Returns [G, V, bh, W, 4]: band `rank` of every rank's partial, indexed by source
+    rank (= plane order, back first), padded to the tallest band bh."""
+    G, rank = _world(group)
+    V, H, W, C = ct.shape
+    bands = band_bounds(H, G)
+    bh = max(e - b for b, e in bands)
+    send = ct.new_zeros((G, V, bh, W, C))
+    for k, (b, e) in enumerate(bands):
+        send[k, :, : e - b] = ct[:, b:e]
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    b, e = bands[rank]
+    return recv[:, :, : e - b]
+
+
+def gather_frames(band: torch.Tensor, height: int, group=None, dst: int = 0) -> Optional[torch.Tensor]:
+    """Gather RGB row bands [V, bh_k, W, 3] (band k on rank k) into [V, H, W, 3] on dst."""
+    G, rank = _world(group)
+    bands = band_bounds(height, G)
+    bh = max(e - b for b, e in bands)
+    V, h, W, C = band.shape
+    padded = band.new_zeros((V, bh, W, C))
+    padded[:, :h] = band
+    gathered = [torch.empty_like(padded) for _ in range(G)] if rank == dst else None
+    dist.gather(padded, gathered, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([g[:, : e - b] for g, (b, e) in zip(gathered, bands)], dim=1)
+
+
+def combine_partials(parts: torch.Tensor,
+                     combine: Optional[Callable[[torch.Tensor], torch.Tensor]] = None) -> torch.Tensor:
+    """Ordered back-to-front over-combine of [G, ...,4] partials -> [..., 3] (HIP kernel)."""
+    if combine is None:
+        from . import _lib
+        combine = _lib.combine_ct
+    return combine(parts)
+
+
+def render_plane_sharded(packed_local: torch.Tensor, homs_local: torch.Tensor, height: int, group=None,
+                         dst: int = 0) -> Optional[torch.Tensor]:
+    """Plane-sharded render of V views.
+
+    packed_local: this rank's planes, packed [P_local, H, W, 4] (rank 0 holds the
+    back-most range, which contains the reference's plane 0); homs_local
+    [V, P_local, 9].  Returns the final frames [V, H, W, 3] on dst, None elsewhere."""
+    from . import _lib
+    G, rank = _world(group)
+    ct = _lib.render_packed_ct(packed_local, homs_local, back=(rank == 0))
+    parts = exchange_bands(ct, group)
+    band = combine_partials(parts)
+    return gather_frames(band, height, group, dst)
+
+
+def view_shard(n_views: int, rank: int, world: int) -> slice:
+    b, e = shard_range(n_views, rank, world)
+    return slice(b, e)
+
+
+def render_view_sharded(packed: torch.Tensor, homs_all: torch.Tensor, group=None) -> torch.Tensor:
+    """This rank's frames of a view-sharded camera path (no collective)."""
+    from . import _lib
+    G, rank = _world(group)
+    sl = view_shard(homs_all.shape[0], rank, G)
+    return _lib.render_packed(packed, homs_all[sl])

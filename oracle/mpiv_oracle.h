@@ -10,6 +10,9 @@ extern "C" {
 /* mpi [B,H,W,P,4] with strides st[5]; homs [B][P][9] row-major; out [B,H,W,3] contiguous */
 void oracle_render(const float *mpi, const int64_t st[5], int B, int H, int W, int P,
                    const float *homs, float *out, int nthreads);
+/* plane-range partial (C,T) [B,H,W,4] of planes [p0,p1); back: range holds plane 0 */
+void oracle_render_ct(const float *mpi, const int64_t st[5], int B, int H, int W, int P, int p0, int p1,
+                      int back, const float *homs, float *out, int nthreads);
 /* img [B,Hs,Ws,C] strides st[4]; ki [B][9]; proj [B][16]; depths [D] fp32; out [B,Ht,Wt,D*C] */
 void oracle_plane_sweep(const float *img, const int64_t st[4], int B, int Hs, int Ws, int C,
                         const float *ki, const float *proj, const float *depths, int D,

@@ -31,6 +31,7 @@ def lib():
             build()
         L = ctypes.CDLL(_SO)
         L.oracle_render.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, _f, ctypes.c_int]
+        L.oracle_render_ct.argtypes = [_f, _i64] + [ctypes.c_int] * 7 + [_f, _f, ctypes.c_int]
         L.oracle_plane_sweep.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, _f, _f] + \
             [ctypes.c_int] * 3 + [_f, ctypes.c_int]
         L.oracle_grid_sample.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, ctypes.c_int, ctypes.c_int,
@@ -60,6 +61,27 @@ def render(mpi: np.ndarray, homs: np.ndarray, nthreads: int = 0) -> np.ndarray:
     out = np.empty((B, H, W, 3), np.float32)
     lib().oracle_render(_fp(mpi), _strides(mpi), B, H, W, P, _fp(homs), _fp(out), _threads(nthreads))
     return out
+
+
+def render_ct(mpi: np.ndarray, homs: np.ndarray, p0: int, p1: int, back: bool, nthreads: int = 0) -> np.ndarray:
+    """Plane-range partial (C, T) -> [B,H,W,4] (plane sharding)."""
+    assert mpi.dtype == np.float32 and mpi.ndim == 5
+    B, H, W, P, _ = mpi.shape
+    homs = np.ascontiguousarray(homs, dtype=np.float32).reshape(B, P, 9)
+    out = np.empty((B, H, W, 4), np.float32)
+    lib().oracle_render_ct(_fp(mpi), _strides(mpi), B, H, W, P, p0, p1, int(back), _fp(homs), _fp(out),
+                           _threads(nthreads))
+    return out
+
+
+def combine_ct(parts: np.ndarray) -> np.ndarray:
+    """parts [G, ..., 4] ordered back->front -> [..., 3]: (Cf,Tf) o (Cb,Tb) = (Cf + Tf*Cb, Tf*Tb)."""
+    acc = parts[-1].astype(np.float32).copy()
+    for k in range(parts.shape[0] - 2, -1, -1):
+        b = parts[k]
+        acc[..., :3] = np.float32(acc[..., 3:4] * b[..., :3] + acc[..., :3])
+        acc[..., 3] = acc[..., 3] * b[..., 3]
+    return acc[..., :3]
 
 
 def plane_sweep(img: np.ndarray, ki: np.ndarray, proj: np.ndarray, depths, tgt_h: int, tgt_w: int,

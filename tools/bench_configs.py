@@ -1,0 +1,170 @@
+#!/usr/bin/env python3
+"""Per-config GPU timings for every BASELINE.json config (bench.py covers the
+headline config 4).  One JSON line per measurement: kernel time from HIP events
+on the launching stream (median of --iters after --warmup), throughput and the
+achieved fraction of the 8 TB/s HBM roofline on ALGORITHMIC bytes.
+
+    python tools/bench_configs.py [--iters 20] [--only c1,c2,c3,c4,c5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import mpi_vision_amd as mv  # noqa: E402
+from mpi_vision_amd import _host, _lib, configs  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, iters, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        fn()
+        b.record(s)
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return statistics.median(ts), min(ts)
+
+
+def report(name, ms, ms_min, alg_bytes, mpix=None, extra=None):
+    gbs = alg_bytes / (ms * 1e-3) / 1e9
+    r = {"config": name, "ms_median": round(ms, 4), "ms_min": round(ms_min, 4), "alg_GB": round(alg_bytes / 1e9, 4),
+         "achieved_GBs": round(gbs, 1), "roofline_frac": round(gbs / PEAK, 4)}
+    if mpix is not None:
+        r["Mpix_per_s"] = round(mpix / (ms * 1e-3), 1)
+    if extra:
+        r.update(extra)
+    print(json.dumps(r), flush=True)
+
+
+def gen_mpi(H, W, P, seed, dev):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    m = torch.rand((1, H, W, P, 4), generator=g, device=dev)
+    m[..., :3].mul_(2).sub_(1)
+    m[:, :, :, 0, 3] = 1.0
+    return m
+
+
+def c1(dev, it, wu):
+    c = configs.config1_camera()
+    H, W, P = c["H"], c["W"], c["P"]
+    mpi = gen_mpi(H, W, P, 0, dev)
+    pose = configs.f32(c["poses"][:1]).to(dev)
+    K = configs.f32([c["K"]]).to(dev)
+    d = configs.f32(c["depths"]).to(dev)
+    ms, mn = timed(lambda: mv.mpi_render_view_torch(mpi, pose, d, K), it, wu)
+    report("c1 test-MPI 640x400x10, 1 pose, mpi_render_view_torch end-to-end (host H + native kernel)", ms, mn,
+           P * H * W * 16 + H * W * 12, H * W / 1e6)
+    homs = _host.render_homographies(pose, d, K, 1).to(dev)
+    out = torch.empty((1, H, W, 3), device=dev)
+    ms, mn = timed(lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out,
+                                      _lib._stream(dev)), it, wu)
+    report("c1 native kernel only", ms, mn, P * H * W * 16 + H * W * 12, H * W / 1e6)
+
+
+def c2(dev, it, wu):
+    c = configs.config2()
+    H, W, P = c["H"], c["W"], c["P"]
+    V = len(c["poses"])
+    mpi = gen_mpi(H, W, P, 0, dev)
+    homs = _host.render_homographies(configs.f32(c["poses"]), configs.f32(c["depths"]),
+                                     configs.f32([c["K"]] * V), V).to(dev)
+    packed = _lib.pack_planes(mpi[0])
+    out = torch.empty((V, H, W, 3), device=dev)
+    per_view = P * H * W * 16 + H * W * 12
+    ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it, wu)
+    report(f"c2 1024x576x32, {V} views, packed kernel", ms, mn, V * per_view, V * H * W / 1e6)
+    ms, mn = timed(lambda: _lib.pack_planes(mpi[0]), it, wu)
+    report("c2 pack (one-time per MPI)", ms, mn, 2 * P * H * W * 16)
+    mpi5 = mpi.expand(V, H, W, P, 4)
+    ms, mn = timed(lambda: _lib._call("mpiv_render", mpi5, _lib._strides(mpi5), V, H, W, P, homs, out,
+                                      _lib._stream(dev)), max(3, it // 4), 1)
+    report(f"c2 native kernel, {V} views (no pack)", ms, mn, V * per_view, V * H * W / 1e6)
+
+
+def c3(dev, it, wu):
+    c = configs.config3()
+    S, H, W, D = c["S"], c["H"], c["W"], c["D"]
+    g = torch.Generator(device=dev).manual_seed(1)
+    img = torch.rand((S, H, W, 3), generator=g, device=dev)
+    K = configs.f32([c["K"]] * S)
+    ki, proj = _host.psv_matrices(K, K, configs.f32(c["poses"]))
+    ki, proj = ki.to(dev), proj.to(dev)
+    d = configs.f32(c["depths"]).to(dev)
+    out = torch.empty((S, H, W, D * 3), device=dev)
+    fn = lambda: _lib._call("mpiv_plane_sweep", img, _lib._strides(img), S, H, W, 3, ki, proj, d, D, H, W, out,  # noqa: E731
+                            _lib._stream(dev))
+    ms, mn = timed(fn, it, wu)
+    report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes", ms, mn, S * H * W * 12 + S * D * H * W * 12,
+           extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
+
+
+def c4(dev, it, wu):
+    c = configs.config4()
+    H, W, P = c["H"], c["W"], c["P"]
+    mpi = gen_mpi(H, W, P, 0, dev)
+    packed = _lib.pack_planes(mpi[0])
+    per_view = P * H * W * 16 + H * W * 12
+    for V in (1, 8, 125):
+        homs = _host.render_homographies(configs.f32(c["poses"][:V]), configs.f32(c["depths"]),
+                                         configs.f32([c["K"]] * V), V).to(dev)
+        out = torch.empty((V, H, W, 3), device=dev)
+        ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it if V < 125 else max(3, it // 4), 1)
+        report(f"c4 1024^2x128 packed, {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
+    homs = _host.render_homographies(configs.f32(c["poses"][:1]), configs.f32(c["depths"]),
+                                     configs.f32([c["K"]]), 1).to(dev)
+    out = torch.empty((1, H, W, 3), device=dev)
+    ms, mn = timed(lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out,
+                                      _lib._stream(dev)), it, wu)
+    report("c4 native kernel (reference layout in place), 1 view", ms, mn, per_view, H * W / 1e6)
+
+
+def c5(dev, it, wu):
+    """Per-GPU share of the 8-way plane-sharded 4096x2160x256 render + the combine."""
+    c = configs.config5()
+    H, W, P = c["H"], c["W"], c["P"]
+    G = 8
+    PL = P // G
+    g = torch.Generator(device=dev).manual_seed(0)
+    packed = torch.rand((PL, H, W, 4), generator=g, device=dev)
+    homs = _host.render_homographies(configs.f32(c["poses"]), configs.f32(c["depths"]), configs.f32([c["K"]]), 1)
+    homs_local = homs[:, :PL].contiguous().to(dev)
+    ct = torch.empty((1, H, W, 4), device=dev)
+    ms, mn = timed(lambda: _lib.render_packed_ct(packed, homs_local, back=True, out=ct), it, wu)
+    report(f"c5 plane shard: {PL} of {P} planes, 4096x2160 partial (C,T)", ms, mn, PL * H * W * 16 + H * W * 16,
+           H * W / 1e6)
+    bh = H // G
+    parts = torch.rand((G, 1, bh, W, 4), device=dev)
+    ms, mn = timed(lambda: _lib.combine_ct(parts), it, wu)
+    report(f"c5 ordered combine of {G} band partials ({bh}x{W})", ms, mn, G * bh * W * 16 + bh * W * 12)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--only", default="c1,c2,c3,c4,c5")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    for name in a.only.split(","):
+        globals()[name](dev, a.iters, a.warmup)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
