@@ -85,6 +85,16 @@ int mpiv_plane_sweep(const float *img, const int64_t img_strides[4], int B, int 
                      const float *ki, const float *proj, const float *depths, int D, int Ht, int Wt,
                      float *out, void *stream);
 
+/* Source images for the fast sweep: [B,Hs,Ws,C] (C <= 4, element strides) ->
+ * img4 [B][Hs*Ws] 16-B texels (channels >= C zero), 16-B aligned. */
+int mpiv_pad_texels(const float *img, const int64_t img_strides[4], int B, int Hs, int Ws, int C, float *img4,
+                    void *stream);
+
+/* plane_sweep_torch* on padded texels (mpiv_pad_texels), C <= 4, Hs*Ws*16 < 2 GiB:
+ * same contract and bit-identical output as mpiv_plane_sweep. */
+int mpiv_plane_sweep_padded(const float *img4, int B, int Hs, int Ws, int C, const float *ki, const float *proj,
+                            const float *depths, int D, int Ht, int Wt, float *out, void *stream);
+
 /* projective_inverse_warp_torch / projective_inverse_warp_torch2 with a per-pixel
  * depth map (utils.py:409-450, 725-769).
  * depth: [B,Ht,Wt] element strides depth_strides[3]; out [B,Ht,Wt,C] contiguous. */

@@ -36,11 +36,17 @@ _SIGS = {
     "mpiv_cam2pixel": [_vp, _vp, _int, _i64, _vp, _vp],
     "mpiv_plane_coords": [_vp, _int, _i64, _vp, _int, _int, _vp, _vp],
     "mpiv_selftest_div_const": [_int, _vp, _vp],
+    "mpiv_pad_texels": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
+    "mpiv_plane_sweep_padded": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error")
 ABI_VERSION = 1
 
 _lib = None
+
+# How mpi_render_view_torch renders a non-broadcast MPI batch: "auto" (pack per view
+# when P >= 8, else read in place), "pack", or "native" (the in-place kernel).
+RENDER_POLICY = "auto"
 
 
 def load():
@@ -179,6 +185,15 @@ def render(rgba_layers: torch.Tensor, homs: torch.Tensor) -> torch.Tensor:
         return render_packed(pack_planes(rgba_layers[0]), homs)
     h = _up(homs, dev)
     out = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32)
+    if RENDER_POLICY == "pack" or (RENDER_POLICY == "auto" and P >= 8 and H * W * 16 < 0x7FFFFF00):
+        # per view: pack its MPI plane-major (one coalesced transpose pass) and render
+        # from the packed copy -- the gathers of the in-place layout touch one 128-B
+        # line per 16-B texel, which is slower than paying the pack
+        packed = torch.empty((P, H, W, 4), device=dev, dtype=torch.float32)
+        for b in range(B):
+            _call("mpiv_pack_planes", rgba_layers[b], _strides(rgba_layers[b]), H, W, P, packed, _stream(dev))
+            _call("mpiv_render_packed", packed, H, W, P, h[b:b + 1], 1, out[b:b + 1], _stream(dev))
+        return out
     _call("mpiv_render", rgba_layers, _strides(rgba_layers), B, H, W, P, h, out, _stream(dev))
     return out
 
@@ -189,13 +204,22 @@ def render(rgba_layers: torch.Tensor, homs: torch.Tensor) -> torch.Tensor:
 
 def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.Tensor, tgt_h: int,
                 tgt_w: int) -> torch.Tensor:
+    """[B,Hs,Ws,C] -> PSV [B,tgt_h,tgt_w,D*C].  C <= 4: the source is padded once to
+    16-B texels (B*Hs*Ws*16 bytes) and swept by the buffer-load kernel; otherwise the
+    generic strided kernel."""
     dev = _dev(img)
     B, Hs, Ws, C = img.shape
     d = torch.tensor([float(x) for x in depth_planes], dtype=torch.float32)
     D = d.shape[0]
     out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
-    _call("mpiv_plane_sweep", img, _strides(img), B, Hs, Ws, C, _up(ki, dev), _up(proj, dev),
-          _up(d, dev), D, tgt_h, tgt_w, out, _stream(dev))
+    kid, projd, dd = _up(ki, dev), _up(proj, dev), _up(d, dev)
+    if C <= 4 and Hs * Ws * 16 < 0x7FFFFF00:
+        img4 = torch.empty((B, Hs, Ws, 4), device=dev, dtype=torch.float32)
+        _call("mpiv_pad_texels", img, _strides(img), B, Hs, Ws, C, img4, _stream(dev))
+        _call("mpiv_plane_sweep_padded", img4, B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out, _stream(dev))
+    else:
+        _call("mpiv_plane_sweep", img, _strides(img), B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out,
+              _stream(dev))
     return out
 
 

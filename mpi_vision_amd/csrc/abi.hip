@@ -148,6 +148,42 @@ int mpiv_plane_sweep(const float* img, const int64_t st[4], int B, int Hs, int W
     return launched("mpiv_plane_sweep");
 }
 
+int mpiv_pad_texels(const float* img, const int64_t st[4], int B, int Hs, int Ws, int C, float* img4,
+                    void* stream) {
+    if (!img || !st || !img4) return fail(MPIV_ERR_ARG, "mpiv_pad_texels: null pointer");
+    if (B <= 0 || Hs <= 0 || Ws <= 0 || C <= 0 || C > 4) return fail(MPIV_ERR_ARG, "mpiv_pad_texels: bad shape");
+    if (!aligned16(img4)) return fail(MPIV_ERR_ARG, "mpiv_pad_texels: img4 must be 16-byte aligned");
+    if (B > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_pad_texels: too large");
+    const ImgStrides s{st[0], st[1], st[2], st[3]};
+    pad_texels_kernel<<<dim3(blocks((int64_t)Hs * Ws, 256), B), 256, 0, S(stream)>>>(img, s, Hs, Ws, C,
+                                                                                   reinterpret_cast<float4*>(img4));
+    return launched("mpiv_pad_texels");
+}
+
+int mpiv_plane_sweep_padded(const float* img4, int B, int Hs, int Ws, int C, const float* ki, const float* proj,
+                            const float* depths, int D, int Ht, int Wt, float* out, void* stream) {
+    if (!img4 || !ki || !proj || !depths || !out) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: null pointer");
+    if (B <= 0 || Hs <= 0 || Ws <= 0 || C <= 0 || C > 4 || D <= 0 || Ht <= 0 || Wt <= 0)
+        return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: bad shape");
+    if (!aligned16(img4)) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: img4 must be 16-byte aligned");
+    if ((int64_t)Hs * Ws * 16 >= (int64_t)kOOB) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: image > 2 GiB");
+    const int64_t per_view = (int64_t)Ht * Wt * D;
+    if (B > kMaxGridYZ || per_view >= (1ll << 31)) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: too large");
+    const FastDiv fd_d = make_fastdiv((unsigned)D), fd_w = make_fastdiv((unsigned)Wt);
+    const SweepParams sp = sweep_params(B, Hs, Ws, C, D, Ht, Wt);
+    const float rc_hs = 1.0f / sp.fhs, rc_ws = 1.0f / sp.fws;
+    const float4* im = reinterpret_cast<const float4*>(img4);
+    const dim3 grid(blocks(per_view, 256), B, 1);
+    hipStream_t q = S(stream);
+    switch (C) {
+        case 1: plane_sweep_rgba_kernel<1><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out); break;
+        case 2: plane_sweep_rgba_kernel<2><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out); break;
+        case 3: plane_sweep_rgba_kernel<3><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out); break;
+        default: plane_sweep_rgba_kernel<4><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out); break;
+    }
+    return launched("mpiv_plane_sweep_padded");
+}
+
 int mpiv_inverse_warp(const float* img, const int64_t st[4], int B, int Hs, int Ws, int C, const float* ki,
                       const float* proj, const float* depth, const int64_t dst[3], int Ht, int Wt, float* out,
                       void* stream) {

@@ -31,6 +31,33 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, in
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
 }
 
+// Exact unsigned division n / d by a launch-constant d >= 1 for n < 2^31
+// (Granlund-Montgomery: q = (mulhi(n, m) + n) >> s with m = floor(2^32 (2^s - d) / d) + 1,
+// s = ceil(log2 d)); replaces the ~40-instruction 64-bit division in index math.
+struct FastDiv {
+    unsigned d, m;
+    int s;
+};
+
+inline FastDiv make_fastdiv(unsigned d) {
+    FastDiv f;
+    f.d = d;
+    int s = 0;
+    while ((1ull << s) < d) ++s;
+    f.s = s;
+    f.m = (unsigned)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
+    return f;
+}
+
+__host__ __device__ __forceinline__ unsigned fast_div(unsigned n, const FastDiv& f) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const unsigned t = __umulhi(n, f.m);
+#else
+    const unsigned t = (unsigned)(((unsigned long long)n * f.m) >> 32);
+#endif
+    return (t + n) >> f.s;
+}
+
 // Correctly rounded fp32 division.  hipcc's default expansion of `a / b` is the
 // IEEE-exact v_div_scale / v_rcp / fma / v_div_fmas / v_div_fixup sequence; it is
 // kept verbatim (a reciprocal-multiply shifts coordinates by 1 ulp -> ~1e-4 output
@@ -122,6 +149,55 @@ __device__ __forceinline__ void hom_sample_pos(const float* __restrict__ h, floa
     const float cy = div_rn(div_rn(v, w), wm1);  //          y / (W-1)
     px = unnormalize(to_grid(cx), half_w);
     py = unnormalize(to_grid(cy), half_h);
+}
+
+// ---------------------------------------------------------------------------
+// 16-B texel gathers from a plane of float4 texels through a buffer resource
+// ---------------------------------------------------------------------------
+
+// One bilinear sample in flight: the four 16-B taps (already issued) + weights.
+struct TapSet {
+    f32x4 a, b, c, d;           // NW, NE, SW, SE texels (0 where outside the plane)
+    float nw, ne, sw, se;
+};
+
+// Issue the four tap loads of one sample of one packed plane.  Taps outside the
+// plane (and every tap when `live` is false) get the out-of-range offset, so the
+// buffer unit returns 0 for them without a memory access: grid_sample's zeros
+// padding, per tap.
+__device__ __forceinline__ void issue_taps(__amdgpu_buffer_rsrc_t r, int W, int H, float px, float py, bool live,
+                                           TapSet& t) {
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
+    // clamp to [-2, W] / [-2, H] so the int conversion is defined and every tap index
+    // outside [0, W) / [0, H) stays outside; unsigned compares then test the range
+    const unsigned ux = (unsigned)(int)__builtin_fminf(__builtin_fmaxf(fx0, -2.0f), (float)W);
+    const unsigned uy = (unsigned)(int)__builtin_fminf(__builtin_fmaxf(fy0, -2.0f), (float)H);
+    const unsigned uw = (unsigned)W, uh = (unsigned)H;
+    const int off = ((int)uy * W + (int)ux) * 16;
+    const int row = W * 16;
+    t.a = llvm_raw_buffer_load_v4f32(r, (live && ux < uw && uy < uh) ? off : kOOB, 0, 0);
+    t.b = llvm_raw_buffer_load_v4f32(r, (live && ux + 1 < uw && uy < uh) ? off + 16 : kOOB, 0, 0);
+    t.c = llvm_raw_buffer_load_v4f32(r, (live && ux < uw && uy + 1 < uh) ? off + row : kOOB, 0, 0);
+    t.d = llvm_raw_buffer_load_v4f32(r, (live && ux + 1 < uw && uy + 1 < uh) ? off + row + 16 : kOOB, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 blend_taps(const TapSet& t) {
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float acc = t.a[k] * t.nw;
+        acc = __builtin_fmaf(t.b[k], t.ne, acc);
+        acc = __builtin_fmaf(t.c[k], t.sw, acc);
+        acc = __builtin_fmaf(t.d[k], t.se, acc);
+        o[k] = acc;
+    }
+    return o;
 }
 
 }  // namespace mpiv

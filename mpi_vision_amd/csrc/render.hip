@@ -66,51 +66,6 @@ __device__ __forceinline__ void render_pos(const float* __restrict__ h, float fx
 // packed plane-major layout
 // ---------------------------------------------------------------------------
 
-// One bilinear sample in flight: the four 16-B taps (already issued) + weights.
-struct TapSet {
-    f32x4 a, b, c, d;           // NW, NE, SW, SE texels (0 where outside the plane)
-    float nw, ne, sw, se;
-};
-
-// Issue the four tap loads of one sample of one packed plane.  Taps outside the
-// plane (and every tap when `live` is false) get the out-of-range offset, so the
-// buffer unit returns 0 for them without a memory access: grid_sample's zeros
-// padding, per tap.
-__device__ __forceinline__ void issue_taps(__amdgpu_buffer_rsrc_t r, const RenderGeom& g, float px, float py,
-                                           bool live, TapSet& t) {
-    const float fx0 = floorf(px), fy0 = floorf(py);
-    const float wx = px - fx0, ex = 1.0f - wx;
-    const float wy = py - fy0, sy = 1.0f - wy;
-    t.nw = sy * ex;
-    t.ne = sy * wx;
-    t.sw = wy * ex;
-    t.se = wy * wx;
-    // clamp to [-2, W] / [-2, H] so the int conversion is defined and every tap index
-    // outside [0, W) / [0, H) stays outside; unsigned compares then test the range
-    const unsigned ux = (unsigned)(int)__builtin_fminf(__builtin_fmaxf(fx0, -2.0f), (float)g.W);
-    const unsigned uy = (unsigned)(int)__builtin_fminf(__builtin_fmaxf(fy0, -2.0f), (float)g.H);
-    const unsigned uw = (unsigned)g.W, uh = (unsigned)g.H;
-    const int off = ((int)uy * g.W + (int)ux) * 16;
-    const int row = g.W * 16;
-    t.a = llvm_raw_buffer_load_v4f32(r, (live && ux < uw && uy < uh) ? off : kOOB, 0, 0);
-    t.b = llvm_raw_buffer_load_v4f32(r, (live && ux + 1 < uw && uy < uh) ? off + 16 : kOOB, 0, 0);
-    t.c = llvm_raw_buffer_load_v4f32(r, (live && ux < uw && uy + 1 < uh) ? off + row : kOOB, 0, 0);
-    t.d = llvm_raw_buffer_load_v4f32(r, (live && ux + 1 < uw && uy + 1 < uh) ? off + row + 16 : kOOB, 0, 0);
-}
-
-__device__ __forceinline__ f32x4 blend_taps(const TapSet& t) {
-    f32x4 o;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        float acc = t.a[k] * t.nw;
-        acc = __builtin_fmaf(t.b[k], t.ne, acc);
-        acc = __builtin_fmaf(t.c[k], t.sw, acc);
-        acc = __builtin_fmaf(t.d[k], t.se, acc);
-        o[k] = acc;
-    }
-    return o;
-}
-
 // Bijective XCD-aware block order: the dispatcher deals blocks round-robin over the
 // 8 XCDs (MI355X_MICROARCH.md §Workgroup dispatch), so hardware block b is given the
 // logical id  start(b % 8) + b / 8, i.e. each XCD walks one contiguous range of
@@ -162,7 +117,7 @@ __global__ __launch_bounds__(256) void render_packed_kernel(const float4* __rest
         const int q = p < last ? p : last;
         float px, py;
         render_pos<FAST>(hv + (int64_t)q * 9, fx, fy, g, px, py);
-        issue_taps(make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes), g, px, py, p <= last, ts);
+        issue_taps(make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes), g.W, g.H, px, py, p <= last, ts);
     };
     auto consume = [&](const TapSet& ts, bool first) {
         const f32x4 s = blend_taps(ts);

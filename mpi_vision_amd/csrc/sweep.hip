@@ -78,6 +78,61 @@ __global__ __launch_bounds__(256) void plane_sweep_kernel(const float* __restric
     }
 }
 
+// Source images padded to 16-B texels: [B][Hs*Ws] float4, channels >= C zero.
+__global__ __launch_bounds__(256) void pad_texels_kernel(const float* __restrict__ img, ImgStrides s, int Hs,
+                                                         int Ws, int C, float4* __restrict__ out) {
+    const int64_t npix = (int64_t)Hs * Ws;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (i >= npix) return;
+    const int y = (int)(i / Ws), x = (int)(i % Ws);
+    const float* t = img + b * s.b + y * s.y + x * s.x;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < C && c < 4; ++c) v[c] = t[c * s.c];
+    out[b * npix + i] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// Plane sweep over padded 16-B texels (C <= 4): four 16-B buffer loads per sample
+// with out-of-range taps zeroed by the buffer unit, and the two launch-constant
+// divisions (x / Hs, y / Ws) through div_const (FAST, Hs and Ws >= 1 always hold).
+// Work-items are (pixel, depth) with depth fastest, so a wave's C-float results are
+// one contiguous run of the volume.
+template <int C>
+__global__ __launch_bounds__(256) void plane_sweep_rgba_kernel(const float4* __restrict__ img4, SweepParams sp,
+                                                               float rc_hs, float rc_ws, FastDiv fd_d, FastDiv fd_w,
+                                                               const float* __restrict__ ki,
+                                                               const float* __restrict__ proj,
+                                                               const float* __restrict__ depths,
+                                                               float* __restrict__ out) {
+    const unsigned per_view = (unsigned)sp.Ht * sp.Wt * sp.D;  // < 2^31, checked on the host
+    const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (gid >= per_view) return;
+    const unsigned pix = fast_div(gid, fd_d);
+    const int d = (int)(gid - pix * sp.D);
+    const unsigned yy = fast_div(pix, fd_w);
+    const int y = (int)yy, x = (int)(pix - yy * sp.Wt);
+    float rx, ry, rz;
+    ray(ki + (int64_t)b * 9, (float)x, (float)y, rx, ry, rz);
+    const float* m = proj + (int64_t)b * 16;
+    const float dep = depths[d];
+    const float X = rx * dep, Y = ry * dep, Z = rz * dep;
+    const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+    const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+    const float pz = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11];
+    const float den = pz + 1e-10f;
+    const float cx = div_const(div_rn(pu, den) + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
+    const float cy = div_const(div_rn(pv, den) + 0.5f, sp.fws, rc_ws);  //          y / W
+    const float px = unnormalize(to_grid(cx), sp.half_ws);
+    const float py = unnormalize(to_grid(cy), sp.half_hs);
+    TapSet t;
+    issue_taps(make_rsrc(img4 + (int64_t)b * sp.Hs * sp.Ws, sp.Hs * sp.Ws * 16), sp.Ws, sp.Hs, px, py, true, t);
+    const f32x4 v = blend_taps(t);
+    float* o = out + ((int64_t)b * per_view + gid) * C;
+#pragma unroll
+    for (int c = 0; c < C; ++c) o[c] = v[c];
+}
+
 // projective_inverse_warp_torch[2] with a per-pixel depth map [B, Ht, Wt] (any
 // strides) -> [B, Ht, Wt, C]
 __global__ __launch_bounds__(256) void inverse_warp_kernel(const float* __restrict__ img, ImgStrides s,

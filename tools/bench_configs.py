@@ -132,6 +132,14 @@ def c4(dev, it, wu):
     ms, mn = timed(lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out,
                                       _lib._stream(dev)), it, wu)
     report("c4 native kernel (reference layout in place), 1 view", ms, mn, per_view, H * W / 1e6)
+    pose = configs.f32(c["poses"][:1]).to(dev)
+    K = configs.f32([c["K"]]).to(dev)
+    d = configs.f32(c["depths"]).to(dev)
+    for policy in ("pack", "native"):
+        _lib.RENDER_POLICY = policy
+        ms, mn = timed(lambda: mv.mpi_render_view_torch(mpi, pose, d, K), it, wu)
+        report(f"c4 mpi_render_view_torch end-to-end, 1 view, policy={policy}", ms, mn, per_view, H * W / 1e6)
+    _lib.RENDER_POLICY = "auto"
 
 
 def c5(dev, it, wu):
