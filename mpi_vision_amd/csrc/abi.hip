@@ -173,7 +173,7 @@ int mpiv_plane_sweep_padded(const float* img4, int B, int Hs, int Ws, int C, con
     const SweepParams sp = sweep_params(B, Hs, Ws, C, D, Ht, Wt);
     const float rc_hs = 1.0f / sp.fhs, rc_ws = 1.0f / sp.fws;
     const float4* im = reinterpret_cast<const float4*>(img4);
-    const dim3 grid(blocks(per_view, 256), B, 1);
+    const dim3 grid(blocks(per_view, 256 * kSweepILP), B, 1);
     hipStream_t q = S(stream);
     switch (C) {
         case 1: plane_sweep_rgba_kernel<1><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out); break;

@@ -97,6 +97,9 @@ __global__ __launch_bounds__(256) void pad_texels_kernel(const float* __restrict
 // divisions (x / Hs, y / Ws) through div_const (FAST, Hs and Ws >= 1 always hold).
 // Work-items are (pixel, depth) with depth fastest, so a wave's C-float results are
 // one contiguous run of the volume.
+constexpr int kSweepILP = 4;       // (pixel, depth) items per work-item, loads issued together
+constexpr int kSweepMaxLdsD = 1024; // depths staged in LDS up to this many planes
+
 template <int C>
 __global__ __launch_bounds__(256) void plane_sweep_rgba_kernel(const float4* __restrict__ img4, SweepParams sp,
                                                                float rc_hs, float rc_ws, FastDiv fd_d, FastDiv fd_w,
@@ -104,33 +107,53 @@ __global__ __launch_bounds__(256) void plane_sweep_rgba_kernel(const float4* __r
                                                                const float* __restrict__ proj,
                                                                const float* __restrict__ depths,
                                                                float* __restrict__ out) {
+    __shared__ float s_dep[kSweepMaxLdsD];
+    const bool lds_dep = sp.D <= kSweepMaxLdsD;
+    if (lds_dep)
+        for (int i = threadIdx.x; i < sp.D; i += blockDim.x) s_dep[i] = depths[i];
+    __syncthreads();
     const unsigned per_view = (unsigned)sp.Ht * sp.Wt * sp.D;  // < 2^31, checked on the host
-    const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
-    if (gid >= per_view) return;
-    const unsigned pix = fast_div(gid, fd_d);
-    const int d = (int)(gid - pix * sp.D);
-    const unsigned yy = fast_div(pix, fd_w);
-    const int y = (int)yy, x = (int)(pix - yy * sp.Wt);
-    float rx, ry, rz;
-    ray(ki + (int64_t)b * 9, (float)x, (float)y, rx, ry, rz);
+    const float* k9 = ki + (int64_t)b * 9;
     const float* m = proj + (int64_t)b * 16;
-    const float dep = depths[d];
-    const float X = rx * dep, Y = ry * dep, Z = rz * dep;
-    const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
-    const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
-    const float pz = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11];
-    const float den = pz + 1e-10f;
-    const float cx = div_const(div_rn(pu, den) + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
-    const float cy = div_const(div_rn(pv, den) + 0.5f, sp.fws, rc_ws);  //          y / W
-    const float px = unnormalize(to_grid(cx), sp.half_ws);
-    const float py = unnormalize(to_grid(cy), sp.half_hs);
-    TapSet t;
-    issue_taps(make_rsrc(img4 + (int64_t)b * sp.Hs * sp.Ws, sp.Hs * sp.Ws * 16), sp.Ws, sp.Hs, px, py, true, t);
-    const f32x4 v = blend_taps(t);
-    float* o = out + ((int64_t)b * per_view + gid) * C;
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(img4 + (int64_t)b * sp.Hs * sp.Ws, sp.Hs * sp.Ws * 16);
+    float* ob = out + (int64_t)b * per_view * C;
+    const unsigned base = blockIdx.x * (blockDim.x * kSweepILP) + threadIdx.x;
+    TapSet t[kSweepILP];
+    // phase 1: coordinates + tap loads of all items (kSweepILP x 4 loads in flight)
 #pragma unroll
-    for (int c = 0; c < C; ++c) o[c] = v[c];
+    for (int k = 0; k < kSweepILP; ++k) {
+        const unsigned gid = base + k * blockDim.x;
+        const bool live = gid < per_view;
+        const unsigned g = live ? gid : 0;
+        const unsigned pix = fast_div(g, fd_d);
+        const int d = (int)(g - pix * sp.D);
+        const unsigned yy = fast_div(pix, fd_w);
+        const float fy = (float)(int)yy, fx = (float)(int)(pix - yy * sp.Wt);
+        float rx, ry, rz;
+        ray(k9, fx, fy, rx, ry, rz);
+        const float dep = lds_dep ? s_dep[d] : depths[d];
+        const float X = rx * dep, Y = ry * dep, Z = rz * dep;
+        const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+        const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+        const float pz = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11];
+        const float den = pz + 1e-10f;
+        const float cx = div_const(div_rn(pu, den) + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
+        const float cy = div_const(div_rn(pv, den) + 0.5f, sp.fws, rc_ws);  //          y / W
+        issue_taps(r, sp.Ws, sp.Hs, unnormalize(to_grid(cx), sp.half_ws), unnormalize(to_grid(cy), sp.half_hs),
+                   live, t[k]);
+    }
+    // phase 2: blend + coalesced stores (consecutive work-items = consecutive depths)
+#pragma unroll
+    for (int k = 0; k < kSweepILP; ++k) {
+        const unsigned gid = base + k * blockDim.x;
+        const f32x4 v = blend_taps(t[k]);
+        if (gid < per_view) {
+            float* o = ob + (int64_t)gid * C;
+#pragma unroll
+            for (int c = 0; c < C; ++c) o[c] = v[c];
+        }
+    }
 }
 
 // projective_inverse_warp_torch[2] with a per-pixel depth map [B, Ht, Wt] (any

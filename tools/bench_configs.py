@@ -109,8 +109,19 @@ def c3(dev, it, wu):
     out = torch.empty((S, H, W, D * 3), device=dev)
     fn = lambda: _lib._call("mpiv_plane_sweep", img, _lib._strides(img), S, H, W, 3, ki, proj, d, D, H, W, out,  # noqa: E731
                             _lib._stream(dev))
+    alg = S * H * W * 12 + S * D * H * W * 12
     ms, mn = timed(fn, it, wu)
-    report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes", ms, mn, S * H * W * 12 + S * D * H * W * 12,
+    report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, generic strided kernel", ms, mn, alg,
+           extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
+    img4 = torch.empty((S, H, W, 4), device=dev)
+    pad = lambda: _lib._call("mpiv_pad_texels", img, _lib._strides(img), S, H, W, 3, img4, _lib._stream(dev))  # noqa: E731
+    sweep = lambda: _lib._call("mpiv_plane_sweep_padded", img4, S, H, W, 3, ki, proj, d, D, H, W, out,  # noqa: E731
+                               _lib._stream(dev))
+    ms, mn = timed(sweep, it, wu)
+    report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, padded-texel kernel", ms, mn, alg,
+           extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
+    ms, mn = timed(lambda: (pad(), sweep()), it, wu)
+    report("c3 PSV plane_sweep_torch path (pad + padded kernel)", ms, mn, alg,
            extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
 
 
