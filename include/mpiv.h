@@ -95,6 +95,14 @@ int mpiv_pad_texels(const float *img, const int64_t img_strides[4], int B, int H
 int mpiv_plane_sweep_padded(const float *img4, int B, int Hs, int Ws, int C, const float *ki, const float *proj,
                             const float *depths, int D, int Ht, int Wt, float *out, void *stream);
 
+/* The same, writing into a wider tensor: element (b, pixel, d, c) goes to
+ * out[b*out_bstride + pixel*out_pstride + d*C + c] (format_network_input_torch,
+ * utils.py:473-498, writes each source's volume at its channel offset of the
+ * concatenated network input).  out_pstride >= D*C. */
+int mpiv_plane_sweep_padded_into(const float *img4, int B, int Hs, int Ws, int C, const float *ki,
+                                 const float *proj, const float *depths, int D, int Ht, int Wt, float *out,
+                                 int64_t out_bstride, int64_t out_pstride, void *stream);
+
 /* projective_inverse_warp_torch / projective_inverse_warp_torch2 with a per-pixel
  * depth map (utils.py:409-450, 725-769).
  * depth: [B,Ht,Wt] element strides depth_strides[3]; out [B,Ht,Wt,C] contiguous. */

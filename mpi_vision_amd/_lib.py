@@ -38,6 +38,8 @@ _SIGS = {
     "mpiv_selftest_div_const": [_int, _vp, _vp],
     "mpiv_pad_texels": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_plane_sweep_padded": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
+    "mpiv_plane_sweep_padded_into": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,
+                                     _vp],
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error")
 ABI_VERSION = 1
@@ -220,6 +222,29 @@ def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.T
     else:
         _call("mpiv_plane_sweep", img, _strides(img), B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out,
               _stream(dev))
+    return out
+
+
+def network_input(ref_image, psv_src_images, rel_poses, depth_planes, intrinsics) -> torch.Tensor:
+    """format_network_input_torch: [B,H,W,3] ref + S PSVs of the 3-channel slices of
+    psv_src_images, each swept directly into its channel range of one output."""
+    from ._host import psv_matrices
+    dev = _dev(ref_image, psv_src_images)
+    B, H, W, _ = ref_image.shape
+    S = len(rel_poses)
+    d = torch.tensor([float(x) for x in depth_planes], dtype=torch.float32)
+    D = d.shape[0]
+    Ctot = 3 + S * D * 3
+    out = torch.empty((B, H, W, Ctot), device=dev, dtype=torch.float32)
+    out[..., :3].copy_(ref_image)  # the concat's first slice is a plain copy (utils.py:491)
+    dd = _up(d, dev)
+    img4 = torch.empty((B, H, W, 4), device=dev, dtype=torch.float32)
+    for i, pose in enumerate(rel_poses):
+        src = psv_src_images[:, :, :, i * 3:(i + 1) * 3]
+        ki, proj = psv_matrices(intrinsics, intrinsics, pose)
+        _call("mpiv_pad_texels", src, _strides(src), B, H, W, 3, img4, _stream(dev))
+        _call("mpiv_plane_sweep_padded_into", img4, B, H, W, 3, _up(ki, dev), _up(proj, dev), dd, D, H, W,
+              out[..., 3 + i * D * 3:], H * W * Ctot, Ctot, _stream(dev))
     return out
 
 

@@ -160,12 +160,15 @@ int mpiv_pad_texels(const float* img, const int64_t st[4], int B, int Hs, int Ws
     return launched("mpiv_pad_texels");
 }
 
-int mpiv_plane_sweep_padded(const float* img4, int B, int Hs, int Ws, int C, const float* ki, const float* proj,
-                            const float* depths, int D, int Ht, int Wt, float* out, void* stream) {
+int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C, const float* ki,
+                                 const float* proj, const float* depths, int D, int Ht, int Wt, float* out,
+                                 int64_t out_bstride, int64_t out_pstride, void* stream) {
     if (!img4 || !ki || !proj || !depths || !out) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: null pointer");
     if (B <= 0 || Hs <= 0 || Ws <= 0 || C <= 0 || C > 4 || D <= 0 || Ht <= 0 || Wt <= 0)
         return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: bad shape");
     if (!aligned16(img4)) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: img4 must be 16-byte aligned");
+    if (out_pstride < (int64_t)D * C || out_pstride > (1 << 30) || out_bstride < (int64_t)Ht * Wt * out_pstride)
+        return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: bad output strides");
     if ((int64_t)Hs * Ws * 16 >= (int64_t)kOOB) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: image > 2 GiB");
     const int64_t per_view = (int64_t)Ht * Wt * D;
     if (B > kMaxGridYZ || per_view >= (1ll << 31)) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: too large");
@@ -176,12 +179,18 @@ int mpiv_plane_sweep_padded(const float* img4, int B, int Hs, int Ws, int C, con
     const dim3 grid(blocks(per_view, 256 * kSweepILP), B, 1);
     hipStream_t q = S(stream);
     switch (C) {
-        case 1: plane_sweep_rgba_kernel<1><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out); break;
-        case 2: plane_sweep_rgba_kernel<2><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out); break;
-        case 3: plane_sweep_rgba_kernel<3><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out); break;
-        default: plane_sweep_rgba_kernel<4><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out); break;
+        case 1: plane_sweep_rgba_kernel<1><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out, out_bstride, (int)out_pstride); break;
+        case 2: plane_sweep_rgba_kernel<2><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out, out_bstride, (int)out_pstride); break;
+        case 3: plane_sweep_rgba_kernel<3><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out, out_bstride, (int)out_pstride); break;
+        default: plane_sweep_rgba_kernel<4><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out, out_bstride, (int)out_pstride); break;
     }
     return launched("mpiv_plane_sweep_padded");
+}
+
+int mpiv_plane_sweep_padded(const float* img4, int B, int Hs, int Ws, int C, const float* ki, const float* proj,
+                            const float* depths, int D, int Ht, int Wt, float* out, void* stream) {
+    return mpiv_plane_sweep_padded_into(img4, B, Hs, Ws, C, ki, proj, depths, D, Ht, Wt, out,
+                                        (int64_t)Ht * Wt * D * C, (int64_t)D * C, stream);
 }
 
 int mpiv_inverse_warp(const float* img, const int64_t st[4], int B, int Hs, int Ws, int C, const float* ki,

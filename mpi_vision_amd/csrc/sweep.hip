@@ -106,7 +106,8 @@ __global__ __launch_bounds__(256) void plane_sweep_rgba_kernel(const float4* __r
                                                                const float* __restrict__ ki,
                                                                const float* __restrict__ proj,
                                                                const float* __restrict__ depths,
-                                                               float* __restrict__ out) {
+                                                               float* __restrict__ out, int64_t out_bstride,
+                                                               int out_pstride) {
     __shared__ float s_dep[kSweepMaxLdsD];
     const bool lds_dep = sp.D <= kSweepMaxLdsD;
     if (lds_dep)
@@ -117,7 +118,10 @@ __global__ __launch_bounds__(256) void plane_sweep_rgba_kernel(const float4* __r
     const float* k9 = ki + (int64_t)b * 9;
     const float* m = proj + (int64_t)b * 16;
     const __amdgpu_buffer_rsrc_t r = make_rsrc(img4 + (int64_t)b * sp.Hs * sp.Ws, sp.Hs * sp.Ws * 16);
-    float* ob = out + (int64_t)b * per_view * C;
+    // output element of (pixel, d, c): b*out_bstride + pixel*out_pstride + d*C + c
+    // (out_pstride = D*C for a bare volume; larger when writing into a wider tensor,
+    // e.g. format_network_input_torch's concatenated channels)
+    float* ob = out + (int64_t)b * out_bstride;
     const unsigned base = blockIdx.x * (blockDim.x * kSweepILP) + threadIdx.x;
     TapSet t[kSweepILP];
     // phase 1: coordinates + tap loads of all items (kSweepILP x 4 loads in flight)
@@ -149,7 +153,8 @@ __global__ __launch_bounds__(256) void plane_sweep_rgba_kernel(const float4* __r
         const unsigned gid = base + k * blockDim.x;
         const f32x4 v = blend_taps(t[k]);
         if (gid < per_view) {
-            float* o = ob + (int64_t)gid * C;
+            const unsigned pix = fast_div(gid, fd_d);
+            float* o = ob + (int64_t)pix * out_pstride + (gid - pix * sp.D) * C;
 #pragma unroll
             for (int c = 0; c < C; ++c) o[c] = v[c];
         }

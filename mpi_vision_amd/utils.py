@@ -176,6 +176,17 @@ def plane_sweep_torch(img, depth_planes, pose, intrinsics):
     return _lib.plane_sweep(img, depth_planes, ki, proj, height, width)
 
 
+def format_network_input_torch(self, ref_image, psv_src_images, ref_pose, psv_src_poses, planes, intrinsics):
+    """Network input [B, H, W, 3 + S*D*3]: the reference image followed by one plane-sweep
+    volume per extra source (utils.py:473-498; the unused leading `self` is kept).
+    Each source's volume is swept straight into its channel slice of the output
+    (no per-source tensors, no torch.cat)."""
+    S = psv_src_poses.shape[1]
+    inv_ref = torch.inverse(_host._cpu32(ref_pose))
+    rel = [torch.matmul(_host._cpu32(psv_src_poses[:, i]), inv_ref) for i in range(S)]  # utils.py:493
+    return _lib.network_input(ref_image, psv_src_images, rel, planes, intrinsics)
+
+
 def plane_sweep_torch_one(img, depth_planes, pose, intrinsics):
     """Unbatched PSV of img [H, W, C]; returns [1, H, W, D*C] (utils.py:513-533)."""
     return plane_sweep_torch(img.unsqueeze(0), depth_planes, pose.unsqueeze(0),

@@ -70,3 +70,12 @@ def test_plane_sweep_c3(large, meta, dev):
     np.testing.assert_array_equal(flat[idx].cpu().numpy(), large["c3_val"])
     for i in range(c3["S"]):
         assert sha256(out[i]) == meta["large"]["c3"]["per_source_sha"][i]
+
+
+def test_format_network_input(small, dev):
+    """format_network_input_torch (utils.py:473-498): ref image + one PSV per source,
+    concatenated on channels; bit-exact."""
+    t = {k: torch.tensor(small[f"fni_{k}"]) for k in ("ref", "src", "ref_pose", "src_poses", "K")}
+    out = mv.format_network_input_torch(None, t["ref"].to(dev), t["src"].to(dev), t["ref_pose"].to(dev),
+                                        t["src_poses"].to(dev), list(small["fni_planes"]), t["K"].to(dev))
+    assert_bits(out.cpu().numpy(), small["fni_out"])

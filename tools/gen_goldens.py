@@ -185,6 +185,18 @@ def small_cases(ref):
                psv_two_depths=np.array(d2), psv_two_out=res.numpy())
     meta["psv_two"] = dict(H=48, W=64, C=3, seed=23, tgt_h=36, tgt_w=160, img_sha=sha(img2))
 
+    # --- format_network_input_torch (multi-source PSV + ref image), utils.py:473-498
+    gf = torch.Generator().manual_seed(41)
+    ref_img = torch.rand((2, 24, 32, 3), generator=gf)
+    src_imgs = torch.rand((2, 24, 32, 6), generator=gf)   # two PSV sources
+    ref_pose = f32([rand_pose(g, 0.05, 0.2), rand_pose(g, 0.05, 0.2)])
+    src_poses = f32([[rand_pose(g, 0.05, 0.2), rand_pose(g, 0.05, 0.2)] for _ in range(2)])  # [B,2,4,4]
+    Kf = f32([configs.intrinsics_matrix(30.0, 31.0, 16.0, 12.0), configs.intrinsics_matrix(29.0, 29.0, 15.5, 12.5)])
+    planes_f = ref.inv_depths(1, 50, 4)
+    res = ref.format_network_input_torch(None, ref_img, src_imgs, ref_pose, src_poses, planes_f, Kf)
+    out.update(fni_ref=ref_img.numpy(), fni_src=src_imgs.numpy(), fni_ref_pose=ref_pose.numpy(),
+               fni_src_poses=src_poses.numpy(), fni_K=Kf.numpy(), fni_planes=np.array(planes_f), fni_out=res.numpy())
+
     # --- sampler wrappers -------------------------------------------------------
     gs = torch.Generator().manual_seed(31)
     imgs = torch.rand((2, 3, 20, 25, 4), generator=gs)
