@@ -80,6 +80,36 @@ __device__ __forceinline__ float div_const(float x, float c, float rc) {
     return __builtin_fmaf(r, rc, q);
 }
 
+// Correctly rounded u / w and v / w sharing one reciprocal.  This is hipcc's IEEE
+// division sequence (v_rcp + one Newton step, q = a*y, two residual corrections;
+// the last is what v_div_fmas computes) without v_div_scale / v_div_fixup, which are
+// identities unless an operand or the quotient leaves the normal range.  The guard
+// keeps the fast path where they are identities for every quotient that can move a
+// sample position (|q| >= 2^-26: smaller quotients round -1 + 2q/(H-1) to -1
+// regardless); anything else takes the plain IEEE division.
+__device__ __forceinline__ float div_core(float a, float b, float y) {
+    float q = a * y;
+    float r = __builtin_fmaf(-b, q, a);
+    q = __builtin_fmaf(r, y, q);
+    r = __builtin_fmaf(-b, q, a);
+    return __builtin_fmaf(r, y, q);
+}
+
+__device__ __forceinline__ void div2_rn(float u, float v, float w, float& qu, float& qv) {
+    const float aw = __builtin_fabsf(w);
+    const bool safe = aw >= 0x1p-60f && aw <= 0x1p60f && __builtin_fmaxf(__builtin_fabsf(u), __builtin_fabsf(v)) <= 0x1p60f;
+    if (__builtin_expect(safe, 1)) {
+        float y = __builtin_amdgcn_rcpf(w);
+        const float e = __builtin_fmaf(-w, y, 1.0f);
+        y = __builtin_fmaf(e, y, y);
+        qu = div_core(u, w, y);
+        qv = div_core(v, w, y);
+    } else {
+        qu = div_rn(u, w);
+        qv = div_rn(v, w);
+    }
+}
+
 // grid value g in [-1, 1] -> source pixel, align_corners=False (ATen CPU vectorised
 // grid sampler: (g + 1) * (size / 2) - 0.5, contracted to one FMA).
 __device__ __forceinline__ float unnormalize(float g, float half_size) {
@@ -176,15 +206,19 @@ __device__ __forceinline__ void issue_taps(__amdgpu_buffer_rsrc_t r, int W, int 
     t.se = wy * wx;
     // clamp to [-2, W] / [-2, H] so the int conversion is defined and every tap index
     // outside [0, W) / [0, H) stays outside; unsigned compares then test the range
-    const unsigned ux = (unsigned)(int)__builtin_fminf(__builtin_fmaxf(fx0, -2.0f), (float)W);
-    const unsigned uy = (unsigned)(int)__builtin_fminf(__builtin_fmaxf(fy0, -2.0f), (float)H);
+    const unsigned ux = (unsigned)(int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)W);
+    const unsigned uy = (unsigned)(int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)H);
     const unsigned uw = (unsigned)W, uh = (unsigned)H;
-    const int off = ((int)uy * W + (int)ux) * 16;
-    const int row = W * 16;
+    // 24-bit multiply-add (full rate): valid taps have uy < H, W < 2^24; the offset
+    // of an invalid tap is never used
+    const int off = (int)__umul24(uy, (unsigned)W) * 16 + (int)ux * 16;
+    const int off_s = off + W * 16;
+    // the +16 of the east taps is applied after the select so it folds into the
+    // instruction's immediate offset; kOOB - 16 + 16 is still out of range
     t.a = llvm_raw_buffer_load_v4f32(r, (live && ux < uw && uy < uh) ? off : kOOB, 0, 0);
-    t.b = llvm_raw_buffer_load_v4f32(r, (live && ux + 1 < uw && uy < uh) ? off + 16 : kOOB, 0, 0);
-    t.c = llvm_raw_buffer_load_v4f32(r, (live && ux < uw && uy + 1 < uh) ? off + row : kOOB, 0, 0);
-    t.d = llvm_raw_buffer_load_v4f32(r, (live && ux + 1 < uw && uy + 1 < uh) ? off + row + 16 : kOOB, 0, 0);
+    t.b = llvm_raw_buffer_load_v4f32(r, ((live && ux + 1 < uw && uy < uh) ? off : kOOB - 16) + 16, 0, 0);
+    t.c = llvm_raw_buffer_load_v4f32(r, (live && ux < uw && uy + 1 < uh) ? off_s : kOOB, 0, 0);
+    t.d = llvm_raw_buffer_load_v4f32(r, ((live && ux + 1 < uw && uy + 1 < uh) ? off_s : kOOB - 16) + 16, 0, 0);
 }
 
 __device__ __forceinline__ f32x4 blend_taps(const TapSet& t) {

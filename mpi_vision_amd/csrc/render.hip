@@ -53,8 +53,10 @@ __device__ __forceinline__ void render_pos(const float* __restrict__ h, float fx
         const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
         float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
         w = (w == 0.0f) ? w + 1e-8f : w;  // divide_safe_torch, utils.py:38
-        const float cx = div_const(div_rn(u, w), g.hm1, g.rc_hm1);  // SWAPPED x / (H-1), utils.py:188
-        const float cy = div_const(div_rn(v, w), g.wm1, g.rc_wm1);  //         y / (W-1)
+        float qu, qv;
+        div2_rn(u, v, w, qu, qv);
+        const float cx = div_const(qu, g.hm1, g.rc_hm1);  // SWAPPED x / (H-1), utils.py:188
+        const float cy = div_const(qv, g.wm1, g.rc_wm1);  //         y / (W-1)
         px = unnormalize(to_grid(cx), g.half_w);
         py = unnormalize(to_grid(cy), g.half_h);
     } else {
