@@ -86,7 +86,8 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     if (V <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
     if (p_begin < 0 || p_end > P || p_begin >= p_end) return fail(MPIV_ERR_ARG, "%s: bad plane range", nm);
     if (!aligned16(packed) || (ct && !aligned16(out))) return fail(MPIV_ERR_ARG, "%s: 16-byte alignment", nm);
-    if ((int64_t)H * W * 16 >= (int64_t)kOOB) return fail(MPIV_ERR_ARG, "%s: plane larger than 2 GiB", nm);
+    if ((int64_t)H * W * 16 >= (int64_t)kOOB || H >= (1 << 22) || W >= (1 << 22))
+        return fail(MPIV_ERR_ARG, "%s: plane larger than 2 GiB or a side >= 2^22", nm);
     const int64_t nblocks = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;
     if (nblocks > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const float4* pk = reinterpret_cast<const float4*>(packed);
@@ -169,7 +170,8 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
     if (!aligned16(img4)) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: img4 must be 16-byte aligned");
     if (out_pstride < (int64_t)D * C || out_pstride > (1 << 30) || out_bstride < (int64_t)Ht * Wt * out_pstride)
         return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: bad output strides");
-    if ((int64_t)Hs * Ws * 16 >= (int64_t)kOOB) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: image > 2 GiB");
+    if ((int64_t)Hs * Ws * 16 >= (int64_t)kOOB || Hs >= (1 << 22) || Ws >= (1 << 22))
+        return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: image > 2 GiB or a side >= 2^22");
     const int64_t per_view = (int64_t)Ht * Wt * D;
     if (B > kMaxGridYZ || per_view >= (1ll << 31)) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: too large");
     const FastDiv fd_d = make_fastdiv((unsigned)D), fd_w = make_fastdiv((unsigned)Wt);

@@ -209,9 +209,9 @@ __device__ __forceinline__ void issue_taps(__amdgpu_buffer_rsrc_t r, int W, int 
     const unsigned ux = (unsigned)(int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)W);
     const unsigned uy = (unsigned)(int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)H);
     const unsigned uw = (unsigned)W, uh = (unsigned)H;
-    // 24-bit multiply-add (full rate): valid taps have uy < H, W < 2^24; the offset
-    // of an invalid tap is never used
-    const int off = (int)__umul24(uy, (unsigned)W) * 16 + (int)ux * 16;
+    // signed 24-bit multiply (full rate): iy in [-2, H] and W < 2^23; iy = -1 must stay
+    // negative because the south taps of that row are valid
+    const int off = __mul24((int)uy, W) * 16 + (int)ux * 16;
     const int off_s = off + W * 16;
     // the +16 of the east taps is applied after the select so it folds into the
     // instruction's immediate offset; kOOB - 16 + 16 is still out of range
