@@ -150,6 +150,15 @@ int mpiv_cam2pixel(const float *cam, const float *proj, int B, int64_t n, float 
 int mpiv_plane_coords(const float *pts, int M, int64_t n, const float *homs, int Ht, int Wt, float *coords,
                       void *stream);
 
+/* ---- frame codec ------------------------------------------------------------ */
+
+/* preprocess_image_torch (utils.py:334-342): out = in*2 - 1, n contiguous floats */
+int mpiv_preprocess(const float *in, int64_t n, float *out, void *stream);
+
+/* deprocess_image_torch (utils.py:344-352): out = uint8(((in+1)/2)*255) with torch's
+ * CPU cast semantics (truncate to int32, keep the low byte; NaN / out of int32 -> 0) */
+int mpiv_deprocess_u8(const float *in, int64_t n, uint8_t *out, void *stream);
+
 /* ---- diagnostics ------------------------------------------------------------ */
 
 /* Exhaustive self-check of the render's launch-constant division (x / (H-1),

@@ -38,6 +38,8 @@ _SIGS = {
     "mpiv_selftest_div_const": [_int, _vp, _vp],
     "mpiv_pad_texels": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_plane_sweep_padded": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
+    "mpiv_preprocess": [_vp, _i64, _vp, _vp],
+    "mpiv_deprocess_u8": [_vp, _i64, _vp, _vp],
     "mpiv_plane_sweep_padded_into": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,
                                      _vp],
 }
@@ -222,6 +224,22 @@ def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.T
     else:
         _call("mpiv_plane_sweep", img, _strides(img), B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out,
               _stream(dev))
+    return out
+
+
+def preprocess(image: torch.Tensor) -> torch.Tensor:
+    dev = _dev(image)
+    src = image.contiguous()
+    out = torch.empty_like(src)
+    _call("mpiv_preprocess", src, src.numel(), out, _stream(dev))
+    return out
+
+
+def deprocess_u8(image: torch.Tensor) -> torch.Tensor:
+    dev = _dev(image)
+    src = image.contiguous()
+    out = torch.empty(src.shape, device=dev, dtype=torch.uint8)
+    _call("mpiv_deprocess_u8", src, src.numel(), out, _stream(dev))
     return out
 
 

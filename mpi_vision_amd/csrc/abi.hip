@@ -273,6 +273,20 @@ int mpiv_plane_coords(const float* pts, int M, int64_t n, const float* homs, int
     return launched("mpiv_plane_coords");
 }
 
+int mpiv_preprocess(const float* in, int64_t n, float* out, void* stream) {
+    if (!in || !out) return fail(MPIV_ERR_ARG, "mpiv_preprocess: null pointer");
+    if (n <= 0) return fail(MPIV_ERR_ARG, "mpiv_preprocess: bad size");
+    preprocess_kernel<<<blocks(n, 256), 256, 0, S(stream)>>>(in, n, out);
+    return launched("mpiv_preprocess");
+}
+
+int mpiv_deprocess_u8(const float* in, int64_t n, uint8_t* out, void* stream) {
+    if (!in || !out) return fail(MPIV_ERR_ARG, "mpiv_deprocess_u8: null pointer");
+    if (n <= 0) return fail(MPIV_ERR_ARG, "mpiv_deprocess_u8: bad size");
+    deprocess_u8_kernel<<<blocks(n, 256), 256, 0, S(stream)>>>(in, n, out);
+    return launched("mpiv_deprocess_u8");
+}
+
 int mpiv_selftest_div_const(int divisor, unsigned long long* mismatches, void* stream) {
     if (!mismatches || divisor < 1) return fail(MPIV_ERR_ARG, "mpiv_selftest_div_const: bad args");
     const float c = (float)divisor;

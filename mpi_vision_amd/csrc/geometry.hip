@@ -99,6 +99,25 @@ __global__ __launch_bounds__(256) void plane_coords_kernel(const float* __restri
     o[1] = div_rn(div_rn(v, w), wm1);
 }
 
+// preprocess_image_torch (utils.py:334-342): x*2 - 1 == one fma (2x is exact)
+__global__ __launch_bounds__(256) void preprocess_kernel(const float* __restrict__ in, int64_t n,
+                                                         float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = __builtin_fmaf(2.0f, in[i], -1.0f);
+}
+
+// deprocess_image_torch (utils.py:344-352): ((x + 1) / 2) * 255 then torch's CPU
+// float -> uint8 cast, which truncates to int32 (cvttss2si: out of range / NaN give
+// INT_MIN) and keeps the low byte.
+__global__ __launch_bounds__(256) void deprocess_u8_kernel(const float* __restrict__ in, int64_t n,
+                                                           uint8_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float v = ((in[i] + 1.0f) * 0.5f) * 255.0f;  // /2 == *0.5 exactly
+    const int q = (__builtin_fabsf(v) < 2147483648.0f) ? (int)v : (int)0x80000000;
+    out[i] = (uint8_t)(q & 0xFF);
+}
+
 // Self-check of div_const (mpiv_common.hpp): every fp32 bit pattern x (a grid-strided
 // sweep of all 2^32) against the IEEE quotient x / c.  Counts mismatches among finite,
 // non-NaN x whose exact quotient matters for a sample position (|x / c| >= 2^-26).

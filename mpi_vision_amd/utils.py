@@ -16,6 +16,8 @@ from __future__ import annotations
 import torch
 
 from . import _host, _lib
+from .camera import (deprocess_image_torch, make_intrinsics_matrix, parse_camera_lines,  # noqa: F401
+                     preprocess_image_torch, read_file_lines, scale_intrinsics)
 
 # The reference keeps a module-level device (utils.py:5).  Every helper reads it
 # at call time, exactly like the reference does.

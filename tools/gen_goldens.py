@@ -197,6 +197,30 @@ def small_cases(ref):
     out.update(fni_ref=ref_img.numpy(), fni_src=src_imgs.numpy(), fni_ref_pose=ref_pose.numpy(),
                fni_src_poses=src_poses.numpy(), fni_K=Kf.numpy(), fni_planes=np.array(planes_f), fni_out=res.numpy())
 
+    # --- camera-path I/O (utils.py:535-598, 689-721): RealEstate10K-style camera file
+    lines = ["https://www.youtube.com/watch?v=abcDEF123_x"]
+    gc = np.random.default_rng(5)
+    for k in range(4):
+        vals = [str(1000000 + 33366 * k)] + [repr(float(v)) for v in gc.uniform(0.3, 0.9, 4)] + ["0.0", "0.0"] + \
+               [repr(float(v)) for v in gc.uniform(-1, 1, 12)]
+        lines.append(" ".join(vals))
+    cam_txt = "\n".join(["# a comment line"] + lines) + "\n"
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as fh:
+        fh.write(cam_txt)
+    read_back = ref.read_file_lines(fh.name)
+    os.unlink(fh.name)
+    parsed = ref.parse_camera_lines(read_back)
+    meta["camera"] = dict(text=cam_txt, read_file_lines=read_back, parsed=parsed)
+    intr = torch.Tensor([[0.5, 0.0, 0.5], [0.0, 0.6, 0.45], [0.0, 0.0, 1.0]])
+    out.update(cam_scaled=ref.scale_intrinsics(intr, 400, 640).numpy(),
+               cam_make=ref.make_intrinsics_matrix(554.25, 560.5, 320.0, 200.0).numpy())
+    gq = torch.Generator().manual_seed(51)
+    out.update(pre_in=torch.rand((2, 5, 6, 3), generator=gq).numpy())
+    out.update(pre_out=ref.preprocess_image_torch(torch.tensor(out["pre_in"])).numpy())
+    dep_in = torch.rand((2, 5, 6, 3), generator=gq) * 2.2 - 1.1
+    out.update(dep_in=dep_in.numpy(), dep_out=ref.deprocess_image_torch(dep_in).numpy())
+
     # --- sampler wrappers -------------------------------------------------------
     gs = torch.Generator().manual_seed(31)
     imgs = torch.rand((2, 3, 20, 25, 4), generator=gs)
