@@ -62,6 +62,11 @@ int mpiv_pack_planes(const float *mpi_view, const int64_t strides[4], int H, int
 int mpiv_render_packed(const float *packed, int H, int W, int P, const float *homs, int V,
                        float *out, void *stream);
 
+/* The same with the direct-gather kernel (no LDS staging): identical output; kept
+ * for A/B measurement and for plane counts beyond the LDS kernel's box table. */
+int mpiv_render_packed_direct(const float *packed, int H, int W, int P, const float *homs, int V,
+                              float *out, void *stream);
+
 /* Plane-range partial for plane sharding: planes [p_begin, p_end)
  * of a packed MPI -> ct [V,H,W,4] = (C rgb, T).  back != 0: the range holds the
  * reference's plane 0 (its alpha ignored, utils.py:152-153) -> T = 0. */

@@ -24,6 +24,7 @@ _SIGS = {
     "mpiv_render": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp],
     "mpiv_pack_planes": [_vp, _c_i64p, _int, _int, _int, _vp, _vp],
     "mpiv_render_packed": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
+    "mpiv_render_packed_direct": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_render_packed_ct": [_vp, _int, _int, _int, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_combine_ct": [_vp, _int, _i64, _vp, _vp],
     "mpiv_plane_sweep": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],

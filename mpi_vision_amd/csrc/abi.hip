@@ -9,6 +9,7 @@
 
 #include "../../include/mpiv.h"
 #include "render.hip"
+#include "render_lds.hip"
 #include "sweep.hip"
 #include "geometry.hip"
 
@@ -80,7 +81,7 @@ int mpiv_pack_planes(const float* mpi, const int64_t st[4], int H, int W, int P,
 }
 
 static int render_packed_impl(const float* packed, int H, int W, int P, int p_begin, int p_end, int back,
-                              const float* homs, int V, float* out, bool ct, void* stream) {
+                              const float* homs, int V, float* out, bool ct, int variant, void* stream) {
     const char* nm = ct ? "mpiv_render_packed_ct" : "mpiv_render_packed";
     if (!packed || !homs || !out) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
     if (V <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
@@ -88,14 +89,25 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     if (!aligned16(packed) || (ct && !aligned16(out))) return fail(MPIV_ERR_ARG, "%s: 16-byte alignment", nm);
     if ((int64_t)H * W * 16 >= (int64_t)kOOB || H >= (1 << 22) || W >= (1 << 22))
         return fail(MPIV_ERR_ARG, "%s: plane larger than 2 GiB or a side >= 2^22", nm);
-    const int64_t nblocks = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;
-    if (nblocks > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const float4* pk = reinterpret_cast<const float4*>(packed);
     const int64_t ps = (int64_t)H * W;
     const RenderGeom g = make_geom(H, W, P);
     const bool fast = H >= 2 && W >= 2;  // div_const needs divisors >= 1
-    const dim3 grid((unsigned)nblocks), blk(256);
     hipStream_t st = S(stream);
+    if (variant == 0 && fast && p_end - p_begin <= kLMaxP) {
+        // default: footprints staged through LDS (render_lds.hip)
+        const int64_t nb = (int64_t)blocks(W, kLTX) * blocks(H, kLTY) * V;
+        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+        const dim3 grid((unsigned)nb), blk(kLThreads);
+        if (ct)
+            render_lds_kernel<true, true><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
+        else
+            render_lds_kernel<false, true><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
+        return launched(nm);
+    }
+    const int64_t nblocks = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;
+    if (nblocks > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+    const dim3 grid((unsigned)nblocks), blk(256);
     if (ct && fast)
         render_packed_kernel<true, true><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
     else if (ct)
@@ -109,12 +121,17 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
 
 int mpiv_render_packed(const float* packed, int H, int W, int P, const float* homs, int V, float* out,
                        void* stream) {
-    return render_packed_impl(packed, H, W, P, 0, P, 1, homs, V, out, false, stream);
+    return render_packed_impl(packed, H, W, P, 0, P, 1, homs, V, out, false, 0, stream);
+}
+
+int mpiv_render_packed_direct(const float* packed, int H, int W, int P, const float* homs, int V, float* out,
+                              void* stream) {
+    return render_packed_impl(packed, H, W, P, 0, P, 1, homs, V, out, false, 1, stream);
 }
 
 int mpiv_render_packed_ct(const float* packed, int H, int W, int P, int p_begin, int p_end, int back,
                           const float* homs, int V, float* ct, void* stream) {
-    return render_packed_impl(packed, H, W, P, p_begin, p_end, back, homs, V, ct, true, stream);
+    return render_packed_impl(packed, H, W, P, p_begin, p_end, back, homs, V, ct, true, 0, stream);
 }
 
 int mpiv_combine_ct(const float* parts, int G, int64_t n, float* out, void* stream) {
