@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Run one render-kernel variant a few times (for rocprofv3 --pmc passes).
+
+    python tools/pmc_render.py --variant lds|direct --views 8 --iters 3
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from mpi_vision_amd import _host, _lib, configs  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--variant", default="lds")
+ap.add_argument("--views", type=int, default=8)
+ap.add_argument("--iters", type=int, default=3)
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+c = configs.config4()
+H, W, P, V = c["H"], c["W"], c["P"], a.views
+g = torch.Generator(device=dev).manual_seed(0)
+packed = torch.rand((P, H, W, 4), generator=g, device=dev)
+homs = _host.render_homographies(configs.f32(c["poses"][:V]), configs.f32(c["depths"]),
+                                 configs.f32([c["K"]] * V), V).to(dev)
+out = torch.empty((V, H, W, 3), device=dev)
+name = "mpiv_render_packed" if a.variant == "lds" else "mpiv_render_packed_direct"
+for _ in range(a.iters):
+    _lib._call(name, packed, H, W, P, homs, V, out, _lib._stream(dev))
+torch.cuda.synchronize()
+print("done", a.variant, V)
