@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--views", type=int, default=125, help="views rendered per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
-    ap.add_argument("--kernel", choices=["packed", "native"], default="packed")
+    ap.add_argument("--kernel", choices=["packed", "packed_lds", "native"], default="packed")
     return ap.parse_args()
 
 
@@ -132,7 +132,8 @@ def main():
     view[:, :, 0, 3] = 1.0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    packed = _lib.pack_planes(view) if args.kernel == "packed" else None
+    packed = _lib.pack_planes(view) if args.kernel.startswith("packed") else None
+    entry = "mpiv_render_packed_lds" if args.kernel == "packed_lds" else "mpiv_render_packed"
     torch.cuda.synchronize()
     pack_ms = (time.perf_counter() - t0) * 1e3
     mpi5 = view.unsqueeze(0).expand(V, H, W, P, 4)
@@ -155,8 +156,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def launch(s, h_dev):
-        if args.kernel == "packed":
-            _lib._call("mpiv_render_packed", packed, H, W, P, h_dev, V, out,
+        if args.kernel.startswith("packed"):
+            _lib._call(entry, packed, H, W, P, h_dev, V, out,
                        _lib._stream(dev))
         else:
             _lib._call("mpiv_render", mpi5, _lib._strides(mpi5), V, H, W, P, h_dev,
@@ -217,7 +218,8 @@ def main():
                        "views_per_s": round(value / (H * W / 1e6), 2), "pack_ms_once": round(pack_ms, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "render_packed_kernel" if args.kernel == "packed" else "render_native_kernel",
+                         "kernel": {"packed": "render_packed_kernel", "packed_lds": "render_lds_kernel"}.get(
+                             args.kernel, "render_native_kernel"),
                          "kernel_ms_per_launch": round(kern_ms, 3),
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": None,
@@ -225,9 +227,9 @@ def main():
         if world == 1 and args.cpu_seconds > 0:
             # the GPU frames of the first views of step 0, to cross-check the CPU sample bit-exactly
             hs = host_homs(0)
-            _lib._call("mpiv_render_packed" if args.kernel == "packed" else "mpiv_render",
+            _lib._call(entry if packed is not None else "mpiv_render",
                        *([packed, H, W, P, hs[:1].to(dev), 1, out, _lib._stream(dev)]
-                         if args.kernel == "packed" else
+                         if packed is not None else
                          [mpi5[:1], _lib._strides(mpi5[:1]), 1, H, W, P, hs[:1].to(dev),
                           out, _lib._stream(dev)]))
             torch.cuda.synchronize()

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 1
+#define MPIV_ABI_VERSION 2
 
 enum {
     MPIV_OK = 0,
@@ -51,21 +51,24 @@ int mpiv_render(const float *mpi, const int64_t mpi_strides[5], int B, int H, in
                 const float *homs, float *out, void *stream);
 
 /* Layout pack for repeated rendering of one MPI: one view [H,W,P,4] (element
- * strides strides[4] = H,W,P,C) -> plane-major packed [P][H][W][4] (16-B aligned,
- * contiguous).  No reference counterpart (the reference re-materialises the
- * plane-major copy on every call, utils.py:121). */
+ * strides strides[4] = H,W,P,C) -> plane-major packed [P][H+4][W+4][4] (16-B
+ * aligned, contiguous) with a 2-texel zero border around every plane; image texel
+ * (x, y) of plane p is packed[p][y+2][x+2].  The border is grid_sample's zero
+ * padding made explicit, so the render kernels need no per-tap range test.  No
+ * reference counterpart (the reference re-materialises a plane-major copy on every
+ * call, utils.py:121). */
 int mpiv_pack_planes(const float *mpi_view, const int64_t strides[4], int H, int W, int P,
                      float *packed, void *stream);
 
-/* mpi_render_view_torch on a packed MPI for V views at once.
+/* mpi_render_view_torch on a packed MPI (mpiv_pack_planes layout) for V views at once.
  * homs [V][P][9]; out [V,H,W,3] contiguous. */
 int mpiv_render_packed(const float *packed, int H, int W, int P, const float *homs, int V,
                        float *out, void *stream);
 
-/* The same with the direct-gather kernel (no LDS staging): identical output; kept
- * for A/B measurement and for plane counts beyond the LDS kernel's box table. */
-int mpiv_render_packed_direct(const float *packed, int H, int W, int P, const float *homs, int V,
-                              float *out, void *stream);
+/* The same with the LDS-staged kernel (per-tile plane footprints staged by LDS-DMA):
+ * identical output; kept for A/B measurement. */
+int mpiv_render_packed_lds(const float *packed, int H, int W, int P, const float *homs, int V,
+                           float *out, void *stream);
 
 /* Plane-range partial for plane sharding: planes [p_begin, p_end)
  * of a packed MPI -> ct [V,H,W,4] = (C rgb, T).  back != 0: the range holds the

@@ -24,7 +24,7 @@ _SIGS = {
     "mpiv_render": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp],
     "mpiv_pack_planes": [_vp, _c_i64p, _int, _int, _int, _vp, _vp],
     "mpiv_render_packed": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
-    "mpiv_render_packed_direct": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
+    "mpiv_render_packed_lds": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_render_packed_ct": [_vp, _int, _int, _int, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_combine_ct": [_vp, _int, _i64, _vp, _vp],
     "mpiv_plane_sweep": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
@@ -45,7 +45,7 @@ _SIGS = {
                                      _vp],
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib = None
 
@@ -125,21 +125,42 @@ def _p(t: torch.Tensor):
 # render
 # ---------------------------------------------------------------------------
 
-def pack_planes(view: torch.Tensor) -> torch.Tensor:
-    """One MPI view [H, W, P, 4] (any strides) -> packed plane-major [P, H, W, 4]."""
+PAD = 2  # zero-border texels around every packed plane (include/mpiv.h)
+
+
+def packed_shape(H: int, W: int, P: int):
+    return (P, H + 2 * PAD, W + 2 * PAD, 4)
+
+
+def packed_hw(packed: torch.Tensor):
+    """(P, H, W) of a packed MPI [P, H+4, W+4, 4]."""
+    if packed.dim() != 4 or packed.shape[-1] != 4 or not packed.is_contiguous():
+        raise RuntimeError(f"packed MPI must be a contiguous [P, H+4, W+4, 4] tensor, got {tuple(packed.shape)}")
+    return packed.shape[0], packed.shape[1] - 2 * PAD, packed.shape[2] - 2 * PAD
+
+
+def pack_planes(view: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """One MPI view [H, W, P, 4] (any strides) -> packed plane-major [P, H+4, W+4, 4]
+    with a 2-texel zero border (image texel (x, y) of plane p at [p, y+2, x+2])."""
     dev = _dev(view)
     H, W, P, C = view.shape
     if C != 4:
         raise RuntimeError(f"MPI texels must have 4 channels (RGBA), got {C}")
-    packed = torch.empty((P, H, W, 4), device=dev, dtype=torch.float32)
+    packed = torch.empty(packed_shape(H, W, P), device=dev, dtype=torch.float32) if out is None else out
     _call("mpiv_pack_planes", view, _strides(view), H, W, P, packed, _stream(dev))
     return packed
 
 
+def unpack_planes(packed: torch.Tensor) -> torch.Tensor:
+    """Inverse view of pack_planes: [P, H+4, W+4, 4] -> [H, W, P, 4] (a strided view)."""
+    P, H, W = packed_hw(packed)
+    return packed[:, PAD:PAD + H, PAD:PAD + W].permute(1, 2, 0, 3)
+
+
 def render_packed(packed: torch.Tensor, homs: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """packed [P,H,W,4] + homs [V,P,9] (host or device) -> [V,H,W,3]."""
+    """packed [P,H+4,W+4,4] + homs [V,P,9] (host or device) -> [V,H,W,3]."""
     dev = _dev(packed)
-    P, H, W, _ = packed.shape
+    P, H, W = packed_hw(packed)
     V = homs.shape[0]
     h = _up(homs.reshape(V, P, 9), dev)
     if out is None:
@@ -152,7 +173,7 @@ def render_packed_ct(packed: torch.Tensor, homs: torch.Tensor, back: bool, p_beg
                      p_end: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """Plane-range partial (C, T) [V,H,W,4] for plane sharding."""
     dev = _dev(packed)
-    P, H, W, _ = packed.shape
+    P, H, W = packed_hw(packed)
     p_end = P if p_end is None else p_end
     V = homs.shape[0]
     h = _up(homs.reshape(V, P, 9), dev)
@@ -190,11 +211,11 @@ def render(rgba_layers: torch.Tensor, homs: torch.Tensor) -> torch.Tensor:
         return render_packed(pack_planes(rgba_layers[0]), homs)
     h = _up(homs, dev)
     out = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32)
-    if RENDER_POLICY == "pack" or (RENDER_POLICY == "auto" and P >= 8 and H * W * 16 < 0x7FFFFF00):
+    if RENDER_POLICY == "pack" or (RENDER_POLICY == "auto" and P >= 8 and (H + 4) * (W + 4) * 16 < 0x7FFFFF00):
         # per view: pack its MPI plane-major (one coalesced transpose pass) and render
         # from the packed copy -- the gathers of the in-place layout touch one 128-B
         # line per 16-B texel, which is slower than paying the pack
-        packed = torch.empty((P, H, W, 4), device=dev, dtype=torch.float32)
+        packed = torch.empty(packed_shape(H, W, P), device=dev, dtype=torch.float32)
         for b in range(B):
             _call("mpiv_pack_planes", rgba_layers[b], _strides(rgba_layers[b]), H, W, P, packed, _stream(dev))
             _call("mpiv_render_packed", packed, H, W, P, h[b:b + 1], 1, out[b:b + 1], _stream(dev))

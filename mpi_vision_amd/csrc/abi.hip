@@ -71,15 +71,18 @@ int mpiv_pack_planes(const float* mpi, const int64_t st[4], int H, int W, int P,
     if (!mpi || !st || !packed) return fail(MPIV_ERR_ARG, "mpiv_pack_planes: null pointer");
     if (H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "mpiv_pack_planes: bad shape");
     if (!aligned16(packed)) return fail(MPIV_ERR_ARG, "mpiv_pack_planes: packed must be 16-byte aligned");
-    const int64_t npix = (int64_t)H * W;
-    if (blocks(P, kPackPl) > kMaxGridYZ || (npix + kPackPix - 1) / kPackPix > kMaxGridX)
-        return fail(MPIV_ERR_ARG, "mpiv_pack_planes: too large");
+    if ((int64_t)(H + 2 * kPad) * (W + 2 * kPad) * 16 >= (int64_t)kOOB)
+        return fail(MPIV_ERR_ARG, "mpiv_pack_planes: padded plane larger than 2 GiB");
+    const int64_t npix = (int64_t)(H + 2 * kPad) * (W + 2 * kPad);
+    if (blocks(P, kPackPl) > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_pack_planes: too many planes");
     const NativeStrides s{0, st[0], st[1], st[2], st[3]};
     dim3 grid(blocks(npix, kPackPix), blocks(P, kPackPl), 1);
-    pack_planes_kernel<<<grid, 256, 0, S(stream)>>>(mpi, s, H, W, P, reinterpret_cast<float4*>(packed), npix);
+    pack_planes_kernel<<<grid, 256, 0, S(stream)>>>(mpi, s, H, W, P, make_fastdiv((unsigned)(W + 2 * kPad)),
+                                                    reinterpret_cast<float4*>(packed), npix);
     return launched("mpiv_pack_planes");
 }
 
+// variant 0: direct gathers (render_packed_kernel, the default); 1: LDS-staged footprints
 static int render_packed_impl(const float* packed, int H, int W, int P, int p_begin, int p_end, int back,
                               const float* homs, int V, float* out, bool ct, int variant, void* stream) {
     const char* nm = ct ? "mpiv_render_packed_ct" : "mpiv_render_packed";
@@ -87,15 +90,15 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     if (V <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
     if (p_begin < 0 || p_end > P || p_begin >= p_end) return fail(MPIV_ERR_ARG, "%s: bad plane range", nm);
     if (!aligned16(packed) || (ct && !aligned16(out))) return fail(MPIV_ERR_ARG, "%s: 16-byte alignment", nm);
-    if ((int64_t)H * W * 16 >= (int64_t)kOOB || H >= (1 << 22) || W >= (1 << 22))
-        return fail(MPIV_ERR_ARG, "%s: plane larger than 2 GiB or a side >= 2^22", nm);
+    if ((int64_t)(H + 2 * kPad) * (W + 2 * kPad) * 16 >= (int64_t)kOOB || H >= (1 << 22) || W >= (1 << 22))
+        return fail(MPIV_ERR_ARG, "%s: padded plane larger than 2 GiB or a side >= 2^22", nm);
     const float4* pk = reinterpret_cast<const float4*>(packed);
-    const int64_t ps = (int64_t)H * W;
+    const int64_t ps = (int64_t)(H + 2 * kPad) * (W + 2 * kPad);
     const RenderGeom g = make_geom(H, W, P);
     const bool fast = H >= 2 && W >= 2;  // div_const needs divisors >= 1
     hipStream_t st = S(stream);
-    if (variant == 0 && fast && p_end - p_begin <= kLMaxP) {
-        // default: footprints staged through LDS (render_lds.hip)
+    if (variant == 1 && fast && p_end - p_begin <= kLMaxP) {
+        // footprints staged through LDS (render_lds.hip)
         const int64_t nb = (int64_t)blocks(W, kLTX) * blocks(H, kLTY) * V;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
         const dim3 grid((unsigned)nb), blk(kLThreads);
@@ -124,8 +127,8 @@ int mpiv_render_packed(const float* packed, int H, int W, int P, const float* ho
     return render_packed_impl(packed, H, W, P, 0, P, 1, homs, V, out, false, 0, stream);
 }
 
-int mpiv_render_packed_direct(const float* packed, int H, int W, int P, const float* homs, int V, float* out,
-                              void* stream) {
+int mpiv_render_packed_lds(const float* packed, int H, int W, int P, const float* homs, int V, float* out,
+                           void* stream) {
     return render_packed_impl(packed, H, W, P, 0, P, 1, homs, V, out, false, 1, stream);
 }
 

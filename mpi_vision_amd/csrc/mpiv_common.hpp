@@ -65,18 +65,17 @@ __host__ __device__ __forceinline__ unsigned fast_div(unsigned n, const FastDiv&
 __device__ __forceinline__ float div_rn(float a, float b) { return a / b; }
 
 // Correctly rounded x / c for a launch-uniform divisor c >= 1, given rc = RN(1/c)
-// (computed on the host as 1.0f / c).  This is the core of the hardware IEEE division
-// sequence (q = a*y; two residual corrections r = fma(-b, q, a), q = fma(r, y, q)) with
-// the per-element v_rcp + Newton step replaced by the exactly rounded reciprocal and
-// v_div_scale / v_div_fixup dropped: those only act when |x| or the quotient leaves
-// the normal range, and there (|x / c| < 2^-26, or x = +-inf) the quotient cannot
-// change the sample position: -1 + 2*cx rounds to -1 for any |cx| < 2^-26, and an
-// infinite coordinate yields NaN weights either way.  5 VALU instead of 11.
+// (computed on the host as 1.0f / c): q = RN(x*rc) is faithful, its residual
+// r = fma(-c, q, x) is exact, and one correction fma(r, rc, q) then rounds to RN(x/c)
+// (Markstein's theorem for a correctly rounded reciprocal).  v_div_scale / v_div_fixup
+// are not needed: they only act when |x| or the quotient leaves the normal range, and
+// there (|x / c| < 2^-26, or x = +-inf) the quotient cannot change the sample position:
+// -1 + 2*cx rounds to -1 for any |cx| < 2^-26, and an infinite coordinate yields NaN
+// weights either way.  Checked against IEEE division for all 2^32 inputs and the
+// divisors of tests/test_render_gpu.py::test_div_const_exhaustive.  3 VALU instead of 11.
 __device__ __forceinline__ float div_const(float x, float c, float rc) {
-    float q = x * rc;
-    float r = __builtin_fmaf(-c, q, x);
-    q = __builtin_fmaf(r, rc, q);
-    r = __builtin_fmaf(-c, q, x);
+    const float q = x * rc;
+    const float r = __builtin_fmaf(-c, q, x);
     return __builtin_fmaf(r, rc, q);
 }
 
@@ -95,16 +94,35 @@ __device__ __forceinline__ float div_core(float a, float b, float y) {
     return __builtin_fmaf(r, y, q);
 }
 
-__device__ __forceinline__ void div2_rn(float u, float v, float w, float& qu, float& qv) {
+__device__ __forceinline__ bool div2_safe(float u, float v, float w) {
     const float aw = __builtin_fabsf(w);
-    const bool safe = aw >= 0x1p-60f && aw <= 0x1p60f && __builtin_fmaxf(__builtin_fabsf(u), __builtin_fabsf(v)) <= 0x1p60f;
-    if (__builtin_expect(safe, 1)) {
+    return aw >= 0x1p-60f && aw <= 0x1p60f && __builtin_fmaxf(__builtin_fabsf(u), __builtin_fabsf(v)) <= 0x1p60f;
+}
+
+__device__ __forceinline__ void div2_rn(float u, float v, float w, float& qu, float& qv) {
+    if (__builtin_expect(div2_safe(u, v, w), 1)) {
         float y = __builtin_amdgcn_rcpf(w);
         const float e = __builtin_fmaf(-w, y, 1.0f);
         y = __builtin_fmaf(e, y, y);
         qu = div_core(u, w, y);
         qv = div_core(v, w, y);
     } else {
+        qu = div_rn(u, w);
+        qv = div_rn(v, w);
+    }
+}
+
+// divide_safe_torch (utils.py:35-39) fused with div2_rn: w == 0 -> w + 1e-8, then u/w, v/w.
+// The guard lives in the rare branch only: w == 0 fails div2_safe.
+__device__ __forceinline__ void divide_safe2(float u, float v, float w, float& qu, float& qv) {
+    if (__builtin_expect(div2_safe(u, v, w), 1)) {
+        float y = __builtin_amdgcn_rcpf(w);
+        const float e = __builtin_fmaf(-w, y, 1.0f);
+        y = __builtin_fmaf(e, y, y);
+        qu = div_core(u, w, y);
+        qv = div_core(v, w, y);
+    } else {
+        w = (w == 0.0f) ? w + 1e-8f : w;  // utils.py:38
         qu = div_rn(u, w);
         qv = div_rn(v, w);
     }
@@ -219,6 +237,35 @@ __device__ __forceinline__ void issue_taps(__amdgpu_buffer_rsrc_t r, int W, int 
     t.b = llvm_raw_buffer_load_v4f32(r, ((live && ux + 1 < uw && uy < uh) ? off : kOOB - 16) + 16, 0, 0);
     t.c = llvm_raw_buffer_load_v4f32(r, (live && ux < uw && uy + 1 < uh) ? off_s : kOOB, 0, 0);
     t.d = llvm_raw_buffer_load_v4f32(r, ((live && ux + 1 < uw && uy + 1 < uh) ? off_s : kOOB - 16) + 16, 0, 0);
+}
+
+// Packed planes carry a kPad-texel zero border: plane p is [(H + 4)][(W + 4)] float4 and
+// image texel (x, y) sits at ((y + 2) * Wp + x + 2), Wp = W + 4.  Clamping floor(px) into
+// [-2, W] and floor(py) into [-2, H] keeps every tap of a sample inside the padded plane,
+// and a clamped tap lands in the border exactly when the true tap is outside the image
+// (both taps of an axis are outside whenever the clamp moved it), so the zeros padding
+// of grid_sample needs no per-tap test: 6 VALU of address math for the four taps.
+constexpr int kPad = 2;
+
+// org = byte offset of image texel (0, 0) in the padded plane; row = Wp * 16.
+__device__ __forceinline__ void issue_taps_padded(__amdgpu_buffer_rsrc_t r, int W, int H, int Wp, int org,
+                                                  int row, float px, float py, TapSet& t) {
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
+    // med3 also maps NaN to a bound, so the index is always defined (the NaN weights
+    // still make the sample NaN, as in the reference)
+    const int cx = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)W);
+    const int cy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)H);
+    const int off = (__mul24(cy, Wp) + cx) * 16 + org;  // >= 0, < plane bytes
+    t.a = llvm_raw_buffer_load_v4f32(r, off, 0, 0);
+    t.b = llvm_raw_buffer_load_v4f32(r, off + 16, 0, 0);
+    t.c = llvm_raw_buffer_load_v4f32(r, off, row, 0);
+    t.d = llvm_raw_buffer_load_v4f32(r, off + 16, row, 0);
 }
 
 __device__ __forceinline__ f32x4 blend_taps(const TapSet& t) {

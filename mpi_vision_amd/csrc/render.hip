@@ -11,10 +11,12 @@
 // Two texel layouts:
 //  * native  -- the reference's [B,H,W,P,4] tensor, any strides (incl. a stride-0
 //               broadcast batch); 4 texel channels are gathered per tap.
-//  * packed  -- plane-major [P][H][W] float4 (mpiv_pack_planes).  A wave's 64
-//               pixels are one output row, so each of the 4 bilinear taps is one
-//               16-B-per-lane load over ~1 KiB of consecutive texels of ONE plane:
-//               full 128-B lines, reused by the NE/SE taps and the next row's wave.
+//  * packed  -- plane-major [P][H+4][W+4] float4 with a 2-texel zero border
+//               (mpiv_pack_planes).  A wave's 64 pixels are one output row, so each
+//               of the 4 bilinear taps is one 16-B-per-lane load over ~1 KiB of
+//               consecutive texels of ONE plane: full 128-B lines, reused by the
+//               NE/SE taps and the next row's wave.  The border makes grid_sample's
+//               zero padding free (issue_taps_padded: no per-tap range test).
 #include "mpiv_common.hpp"
 
 namespace mpiv {
@@ -24,7 +26,10 @@ constexpr int kTileY = 4;   // 4 waves per 256-thread block
 
 struct RenderGeom {
     int H, W, P;
-    int plane_bytes;            // H*W*16 (< 2 GiB, checked on the host)
+    int Wp;                     // padded row pitch W + 4 (texels)
+    int org;                    // byte offset of texel (0, 0) in a padded plane
+    int row;                    // Wp * 16
+    int plane_bytes;            // (H+4)*(W+4)*16 (< 2 GiB, checked on the host)
     float hm1, wm1;             // H-1, W-1: the reference's (swapped) normalisers
     float rc_hm1, rc_wm1;       // RN(1/(H-1)), RN(1/(W-1)) for div_const
     float half_w, half_h;       // grid_sample unnormalise scales W/2, H/2
@@ -33,7 +38,10 @@ struct RenderGeom {
 inline RenderGeom make_geom(int H, int W, int P) {
     RenderGeom g;
     g.H = H; g.W = W; g.P = P;
-    g.plane_bytes = (int)((int64_t)H * W * 16);
+    g.Wp = W + 2 * kPad;
+    g.row = g.Wp * 16;
+    g.org = (kPad * g.Wp + kPad) * 16;
+    g.plane_bytes = (int)((int64_t)(H + 2 * kPad) * g.Wp * 16);
     g.hm1 = (float)(H - 1);
     g.wm1 = (float)(W - 1);
     g.rc_hm1 = 1.0f / g.hm1;
@@ -51,10 +59,9 @@ __device__ __forceinline__ void render_pos(const float* __restrict__ h, float fx
     if (FAST) {
         const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
         const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
-        float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
-        w = (w == 0.0f) ? w + 1e-8f : w;  // divide_safe_torch, utils.py:38
+        const float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
         float qu, qv;
-        div2_rn(u, v, w, qu, qv);
+        divide_safe2(u, v, w, qu, qv);  // divide_safe_torch, utils.py:35-39
         const float cx = div_const(qu, g.hm1, g.rc_hm1);  // SWAPPED x / (H-1), utils.py:188
         const float cy = div_const(qv, g.wm1, g.rc_wm1);  //         y / (W-1)
         px = unnormalize(to_grid(cx), g.half_w);
@@ -112,14 +119,15 @@ __global__ __launch_bounds__(256) void render_packed_kernel(const float4* __rest
     float cr = -0.0f, cg = -0.0f, cb = -0.0f, t = 1.0f;
     const bool replace_first = !CT || back;
     const int last = p_end - 1;
-    // plane p's taps; past the range the loads are issued with OOB offsets (no memory
-    // traffic, result unused) so every iteration issues unconditionally and the
-    // compiler can count vmcnt exactly
+    // plane p's taps; past the range the last plane is re-issued (L2-hot, result
+    // unused) so every iteration issues unconditionally and the compiler can count
+    // vmcnt exactly
     auto issue = [&](int p, TapSet& ts) {
         const int q = p < last ? p : last;
         float px, py;
         render_pos<FAST>(hv + (int64_t)q * 9, fx, fy, g, px, py);
-        issue_taps(make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes), g.W, g.H, px, py, p <= last, ts);
+        issue_taps_padded(make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes), g.W, g.H, g.Wp, g.org,
+                          g.row, px, py, ts);
     };
     auto consume = [&](const TapSet& ts, bool first) {
         const f32x4 s = blend_taps(ts);
@@ -223,20 +231,20 @@ __global__ __launch_bounds__(256) void render_native_kernel(const float* __restr
 }
 
 // ---------------------------------------------------------------------------
-// layout pack: one view of [H,W,P,C=4] (any strides) -> [P][H][W] float4
-// A block moves 64 pixels x 16 planes through LDS so both sides are coalesced:
-// reads are 16 planes x 16 B = 256 B per pixel, writes 64 pixels x 16 B = 1 KiB
-// per plane.
+// layout pack: one view of [H,W,P,C=4] (any strides) -> [P][H+4][W+4] float4 with a
+// 2-texel zero border.  A block moves 64 padded pixels x 16 planes through LDS so both
+// sides are coalesced: reads are 16 planes x 16 B = 256 B per pixel, writes 64 pixels
+// x 16 B = 1 KiB per plane; border pixels are written as zeros.
 // ---------------------------------------------------------------------------
 
 constexpr int kPackPix = 64;
 constexpr int kPackPl = 16;
 
 __global__ __launch_bounds__(256) void pack_planes_kernel(const float* __restrict__ mpi, NativeStrides s,
-                                                          int H, int W, int P, float4* __restrict__ packed,
-                                                          int64_t plane_stride) {
+                                                          int H, int W, int P, FastDiv wp_div,
+                                                          float4* __restrict__ packed, int64_t plane_stride) {
     __shared__ float4 tile[kPackPl][kPackPix + 1];
-    const int64_t npix = (int64_t)H * W;
+    const int64_t npix = plane_stride;  // (H+4)*(W+4) < 2^27
     const int64_t pix0 = (int64_t)blockIdx.x * kPackPix;
     const int p0 = blockIdx.y * kPackPl;
     // load: thread -> (pixel i, plane j), plane fastest
@@ -246,12 +254,15 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const float* __restric
         const int p = p0 + j;
         float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
         if (pix < npix && p < P) {
-            const int yy = (int)(pix / W), xx = (int)(pix % W);
-            const float* src = mpi + (int64_t)yy * s.y + (int64_t)xx * s.x + (int64_t)p * s.p;
-            if (s.c == 1 && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
-                val = *reinterpret_cast<const float4*>(src);
-            } else {
-                val = make_float4(src[0], src[s.c], src[2 * s.c], src[3 * s.c]);
+            const int yp = (int)fast_div((unsigned)pix, wp_div);
+            const int yy = yp - kPad, xx = (int)pix - yp * (int)wp_div.d - kPad;
+            if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
+                const float* src = mpi + (int64_t)yy * s.y + (int64_t)xx * s.x + (int64_t)p * s.p;
+                if (s.c == 1 && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
+                    val = *reinterpret_cast<const float4*>(src);
+                } else {
+                    val = make_float4(src[0], src[s.c], src[2 * s.c], src[3 * s.c]);
+                }
             }
         }
         tile[j][i] = val;

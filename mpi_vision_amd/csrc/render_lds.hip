@@ -1,13 +1,12 @@
 // render_lds.hip -- the fused warp + over-composite with plane texels staged through
-// LDS (the default packed-layout render on gfx950).
+// LDS (A/B variant of the packed-layout render on gfx950, mpiv_render_packed_lds).
 //
 // Why: the direct kernel (render.hip) gathers four 16-B taps per plane-pixel through
 // the vector L1 (64 B per plane-pixel); at ~64 B/clk/CU that data path, not HBM or
-// VALU, bounds it (measured 524 G plane-pixel/s = 62 B/clk/CU).  Here each block
-// stages the source footprint of its output tile once per plane -- with LDS-DMA
-// (buffer_load ... lds: no VGPRs, coalesced 1-KiB rows) -- and the taps become
-// ds_read_b128s.  The footprint of a 64x8 tile is ~66x10 texels, so the L1/L2 traffic
-// drops ~2.5x and the kernel becomes VALU-bound.
+// VALU, bounds it (measured 547 G plane-pixel/s = 57-65 B/clk/CU).  Here each block
+// stages the source footprint of its output tile once per plane (coalesced 1-KiB
+// rows through registers) and the taps become ds_read_b128s.  The footprint of a
+// 64x8 tile is ~66x10 texels, so the L1/L2 traffic drops ~2.5x.
 //
 // Per block (512 threads = 8 waves, one 64-pixel output row per wave):
 //  1. prologue: every (plane, tile-corner) pair is pushed through the exact
@@ -18,11 +17,13 @@
 //     pixels land within one texel of the corner box: the margin covers them.
 //     Planes whose w changes sign over the tile, whose positions are non-finite, or
 //     whose box does not fit the staging buffer are rendered "direct" (global taps).
-//  2. loop over planes with two LDS buffers: plane p+1's footprint is DMA'd while
-//     plane p is composited; one s_waitcnt vmcnt(0) + barrier per plane.
-// Texels outside the image are loaded as zeros (out-of-range buffer offsets), and tap
-// indices are clamped into the box, whose clipped border columns/rows are zero, so
-// the LDS path needs no per-tap validity test: grid_sample's zero padding falls out.
+//  2. loop over planes with two LDS buffers: plane p+1's footprint is loaded into
+//     registers while plane p is composited, then written to the other buffer; one
+//     barrier per plane.
+// Boxes are clipped to the packed planes' 2-texel zero border ([-2, W+1] x [-2, H+1]),
+// so every staged texel is real memory and texels outside the image stage as zeros;
+// tap indices are clamped into the box, so the LDS path needs no per-tap validity
+// test: grid_sample's zero padding falls out.
 #include "mpiv_common.hpp"
 
 namespace mpiv {
@@ -102,32 +103,42 @@ __global__ __launch_bounds__(kLThreads, 8) void render_lds_kernel(const float4* 
     __syncthreads();
     const int pitch = s_pitch;  // common row pitch of the staged footprints
 
-    // this thread's share of the DMA: footprint texels (wave + 8*j)*64 + lane, j = 0, 1
-    int row_j[2], col_j[2];
+    // this thread's share of a footprint: texels (wave + 8*j)*64 + lane, j = 0, 1, as
+    // offsets (in texels) from the box origin in the padded plane
+    int rel_j[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int idx = (wave + kLTY * j) * kWave + lane;
-        row_j[j] = pitch > 0 ? idx / pitch : 0;
-        col_j[j] = idx - row_j[j] * pitch;
+        const int row = pitch > 0 ? idx / pitch : 0;
+        rel_j[j] = row * g.Wp + (idx - row * pitch);
     }
 
     auto lds_mode = [&](const int4& bx) { return bx.w == 0 && bx.z * pitch <= kLCap; };
 
-    auto stage = [&](int pl, int buf) {
-        const int4 bx = s_box[pl - p_begin];
-        if (!lds_mode(bx)) return;
-        const int nfp = bx.z * pitch;
+    // Register staging: plane p+1's footprint is loaded into registers at the top of
+    // iteration p and written to the other LDS buffer after plane p is composited, so
+    // its load latency hides behind a whole plane of work.  (LDS-DMA would skip the
+    // registers, but hipcc cannot tell which LDS bytes a buffer_load ... lds writes
+    // and drains it with vmcnt(0) before every ds_read, serialising the pipeline.)
+    // Lanes past the footprint may run off the plane: the buffer range check returns
+    // zeros for them and their LDS slots are never read.
+    f32x4 stg[2];
+    auto fetch = [&](int pl, const int4& bx) {
         const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)pl * plane_stride, g.plane_bytes);
+        const int box_org = (bx.y + kPad) * g.Wp + bx.x + kPad;  // >= 0: boxes start at -2
+        const int nfp = bx.z * pitch;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int base = (wave + kLTY * j) * kWave;  // wave-uniform
-            if (base < nfp) {
-                const int gx = bx.x + col_j[j], gy = bx.y + row_j[j];
-                const bool in = (unsigned)gx < (unsigned)g.W && (unsigned)gy < (unsigned)g.H;
-                const int off = in ? (__mul24(gy, g.W) + gx) * 16 : kOOB;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    r, (__attribute__((address_space(3))) void*)&s_tex[buf][base], 16, off, 0, 0, 0);
-            }
+            if (base < nfp) stg[j] = llvm_raw_buffer_load_v4f32(r, (box_org + rel_j[j]) * 16, 0, 0);
+        }
+    };
+    auto commit = [&](int buf, const int4& bx) {
+        const int nfp = bx.z * pitch;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int base = (wave + kLTY * j) * kWave;
+            if (base < nfp) *reinterpret_cast<f32x4*>(&s_tex[buf][base + lane]) = stg[j];
         }
     };
 
@@ -135,13 +146,20 @@ __global__ __launch_bounds__(kLThreads, 8) void render_lds_kernel(const float4* 
     float cr = -0.0f, cg = -0.0f, cb = -0.0f, t = 1.0f;
     const bool replace_first = !CT || back;
 
-    stage(p_begin, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int4 bx_next = s_box[0];
+    if (lds_mode(bx_next)) {
+        fetch(p_begin, bx_next);
+        commit(0, bx_next);
+    }
     __syncthreads();
     for (int p = p_begin; p < p_end; ++p) {
         const int buf = (p - p_begin) & 1;
-        if (p + 1 < p_end) stage(p + 1, buf ^ 1);
-        const int4 bx = s_box[p - p_begin];
+        const int4 bx = bx_next;
+        const bool more = p + 1 < p_end;
+        if (more) {
+            bx_next = s_box[p + 1 - p_begin];
+            if (lds_mode(bx_next)) fetch(p + 1, bx_next);
+        }
         if (active) {
             float px, py;
             render_pos<FAST>(hv + (int64_t)p * 9, fx, fy, g, px, py);
@@ -155,18 +173,29 @@ __global__ __launch_bounds__(kLThreads, 8) void render_lds_kernel(const float4* 
                 ts.ne = sy * wx;
                 ts.sw = wy * ex;
                 ts.se = wy * wx;
-                const int ix = (int)__builtin_amdgcn_fmed3f(fx0, (float)bx.x, (float)(bx.x + pitch - 2));
-                const int iy = (int)__builtin_amdgcn_fmed3f(fy0, (float)bx.y, (float)(bx.y + bx.z - 2));
-                const float4* st = &s_tex[buf][(iy - bx.y) * pitch + (ix - bx.x)];
+                // clamp into the box; past the image (x > W) the clamp stops at W so the
+                // taps land in the zero border, never in staged columns that wrapped
+                // into the next padded row
+                const float ix = __builtin_amdgcn_fmed3f(fx0, (float)bx.x, (float)min(bx.x + pitch - 2, g.W));
+                const float iy = __builtin_amdgcn_fmed3f(fy0, (float)bx.y, (float)(bx.y + bx.z - 2));
+                // (iy - y_lo) * pitch + (ix - x_lo), exact in fp32 (|values| < 2^24)
+                const int li = (int)(__builtin_fmaf(iy, (float)pitch, ix) - (float)(bx.y * pitch + bx.x));
+                const float4* st = &s_tex[buf][li];
                 ts.a = *reinterpret_cast<const f32x4*>(st);
                 ts.b = *reinterpret_cast<const f32x4*>(st + 1);
                 ts.c = *reinterpret_cast<const f32x4*>(st + pitch);
                 ts.d = *reinterpret_cast<const f32x4*>(st + pitch + 1);
                 s = blend_taps(ts);
+                // pin the blend inside this branch: if it sinks below the join, the two
+                // paths' tap registers merge and hipcc drains vmcnt (the in-flight
+                // prefetch) before these ds_reads
+                asm volatile("" : "+v"(s));
             } else {
                 TapSet ts;
-                issue_taps(make_rsrc(planes + (int64_t)p * plane_stride, g.plane_bytes), g.W, g.H, px, py, true, ts);
+                issue_taps_padded(make_rsrc(planes + (int64_t)p * plane_stride, g.plane_bytes), g.W, g.H, g.Wp,
+                                  g.org, g.row, px, py, ts);
                 s = blend_taps(ts);
+                asm volatile("" : "+v"(s));
             }
             const float a = (replace_first && p == p_begin) ? 1.0f : s[3];
             const float om = 1.0f - a;
@@ -175,7 +204,7 @@ __global__ __launch_bounds__(kLThreads, 8) void render_lds_kernel(const float4* 
             cb = over(s[2], a, om, cb);
             if (CT) t = t * om;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (more && lds_mode(bx_next)) commit(buf ^ 1, bx_next);
         __syncthreads();
     }
     if (!active) return;

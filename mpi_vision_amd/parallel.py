@@ -90,7 +90,7 @@ def render_plane_sharded(packed_local: torch.Tensor, homs_local: torch.Tensor, h
                          dst: int = 0) -> Optional[torch.Tensor]:
     """Plane-sharded render of V views.
 
-    packed_local: this rank's planes, packed [P_local, H, W, 4] (rank 0 holds the
+    packed_local: this rank's planes, packed [P_local, H+4, W+4, 4] (_lib.pack_planes) (rank 0 holds the
     back-most range, which contains the reference's plane 0); homs_local
     [V, P_local, 9].  Returns the final frames [V, H, W, 3] on dst, None elsewhere."""
     from . import _lib

@@ -21,6 +21,10 @@ void oracle_plane_sweep(const float *img, const int64_t st[4], int B, int Hs, in
 void oracle_grid_sample(const float *in, const int64_t ist[4], int N, int C, int Hi, int Wi,
                         const float *coords, int Ho, int Wo, float *out, const int64_t ost[4],
                         int nthreads);
+/* d(render)/d(mpi) like the reference's autograd: dout [B,H,W,3] contiguous ->
+ * dmpi [B,H,W,P,4] contiguous (overwritten); vec = grid_sampler's Vec<float> width */
+void oracle_render_backward(const float *mpi, const int64_t st[5], int B, int H, int W, int P,
+                            const float *homs, const float *dout, float *dmpi, int vec, int nthreads);
 /* layers [P][n][4] contiguous; out [n][3] */
 void oracle_over_composite(const float *layers, int P, int64_t n, float *out);
 #ifdef __cplusplus

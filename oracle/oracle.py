@@ -37,6 +37,8 @@ def lib():
         L.oracle_grid_sample.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, ctypes.c_int, ctypes.c_int,
                                                                           _f, _i64, ctypes.c_int]
         L.oracle_over_composite.argtypes = [_f, ctypes.c_int, ctypes.c_int64, _f]
+        L.oracle_render_backward.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, _f, _f, ctypes.c_int,
+                                                                             ctypes.c_int]
         _lib = L
     return _lib
 
@@ -60,6 +62,25 @@ def render(mpi: np.ndarray, homs: np.ndarray, nthreads: int = 0) -> np.ndarray:
     homs = np.ascontiguousarray(homs, dtype=np.float32).reshape(B, P, 9)
     out = np.empty((B, H, W, 3), np.float32)
     lib().oracle_render(_fp(mpi), _strides(mpi), B, H, W, P, _fp(homs), _fp(out), _threads(nthreads))
+    return out
+
+
+# grid_sampler_2d_backward's chunk width (Vec<float>::size() of the kernel ATen dispatched) on the host that
+# produced tests/golden/grad.npz: 8 reproduces every golden bit for bit, 16 does not
+GRID_VEC = 8
+
+
+def render_backward(mpi: np.ndarray, homs: np.ndarray, dout: np.ndarray, vec: int = GRID_VEC,
+                    nthreads: int = 0) -> np.ndarray:
+    """d(render)/d(mpi) for mpi [B,H,W,P,4] (any strides), homs [B,P,9], dout [B,H,W,3]
+    -> [B,H,W,P,4], in the reference autograd's arithmetic order (bit-exact)."""
+    assert mpi.dtype == np.float32 and mpi.ndim == 5 and mpi.shape[-1] == 4
+    B, H, W, P, _ = mpi.shape
+    homs = np.ascontiguousarray(homs, dtype=np.float32).reshape(B, P, 9)
+    dout = np.ascontiguousarray(dout, dtype=np.float32).reshape(B, H, W, 3)
+    out = np.empty((B, H, W, P, 4), np.float32)
+    lib().oracle_render_backward(_fp(mpi), _strides(mpi), B, H, W, P, _fp(homs), _fp(dout), _fp(out), vec,
+                                 _threads(nthreads))
     return out
 
 

@@ -44,7 +44,9 @@ def test_native_and_packed_kernels_agree_with_oracle(name, small, meta, dev):
     assert_bits(nat.cpu().numpy(), want)
     for b in range(B):
         packed = _lib.pack_planes(dmpi[b])
-        assert torch.equal(packed.cpu(), mpi[b].permute(2, 0, 1, 3).contiguous())
+        want_pk = torch.zeros(_lib.packed_shape(H, W, P))
+        want_pk[:, 2:2 + H, 2:2 + W] = mpi[b].permute(2, 0, 1, 3)
+        assert torch.equal(packed.cpu(), want_pk)  # interior = plane-major texels, border = 0
         pk = _lib.render_packed(packed, homs[b:b + 1])
         assert_bits(pk.cpu().numpy(), want[b:b + 1])
 
@@ -139,8 +141,8 @@ def test_render_errors(dev):
         mv.mpi_render_view_torch(mpi, pose.expand(2, 4, 4), torch.tensor([2.0, 1.0], device=dev), K.expand(2, 3, 3))
 
 
-@pytest.mark.parametrize("divisor", [1, 2, 3, 7, 36, 39, 71, 127, 159, 255, 399, 575, 639, 767, 1023, 1079,
-                                     2159, 4095, 65535])
+@pytest.mark.parametrize("divisor", [1, 2, 3, 7, 36, 39, 47, 48, 63, 64, 71, 95, 96, 127, 159, 255, 399, 400,
+                                     575, 576, 639, 640, 767, 768, 1023, 1024, 1079, 2159, 4095, 65535])
 def test_div_const_exhaustive(divisor, dev):
     """The render's launch-constant division equals IEEE x / c for every fp32 x whose
     quotient can affect a sample position (all 2^32 bit patterns)."""
@@ -151,7 +153,7 @@ def test_div_const_exhaustive(divisor, dev):
 
 @pytest.mark.parametrize("name", RENDER_CASES)
 def test_lds_and_direct_kernels_identical(name, small, meta, dev):
-    """The LDS-staged render (default) and the direct-gather render agree bit for bit,
+    """The LDS-staged render and the direct-gather render (default) agree bit for bit,
     including planes that fall back to direct gathers (large motion, 'render_big')."""
     mpi = render_case_inputs(meta["small"], name)
     B, H, W, P, _ = mpi.shape
@@ -161,8 +163,8 @@ def test_lds_and_direct_kernels_identical(name, small, meta, dev):
         h = homs[b:b + 1].to(dev)
         a = torch.empty((1, H, W, 3), device=dev)
         d = torch.empty((1, H, W, 3), device=dev)
-        _lib._call("mpiv_render_packed", packed, H, W, P, h, 1, a, _lib._stream(dev))
-        _lib._call("mpiv_render_packed_direct", packed, H, W, P, h, 1, d, _lib._stream(dev))
+        _lib._call("mpiv_render_packed_lds", packed, H, W, P, h, 1, a, _lib._stream(dev))
+        _lib._call("mpiv_render_packed", packed, H, W, P, h, 1, d, _lib._stream(dev))
         assert_bits(a.cpu().numpy(), d.cpu().numpy(), f"{name}[{b}] lds vs direct")
         assert_bits(a.cpu().numpy(), small[f"{name}_out"][b:b + 1], f"{name}[{b}] lds vs reference")
 
@@ -187,3 +189,6 @@ def test_lds_kernel_extreme_poses(dev):
     packed = _lib.pack_planes(mpi[0].to(dev))
     got = _lib.render_packed(packed, homs)
     assert_bits(got.cpu().numpy(), want)
+    out = torch.empty_like(got)
+    _lib._call("mpiv_render_packed_lds", packed, H, W, P, homs.to(dev), V, out, _lib._stream(dev))
+    assert_bits(out.cpu().numpy(), want)

@@ -136,10 +136,10 @@ def c4(dev, it, wu):
                                          configs.f32([c["K"]] * V), V).to(dev)
         out = torch.empty((V, H, W, 3), device=dev)
         ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it if V < 125 else max(3, it // 4), 1)
-        report(f"c4 1024^2x128 packed (LDS-staged), {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
-        ms, mn = timed(lambda: _lib._call("mpiv_render_packed_direct", packed, H, W, P, homs, V, out,
-                                          _lib._stream(dev)), it if V < 125 else max(3, it // 4), 1)
         report(f"c4 1024^2x128 packed (direct gathers), {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
+        ms, mn = timed(lambda: _lib._call("mpiv_render_packed_lds", packed, H, W, P, homs, V, out,
+                                          _lib._stream(dev)), it if V < 125 else max(3, it // 4), 1)
+        report(f"c4 1024^2x128 packed (LDS-staged), {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
     homs = _host.render_homographies(configs.f32(c["poses"][:1]), configs.f32(c["depths"]),
                                      configs.f32([c["K"]]), 1).to(dev)
     out = torch.empty((1, H, W, 3), device=dev)
@@ -163,7 +163,8 @@ def c5(dev, it, wu):
     G = 8
     PL = P // G
     g = torch.Generator(device=dev).manual_seed(0)
-    packed = torch.rand((PL, H, W, 4), generator=g, device=dev)
+    packed = torch.zeros(_lib.packed_shape(H, W, PL), device=dev)
+    packed[:, 2:2 + H, 2:2 + W].uniform_(generator=g)
     homs = _host.render_homographies(configs.f32(c["poses"]), configs.f32(c["depths"]), configs.f32([c["K"]]), 1)
     homs_local = homs[:, :PL].contiguous().to(dev)
     ct = torch.empty((1, H, W, 4), device=dev)

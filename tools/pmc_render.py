@@ -22,11 +22,12 @@ dev = torch.device("cuda:0")
 c = configs.config4()
 H, W, P, V = c["H"], c["W"], c["P"], a.views
 g = torch.Generator(device=dev).manual_seed(0)
-packed = torch.rand((P, H, W, 4), generator=g, device=dev)
+packed = torch.zeros(_lib.packed_shape(H, W, P), device=dev)
+packed[:, 2:2 + H, 2:2 + W].uniform_(generator=g)
 homs = _host.render_homographies(configs.f32(c["poses"][:V]), configs.f32(c["depths"]),
                                  configs.f32([c["K"]] * V), V).to(dev)
 out = torch.empty((V, H, W, 3), device=dev)
-name = "mpiv_render_packed" if a.variant == "lds" else "mpiv_render_packed_direct"
+name = "mpiv_render_packed_lds" if a.variant == "lds" else "mpiv_render_packed"
 for _ in range(a.iters):
     _lib._call(name, packed, H, W, P, homs, V, out, _lib._stream(dev))
 torch.cuda.synchronize()
