@@ -23,6 +23,7 @@
 #ifndef MPIV_H
 #define MPIV_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -79,6 +80,25 @@ int mpiv_render_packed_ct(const float *packed, int H, int W, int P, int p_begin,
 /* Ordered over-operator combine: parts [G][n][4] (C,T), index 0 = back-most range
  * -> out [n][3].  (Cf,Tf) o (Cb,Tb) = (Cf + Tf*Cb, Tf*Tb). */
 int mpiv_combine_ct(const float *parts, int G, int64_t n, float *out, void *stream);
+
+/* ---- render backward ------------------------------------------------------ */
+
+/* Workspace bytes mpiv_render_backward needs for one H x W x P MPI (reused across
+ * views): ~60 B per plane-pixel + 8 B per plane-texel. */
+size_t mpiv_render_backward_workspace_size(int H, int W, int P);
+
+/* d(mpi_render_view_torch)/d(rgba_layers) (utils.py:267-294 under autograd), bit-exact
+ * to the reference's CPU autograd: the over-composite adjoint followed by
+ * grid_sampler_2d_backward's scatter, summed per texel in ATen's order.
+ * packed:  the MPI in mpiv_pack_planes layout; homs [V][P][9] (the forward's);
+ * dout:    [V,H,W,3] contiguous incoming gradient;
+ * dmpi:    [V,H,W,P,4] with element strides dmpi_strides[5]: view v's gradient is
+ *          written (not accumulated) to dmpi + v*dmpi_strides[0];
+ * workspace: >= mpiv_render_backward_workspace_size(H, W, P) bytes, 256-B aligned.
+ * Deterministic (no float atomics); H*W < 2^26. */
+int mpiv_render_backward(const float *packed, int H, int W, int P, const float *homs, int V,
+                         const float *dout, float *dmpi, const int64_t dmpi_strides[5], void *workspace,
+                         size_t workspace_bytes, void *stream);
 
 /* ---- plane sweep -------------------------------------------------------- */
 

@@ -41,10 +41,11 @@ _SIGS = {
     "mpiv_plane_sweep_padded": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
     "mpiv_preprocess": [_vp, _i64, _vp, _vp],
     "mpiv_deprocess_u8": [_vp, _i64, _vp, _vp],
+    "mpiv_render_backward": [_vp, _int, _int, _int, _vp, _int, _vp, _vp, _c_i64p, _vp, ctypes.c_size_t, _vp],
     "mpiv_plane_sweep_padded_into": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,
                                      _vp],
 }
-EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error")
+EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size")
 ABI_VERSION = 2
 
 _lib = None
@@ -68,6 +69,8 @@ def load():
             fn.restype = ctypes.c_int
         L.mpiv_abi_version.restype = ctypes.c_int
         L.mpiv_last_error.restype = ctypes.c_char_p
+        L.mpiv_render_backward_workspace_size.argtypes = [_int, _int, _int]
+        L.mpiv_render_backward_workspace_size.restype = ctypes.c_size_t
         if L.mpiv_abi_version() != ABI_VERSION:
             raise RuntimeError("mpi_vision_amd: libmpiv.so ABI version mismatch")
         _lib = L
@@ -222,6 +225,52 @@ def render(rgba_layers: torch.Tensor, homs: torch.Tensor) -> torch.Tensor:
         return out
     _call("mpiv_render", rgba_layers, _strides(rgba_layers), B, H, W, P, h, out, _stream(dev))
     return out
+
+
+def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.Tensor) -> torch.Tensor:
+    """d(mpi_render_view_torch)/d(rgba_layers): rgba_layers [B,H,W,P,4] (any strides, incl. a
+    stride-0 broadcast batch), homs [B,P,9] (the forward's), dout [B,H,W,3] ->
+    [B,H,W,P,4] contiguous, one gradient per view (a broadcast input's views are summed
+    by autograd's expand backward, as in the reference).  Bit-exact to the reference's
+    CPU autograd (render_bwd.hip)."""
+    dev = _dev(rgba_layers, dout)
+    B, H, W, P, _ = rgba_layers.shape
+    if tuple(dout.shape) != (B, H, W, 3):
+        raise RuntimeError(f"grad_output must be [{B},{H},{W},3], got {tuple(dout.shape)}")
+    L = load()
+    ws = torch.empty(L.mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    grad = torch.empty((B, H, W, P, 4), device=dev, dtype=torch.float32)
+    h = _up(homs.reshape(B, P, 9), dev)
+    dout = dout.contiguous()
+    gst = _strides(grad)
+    if B > 1 and rgba_layers.stride(0) == 0:  # broadcast MPI: pack once, all views
+        packed = pack_planes(rgba_layers[0])
+        _call("mpiv_render_backward", packed, H, W, P, h, B, dout, grad, gst, ws, ws.numel(), _stream(dev))
+        return grad
+    packed = torch.empty(packed_shape(H, W, P), device=dev, dtype=torch.float32)
+    for b in range(B):
+        pack_planes(rgba_layers[b], out=packed)
+        _call("mpiv_render_backward", packed, H, W, P, h[b:b + 1], 1, dout[b:b + 1], grad[b:b + 1], gst, ws,
+              ws.numel(), _stream(dev))
+    return grad
+
+
+class RenderFunction(torch.autograd.Function):
+    """Autograd node of the fused render: forward = render(), backward =
+    render_backward() (w.r.t. rgba_layers; homographies come from poses and
+    intrinsics, which the reference's training never differentiates)."""
+
+    @staticmethod
+    def forward(ctx, rgba_layers, homs):
+        ctx.save_for_backward(rgba_layers)
+        ctx.homs = homs
+        return render(rgba_layers, homs)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (rgba_layers,) = ctx.saved_tensors
+        grad = render_backward(rgba_layers, ctx.homs, dout) if ctx.needs_input_grad[0] else None
+        return grad, None
 
 
 # ---------------------------------------------------------------------------

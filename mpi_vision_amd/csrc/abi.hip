@@ -10,6 +10,7 @@
 #include "../../include/mpiv.h"
 #include "render.hip"
 #include "render_lds.hip"
+#include "render_bwd.hip"
 #include "sweep.hip"
 #include "geometry.hip"
 
@@ -135,6 +136,97 @@ int mpiv_render_packed_lds(const float* packed, int H, int W, int P, const float
 int mpiv_render_packed_ct(const float* packed, int H, int W, int P, int p_begin, int p_end, int back,
                           const float* homs, int V, float* ct, void* stream) {
     return render_packed_impl(packed, H, W, P, p_begin, p_end, back, homs, V, ct, true, 0, stream);
+}
+
+// ---- render backward (render_bwd.hip) ----------------------------------------------
+
+namespace {
+
+inline size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
+
+// workspace carve-up for one view; returns the total size in bytes
+size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
+    const size_t n = (size_t)P * H * W;
+    const size_t nk = (size_t)P * (H + 1) * (W + 1);
+    const size_t nb = (nk + kScanTile - 1) / kScanTile;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* p = base ? base + off : nullptr;
+        off += align256(bytes);
+        return p;
+    };
+    char* prev = take(n * 16);
+    char* ds = take(n * 16);
+    char* fw = take(n * 8);
+    char* key = take(n * 4);
+    char* count = take(nk * 4);
+    char* offs = take((nk + 1) * 4);
+    char* ids = take(n * 4);
+    char* bsum = take(nb * 4);
+    if (ws) {
+        ws->prev = reinterpret_cast<float4*>(prev);
+        ws->ds = reinterpret_cast<float4*>(ds);
+        ws->fw = reinterpret_cast<float2*>(fw);
+        ws->key = reinterpret_cast<int*>(key);
+        ws->count = reinterpret_cast<int*>(count);
+        ws->offs = reinterpret_cast<int*>(offs);
+        ws->ids = reinterpret_cast<int*>(ids);
+        ws->bsum = reinterpret_cast<int*>(bsum);
+    }
+    return off;
+}
+
+}  // namespace
+
+size_t mpiv_render_backward_workspace_size(int H, int W, int P) {
+    if (H <= 0 || W <= 0 || P <= 0) return 0;
+    return bwd_layout(H, W, P, nullptr, nullptr);
+}
+
+int mpiv_render_backward(const float* packed, int H, int W, int P, const float* homs, int V, const float* dout,
+                         float* dmpi, const int64_t st[5], void* workspace, size_t ws_bytes, void* stream) {
+    const char* nm = "mpiv_render_backward";
+    if (!packed || !homs || !dout || !dmpi || !st || !workspace) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (V <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    if (!aligned16(packed) || (reinterpret_cast<uintptr_t>(workspace) & 255))
+        return fail(MPIV_ERR_ARG, "%s: packed must be 16-byte and workspace 256-byte aligned", nm);
+    if ((int64_t)(H + 2 * kPad) * (W + 2 * kPad) * 16 >= (int64_t)kOOB || H >= (1 << 22) || W >= (1 << 22))
+        return fail(MPIV_ERR_ARG, "%s: padded plane larger than 2 GiB or a side >= 2^22", nm);
+    // bucket / pixel ids and order keys are 32-bit: P*(H+1)*(W+1) + 1 < 2^31, H*W < 2^26
+    if ((int64_t)P * (H + 1) * (W + 1) + 1 >= ((int64_t)1 << 31) || (int64_t)H * W >= ((int64_t)1 << 26))
+        return fail(MPIV_ERR_ARG, "%s: MPI too large for one backward launch", nm);
+    BwdWs ws;
+    const size_t need = bwd_layout(H, W, P, static_cast<char*>(workspace), &ws);
+    if (ws_bytes < need) return fail(MPIV_ERR_ARG, "%s: workspace too small (%zu < %zu bytes)", nm, ws_bytes, need);
+    const RenderGeom g = make_geom(H, W, P);
+    const bool fast = H >= 2 && W >= 2;
+    const float4* pk = reinterpret_cast<const float4*>(packed);
+    const int64_t ps = (int64_t)(H + 2 * kPad) * (W + 2 * kPad);
+    const int HW = H * W;
+    const int K = (H + 1) * (W + 1);
+    const int64_t nk = (int64_t)P * K;
+    const int64_t nq = (int64_t)P * HW;
+    const unsigned nb = (unsigned)((nk + kScanTile - 1) / kScanTile);
+    const GradOut so{st[1], st[2], st[3], st[4]};
+    hipStream_t q = S(stream);
+    if (hipMemsetAsync(ws.count, 0, (size_t)nk * 4, q) != hipSuccess)
+        return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
+    const unsigned tiles = blocks(W, kTileX) * blocks(H, kTileY);
+    for (int v = 0; v < V; ++v) {
+        const float* hv = homs + (int64_t)v * P * 9;
+        const float* dv = dout + (int64_t)v * HW * 3;
+        if (fast)
+            render_bwd_chain_kernel<true><<<tiles, 256, 0, q>>>(pk, ps, g, hv, dv, ws);
+        else
+            render_bwd_chain_kernel<false><<<tiles, 256, 0, q>>>(pk, ps, g, hv, dv, ws);
+        scan_tile_sums_kernel<<<nb, kScanBlock, 0, q>>>(ws.count, nk, ws.bsum);
+        scan_tile_offsets_kernel<<<1, kScanBlock, 0, q>>>(ws.bsum, (int)nb);
+        scan_apply_kernel<<<nb, kScanBlock, 0, q>>>(ws.count, nk, ws.bsum, ws.offs);
+        bucket_fill_kernel<<<blocks(nq, 256), 256, 0, q>>>(P, HW, K, ws);
+        bucket_sort_kernel<<<blocks(nk, 256), 256, 0, q>>>(nk, ws);
+        render_bwd_gather_kernel<<<blocks(nq, 256), 256, 0, q>>>(H, W, P, ws, dmpi + (int64_t)v * st[0], so);
+    }
+    return launched(nm);
 }
 
 int mpiv_combine_ct(const float* parts, int G, int64_t n, float* out, void* stream) {

@@ -140,11 +140,17 @@ def mpi_render_view_torch(rgba_layers, tgt_pose, planes, intrinsics):
 
     `planes` must be a tensor of P depths, far->near (a list raises AttributeError,
     as in the reference, utils.py:279).  The whole warp + over-composite runs as ONE
-    fused HIP kernel; the MPI may be a stride-0 broadcast over the batch."""
+    fused HIP kernel; the MPI may be a stride-0 broadcast over the batch.  When
+    rgba_layers requires grad the result is differentiable w.r.t. it (HIP backward,
+    bit-exact to the reference's autograd)."""
     batch_size = tgt_pose.shape[0]
     n_planes = len(planes)
     depths = planes.reshape([n_planes, 1])  # AttributeError on a list, like the reference
     homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
+    if torch.is_grad_enabled() and rgba_layers.requires_grad:
+        # training (ipynb cell 12): the adjoint runs in HIP too, bit-exact to the
+        # reference's autograd (render_bwd.hip)
+        return _lib.RenderFunction.apply(rgba_layers, homs)
     return _lib.render(rgba_layers, homs)
 
 

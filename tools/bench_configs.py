@@ -177,11 +177,27 @@ def c5(dev, it, wu):
     report(f"c5 ordered combine of {G} band partials ({bh}x{W})", ms, mn, G * bh * W * 16 + bh * W * 12)
 
 
+def bwd(dev, it, wu):
+    """Render backward (d render / d rgba_layers, bit-exact adjoint) per view at the
+    config-2 and config-4 sizes; bytes = the MPI read by the forward recompute + its
+    gradient written (P*H*W*32) -- the workspace traffic is reported, not counted."""
+    for name, c in (("c2", configs.config2()), ("c4", configs.config4())):
+        H, W, P = c["H"], c["W"], c["P"]
+        mpi = gen_mpi(H, W, P, 0, dev)
+        homs = _host.render_homographies(configs.f32(c["poses"][:1]), configs.f32(c["depths"]),
+                                         configs.f32([c["K"]]), 1)
+        dout = torch.rand((1, H, W, 3), device=dev) * 2 - 1
+        ms, mn = timed(lambda: _lib.render_backward(mpi, homs, dout), max(3, it // 4), 1)
+        ws = _lib.load().mpiv_render_backward_workspace_size(H, W, P)
+        report(f"{name} render backward {W}x{H}x{P}, 1 view (pack + chain + scan + bucket + gather)", ms, mn,
+               P * H * W * 32, H * W / 1e6, extra={"workspace_GB": round(ws / 1e9, 3)})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--only", default="c1,c2,c3,c4,c5")
+    ap.add_argument("--only", default="c1,c2,c3,c4,c5,bwd")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     for name in a.only.split(","):
