@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 2
+#define MPIV_ABI_VERSION 3
 
 enum {
     MPIV_OK = 0,
@@ -114,11 +114,12 @@ int mpiv_plane_sweep(const float *img, const int64_t img_strides[4], int B, int 
                      float *out, void *stream);
 
 /* Source images for the fast sweep: [B,Hs,Ws,C] (C <= 4, element strides) ->
- * img4 [B][Hs*Ws] 16-B texels (channels >= C zero), 16-B aligned. */
+ * img4 [B][Hs+4][Ws+4] 16-B texels (channels >= C zero) with a 2-texel zero border
+ * (the packed-plane convention of mpiv_pack_planes), 16-B aligned. */
 int mpiv_pad_texels(const float *img, const int64_t img_strides[4], int B, int Hs, int Ws, int C, float *img4,
                     void *stream);
 
-/* plane_sweep_torch* on padded texels (mpiv_pad_texels), C <= 4, Hs*Ws*16 < 2 GiB:
+/* plane_sweep_torch* on padded texels (mpiv_pad_texels), C <= 4, (Hs+4)*(Ws+4)*16 < 2 GiB:
  * same contract and bit-identical output as mpiv_plane_sweep. */
 int mpiv_plane_sweep_padded(const float *img4, int B, int Hs, int Ws, int C, const float *ki, const float *proj,
                             const float *depths, int D, int Ht, int Wt, float *out, void *stream);

@@ -46,7 +46,7 @@ _SIGS = {
                                      _vp],
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lib = None
 
@@ -280,21 +280,34 @@ class RenderFunction(torch.autograd.Function):
 def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.Tensor, tgt_h: int,
                 tgt_w: int) -> torch.Tensor:
     """[B,Hs,Ws,C] -> PSV [B,tgt_h,tgt_w,D*C].  C <= 4: the source is padded once to
-    16-B texels (B*Hs*Ws*16 bytes) and swept by the buffer-load kernel; otherwise the
-    generic strided kernel."""
+    16-B texels with a zero border (B*(Hs+4)*(Ws+4)*16 bytes) and swept by the
+    buffer-load kernel; otherwise the generic strided kernel."""
     dev = _dev(img)
     B, Hs, Ws, C = img.shape
     d = torch.tensor([float(x) for x in depth_planes], dtype=torch.float32)
     D = d.shape[0]
     out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
     kid, projd, dd = _up(ki, dev), _up(proj, dev), _up(d, dev)
-    if C <= 4 and Hs * Ws * 16 < 0x7FFFFF00:
-        img4 = torch.empty((B, Hs, Ws, 4), device=dev, dtype=torch.float32)
-        _call("mpiv_pad_texels", img, _strides(img), B, Hs, Ws, C, img4, _stream(dev))
+    if C <= 4 and (Hs + 4) * (Ws + 4) * 16 < 0x7FFFFF00:
+        img4 = pad_texels(img)
         _call("mpiv_plane_sweep_padded", img4, B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out, _stream(dev))
     else:
         _call("mpiv_plane_sweep", img, _strides(img), B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out,
               _stream(dev))
+    return out
+
+
+def pad_texels(img: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """[B,Hs,Ws,C<=4] (any strides) -> [B,Hs+4,Ws+4,4] 16-B texels with a 2-texel zero
+    border (mpiv_pad_texels layout)."""
+    dev = _dev(img)
+    B, Hs, Ws, C = img.shape
+    shape = (B, Hs + 4, Ws + 4, 4)
+    if out is None:
+        out = torch.empty(shape, device=dev, dtype=torch.float32)
+    elif tuple(out.shape) != shape or not out.is_contiguous():
+        raise RuntimeError(f"pad_texels: out must be a contiguous {shape} tensor")
+    _call("mpiv_pad_texels", img, _strides(img), B, Hs, Ws, C, out, _stream(dev))
     return out
 
 
@@ -327,11 +340,11 @@ def network_input(ref_image, psv_src_images, rel_poses, depth_planes, intrinsics
     out = torch.empty((B, H, W, Ctot), device=dev, dtype=torch.float32)
     out[..., :3].copy_(ref_image)  # the concat's first slice is a plain copy (utils.py:491)
     dd = _up(d, dev)
-    img4 = torch.empty((B, H, W, 4), device=dev, dtype=torch.float32)
+    img4 = torch.empty((B, H + 4, W + 4, 4), device=dev, dtype=torch.float32)
     for i, pose in enumerate(rel_poses):
         src = psv_src_images[:, :, :, i * 3:(i + 1) * 3]
         ki, proj = psv_matrices(intrinsics, intrinsics, pose)
-        _call("mpiv_pad_texels", src, _strides(src), B, H, W, 3, img4, _stream(dev))
+        pad_texels(src, out=img4)
         _call("mpiv_plane_sweep_padded_into", img4, B, H, W, 3, _up(ki, dev), _up(proj, dev), dd, D, H, W,
               out[..., 3 + i * D * 3:], H * W * Ctot, Ctot, _stream(dev))
     return out

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdarg>
 #include <cstring>
+#include <cstdlib>
 
 #include "../../include/mpiv.h"
 #include "render.hip"
@@ -266,10 +267,13 @@ int mpiv_pad_texels(const float* img, const int64_t st[4], int B, int Hs, int Ws
     if (!img || !st || !img4) return fail(MPIV_ERR_ARG, "mpiv_pad_texels: null pointer");
     if (B <= 0 || Hs <= 0 || Ws <= 0 || C <= 0 || C > 4) return fail(MPIV_ERR_ARG, "mpiv_pad_texels: bad shape");
     if (!aligned16(img4)) return fail(MPIV_ERR_ARG, "mpiv_pad_texels: img4 must be 16-byte aligned");
+    if ((int64_t)(Hs + 2 * kPad) * (Ws + 2 * kPad) * 16 >= (int64_t)kOOB)
+        return fail(MPIV_ERR_ARG, "mpiv_pad_texels: padded image larger than 2 GiB");
     if (B > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_pad_texels: too large");
     const ImgStrides s{st[0], st[1], st[2], st[3]};
-    pad_texels_kernel<<<dim3(blocks((int64_t)Hs * Ws, 256), B), 256, 0, S(stream)>>>(img, s, Hs, Ws, C,
-                                                                                   reinterpret_cast<float4*>(img4));
+    const int64_t npix = (int64_t)(Hs + 2 * kPad) * (Ws + 2 * kPad);
+    pad_texels_kernel<<<dim3(blocks(npix, 256), B), 256, 0, S(stream)>>>(
+        img, s, Hs, Ws, C, make_fastdiv((unsigned)(Ws + 2 * kPad)), reinterpret_cast<float4*>(img4));
     return launched("mpiv_pad_texels");
 }
 
@@ -280,24 +284,68 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
     if (B <= 0 || Hs <= 0 || Ws <= 0 || C <= 0 || C > 4 || D <= 0 || Ht <= 0 || Wt <= 0)
         return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: bad shape");
     if (!aligned16(img4)) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: img4 must be 16-byte aligned");
-    if (out_pstride < (int64_t)D * C || out_pstride > (1 << 30) || out_bstride < (int64_t)Ht * Wt * out_pstride)
+    if (out_pstride < (int64_t)D * C || out_pstride > (1 << 30) || out_bstride < (int64_t)Ht * Wt * out_pstride ||
+        (int64_t)Ht * Wt >= (1ll << 31))
         return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: bad output strides");
-    if ((int64_t)Hs * Ws * 16 >= (int64_t)kOOB || Hs >= (1 << 22) || Ws >= (1 << 22))
-        return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: image > 2 GiB or a side >= 2^22");
-    const int64_t per_view = (int64_t)Ht * Wt * D;
+    if ((int64_t)(Hs + 2 * kPad) * (Ws + 2 * kPad) * 16 >= (int64_t)kOOB || Hs >= (1 << 22) || Ws >= (1 << 22))
+        return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: padded image > 2 GiB or a side >= 2^22");
+    const int NG = (D + kSweepDG - 1) / kSweepDG;
+    const int64_t per_view = (int64_t)Ht * Wt * NG;
     if (B > kMaxGridYZ || per_view >= (1ll << 31)) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: too large");
-    const FastDiv fd_d = make_fastdiv((unsigned)D), fd_w = make_fastdiv((unsigned)Wt);
+    const FastDiv fd_g = make_fastdiv((unsigned)NG), fd_w = make_fastdiv((unsigned)Wt);
     const SweepParams sp = sweep_params(B, Hs, Ws, C, D, Ht, Wt);
     const float rc_hs = 1.0f / sp.fhs, rc_ws = 1.0f / sp.fws;
+    PadGeom pg;
+    pg.Wp = Ws + 2 * kPad;
+    pg.row = pg.Wp * 16;
+    pg.org = (kPad * pg.Wp + kPad) * 16;
+    pg.plane_bytes = (int)((int64_t)(Hs + 2 * kPad) * pg.Wp * 16);
     const float4* im = reinterpret_cast<const float4*>(img4);
-    const dim3 grid(blocks(per_view, 256 * kSweepILP), B, 1);
-    hipStream_t q = S(stream);
-    switch (C) {
-        case 1: plane_sweep_rgba_kernel<1><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out, out_bstride, (int)out_pstride); break;
-        case 2: plane_sweep_rgba_kernel<2><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out, out_bstride, (int)out_pstride); break;
-        case 3: plane_sweep_rgba_kernel<3><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out, out_bstride, (int)out_pstride); break;
-        default: plane_sweep_rgba_kernel<4><<<grid, 256, 0, q>>>(im, sp, rc_hs, rc_ws, fd_d, fd_w, ki, proj, depths, out, out_bstride, (int)out_pstride); break;
+    const dim3 grid(blocks(per_view, 256), B, 1);
+    // 16-B group stores need 16-B aligned output rows; the LDS-staged store needs the
+    // dense volume layout (each view one contiguous run of items)
+    const bool vec = aligned16(out) && out_pstride % 4 == 0 && out_bstride % 4 == 0;
+    const bool dense = vec && out_pstride == (int64_t)NG * kSweepDG * C;
+    int store = dense ? 2 : vec ? 1 : 0;
+    bool tile = true;
+    if (const char* e = getenv("MPIV_SWEEP_STORE")) {  // A/B only: the grouped kernel's store modes
+        store = min(store, atoi(e));
+        tile = false;
     }
+    hipStream_t q = S(stream);
+    if (tile) {
+        const int npix = Ht * Wt;
+        const int last = D - ((D - 1) / kTileD) * kTileD;  // depths in the last chunk
+        const dim3 tgrid(blocks(npix, kTileP), B, 1);
+        const FastDiv fw = make_fastdiv((unsigned)Wt), ff = make_fastdiv((unsigned)(kTileD * C)),
+                      fl = make_fastdiv((unsigned)(last * C));
+#define MPIV_TILE(CC)                                                                                            \
+    plane_sweep_tile_kernel<CC><<<tgrid, 256, 0, q>>>(im, sp, pg, rc_hs, rc_ws, fw, ff, fl, ki, proj, depths, out, \
+                                                      out_bstride, out_pstride)
+        switch (C) {
+            case 1: MPIV_TILE(1); break;
+            case 2: MPIV_TILE(2); break;
+            case 3: MPIV_TILE(3); break;
+            default: MPIV_TILE(4); break;
+        }
+#undef MPIV_TILE
+        return launched("mpiv_plane_sweep_padded");
+    }
+#define MPIV_SWEEP(CC, VV)                                                                                  \
+    plane_sweep_group_kernel<CC, VV><<<grid, 256, 0, q>>>(im, sp, pg, rc_hs, rc_ws, fd_g, fd_w, ki, proj, depths, \
+                                                          out, out_bstride, (int)out_pstride)
+#define MPIV_SWEEP_C(CC)                   \
+    if (store == 2) MPIV_SWEEP(CC, 2);     \
+    else if (store == 1) MPIV_SWEEP(CC, 1); \
+    else MPIV_SWEEP(CC, 0)
+    switch (C) {
+        case 1: MPIV_SWEEP_C(1); break;
+        case 2: MPIV_SWEEP_C(2); break;
+        case 3: MPIV_SWEEP_C(3); break;
+        default: MPIV_SWEEP_C(4); break;
+    }
+#undef MPIV_SWEEP_C
+#undef MPIV_SWEEP
     return launched("mpiv_plane_sweep_padded");
 }
 

@@ -78,86 +78,204 @@ __global__ __launch_bounds__(256) void plane_sweep_kernel(const float* __restric
     }
 }
 
-// Source images padded to 16-B texels: [B][Hs*Ws] float4, channels >= C zero.
+// Source images as 16-B texels with a 2-texel zero border (the render's packed-plane
+// convention, mpiv_common.hpp issue_taps_padded): [B][Hs+4][Ws+4] float4, channels >= C
+// zero.  Border texels are written as zeros, so the sweep needs no per-tap range test.
 __global__ __launch_bounds__(256) void pad_texels_kernel(const float* __restrict__ img, ImgStrides s, int Hs,
-                                                         int Ws, int C, float4* __restrict__ out) {
-    const int64_t npix = (int64_t)Hs * Ws;
+                                                         int Ws, int C, FastDiv fd_wp, float4* __restrict__ out) {
+    const int Wp = Ws + 2 * kPad;
+    const int64_t npix = (int64_t)(Hs + 2 * kPad) * Wp;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
     if (i >= npix) return;
-    const int y = (int)(i / Ws), x = (int)(i % Ws);
-    const float* t = img + b * s.b + y * s.y + x * s.x;
+    const int yp = (int)fast_div((unsigned)i, fd_wp);
+    const int y = yp - kPad, x = (int)i - yp * Wp - kPad;
     float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < C && c < 4; ++c) v[c] = t[c * s.c];
+    if ((unsigned)y < (unsigned)Hs && (unsigned)x < (unsigned)Ws) {
+        const float* t = img + b * s.b + y * s.y + x * s.x;
+        for (int c = 0; c < C && c < 4; ++c) v[c] = t[c * s.c];
+    }
     out[b * npix + i] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
-// Plane sweep over padded 16-B texels (C <= 4): four 16-B buffer loads per sample
-// with out-of-range taps zeroed by the buffer unit, and the two launch-constant
-// divisions (x / Hs, y / Ws) through div_const (FAST, Hs and Ws >= 1 always hold).
-// Work-items are (pixel, depth) with depth fastest, so a wave's C-float results are
-// one contiguous run of the volume.
-constexpr int kSweepILP = 4;       // (pixel, depth) items per work-item, loads issued together
-constexpr int kSweepMaxLdsD = 1024; // depths staged in LDS up to this many planes
+// Plane sweep over padded 16-B texels (C <= 4).  One work-item = one target pixel x a
+// group of kSweepDG consecutive depths (group fastest, so a wave writes one contiguous
+// run of the volume): the camera ray and the index math are shared by the group, its
+// 4 x kSweepDG tap loads are in flight together, u/den and v/den share one reciprocal
+// (div2_rn), the two launch-constant divisions (x / Hs, y / Ws) use div_const, and
+// the group's kSweepDG*C results leave as 16-B stores when the output rows are
+// 16-B aligned (VEC).
+constexpr int kSweepDG = 4;
+constexpr int kSweepMaxLdsD = 1024;  // depths staged in LDS up to this many planes
 
-template <int C>
-__global__ __launch_bounds__(256) void plane_sweep_rgba_kernel(const float4* __restrict__ img4, SweepParams sp,
-                                                               float rc_hs, float rc_ws, FastDiv fd_d, FastDiv fd_w,
-                                                               const float* __restrict__ ki,
-                                                               const float* __restrict__ proj,
-                                                               const float* __restrict__ depths,
-                                                               float* __restrict__ out, int64_t out_bstride,
-                                                               int out_pstride) {
+struct PadGeom {
+    int Wp, org, row, plane_bytes;  // padded source plane: pitch (texels), (0,0) offset, row bytes, size
+};
+
+// STORE 0: scalar stores; 1: 16-B stores per lane (VEC rows); 2: the block's contiguous
+// output run staged through LDS and written as 16-B stores by consecutive lanes (bare,
+// dense volume only: out_pstride == NG*kSweepDG*C).
+template <int C, int STORE>
+__global__ __launch_bounds__(256) void plane_sweep_group_kernel(const float4* __restrict__ img4, SweepParams sp,
+                                                                PadGeom pg, float rc_hs, float rc_ws, FastDiv fd_g,
+                                                                FastDiv fd_w, const float* __restrict__ ki,
+                                                                const float* __restrict__ proj,
+                                                                const float* __restrict__ depths,
+                                                                float* __restrict__ out, int64_t out_bstride,
+                                                                int out_pstride) {
     __shared__ float s_dep[kSweepMaxLdsD];
+    __shared__ float4 s_out[STORE == 2 ? 256 * C : 1];
     const bool lds_dep = sp.D <= kSweepMaxLdsD;
     if (lds_dep)
         for (int i = threadIdx.x; i < sp.D; i += blockDim.x) s_dep[i] = depths[i];
     __syncthreads();
-    const unsigned per_view = (unsigned)sp.Ht * sp.Wt * sp.D;  // < 2^31, checked on the host
+    const int NG = (sp.D + kSweepDG - 1) / kSweepDG;
+    const unsigned per_view = (unsigned)sp.Ht * sp.Wt * NG;  // < 2^31, checked on the host
+    const unsigned gid0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned gid = STORE == 2 ? min(gid0, per_view - 1) : gid0;  // whole block reaches the barrier
+    if (gid0 >= per_view && STORE != 2) return;
     const int b = blockIdx.y;
     const float* k9 = ki + (int64_t)b * 9;
     const float* m = proj + (int64_t)b * 16;
-    const __amdgpu_buffer_rsrc_t r = make_rsrc(img4 + (int64_t)b * sp.Hs * sp.Ws, sp.Hs * sp.Ws * 16);
-    // output element of (pixel, d, c): b*out_bstride + pixel*out_pstride + d*C + c
-    // (out_pstride = D*C for a bare volume; larger when writing into a wider tensor,
-    // e.g. format_network_input_torch's concatenated channels)
-    float* ob = out + (int64_t)b * out_bstride;
-    const unsigned base = blockIdx.x * (blockDim.x * kSweepILP) + threadIdx.x;
-    TapSet t[kSweepILP];
-    // phase 1: coordinates + tap loads of all items (kSweepILP x 4 loads in flight)
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(img4 + (int64_t)b * pg.plane_bytes / 16, pg.plane_bytes);
+    const unsigned pix = fast_div(gid, fd_g);
+    const int dg = (int)(gid - pix * NG);
+    const unsigned yy = fast_div(pix, fd_w);
+    const float fy = (float)(int)yy, fx = (float)(int)(pix - yy * sp.Wt);
+    float rx, ry, rz;
+    ray(k9, fx, fy, rx, ry, rz);  // pixel2cam_torch, utils.py:370
+    TapSet t[kSweepDG];
 #pragma unroll
-    for (int k = 0; k < kSweepILP; ++k) {
-        const unsigned gid = base + k * blockDim.x;
-        const bool live = gid < per_view;
-        const unsigned g = live ? gid : 0;
-        const unsigned pix = fast_div(g, fd_d);
-        const int d = (int)(g - pix * sp.D);
-        const unsigned yy = fast_div(pix, fd_w);
-        const float fy = (float)(int)yy, fx = (float)(int)(pix - yy * sp.Wt);
-        float rx, ry, rz;
-        ray(k9, fx, fy, rx, ry, rz);
+    for (int j = 0; j < kSweepDG; ++j) {
+        const int d = min(dg * kSweepDG + j, sp.D - 1);  // a partial last group recomputes depth D-1
         const float dep = lds_dep ? s_dep[d] : depths[d];
         const float X = rx * dep, Y = ry * dep, Z = rz * dep;
         const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
         const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
         const float pz = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11];
-        const float den = pz + 1e-10f;
-        const float cx = div_const(div_rn(pu, den) + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
-        const float cy = div_const(div_rn(pv, den) + 0.5f, sp.fws, rc_ws);  //          y / W
-        issue_taps(r, sp.Ws, sp.Hs, unnormalize(to_grid(cx), sp.half_ws), unnormalize(to_grid(cy), sp.half_hs),
-                   live, t[k]);
+        float su, sv;
+        div2_rn(pu, pv, pz + 1e-10f, su, sv);  // cam2pixel_torch, utils.py:388-391
+        const float cx = div_const(su + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
+        const float cy = div_const(sv + 0.5f, sp.fws, rc_ws);  //          y / W
+        issue_taps_padded(r, sp.Ws, sp.Hs, pg.Wp, pg.org, pg.row, unnormalize(to_grid(cx), sp.half_ws),
+                          unnormalize(to_grid(cy), sp.half_hs), t[j]);
     }
-    // phase 2: blend + coalesced stores (consecutive work-items = consecutive depths)
+    float v[kSweepDG * C];
 #pragma unroll
-    for (int k = 0; k < kSweepILP; ++k) {
-        const unsigned gid = base + k * blockDim.x;
-        const f32x4 v = blend_taps(t[k]);
-        if (gid < per_view) {
-            const unsigned pix = fast_div(gid, fd_d);
-            float* o = ob + (int64_t)pix * out_pstride + (gid - pix * sp.D) * C;
+    for (int j = 0; j < kSweepDG; ++j) {
+        const f32x4 s = blend_taps(t[j]);
 #pragma unroll
-            for (int c = 0; c < C; ++c) o[c] = v[c];
+        for (int c = 0; c < C; ++c) v[j * C + c] = s[c];
+    }
+    if (STORE == 2) {
+        // dense volume: item g's kSweepDG*C floats sit at g*kSweepDG*C of this view
+#pragma unroll
+        for (int k = 0; k < C; ++k)
+            s_out[threadIdx.x * C + k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+        __syncthreads();
+        const unsigned n4 = per_view * C;  // float4s in this view's volume
+        float4* ov = reinterpret_cast<float4*>(out + (int64_t)b * out_bstride);
+        const unsigned blk0 = blockIdx.x * blockDim.x * C;
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const unsigned i = k * blockDim.x + threadIdx.x;
+            if (blk0 + i < n4) ov[blk0 + i] = s_out[i];
         }
+        return;
+    }
+    float* o = out + (int64_t)b * out_bstride + (int64_t)pix * out_pstride + dg * kSweepDG * C;
+    if (STORE == 1 && (dg + 1) * kSweepDG <= sp.D) {
+#pragma unroll
+        for (int k = 0; k < C; ++k)  // kSweepDG * C floats = C float4
+            reinterpret_cast<float4*>(o)[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    } else {
+        const int nd = min(kSweepDG, sp.D - dg * kSweepDG);
+#pragma unroll
+        for (int j = 0; j < kSweepDG; ++j)
+            if (j < nd)
+#pragma unroll
+                for (int c = 0; c < C; ++c) o[j * C + c] = v[j * C + c];
+    }
+}
+
+// Tile sweep: a block owns 64 consecutive target pixels (flat index) of one view and
+// sweeps them through all depths; lane = pixel, so each tap load of a wave reads ~64
+// consecutive source texels (one depth: near-constant disparity), the access shape
+// the vector L1 serves fastest, instead of texels scattered along 16 epipolar
+// segments.  Results go to an LDS tile [64 pixels][depth chunk * C] (row stride
+// padded to an odd word count: conflict-free 4-B writes) and leave as coalesced
+// 4-B stores along each pixel's output run -- for the bare volume the whole tile is
+// one contiguous run.  Depths are processed in chunks of kTileD so the LDS tile
+// stays <= 64 KiB; the 4 waves take interleaved depths, kSweepDG at a time.
+constexpr int kTileP = 64;  // pixels per block (one per lane)
+constexpr int kTileD = 64;  // depths per LDS chunk
+
+template <int C>
+__global__ __launch_bounds__(256) void plane_sweep_tile_kernel(const float4* __restrict__ img4, SweepParams sp,
+                                                               PadGeom pg, float rc_hs, float rc_ws, FastDiv fd_w,
+                                                               FastDiv fd_run_full, FastDiv fd_run_last,
+                                                               const float* __restrict__ ki,
+                                                               const float* __restrict__ proj,
+                                                               const float* __restrict__ depths,
+                                                               float* __restrict__ out, int64_t out_bstride,
+                                                               int64_t out_pstride) {
+    constexpr int RS = kTileD * C + 1;  // LDS row stride (words): odd -> conflict-free lane-per-row writes
+    __shared__ float s_tile[kTileP * RS];
+    const int npix = sp.Ht * sp.Wt;
+    const int pix0 = blockIdx.x * kTileP;
+    const int b = blockIdx.y;
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+    const int pix = min(pix0 + lane, npix - 1);  // tail lanes recompute the last pixel
+    const unsigned yy = fast_div((unsigned)pix, fd_w);
+    const float fy = (float)(int)yy, fx = (float)(int)(pix - yy * sp.Wt);
+    const float* m = proj + (int64_t)b * 16;
+    float rx, ry, rz;
+    ray(ki + (int64_t)b * 9, fx, fy, rx, ry, rz);  // pixel2cam_torch, utils.py:370
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(img4 + (int64_t)b * pg.plane_bytes / 16, pg.plane_bytes);
+    const int np = min(kTileP, npix - pix0);
+    float* ob = out + (int64_t)b * out_bstride;
+
+    for (int dc0 = 0; dc0 < sp.D; dc0 += kTileD) {
+        const int nd = min(kTileD, sp.D - dc0);
+        // wave w: depths dc0 + w + 4*i, kSweepDG of them per step
+        for (int i0 = 0; i0 * 4 + wave < nd; i0 += kSweepDG) {
+            TapSet t[kSweepDG];
+#pragma unroll
+            for (int j = 0; j < kSweepDG; ++j) {
+                const int dl = min((i0 + j) * 4 + wave, nd - 1);
+                const float dep = depths[dc0 + dl];
+                const float X = rx * dep, Y = ry * dep, Z = rz * dep;
+                const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+                const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+                const float pz = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11];
+                float su, sv;
+                div2_rn(pu, pv, pz + 1e-10f, su, sv);  // cam2pixel_torch, utils.py:388-391
+                const float cx = div_const(su + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
+                const float cy = div_const(sv + 0.5f, sp.fws, rc_ws);  //          y / W
+                issue_taps_padded(r, sp.Ws, sp.Hs, pg.Wp, pg.org, pg.row, unnormalize(to_grid(cx), sp.half_ws),
+                                  unnormalize(to_grid(cy), sp.half_hs), t[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < kSweepDG; ++j) {
+                const int dl = (i0 + j) * 4 + wave;
+                const f32x4 v = blend_taps(t[j]);
+                if (dl < nd) {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) s_tile[lane * RS + dl * C + c] = v[c];
+                }
+            }
+        }
+        __syncthreads();
+        // write out: per pixel a run of nd*C floats at pix*out_pstride + dc0*C
+        const int run = nd * C;
+        const int total = np * run;
+        const FastDiv fd_run = nd == kTileD ? fd_run_full : fd_run_last;  // divides by run
+        for (int k = threadIdx.x; k < total; k += blockDim.x) {
+            const int p = (int)fast_div((unsigned)k, fd_run);
+            const int e = k - p * run;
+            ob[(int64_t)(pix0 + p) * out_pstride + dc0 * C + e] = s_tile[p * RS + e];
+        }
+        __syncthreads();
     }
 }
 

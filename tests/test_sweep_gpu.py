@@ -79,3 +79,42 @@ def test_format_network_input(small, dev):
     out = mv.format_network_input_torch(None, t["ref"].to(dev), t["src"].to(dev), t["ref_pose"].to(dev),
                                         t["src_poses"].to(dev), list(small["fni_planes"]), t["K"].to(dev))
     assert_bits(out.cpu().numpy(), small["fni_out"])
+
+
+@pytest.mark.parametrize("store", [None, "0", "1", "2"])
+def test_plane_sweep_store_modes(store, small, meta, dev, monkeypatch):
+    """The tile sweep kernel (default) and every output-store path of the grouped
+    kernel (scalar, 16-B per lane, LDS-staged dense run; MPIV_SWEEP_STORE selects it)
+    give the reference bits, incl. a partial last depth group (D = 6, 5) and C = 4."""
+    if store is not None:
+        monkeypatch.setenv("MPIV_SWEEP_STORE", store)
+    img = psv_case_input(meta["small"], "psv_a")
+    out = mv.plane_sweep_torch(img.to(dev), list(small["psv_a_depths"]), _t(small, "psv_a_pose", dev),
+                               _t(small, "psv_a_K", dev))
+    assert_bits(out.cpu().numpy(), small["psv_a_out"])
+    img = psv_case_input(meta["small"], "psv_one")
+    out = mv.plane_sweep_torch_one(img.to(dev), list(small["psv_one_depths"]), _t(small, "psv_one_pose", dev),
+                                   _t(small, "psv_one_K", dev))
+    assert_bits(out.cpu().numpy(), small["psv_one_out"])
+    img = psv_case_input(meta["small"], "psv_two")
+    m = meta["small"]["psv_two"]
+    out = mv.plane_sweep_torch_one2(img.to(dev), list(small["psv_two_depths"]), _t(small, "psv_two_pose", dev),
+                                    _t(small, "psv_two_Ks", dev), _t(small, "psv_two_Kt", dev), m["tgt_h"], m["tgt_w"])
+    assert_bits(out.cpu().numpy(), small["psv_two_out"])
+
+
+def test_plane_sweep_many_depths_vs_oracle(dev):
+    """D = 150 (three LDS depth chunks, a partial last one), C = 2, odd sizes, two views:
+    bit-exact to the oracle."""
+    from mpi_vision_amd import _host
+    from oracle import oracle
+    g = torch.Generator().manual_seed(12)
+    B, H, W, C, D = 2, 37, 83, 2, 150
+    img = torch.rand((B, H, W, C), generator=g)
+    K = configs.f32([configs.intrinsics_matrix(50.0, 52.0, 41.0, 18.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(2.0 * k - 1), (0.1 * k - 0.05, 0.02, 0.01)) for k in range(B)])
+    depths = configs.inv_depths(0.7, 60, D)
+    out = mv.plane_sweep_torch(img.to(dev), depths, poses.to(dev), K.to(dev))
+    ki, proj = _host.psv_matrices(K, K, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, H, W)
+    assert_bits(out.cpu().numpy(), want)

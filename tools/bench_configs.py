@@ -113,13 +113,23 @@ def c3(dev, it, wu):
     ms, mn = timed(fn, it, wu)
     report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, generic strided kernel", ms, mn, alg,
            extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
-    img4 = torch.empty((S, H, W, 4), device=dev)
-    pad = lambda: _lib._call("mpiv_pad_texels", img, _lib._strides(img), S, H, W, 3, img4, _lib._stream(dev))  # noqa: E731
+    img4 = _lib.pad_texels(img)  # [S, H+4, W+4, 4]
+    pad = lambda: _lib.pad_texels(img, out=img4)  # noqa: E731
     sweep = lambda: _lib._call("mpiv_plane_sweep_padded", img4, S, H, W, 3, ki, proj, d, D, H, W, out,  # noqa: E731
                                _lib._stream(dev))
+    pad()
+    ms, mn = timed(lambda: out.fill_(1.0), it, wu)
+    report(f"c3 write-bandwidth reference: torch fill_ of the {S}x{H}x{W}x{D * 3} volume", ms, mn,
+           S * D * H * W * 12)
     ms, mn = timed(sweep, it, wu)
-    report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, padded-texel kernel", ms, mn, alg,
+    report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, tile kernel (default)", ms, mn, alg,
            extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
+    for store in ("0", "1", "2"):
+        os.environ["MPIV_SWEEP_STORE"] = store
+        ms, mn = timed(sweep, it, wu)
+        report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, padded-texel kernel, store mode {store}", ms, mn, alg,
+               extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
+    del os.environ["MPIV_SWEEP_STORE"]
     ms, mn = timed(lambda: (pad(), sweep()), it, wu)
     report("c3 PSV plane_sweep_torch path (pad + padded kernel)", ms, mn, alg,
            extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
