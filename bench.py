@@ -43,7 +43,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--views", type=int, default=125, help="views rendered per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
-    ap.add_argument("--kernel", choices=["packed", "packed_lds", "native"], default="packed")
+    ap.add_argument("--kernel", choices=["packed", "packed_mv", "packed_lds", "native"], default="packed",
+                    help="packed: direct-gather kernel on the packed MPI (default); packed_mv: multi-view "
+                         "LDS kernel (A/B); packed_lds: single-view LDS variant (A/B); native: reference "
+                         "layout read in place")
     return ap.parse_args()
 
 
@@ -80,14 +83,17 @@ def barrier(world):
         dist.barrier()
 
 
-def load_traffic(profile_dir: str):
+def load_traffic(profile_dir: str, kernel: str, views: int):
     """Per-launch HBM bytes of the render kernel from the committed rocprofv3 PMC
-    summary (tools/profile.sh), corrected as MI355X_MICROARCH.md §HBM prescribes."""
+    summary of this same bench command (tools/profile.sh), corrected as
+    MI355X_MICROARCH.md §HBM prescribes; None when no summary matches."""
     path = os.path.join(profile_dir, "render_pmc.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
+    if d.get("kernel") != kernel or d.get("views", views) != views:
+        return None
     return d.get("hbm_bytes_per_launch")
 
 
@@ -118,6 +124,8 @@ def cpu_baseline(mpi_dev: torch.Tensor, homs_all: torch.Tensor, budget_s: float,
 
 def main():
     args = parse()
+    if args.kernel == "packed_mv":
+        os.environ["MPIV_RENDER_MV"] = "1"  # read by libmpiv's dispatch (A/B hook)
     world, rank, dev = dist_setup(args)
     torch.cuda.set_device(dev)
     c4 = configs.config4()
@@ -133,6 +141,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     packed = _lib.pack_planes(view) if args.kernel.startswith("packed") else None
+    kernel_name = {"packed": "render_packed_kernel", "packed_lds": "render_lds_kernel", "native": "render_native_kernel",
+                   "packed_mv": "render_mv_kernel" if V >= 4 else "render_packed_kernel"}[args.kernel]
     entry = "mpiv_render_packed_lds" if args.kernel == "packed_lds" else "mpiv_render_packed"
     torch.cuda.synchronize()
     pack_ms = (time.perf_counter() - t0) * 1e3
@@ -204,7 +214,7 @@ def main():
     value = mpix_total / elapsed
     alg_bytes = V * (P * H * W * 16 + H * W * 12)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(os.path.join(REPO, "profiles"))
+    traffic = load_traffic(os.path.join(REPO, "profiles"), kernel_name, V)
 
     if rank == 0:
         res = {
@@ -218,10 +228,13 @@ def main():
                        "views_per_s": round(value / (H * W / 1e6), 2), "pack_ms_once": round(pack_ms, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": {"packed": "render_packed_kernel", "packed_lds": "render_lds_kernel"}.get(
-                             args.kernel, "render_native_kernel"),
+                         "kernel": kernel_name,
                          "kernel_ms_per_launch": round(kern_ms, 3),
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes,
+                         "note": "achieved = algorithmic bytes (P*H*W*16 + H*W*12 per view) / kernel time; "
+                                 "frac > 1 because the views of one launch re-read the same MPI texels from L2 "
+                                 "(traffic = HBM bytes actually moved, PMC); the kernel is bound by its texture "
+                                 "path and VALU issue, not HBM (DESIGN.md section 4)"},
             "cpu_baseline": None,
         }
         if world == 1 and args.cpu_seconds > 0:

@@ -11,6 +11,7 @@
 #include "../../include/mpiv.h"
 #include "render.hip"
 #include "render_lds.hip"
+#include "render_mv.hip"
 #include "render_bwd.hip"
 #include "sweep.hip"
 #include "geometry.hip"
@@ -37,6 +38,16 @@ int launched(const char* what) {
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+// A/B and test hooks read from the environment (never needed in production use):
+//   MPIV_RENDER_MV=1      launches of >= 4 views use the multi-view LDS kernel (render_mv.hip)
+//   MPIV_SWEEP_TILE=1     the sweep uses the tile kernel; MPIV_SWEEP_STORE=k the grouped one
+//   MPIV_BOX_SHRINK=k     LDS-staged kernels stage boxes k texels narrower per side, which
+//                         forces their per-sample global fallback (tests)
+int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return (e && *e) ? atoi(e) : dflt;
+}
 
 constexpr int64_t kMaxGridYZ = 65535;
 constexpr int64_t kMaxGridX = 2147483647;
@@ -108,6 +119,19 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             render_lds_kernel<true, true><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
         else
             render_lds_kernel<false, true><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
+        return launched(nm);
+    }
+    // several views of one MPI: the multi-view LDS-staged kernel (render_mv.hip) on request
+    // (A/B: it ties the direct kernel on a camera path)
+    if (variant == 0 && fast && V >= kMMinViews && p_end - p_begin <= kMMaxP && env_int("MPIV_RENDER_MV", 0)) {
+        const int64_t nb = (int64_t)blocks(W, kMTX) * blocks(H, kMTY) * ((V + kMVB - 1) / kMVB);
+        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+        const int shrink = env_int("MPIV_BOX_SHRINK", 0);
+        const dim3 grid((unsigned)nb), blk(kMThreads);
+        if (ct)
+            render_mv_kernel<true><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, shrink, homs, out);
+        else
+            render_mv_kernel<false><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, shrink, homs, out);
         return launched(nm);
     }
     const int64_t nblocks = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;
@@ -307,12 +331,28 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
     const bool vec = aligned16(out) && out_pstride % 4 == 0 && out_bstride % 4 == 0;
     const bool dense = vec && out_pstride == (int64_t)NG * kSweepDG * C;
     int store = dense ? 2 : vec ? 1 : 0;
-    bool tile = true;
-    if (const char* e = getenv("MPIV_SWEEP_STORE")) {  // A/B only: the grouped kernel's store modes
-        store = min(store, atoi(e));
-        tile = false;
-    }
+    const char* e_store = getenv("MPIV_SWEEP_STORE");  // A/B only: the grouped kernel's store modes
+    const bool tile = !e_store && (env_int("MPIV_SWEEP_TILE", 0) || D > kSweepMaxLdsD);
+    if (e_store) store = min(store, atoi(e_store));
     hipStream_t q = S(stream);
+    if (!e_store && !tile) {
+        // default: source footprint staged in LDS (plane_sweep_lds_kernel)
+        const int64_t tiles = (int64_t)((Wt + kSLP - 1) / kSLP) * ((Ht + kSLR - 1) / kSLR);
+        if (tiles > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: too large");
+        const dim3 lgrid((unsigned)tiles, B, 1);
+        const int shrink = env_int("MPIV_BOX_SHRINK", 0);
+#define MPIV_LDS(CC)                                                                                          \
+    plane_sweep_lds_kernel<CC><<<lgrid, kSLThreads, 0, q>>>(im, sp, pg, rc_hs, rc_ws, fd_g, ki, proj, depths, out, \
+                                                     out_bstride, out_pstride, (int)vec, shrink)
+        switch (C) {
+            case 1: MPIV_LDS(1); break;
+            case 2: MPIV_LDS(2); break;
+            case 3: MPIV_LDS(3); break;
+            default: MPIV_LDS(4); break;
+        }
+#undef MPIV_LDS
+        return launched("mpiv_plane_sweep_padded");
+    }
     if (tile) {
         const int npix = Ht * Wt;
         const int last = D - ((D - 1) / kTileD) * kTileD;  // depths in the last chunk

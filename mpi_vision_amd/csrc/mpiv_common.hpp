@@ -112,6 +112,17 @@ __device__ __forceinline__ void div2_rn(float u, float v, float w, float& qu, fl
     }
 }
 
+// div2_rn's fast path alone (valid for every lane where div2_safe holds).  Kernels that
+// keep several samples in flight run it for all of them and patch the rare unsafe lanes
+// afterwards, so the common path has no branch between the samples.
+__device__ __forceinline__ void div2_fast(float u, float v, float w, float& qu, float& qv) {
+    float y = __builtin_amdgcn_rcpf(w);
+    const float e = __builtin_fmaf(-w, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    qu = div_core(u, w, y);
+    qv = div_core(v, w, y);
+}
+
 // divide_safe_torch (utils.py:35-39) fused with div2_rn: w == 0 -> w + 1e-8, then u/w, v/w.
 // The guard lives in the rare branch only: w == 0 fails div2_safe.
 __device__ __forceinline__ void divide_safe2(float u, float v, float w, float& qu, float& qv) {
@@ -279,6 +290,80 @@ __device__ __forceinline__ f32x4 blend_taps(const TapSet& t) {
         o[k] = acc;
     }
     return o;
+}
+
+// ---------------------------------------------------------------------------
+// bilinear taps from a footprint staged in LDS (render_mv.hip, sweep.hip)
+// ---------------------------------------------------------------------------
+
+// A staged box holds `rows` rows of `pitch` consecutive texels of a padded plane whose
+// first texel is image texel (xl, yl) (xl, yl >= -2; the last staged row is <= H+1).
+// A tap origin (floor px, floor py) is served from LDS when both of its columns and
+// both of its rows are staged and neither column lies past the padded row end W+1
+// (staged texels beyond it belong to the next padded row): x0 - xl in [0, xspan],
+// y0 - yl in [0, yspan].
+struct LdsBox {
+    float xl, yl;        // box origin (image texel coordinates)
+    float xspan, yspan;  // largest tap-origin offsets served from LDS
+    int pitch;           // staged row pitch (texels)
+};
+
+__device__ __forceinline__ LdsBox make_lds_box(int xl, int yl, int rows, int pitch, int W) {
+    LdsBox b;
+    b.xl = (float)xl;
+    b.yl = (float)yl;
+    b.xspan = (float)(min(xl + pitch - 2, W) - xl);
+    b.yspan = (float)(rows - 2);
+    b.pitch = pitch;
+    return b;
+}
+
+// First half of lds_sample: the weights and the four tap reads (in flight on return).
+__device__ __forceinline__ bool lds_issue(const float4* __restrict__ tex, const LdsBox& b, float px, float py,
+                                          TapSet& t) {
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
+    const float rx = fx0 - b.xl, ry = fy0 - b.yl;  // exact wherever the origin can be staged
+    const float ix = __builtin_amdgcn_fmed3f(rx, 0.0f, b.xspan);
+    const float iy = __builtin_amdgcn_fmed3f(ry, 0.0f, b.yspan);
+    const float4* st = tex + (int)__builtin_fmaf(iy, (float)b.pitch, ix);  // < rows * pitch: exact
+    t.a = *reinterpret_cast<const f32x4*>(st);
+    t.b = *reinterpret_cast<const f32x4*>(st + 1);
+    t.c = *reinterpret_cast<const f32x4*>(st + b.pitch);
+    t.d = *reinterpret_cast<const f32x4*>(st + b.pitch + 1);
+    return (ix == rx) & (iy == ry);
+}
+
+// One bilinear sample from the staged box, with the weights and fma chain of
+// issue_taps_padded + blend_taps.  Returns false when the tap origin is not staged
+// (outside the box, or NaN): the LDS reads were clamped into the box, their result is
+// meaningless, and the caller gathers that sample from global memory instead -- so a
+// staged kernel is bit-identical to the direct one whatever the box covers.
+__device__ __forceinline__ bool lds_sample(const float4* __restrict__ tex, const LdsBox& b, float px, float py,
+                                           f32x4& s) {
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    TapSet t;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
+    const float rx = fx0 - b.xl, ry = fy0 - b.yl;  // exact wherever the origin can be staged
+    const float ix = __builtin_amdgcn_fmed3f(rx, 0.0f, b.xspan);
+    const float iy = __builtin_amdgcn_fmed3f(ry, 0.0f, b.yspan);
+    const float4* st = tex + (int)__builtin_fmaf(iy, (float)b.pitch, ix);  // < rows * pitch: exact
+    t.a = *reinterpret_cast<const f32x4*>(st);
+    t.b = *reinterpret_cast<const f32x4*>(st + 1);
+    t.c = *reinterpret_cast<const f32x4*>(st + b.pitch);
+    t.d = *reinterpret_cast<const f32x4*>(st + b.pitch + 1);
+    s = blend_taps(t);
+    return (ix == rx) & (iy == ry);
 }
 
 }  // namespace mpiv

@@ -279,6 +279,278 @@ __global__ __launch_bounds__(256) void plane_sweep_tile_kernel(const float4* __r
     }
 }
 
+// depth `dep` along a camera ray -> source sample position, the fast exact form of
+// sweep_pos (u/den and v/den share one reciprocal, the two launch-constant divisions use
+// div_const); den = pz + 1e-10 is returned for the LDS sweep's sign test
+__device__ __forceinline__ void sweep_pos_fast(const float* __restrict__ m, float rx, float ry, float rz,
+                                               float dep, const SweepParams& sp, float rc_hs, float rc_ws,
+                                               float& px, float& py, float& den) {
+    const float X = rx * dep, Y = ry * dep, Z = rz * dep;
+    const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+    const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+    const float pz = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11];
+    den = pz + 1e-10f;
+    float su, sv;
+    div2_rn(pu, pv, den, su, sv);  // cam2pixel_torch, utils.py:388-391
+    const float cx = div_const(su + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
+    const float cy = div_const(sv + 0.5f, sp.fws, rc_ws);  //          y / W
+    px = unnormalize(to_grid(cx), sp.half_ws);
+    py = unnormalize(to_grid(cy), sp.half_hs);
+}
+
+// LDS-staged sweep (the default for C <= 4, D <= kSweepMaxLdsD).  A block owns a tile of
+// kSLR target rows x kSLP pixels of one view and sweeps it through ALL depths, so each of
+// its row segments is one contiguous run of the volume (np * D * C floats for the bare
+// volume).  Its source footprint is small and known up front: cam2pixel's homogeneous
+// point (pu, pv, pz) is affine in x, in y and in the depth separately, so while
+// pz + 1e-10 keeps its sign -- trilinear, so its 8 vertex values decide -- every sample
+// of the tile lies in the convex hull of the images of the 8 vertices (x first | last) x
+// (row first | last) x (depth min | max): for a fixed depth the tile maps by a homography
+// onto the hull of its corners, for a fixed pixel the depths map onto a segment.  The box
+// [floor(min) - 1, floor(max) + 2] of the 8 computed vertex positions (render_lds.hip's
+// margin argument) is staged in LDS once, and the tile's samples read their taps there:
+// the vector-L1 tap traffic (64 B per sample, what bounds the global-gather kernels
+// above) shrinks to one box fill per block.  A sample whose tap origin is not staged
+// (image borders, rounding at ill-conditioned geometry, NaN) is gathered from global
+// memory (lds_sample), and a block whose box is invalid or too large gathers everything
+// from global memory: the output is bit-identical whatever the geometry.
+//
+// Stores: a lane's kSweepDG*C results are one 16*C-byte piece and a wave's 64 pieces are
+// one contiguous run of the bare volume, but 16-B stores at a 16*C-byte lane stride
+// reach the L2 as ~C times more, partial, write requests (measured 4x the tile kernel's).
+// So a wave whose 64 groups are complete and dense passes its pieces through a per-wave
+// LDS slot and stores the run with lane-contiguous 16-B stores.
+constexpr int kSLP = 64;                           // target pixels per tile row
+constexpr int kSLR = 4;                            // target rows per tile
+constexpr int kSLThreads = 512;                    // 8 waves
+constexpr int kSLCap = 2560;                       // staged source texels (40 KiB)
+constexpr int kSLFill = kSLCap / kSLThreads;       // staged texels per thread
+
+// wave-scope LDS ordering: every lane's LDS stores before any lane's later loads
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int C>
+__global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
+    const float4* __restrict__ img4, SweepParams sp, PadGeom pg, float rc_hs, float rc_ws, FastDiv fd_g,
+    const float* __restrict__ ki, const float* __restrict__ proj, const float* __restrict__ depths,
+    float* __restrict__ out, int64_t out_bstride, int64_t out_pstride, int vec, int shrink) {
+    constexpr int kWaves = kSLThreads / kWave;
+    __shared__ __attribute__((aligned(16))) float4 s_src[kSLCap];
+    __shared__ float s_dep[kSweepMaxLdsD];
+    __shared__ float s_ext[3][kWaves];  // per wave: min depth, max depth, non-finite depth seen
+    __shared__ int4 s_box;              // x_lo, y_lo, rows, pitch (0: gather from global memory)
+    __shared__ __attribute__((aligned(16))) float4 s_out[kWaves][kWave * C];  // per wave: its run
+    const int segs = (sp.Wt + kSLP - 1) / kSLP;
+    const int b = blockIdx.y;
+    const int ty = blockIdx.x / segs;
+    const int y0 = ty * kSLR, x0 = (blockIdx.x - ty * segs) * kSLP;
+    const int np = min(kSLP, sp.Wt - x0), nr = min(kSLR, sp.Ht - y0);
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+    const float* k9 = ki + (int64_t)b * 9;
+    const float* m = proj + (int64_t)b * 16;
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(img4 + (int64_t)b * (pg.plane_bytes / 16), pg.plane_bytes);
+
+    // depths -> LDS, with their range
+    float dlo = __builtin_inff(), dhi = -__builtin_inff(), bad = 0.0f;
+    for (int i = threadIdx.x; i < sp.D; i += kSLThreads) {
+        const float d = depths[i];
+        s_dep[i] = d;
+        dlo = fminf(dlo, d);
+        dhi = fmaxf(dhi, d);
+        bad = __builtin_isfinite(d) ? bad : 1.0f;
+    }
+#pragma unroll
+    for (int k = 1; k < kWave; k <<= 1) {
+        dlo = fminf(dlo, __shfl_xor(dlo, k));
+        dhi = fmaxf(dhi, __shfl_xor(dhi, k));
+        bad = fmaxf(bad, __shfl_xor(bad, k));
+    }
+    if (lane == 0) {
+        s_ext[0][wave] = dlo;
+        s_ext[1][wave] = dhi;
+        s_ext[2][wave] = bad;
+    }
+    __syncthreads();
+    if (wave == 0) {  // vertex = lane % 8: (first | last pixel) x (first | last row) x (min | max depth)
+        float dmin = s_ext[0][0], dmax = s_ext[1][0], dbad = s_ext[2][0];
+#pragma unroll
+        for (int w = 1; w < kWaves; ++w) {
+            dmin = fminf(dmin, s_ext[0][w]);
+            dmax = fmaxf(dmax, s_ext[1][w]);
+            dbad = fmaxf(dbad, s_ext[2][w]);
+        }
+        const int vtx = lane & 7;
+        float rx, ry, rz;
+        ray(k9, (float)((vtx & 1) ? x0 + np - 1 : x0), (float)((vtx & 2) ? y0 + nr - 1 : y0), rx, ry, rz);
+        float px, py, den;
+        sweep_pos_fast(m, rx, ry, rz, (vtx & 4) ? dmax : dmin, sp, rc_hs, rc_ws, px, py, den);
+        const bool fin = dbad == 0.0f && __builtin_isfinite(px) && __builtin_isfinite(py) &&
+                         __builtin_fabsf(px) < 1e7f && __builtin_fabsf(py) < 1e7f;
+        float xmin = floorf(px), xmax = xmin, ymin = floorf(py), ymax = ymin;
+        int pos = fin && den > 0.0f, neg = fin && den < 0.0f;
+#pragma unroll
+        for (int k = 1; k < 8; k <<= 1) {
+            xmin = fminf(xmin, __shfl_xor(xmin, k));
+            xmax = fmaxf(xmax, __shfl_xor(xmax, k));
+            ymin = fminf(ymin, __shfl_xor(ymin, k));
+            ymax = fmaxf(ymax, __shfl_xor(ymax, k));
+            pos &= __shfl_xor(pos, k);
+            neg &= __shfl_xor(neg, k);
+        }
+        if (lane == 0) {
+            const bool ok = pos || neg;
+            const int xl = ok ? max((int)xmin - 1 + shrink, -2) : 0;
+            const int xh = ok ? min((int)xmax + 2 - shrink, sp.Ws + 1) : 0;
+            const int yl = ok ? max((int)ymin - 1 + shrink, -2) : 0;
+            const int yh = ok ? min((int)ymax + 2 - shrink, sp.Hs + 1) : 0;
+            const int width = xh - xl + 1, rows = yh - yl + 1;
+            const bool fits = ok && width >= 2 && rows >= 2 && width <= kSLCap && rows <= kSLCap &&
+                              width * rows <= kSLCap;
+            s_box = make_int4(xl, yl, rows, fits ? width : 0);
+        }
+    }
+    __syncthreads();
+    const int xl = __builtin_amdgcn_readfirstlane(s_box.x), yl = __builtin_amdgcn_readfirstlane(s_box.y);
+    const int rows = __builtin_amdgcn_readfirstlane(s_box.z), pitch = __builtin_amdgcn_readfirstlane(s_box.w);
+    if (pitch > 0) {  // fill: box texel idx = row * pitch + col <- padded-plane texel
+        const int nfp = rows * pitch;
+        const float rp = 1.0f / (float)pitch;
+        const int org = (yl + kPad) * pg.Wp + xl + kPad;  // >= 0: boxes start at -2
+        f32x4 stg[kSLFill];
+#pragma unroll
+        for (int k = 0; k < kSLFill; ++k) {
+            if (kSLThreads * k < nfp) {
+                const int idx = threadIdx.x + kSLThreads * k;
+                int row = (int)((float)idx * rp);  // idx < 2^12: off by at most one, corrected
+                row -= row * pitch > idx ? 1 : 0;
+                row += (row + 1) * pitch <= idx ? 1 : 0;
+                stg[k] = llvm_raw_buffer_load_v4f32(r, (org + row * pg.Wp + idx - row * pitch) * 16, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kSLFill; ++k)
+            if (kSLThreads * k < nfp) *reinterpret_cast<f32x4*>(&s_src[threadIdx.x + kSLThreads * k]) = stg[k];
+    }
+    __syncthreads();
+
+    // samples: item group g -> (tile row g / (np*NG); pixel, depths kSweepDG*dg ...), groups fastest
+    const int NG = (sp.D + kSweepDG - 1) / kSweepDG;
+    const int nrow = np * NG;  // groups per tile row
+    const int ngr = nr * nrow;
+    const LdsBox lbx = make_lds_box(xl, yl, rows, pitch, sp.Ws);
+    // every group complete and pixels packed: each tile row's output is one dense run
+    const bool dense = vec && sp.D % kSweepDG == 0 && out_pstride == (int64_t)sp.D * C;
+    for (int gi = threadIdx.x; gi < ngr; gi += kSLThreads) {
+        int tr = 0;  // tile row of group gi
+#pragma unroll
+        for (int k = 1; k < kSLR; ++k) tr += gi >= k * nrow ? 1 : 0;
+        const int gr = gi - tr * nrow;
+        const unsigned pl = fast_div((unsigned)gr, fd_g);
+        const int dg = gr - (int)pl * NG;
+        float* ob = out + (int64_t)b * out_bstride + ((int64_t)(y0 + tr) * sp.Wt + x0) * out_pstride;
+        float rx, ry, rz;
+        ray(k9, (float)(x0 + (int)pl), (float)(y0 + tr), rx, ry, rz);  // pixel2cam_torch, utils.py:370
+        // The kSweepDG samples run phase by phase (all positions, all tap reads, all
+        // blends) with the rare fix-ups behind wave-uniform tests, so their LDS reads are
+        // in flight together instead of one round trip per sample.
+        float su[kSweepDG], sv[kSweepDG];
+        bool fast = true;
+#pragma unroll
+        for (int j = 0; j < kSweepDG; ++j) {
+            const float dep = s_dep[min(dg * kSweepDG + j, sp.D - 1)];  // a partial last group repeats D-1
+            const float X = rx * dep, Y = ry * dep, Z = rz * dep;
+            const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+            const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+            const float den = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11] + 1e-10f;
+            fast = fast && div2_safe(pu, pv, den);
+            div2_fast(pu, pv, den, su[j], sv[j]);  // cam2pixel_torch, utils.py:388-391
+        }
+        if (__builtin_amdgcn_ballot_w64(!fast)) {  // rare: a quotient outside the fast path's range
+#pragma unroll
+            for (int j = 0; j < kSweepDG; ++j) {
+                const float dep = s_dep[min(dg * kSweepDG + j, sp.D - 1)];
+                const float X = rx * dep, Y = ry * dep, Z = rz * dep;
+                const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+                const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+                const float den = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11] + 1e-10f;
+                if (!div2_safe(pu, pv, den)) {
+                    su[j] = div_rn(pu, den);
+                    sv[j] = div_rn(pv, den);
+                }
+            }
+        }
+        float px[kSweepDG], py[kSweepDG];
+#pragma unroll
+        for (int j = 0; j < kSweepDG; ++j) {
+            const float cx = div_const(su[j] + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
+            const float cy = div_const(sv[j] + 0.5f, sp.fws, rc_ws);  //          y / W
+            px[j] = unnormalize(to_grid(cx), sp.half_ws);
+            py[j] = unnormalize(to_grid(cy), sp.half_hs);
+        }
+        f32x4 s[kSweepDG];
+        bool staged = pitch > 0;
+        if (staged) {
+            TapSet ts[kSweepDG];
+#pragma unroll
+            for (int j = 0; j < kSweepDG; ++j) staged = lds_issue(s_src, lbx, px[j], py[j], ts[j]) && staged;
+#pragma unroll
+            for (int j = 0; j < kSweepDG; ++j) s[j] = blend_taps(ts[j]);
+        }
+        if (__builtin_amdgcn_ballot_w64(!staged)) {  // wave-uniform test, then per lane
+            if (!staged) {                            // a tap origin not staged: gather from global memory
+                TapSet ts[kSweepDG];
+#pragma unroll
+                for (int j = 0; j < kSweepDG; ++j)
+                    issue_taps_padded(r, sp.Ws, sp.Hs, pg.Wp, pg.org, pg.row, px[j], py[j], ts[j]);
+#pragma unroll
+                for (int j = 0; j < kSweepDG; ++j) s[j] = blend_taps(ts[j]);
+            }
+        }
+        float v[kSweepDG * C];
+#pragma unroll
+        for (int j = 0; j < kSweepDG; ++j)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[j * C + c] = s[j][c];
+        // the wave's first group, and its offset in that group's tile row (wave-uniform)
+        const int gw = __builtin_amdgcn_readfirstlane(gi - lane);
+        int g0 = gw;
+#pragma unroll
+        for (int k = 1; k < kSLR; ++k) g0 -= gw >= k * nrow ? nrow : 0;
+        if (dense && g0 + kWave <= nrow) {  // all 64 groups in one tile row
+            // the wave's 64 pieces are the contiguous run ob[g0*4C .. (g0+64)*4C): through
+            // LDS, then lane-contiguous 16-B stores
+            float4* so = s_out[wave];
+            wave_lds_sync();  // the previous iteration's reads of the slot are done
+#pragma unroll
+            for (int k = 0; k < C; ++k)
+                so[lane * C + k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+            wave_lds_sync();
+            float4* run = reinterpret_cast<float4*>(ob + (int64_t)g0 * kSweepDG * C);
+#pragma unroll
+            for (int k = 0; k < C; ++k) run[k * kWave + lane] = so[k * kWave + lane];
+        } else {
+            float* o = ob + (int64_t)pl * out_pstride + dg * kSweepDG * C;
+            if (vec && (dg + 1) * kSweepDG <= sp.D) {
+#pragma unroll
+                for (int k = 0; k < C; ++k)  // kSweepDG * C floats = C float4
+                    reinterpret_cast<float4*>(o)[k] =
+                        make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+            } else {
+                const int nd = min(kSweepDG, sp.D - dg * kSweepDG);
+#pragma unroll
+                for (int j = 0; j < kSweepDG; ++j)
+                    if (j < nd)
+#pragma unroll
+                        for (int c = 0; c < C; ++c) o[j * C + c] = v[j * C + c];
+            }
+        }
+    }
+}
+
 // projective_inverse_warp_torch[2] with a per-pixel depth map [B, Ht, Wt] (any
 // strides) -> [B, Ht, Wt, C]
 __global__ __launch_bounds__(256) void inverse_warp_kernel(const float* __restrict__ img, ImgStrides s,

@@ -192,3 +192,78 @@ def test_lds_kernel_extreme_poses(dev):
     out = torch.empty_like(got)
     _lib._call("mpiv_render_packed_lds", packed, H, W, P, homs.to(dev), V, out, _lib._stream(dev))
     assert_bits(out.cpu().numpy(), want)
+
+
+def _multiview_case(V, seed=7):
+    """A camera-path stretch plus large rotations / translations (planes partly behind
+    the camera) on an odd-sized MPI: V views, homographies, oracle frames."""
+    from mpi_vision_amd import _host
+    g = torch.Generator().manual_seed(seed)
+    H, W, P = 70, 150, 9
+    mpi = configs.synthetic_mpi(1, H, W, P, 4)
+    n_path = max(V - 5, 1)
+    poses = [configs.pose_from(configs.rot_y(0.3 * k), (0.01 * k, -0.005 * k, 0.002 * k)) for k in range(n_path)]
+    for k in range(V - n_path):
+        t = ((torch.rand(3, generator=g) - 0.5) * (0.5 + k)).tolist()
+        poses.append(configs.pose_from(configs.rot_y((k - 2) * 15.0), t))
+    poses = configs.f32(poses)
+    K = configs.f32([configs.intrinsics_matrix(90.0, 95.0, 70.0, 33.0)] * V)
+    depths = configs.f32(configs.inv_depths(0.3, 30, P))
+    homs = _host.render_homographies(poses, depths, K, V)
+    return mpi, homs
+
+
+@pytest.mark.parametrize("shrink", ["0", "2"])
+def test_multiview_kernel_bit_exact(shrink, dev, monkeypatch):
+    """render_mv_kernel (MPIV_RENDER_MV=1, >= 4 views per launch): 11 views = a full group
+    of 8 + a partial one, bit-exact to the oracle and to the direct-gather kernel (the
+    default).  MPIV_BOX_SHRINK=2 stages every box 2 texels narrower per side than the
+    footprint, which forces the per-sample global fallback on most samples."""
+    monkeypatch.setenv("MPIV_BOX_SHRINK", shrink)
+    monkeypatch.setenv("MPIV_RENDER_MV", "1")
+    mpi, homs = _multiview_case(11)
+    V, P = homs.shape[0], homs.shape[1]
+    H, W = mpi.shape[1], mpi.shape[2]
+    want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.numpy())
+    packed = _lib.pack_planes(mpi[0].to(dev))
+    assert_bits(_lib.render_packed(packed, homs).cpu().numpy(), want, "multi-view")
+    monkeypatch.delenv("MPIV_RENDER_MV")
+    assert_bits(_lib.render_packed(packed, homs).cpu().numpy(), want, "direct")
+
+
+@pytest.mark.parametrize("mv", ["0", "1"])
+def test_multiview_camera_path_many_views(mv, dev, monkeypatch):
+    """A config-4-style sway path (40 consecutive poses of the 1000-pose path, 24 planes,
+    viewer camera) rendered in one launch by the direct and the multi-view kernel:
+    bit-exact."""
+    monkeypatch.setenv("MPIV_RENDER_MV", mv)
+    from mpi_vision_amd import _host
+    H, W, P, V = 96, 160, 24, 40
+    mpi = configs.synthetic_mpi(1, H, W, P, 9)
+    f = configs.focal_from_fov(W)
+    poses = configs.f32(configs.sway_path(1000)[100:100 + V])
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * V)
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(1, 100, P)), K, V)
+    want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.numpy())
+    got = _lib.render_packed(_lib.pack_planes(mpi[0].to(dev)), homs)
+    assert_bits(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("mv", ["0", "1"])
+def test_multiview_ct_partials(mv, dev, monkeypatch):
+    """Plane-range (C, T) partials of 6 views (direct and multi-view kernel) equal the
+    oracle's bit for bit, and their ordered combine equals the sequential render (1e-5)."""
+    monkeypatch.setenv("MPIV_RENDER_MV", mv)
+    mpi, homs = _multiview_case(6, seed=3)
+    V, P = homs.shape[0], homs.shape[1]
+    H, W = mpi.shape[1], mpi.shape[2]
+    full = mpi.expand(V, H, W, P, 4).numpy()
+    packed = _lib.pack_planes(mpi[0].to(dev))
+    cuts = [0, 4, 7, P]
+    parts = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        ct = _lib.render_packed_ct(packed, homs, back=(a == 0), p_begin=a, p_end=b)
+        assert_bits(ct.cpu().numpy(), oracle.render_ct(full, homs.numpy(), a, b, back=(a == 0)), f"ct [{a},{b})")
+        parts.append(ct)
+    got = _lib.combine_ct(torch.stack(parts)).cpu().numpy()
+    np.testing.assert_allclose(got, oracle.render(full, homs.numpy()), rtol=0, atol=1e-5)

@@ -81,12 +81,17 @@ def test_format_network_input(small, dev):
     assert_bits(out.cpu().numpy(), small["fni_out"])
 
 
-@pytest.mark.parametrize("store", [None, "0", "1", "2"])
+@pytest.mark.parametrize("store", [None, "shrink", "tile", "0", "1", "2"])
 def test_plane_sweep_store_modes(store, small, meta, dev, monkeypatch):
-    """The tile sweep kernel (default) and every output-store path of the grouped
-    kernel (scalar, 16-B per lane, LDS-staged dense run; MPIV_SWEEP_STORE selects it)
-    give the reference bits, incl. a partial last depth group (D = 6, 5) and C = 4."""
-    if store is not None:
+    """The LDS-staged sweep (default; "shrink" forces its per-sample global fallback),
+    the tile kernel, and every output-store path of the grouped kernel (scalar, 16-B per
+    lane, LDS-staged dense run; MPIV_SWEEP_STORE selects it) give the reference bits,
+    incl. a partial last depth group (D = 6, 5)."""
+    if store == "shrink":
+        monkeypatch.setenv("MPIV_BOX_SHRINK", "2")
+    elif store == "tile":
+        monkeypatch.setenv("MPIV_SWEEP_TILE", "1")
+    elif store is not None:
         monkeypatch.setenv("MPIV_SWEEP_STORE", store)
     img = psv_case_input(meta["small"], "psv_a")
     out = mv.plane_sweep_torch(img.to(dev), list(small["psv_a_depths"]), _t(small, "psv_a_pose", dev),
@@ -118,3 +123,41 @@ def test_plane_sweep_many_depths_vs_oracle(dev):
     ki, proj = _host.psv_matrices(K, K, poses)
     want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, H, W)
     assert_bits(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("C", [1, 4])
+@pytest.mark.parametrize("shrink", ["0", "3"])
+def test_plane_sweep_lds_vs_oracle(C, shrink, dev, monkeypatch):
+    """The LDS-staged sweep with C = 1 and 4, a target size whose rows end in a partial
+    64-pixel segment, separate source / target intrinsics and sizes (the _one2 geometry):
+    bit-exact to the oracle, also with every staged box shrunk (MPIV_BOX_SHRINK: most
+    samples take the per-sample global fallback)."""
+    from mpi_vision_amd import _host, _lib
+    from oracle import oracle
+    monkeypatch.setenv("MPIV_BOX_SHRINK", shrink)
+    g = torch.Generator().manual_seed(31 + C)
+    B, Hs, Ws, D, Ht, Wt = 2, 45, 97, 11, 38, 131
+    img = torch.rand((B, Hs, Ws, C), generator=g)
+    Ks = configs.f32([configs.intrinsics_matrix(60.0, 61.0, 48.0, 22.0)] * B)
+    Kt = configs.f32([configs.intrinsics_matrix(80.0, 79.0, 65.0, 19.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(3.0 * k - 1.5), (0.2 * k - 0.1, 0.03, -0.02))
+                         for k in range(B)])
+    depths = configs.inv_depths(0.8, 40, D)
+    ki, proj = _host.psv_matrices(Ks, Kt, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Ht, Wt)
+    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Ht, Wt)
+    assert_bits(out.cpu().numpy(), want, f"C={C} shrink={shrink}")
+
+
+def test_plane_sweep_more_depths_than_lds_table(dev):
+    """D = 1030 > the LDS depth table: the tile kernel takes over, still bit-exact."""
+    from mpi_vision_amd import _host, _lib
+    from oracle import oracle
+    g = torch.Generator().manual_seed(5)
+    img = torch.rand((1, 9, 13, 3), generator=g)
+    K = configs.f32([configs.intrinsics_matrix(12.0, 12.5, 6.0, 4.0)])
+    pose = configs.f32([configs.pose_from(configs.rot_y(2.0), (0.05, 0.01, 0.0))])
+    depths = configs.inv_depths(0.5, 50, 1030)
+    ki, proj = _host.psv_matrices(K, K, pose)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, 9, 13)
+    assert_bits(_lib.plane_sweep(img.to(dev), depths, ki, proj, 9, 13).cpu().numpy(), want)

@@ -87,8 +87,12 @@ def c2(dev, it, wu):
     packed = _lib.pack_planes(mpi[0])
     out = torch.empty((V, H, W, 3), device=dev)
     per_view = P * H * W * 16 + H * W * 12
-    ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it, wu)
-    report(f"c2 1024x576x32, {V} views, packed kernel", ms, mn, V * per_view, V * H * W / 1e6)
+    for label, env in (("direct gathers (default)", {}), ("multi-view LDS kernel", {"MPIV_RENDER_MV": "1"})):
+        os.environ.update(env)
+        ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it, wu)
+        for k in env:
+            del os.environ[k]
+        report(f"c2 1024x576x32, {V} views, packed, {label}", ms, mn, V * per_view, V * H * W / 1e6)
     ms, mn = timed(lambda: _lib.pack_planes(mpi[0]), it, wu)
     report("c2 pack (one-time per MPI)", ms, mn, 2 * P * H * W * 16)
     mpi5 = mpi.expand(V, H, W, P, 4)
@@ -121,15 +125,15 @@ def c3(dev, it, wu):
     ms, mn = timed(lambda: out.fill_(1.0), it, wu)
     report(f"c3 write-bandwidth reference: torch fill_ of the {S}x{H}x{W}x{D * 3} volume", ms, mn,
            S * D * H * W * 12)
-    ms, mn = timed(sweep, it, wu)
-    report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, tile kernel (default)", ms, mn, alg,
-           extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
-    for store in ("0", "1", "2"):
-        os.environ["MPIV_SWEEP_STORE"] = store
+    for label, env in (("LDS-staged kernel (default)", {}), ("tile kernel", {"MPIV_SWEEP_TILE": "1"}),
+                       ("grouped kernel, store mode 1", {"MPIV_SWEEP_STORE": "1"}),
+                       ("grouped kernel, store mode 2", {"MPIV_SWEEP_STORE": "2"})):
+        os.environ.update(env)
         ms, mn = timed(sweep, it, wu)
-        report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, padded-texel kernel, store mode {store}", ms, mn, alg,
+        for k in env:
+            del os.environ[k]
+        report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, {label}", ms, mn, alg,
                extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
-    del os.environ["MPIV_SWEEP_STORE"]
     ms, mn = timed(lambda: (pad(), sweep()), it, wu)
     report("c3 PSV plane_sweep_torch path (pad + padded kernel)", ms, mn, alg,
            extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
@@ -145,11 +149,17 @@ def c4(dev, it, wu):
         homs = _host.render_homographies(configs.f32(c["poses"][:V]), configs.f32(c["depths"]),
                                          configs.f32([c["K"]] * V), V).to(dev)
         out = torch.empty((V, H, W, 3), device=dev)
-        ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it if V < 125 else max(3, it // 4), 1)
-        report(f"c4 1024^2x128 packed (direct gathers), {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
+        n_it = it if V < 125 else max(3, it // 4)
+        for label, env in (("direct gathers (default)", {}), ("multi-view LDS kernel", {"MPIV_RENDER_MV": "1"})):
+            os.environ.update(env)
+            ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), n_it, 1)
+            for k in env:
+                del os.environ[k]
+            report(f"c4 1024^2x128 packed, {label}, {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
         ms, mn = timed(lambda: _lib._call("mpiv_render_packed_lds", packed, H, W, P, homs, V, out,
-                                          _lib._stream(dev)), it if V < 125 else max(3, it // 4), 1)
-        report(f"c4 1024^2x128 packed (LDS-staged), {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
+                                          _lib._stream(dev)), n_it, 1)
+        report(f"c4 1024^2x128 packed, single-view LDS variant, {V} views/launch", ms, mn, V * per_view,
+               V * H * W / 1e6)
     homs = _host.render_homographies(configs.f32(c["poses"][:1]), configs.f32(c["depths"]),
                                      configs.f32([c["K"]]), 1).to(dev)
     out = torch.empty((1, H, W, 3), device=dev)

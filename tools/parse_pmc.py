@@ -15,7 +15,7 @@ import os
 import shutil
 import sys
 
-KERNEL = "render_packed_kernel"
+KERNEL = "render_packed_kernel"  # override: argv[3]
 
 
 def rows(path_glob):
@@ -36,11 +36,15 @@ def per_dispatch(counter_rows, name):
 
 
 def main():
+    global KERNEL
     out_dir, tag = sys.argv[1], sys.argv[2]
+    if len(sys.argv) > 3:
+        KERNEL = sys.argv[3]
+    views = int(sys.argv[4]) if len(sys.argv) > 4 else 125
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(repo, "profiles")
     os.makedirs(prof, exist_ok=True)
-    res = {"kernel": KERNEL, "tag": tag}
+    res = {"kernel": KERNEL, "tag": tag, "views": views}
     stats = glob.glob(os.path.join(out_dir, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
@@ -59,6 +63,14 @@ def main():
                    hbm_bytes_per_launch=(2 * f + w) * 1024, hbm_bytes_per_launch_uncorrected=(f + w) * 1024)
     if hit and miss:
         res["l2_hit_rate"] = sum(hit) / (sum(hit) + sum(miss))
+    vrows = rows(os.path.join(out_dir, "VALU", "**", "*counter_collection.csv"))
+    valu, gui = per_dispatch(vrows, "SQ_INSTS_VALU"), per_dispatch(vrows, "GRBM_GUI_ACTIVE")
+    if valu and gui:
+        # VALU issue capacity: 1024 SIMDs x one wave64 instruction per 2 cycles; GRBM_GUI_ACTIVE
+        # sums the 8 XCDs' busy cycles
+        cycles = sum(gui) / len(gui) / 8
+        res["valu_insts_per_launch"] = sum(valu) / len(valu)
+        res["valu_issue_frac"] = res["valu_insts_per_launch"] / (512 * cycles)
     for name in (f"{tag}_render_pmc.json", "render_pmc.json"):
         with open(os.path.join(prof, name), "w") as fh:
             json.dump(res, fh, indent=1)

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Run one render-kernel variant a few times (for rocprofv3 --pmc passes).
 
-    python tools/pmc_render.py --variant lds|direct --views 8 --iters 3
+    python tools/pmc_render.py --variant mv|direct|lds --views 8 --iters 3
+
+direct = the default direct-gather kernel, mv = the multi-view LDS kernel
+(MPIV_RENDER_MV=1), lds = the single-view LDS variant.
 """
 import argparse
 import os
@@ -14,10 +17,12 @@ sys.path.insert(0, REPO)
 from mpi_vision_amd import _host, _lib, configs  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--variant", default="lds")
+ap.add_argument("--variant", default="mv")
 ap.add_argument("--views", type=int, default=8)
 ap.add_argument("--iters", type=int, default=3)
 a = ap.parse_args()
+if a.variant == "mv":
+    os.environ["MPIV_RENDER_MV"] = "1"
 dev = torch.device("cuda:0")
 c = configs.config4()
 H, W, P, V = c["H"], c["W"], c["P"], a.views

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Run the config-3 plane sweep kernel a few times (for rocprofv3 --pmc passes).
 
-    python tools/pmc_sweep.py [--store 0|1|2] [--iters 3]
+    python tools/pmc_sweep.py [--store lds|tile|0|1|2] [--iters 3]
+
+lds = the default LDS-staged kernel, tile = the tile kernel, 0/1/2 = the grouped
+kernel's store modes.
 """
 import argparse
 import os
@@ -14,10 +17,12 @@ sys.path.insert(0, REPO)
 from mpi_vision_amd import _host, _lib, configs  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--store", default="2")
+ap.add_argument("--store", default="lds")
 ap.add_argument("--iters", type=int, default=3)
 a = ap.parse_args()
-if a.store != "tile":
+if a.store == "tile":
+    os.environ["MPIV_SWEEP_TILE"] = "1"
+elif a.store != "lds":
     os.environ["MPIV_SWEEP_STORE"] = a.store
 dev = torch.device("cuda:0")
 c = configs.config3()

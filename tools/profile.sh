@@ -14,8 +14,9 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
     -- python -u "$ROOT/bench.py" $ARGS > "$OUT/trace.log" 2>&1 || { echo "trace pass failed"; tail -5 "$OUT/trace.log"; exit 1; }
-for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE"; do
     name=$(echo "$pass" | tr ' ' '_')
+    [ "$pass" = "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" ] && name=VALU
     timeout -s KILL 240 rocprofv3 --pmc $pass --output-format csv -d "$OUT/$name" -o run \
         -- python -u "$ROOT/bench.py" $ARGS > "$OUT/$name.log" 2>&1 || { echo "pmc pass $pass failed"; tail -5 "$OUT/$name.log"; exit 1; }
 done
