@@ -298,22 +298,34 @@ __device__ __forceinline__ f32x4 blend_taps(const TapSet& t) {
 
 // A staged box holds `rows` rows of `pitch` consecutive texels of a padded plane whose
 // first texel is image texel (xl, yl) (xl, yl >= -2; the last staged row is <= H+1).
-// A tap origin (floor px, floor py) is served from LDS when both of its columns and
-// both of its rows are staged and neither column lies past the padded row end W+1
-// (staged texels beyond it belong to the next padded row): x0 - xl in [0, xspan],
-// y0 - yl in [0, yspan].
+// A tap origin (floor px, floor py) is read from LDS at offsets (x0 - xl, y0 - yl)
+// clamped to [0, xspan] x [0, yspan]: both of its columns and rows are staged and
+// neither column lies past the padded row end W+1 (staged texels beyond it belong to
+// the next padded row), xspan = min(xl + pitch - 2, W) - xl, yspan = rows - 2.
+// The read is exact when the origin needed no clamp, and also when it was clamped
+// onto a box edge that is the padded plane's border (-2, or W / H for the last
+// origin): then both the clamped and the true taps lie outside the image, where the
+// border's zeros are exactly grid_sample's zero padding (issue_taps_padded clamps the
+// same way).  Any other origin is not staged.
 struct LdsBox {
     float xl, yl;        // box origin (image texel coordinates)
     float xspan, yspan;  // largest tap-origin offsets served from LDS
+    float gxl, gxh;      // tap-origin x offsets read exactly: [0, xspan], open at border edges
+    float gyl, gyh;
     int pitch;           // staged row pitch (texels)
 };
 
-__device__ __forceinline__ LdsBox make_lds_box(int xl, int yl, int rows, int pitch, int W) {
+__device__ __forceinline__ LdsBox make_lds_box(int xl, int yl, int rows, int pitch, int W, int H) {
     LdsBox b;
+    const int xspan = min(xl + pitch - 2, W) - xl, yspan = rows - 2;
     b.xl = (float)xl;
     b.yl = (float)yl;
-    b.xspan = (float)(min(xl + pitch - 2, W) - xl);
-    b.yspan = (float)(rows - 2);
+    b.xspan = (float)xspan;
+    b.yspan = (float)yspan;
+    b.gxl = xl == -2 ? -__builtin_inff() : 0.0f;
+    b.gxh = xl + xspan == W ? __builtin_inff() : b.xspan;
+    b.gyl = yl == -2 ? -__builtin_inff() : 0.0f;
+    b.gyh = yl + yspan == H ? __builtin_inff() : b.yspan;
     b.pitch = pitch;
     return b;
 }
@@ -336,34 +348,20 @@ __device__ __forceinline__ bool lds_issue(const float4* __restrict__ tex, const 
     t.b = *reinterpret_cast<const f32x4*>(st + 1);
     t.c = *reinterpret_cast<const f32x4*>(st + b.pitch);
     t.d = *reinterpret_cast<const f32x4*>(st + b.pitch + 1);
-    return (ix == rx) & (iy == ry);
+    return (__builtin_amdgcn_fmed3f(rx, b.gxl, b.gxh) == rx) & (__builtin_amdgcn_fmed3f(ry, b.gyl, b.gyh) == ry);
 }
 
 // One bilinear sample from the staged box, with the weights and fma chain of
 // issue_taps_padded + blend_taps.  Returns false when the tap origin is not staged
-// (outside the box, or NaN): the LDS reads were clamped into the box, their result is
-// meaningless, and the caller gathers that sample from global memory instead -- so a
-// staged kernel is bit-identical to the direct one whatever the box covers.
+// (see LdsBox; NaN included): its result is then meaningless and the caller gathers
+// that sample from global memory instead -- so a staged kernel is bit-identical to the
+// direct one whatever the box covers.
 __device__ __forceinline__ bool lds_sample(const float4* __restrict__ tex, const LdsBox& b, float px, float py,
                                            f32x4& s) {
-    const float fx0 = floorf(px), fy0 = floorf(py);
-    const float wx = px - fx0, ex = 1.0f - wx;
-    const float wy = py - fy0, sy = 1.0f - wy;
     TapSet t;
-    t.nw = sy * ex;
-    t.ne = sy * wx;
-    t.sw = wy * ex;
-    t.se = wy * wx;
-    const float rx = fx0 - b.xl, ry = fy0 - b.yl;  // exact wherever the origin can be staged
-    const float ix = __builtin_amdgcn_fmed3f(rx, 0.0f, b.xspan);
-    const float iy = __builtin_amdgcn_fmed3f(ry, 0.0f, b.yspan);
-    const float4* st = tex + (int)__builtin_fmaf(iy, (float)b.pitch, ix);  // < rows * pitch: exact
-    t.a = *reinterpret_cast<const f32x4*>(st);
-    t.b = *reinterpret_cast<const f32x4*>(st + 1);
-    t.c = *reinterpret_cast<const f32x4*>(st + b.pitch);
-    t.d = *reinterpret_cast<const f32x4*>(st + b.pitch + 1);
+    const bool ok = lds_issue(tex, b, px, py, t);
     s = blend_taps(t);
-    return (ix == rx) & (iy == ry);
+    return ok;
 }
 
 }  // namespace mpiv

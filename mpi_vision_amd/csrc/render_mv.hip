@@ -205,7 +205,7 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
         if (active) {
             const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)p * plane_stride, g.plane_bytes);
             if (staged(bx)) {
-                const LdsBox lbx = make_lds_box(bx.x, bx.y, bx.z, pitch, g.W);
+                const LdsBox lbx = make_lds_box(bx.x, bx.y, bx.z, pitch, g.W, g.H);
                 const float4* tex = s_tex[buf];
                 // kMG views at a time, phase by phase (positions, tap reads, blends), with
                 // the rare fix-ups behind wave-uniform tests: their LDS reads are in flight
