@@ -90,7 +90,13 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
         const float* h = homs + ((int64_t)v * g.P + pl) * 9;
         float px, py;
         render_pos<true>(h, fx, fy, g, px, py);
+        const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
+        const float v2 = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
         float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+        // u, v, w are affine over the tile: corner values a factor 2 inside div2_safe's
+        // range (room for rounding) prove the fast division for every pixel and view
+        int fastv = __builtin_fabsf(w) >= 0x1p-59f && __builtin_fabsf(w) <= 0x1p59f &&
+                    __builtin_fmaxf(__builtin_fabsf(u), __builtin_fabsf(v2)) <= 0x1p59f;
         w = (w == 0.0f) ? w + 1e-8f : w;
         const bool fin = __builtin_isfinite(px) && __builtin_isfinite(py) && __builtin_fabsf(px) < 1e7f &&
                          __builtin_fabsf(py) < 1e7f;
@@ -104,6 +110,7 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
             ymax = fmaxf(ymax, __shfl_xor(ymax, m));
             pos &= __shfl_xor(pos, m);
             neg &= __shfl_xor(neg, m);
+            fastv &= __shfl_xor(fastv, m);
         }
         if (live && (q & (kMI - 1)) == 0) {
             const bool ok = pos || neg;
@@ -114,7 +121,7 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
             const int width = xh - xl + 1, rows = yh - yl + 1;
             const bool staged = ok && width >= 2 && rows >= 2 && width <= kMMaxPitch && rows <= kMCap &&
                                 width * rows <= kMCap;
-            s_box[q / kMI] = make_int4(xl, yl, rows, staged ? 1 : 0);
+            s_box[q / kMI] = make_int4(xl, yl, rows, (staged ? 1 : 0) | (fastv ? 2 : 0));
             if (staged) atomicMax(&s_pitch, width);
         }
     }
@@ -135,7 +142,7 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
         return make_int4(__builtin_amdgcn_readfirstlane(b.x), __builtin_amdgcn_readfirstlane(b.y),
                          __builtin_amdgcn_readfirstlane(b.z), __builtin_amdgcn_readfirstlane(b.w));
     };
-    auto staged = [&](const int4& b) { return b.w != 0 && b.z * pitch <= kMCap; };
+    auto staged = [&](const int4& b) { return (b.w & 1) != 0 && b.z * pitch <= kMCap; };
 
     // register staging (render_lds.hip says why not LDS-DMA); texels past the box are
     // loaded too (real memory or the buffer's zero range) and never read
@@ -206,6 +213,7 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
             const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)p * plane_stride, g.plane_bytes);
             if (staged(bx)) {
                 const LdsBox lbx = make_lds_box(bx.x, bx.y, bx.z, pitch, g.W, g.H);
+                const bool plane_fast = (bx.w & 2) != 0;  // division fast path proven for the tile
                 const float4* tex = s_tex[buf];
                 // kMG views at a time, phase by phase (positions, tap reads, blends), with
                 // the rare fix-ups behind wave-uniform tests: their LDS reads are in flight
@@ -221,7 +229,7 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
                             const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
                             const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
                             const float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
-                            fast = fast && div2_safe(u, v, w);
+                            if (!plane_fast) fast = fast && div2_safe(u, v, w);
                             div2_fast(u, v, w, qu[jj], qv[jj]);
                         }
                         if (__builtin_amdgcn_ballot_w64(!fast)) {  // rare: divide_safe2's slow path
