@@ -71,6 +71,74 @@ __device__ __forceinline__ void render_pos(const float* __restrict__ h, float fx
     }
 }
 
+// render_pos<true> with the (x, y) pair of the recipe as packed fp32 ops (bit-identical:
+// mpiv_common.hpp f32x2).  GUARD: divide_safe2's per-sample range test; without it the
+// caller has proven the fast division for the whole tile (div2_rect_safe).
+struct Hom9 {
+    float h[9];
+};
+
+__device__ __forceinline__ Hom9 load_hom(const float* __restrict__ h) {
+    Hom9 r;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.h[k] = h[k];
+    return r;
+}
+
+// (u, v) and w of pixel (x, y) through a row-major homography (transform_points_torch,
+// utils.py:69-88, in MKL's order), (u, v) as one packed pair
+__device__ __forceinline__ void hom_uvw_pk(const float* __restrict__ h, float fx, float fy, f32x2& uv, float& w) {
+    uv = fma2((f32x2){h[1], h[4]}, splat2(fy), (f32x2){h[0], h[3]} * splat2(fx)) + (f32x2){h[2], h[5]};
+    w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+}
+
+// (u/w, v/w) -> sample position: SWAPPED x / (H-1), y / (W-1) (utils.py:188), then
+// -1 + 2c (utils.py:127) and grid_sample's unnormalise, as packed pairs
+__device__ __forceinline__ f32x2 grid_pos_pk(f32x2 q, const RenderGeom& g) {
+    const f32x2 c = div_const2(q, (f32x2){g.hm1, g.wm1}, (f32x2){g.rc_hm1, g.rc_wm1});
+    const f32x2 gr = fma2(splat2(2.0f), c, splat2(-1.0f));
+    return fma2(gr + 1.0f, (f32x2){g.half_w, g.half_h}, splat2(-0.5f));
+}
+
+template <bool GUARD>
+__device__ __forceinline__ f32x2 render_pos_pk(const float* __restrict__ h, float fx, float fy,
+                                               const RenderGeom& g) {
+    f32x2 uv;
+    float w;
+    hom_uvw_pk(h, fx, fy, uv, w);
+    f32x2 q;
+    if (!GUARD || __builtin_expect(div2_safe(uv.x, uv.y, w), 1)) {
+        q = div2_fast_pk(uv, w);
+    } else {
+        float qu, qv;
+        divide_safe2(uv.x, uv.y, w, qu, qv);  // utils.py:35-39
+        q = (f32x2){qu, qv};
+    }
+    return grid_pos_pk(q, g);
+}
+
+// True when div2_safe(u, v, w) holds for every pixel of [x0, x1] x [y0, y1] (integer
+// coordinates).  Each computed coordinate, e.g. u = fma(h1, y, RN(h0*x)) + h2, is a chain
+// of correctly rounded operations that are each monotone in x (direction: sign of h0)
+// and in y (sign of h1), so over the rectangle it takes its extremes at the corners:
+// corners with |u|, |v| <= 2^60 and w of one sign inside [2^-60, 2^60] bound every
+// interior value exactly (no rounding margin needed).  NaN corners fail the test.
+__device__ __forceinline__ bool div2_rect_safe(const float* __restrict__ h, float x0, float x1, float y0,
+                                               float y1) {
+    bool ok = true, pos = true, neg = true;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float fx = (c & 1) ? x1 : x0, fy = (c & 2) ? y1 : y0;
+        const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
+        const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
+        const float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+        ok = ok && div2_safe(u, v, w);
+        pos = pos && w > 0.0f;
+        neg = neg && w < 0.0f;
+    }
+    return ok && (pos || neg);
+}
+
 // ---------------------------------------------------------------------------
 // packed plane-major layout
 // ---------------------------------------------------------------------------
@@ -97,6 +165,79 @@ __device__ __forceinline__ int xcd_logical_block(int b, int nblocks) {
 //             (Cf, Tf) o (Cb, Tb) = (Cf + Tf*Cb, Tf*Tb)  (SURVEY.md §8e).
 // One work-item = one output pixel of one view.  Plane p+1's four tap loads are
 // issued before plane p is blended, so every wave keeps 8 x 16 B in flight.
+// MODE 0: scalar recipe (H or W < 2); 1: packed recipe with the per-sample division
+// guard; 2: packed recipe, fast division proven for the block's tile and every plane.
+template <bool CT, int MODE>
+__device__ __forceinline__ void render_packed_pixel(const float4* __restrict__ planes, int64_t plane_stride,
+                                                    const RenderGeom& g, int p_begin, int p_end, int back,
+                                                    const float* __restrict__ hv, int x, int y,
+                                                    float* __restrict__ out_px) {
+    const float fx = (float)x, fy = (float)y;
+    // The reference's plane 0 replaces the background: with alpha forced to 1 and the
+    // colour started at -0.0, `out = rgb*1 + (-0)*(1-1)` returns rgb bit for bit (x + -0
+    // == x for every x, signed zeros included), so every plane runs the same code.
+    f32x2 crg = splat2(-0.0f);
+    float cb = -0.0f, t = 1.0f;
+    const bool replace_first = !CT || back;
+    const int last = p_end - 1;
+    // plane p's taps; past the range the last plane is re-issued (L2-hot, result
+    // unused) so every iteration issues unconditionally and the compiler can count
+    // vmcnt exactly
+    // the homography of plane p is fetched (scalar loads) a full iteration ahead, so its
+    // latency hides behind two blends instead of stalling the issue that uses it
+    auto hom = [&](int p) { return load_hom(hv + (int64_t)(p < last ? p : last) * 9); };
+    auto issue = [&](int p, const Hom9& h, TapSet& ts) {
+        const int q = p < last ? p : last;
+        float px, py;
+        if (MODE == 0) {
+            render_pos<false>(h.h, fx, fy, g, px, py);
+        } else {
+            const f32x2 pp = render_pos_pk<MODE == 1>(h.h, fx, fy, g);
+            px = pp.x;
+            py = pp.y;
+        }
+        issue_taps_padded(make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes), g.W, g.H, g.Wp, g.org,
+                          g.row, px, py, ts);
+    };
+    // over (utils.py:155-156) unfused, with the (r, g) pair packed
+    auto consume = [&](const TapSet& ts, bool first) {
+        const f32x4 s = blend_taps(ts);
+        const float a = first ? 1.0f : s[3];
+        const float om = 1.0f - a;
+        crg = s.xy * splat2(a) + crg * splat2(om);
+        cb = over(s[2], a, om, cb);
+        if (CT) t = t * om;
+    };
+    // ping-pong between two tap sets (no register rotation): the next plane's loads
+    // are in flight while the current one is blended.  sched_barrier keeps each issue
+    // block ahead of the previous plane's blend.
+    // Loop invariant: at the top of every iteration exactly A's four loads are in
+    // flight (no mid-loop exits), so the compiler's vmcnt bookkeeping stays exact.
+    TapSet A, B;
+    Hom9 hA = hom(p_begin), hB = hom(p_begin + 1);
+    issue(p_begin, hA, A);
+    hA = hom(p_begin + 2);
+    int p = p_begin;
+    for (; p + 1 < p_end; p += 2) {  // A holds plane p, B will hold p + 1
+        issue(p + 1, hB, B);
+        hB = hom(p + 3);  // used one iteration later
+        __builtin_amdgcn_sched_barrier(0);
+        consume(A, replace_first && p == p_begin);
+        issue(p + 2, hA, A);
+        hA = hom(p + 4);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(B, false);
+    }
+    if (p < p_end) consume(A, replace_first && p == p_begin);
+    if (CT) {
+        *reinterpret_cast<float4*>(out_px) = make_float4(crg.x, crg.y, cb, t);
+    } else {
+        out_px[0] = crg.x;
+        out_px[1] = crg.y;
+        out_px[2] = cb;
+    }
+}
+
 template <bool CT, bool FAST>
 __global__ __launch_bounds__(256) void render_packed_kernel(const float4* __restrict__ planes,
                                                             int64_t plane_stride, RenderGeom g, int V,
@@ -107,62 +248,29 @@ __global__ __launch_bounds__(256) void render_packed_kernel(const float4* __rest
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
     const int v = lb % V;
     const int tile = lb / V;
-    const int x = (tile % tiles_x) * kTileX + (threadIdx.x & (kWave - 1));
-    const int y = (tile / tiles_x) * kTileY + (threadIdx.x >> 6);
-    if (x >= g.W || y >= g.H) return;
-    const float fx = (float)x, fy = (float)y;
+    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * kTileY;
+    const int x = tx0 + (threadIdx.x & (kWave - 1));
+    const int y = ty0 + (threadIdx.x >> 6);
     const float* hv = homs + (int64_t)v * g.P * 9;
-
-    // The reference's plane 0 replaces the background: with alpha forced to 1 and the
-    // colour started at -0.0, `out = rgb*1 + (-0)*(1-1)` returns rgb bit for bit (x + -0
-    // == x for every x, signed zeros included), so every plane runs the same code.
-    float cr = -0.0f, cg = -0.0f, cb = -0.0f, t = 1.0f;
-    const bool replace_first = !CT || back;
-    const int last = p_end - 1;
-    // plane p's taps; past the range the last plane is re-issued (L2-hot, result
-    // unused) so every iteration issues unconditionally and the compiler can count
-    // vmcnt exactly
-    auto issue = [&](int p, TapSet& ts) {
-        const int q = p < last ? p : last;
-        float px, py;
-        render_pos<FAST>(hv + (int64_t)q * 9, fx, fy, g, px, py);
-        issue_taps_padded(make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes), g.W, g.H, g.Wp, g.org,
-                          g.row, px, py, ts);
-    };
-    auto consume = [&](const TapSet& ts, bool first) {
-        const f32x4 s = blend_taps(ts);
-        const float a = first ? 1.0f : s[3];
-        const float om = 1.0f - a;
-        cr = over(s[0], a, om, cr);
-        cg = over(s[1], a, om, cg);
-        cb = over(s[2], a, om, cb);
-        if (CT) t = t * om;
-    };
-    // ping-pong between two tap sets (no register rotation): the next plane's loads
-    // are in flight while the current one is blended.  sched_barrier keeps each issue
-    // block ahead of the previous plane's blend.
-    // Loop invariant: at the top of every iteration exactly A's four loads are in
-    // flight (no mid-loop exits), so the compiler's vmcnt bookkeeping stays exact.
-    TapSet A, B;
-    issue(p_begin, A);
-    int p = p_begin;
-    for (; p + 1 < p_end; p += 2) {  // A holds plane p, B will hold p + 1
-        issue(p + 1, B);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(A, replace_first && p == p_begin);
-        issue(p + 2, A);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(B, false);
+    // block prologue: prove the fast division for the tile, all planes at once
+    bool proven = false;
+    if (FAST) {
+        const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
+        const float y0 = (float)ty0, y1 = (float)min(ty0 + kTileY - 1, g.H - 1);
+        bool ok = true;
+        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256)
+            ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, y0, y1);
+        proven = __syncthreads_and(ok);
     }
-    if (p < p_end) consume(A, replace_first && p == p_begin);
+    if (x >= g.W || y >= g.H) return;
     const int64_t o = ((int64_t)v * g.H + y) * g.W + x;
-    if (CT) {
-        reinterpret_cast<float4*>(out)[o] = make_float4(cr, cg, cb, t);
-    } else {
-        out[o * 3 + 0] = cr;
-        out[o * 3 + 1] = cg;
-        out[o * 3 + 2] = cb;
-    }
+    float* out_px = CT ? out + o * 4 : out + o * 3;
+    if (!FAST)
+        render_packed_pixel<CT, 0>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y, out_px);
+    else if (proven)
+        render_packed_pixel<CT, 2>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y, out_px);
+    else
+        render_packed_pixel<CT, 1>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y, out_px);
 }
 
 // ---------------------------------------------------------------------------

@@ -173,20 +173,19 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
     };
 
     const float fx = (float)x, fy = (float)y;
-    float cr[kMVB], cg[kMVB], cb[kMVB], tt[kMVB];
+    f32x2 crg[kMVB];
+    float cb[kMVB], tt[kMVB];
 #pragma unroll
     for (int j = 0; j < kMVB; ++j) {
-        cr[j] = -0.0f;  // plane p_begin replaces it exactly (render.hip)
-        cg[j] = -0.0f;
+        crg[j] = splat2(-0.0f);  // plane p_begin replaces it exactly (render.hip)
         cb[j] = -0.0f;
         tt[j] = 1.0f;
     }
     const bool replace_first = !CT || back;
-    auto consume = [&](int j, const f32x4& s, bool first) {
+    auto consume = [&](int j, const f32x4& s, bool first) {  // over, (r, g) packed
         const float a = first ? 1.0f : s[3];
         const float om = 1.0f - a;
-        cr[j] = over(s[0], a, om, cr[j]);
-        cg[j] = over(s[1], a, om, cg[j]);
+        crg[j] = s.xy * splat2(a) + crg[j] * splat2(om);
         cb[j] = over(s[2], a, om, cb[j]);
         if (CT) tt[j] = tt[j] * om;
     };
@@ -221,25 +220,27 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
 #pragma unroll
                 for (int j0 = 0; j0 < kMVB; j0 += kMG) {
                     if (j0 < nv) {
-                        float qu[kMG], qv[kMG];
+                        f32x2 q[kMG];
                         bool fast = true;
 #pragma unroll
                         for (int jj = 0; jj < kMG; ++jj) {
-                            const float* h = s_hom[buf][j0 + jj];
-                            const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
-                            const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
-                            const float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
-                            if (!plane_fast) fast = fast && div2_safe(u, v, w);
-                            div2_fast(u, v, w, qu[jj], qv[jj]);
+                            f32x2 uv;
+                            float w;
+                            hom_uvw_pk(s_hom[buf][j0 + jj], fx, fy, uv, w);
+                            if (!plane_fast) fast = fast && div2_safe(uv.x, uv.y, w);
+                            q[jj] = div2_fast_pk(uv, w);
                         }
                         if (__builtin_amdgcn_ballot_w64(!fast)) {  // rare: divide_safe2's slow path
 #pragma unroll
                             for (int jj = 0; jj < kMG; ++jj) {
-                                const float* h = s_hom[buf][j0 + jj];
-                                const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
-                                const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
-                                const float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
-                                if (!div2_safe(u, v, w)) divide_safe2(u, v, w, qu[jj], qv[jj]);
+                                f32x2 uv;
+                                float w;
+                                hom_uvw_pk(s_hom[buf][j0 + jj], fx, fy, uv, w);
+                                if (!div2_safe(uv.x, uv.y, w)) {
+                                    float qu, qv;
+                                    divide_safe2(uv.x, uv.y, w, qu, qv);
+                                    q[jj] = (f32x2){qu, qv};
+                                }
                             }
                         }
                         float px[kMG], py[kMG];
@@ -247,10 +248,9 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
                         bool ok = true;
 #pragma unroll
                         for (int jj = 0; jj < kMG; ++jj) {
-                            const float cx = div_const(qu[jj], g.hm1, g.rc_hm1);  // SWAPPED x / (H-1), utils.py:188
-                            const float cy = div_const(qv[jj], g.wm1, g.rc_wm1);  //         y / (W-1)
-                            px[jj] = unnormalize(to_grid(cx), g.half_w);
-                            py[jj] = unnormalize(to_grid(cy), g.half_h);
+                            const f32x2 pp = grid_pos_pk(q[jj], g);
+                            px[jj] = pp.x;
+                            py[jj] = pp.y;
                             ok = lds_issue(tex, lbx, px[jj], py[jj], ts[jj]) && ok;
                         }
                         f32x4 sm[kMG];
@@ -295,10 +295,10 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
         if (j < nv) {
             const int64_t o = ((int64_t)(vg0 + j) * g.H + y) * g.W + x;
             if (CT) {
-                reinterpret_cast<float4*>(out)[o] = make_float4(cr[j], cg[j], cb[j], tt[j]);
+                reinterpret_cast<float4*>(out)[o] = make_float4(crg[j].x, crg[j].y, cb[j], tt[j]);
             } else {
-                out[o * 3 + 0] = cr[j];
-                out[o * 3 + 1] = cg[j];
+                out[o * 3 + 0] = crg[j].x;
+                out[o * 3 + 1] = crg[j].y;
                 out[o * 3 + 2] = cb[j];
             }
         }
