@@ -12,7 +12,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmpiv.so")
+# MPIV_LIB: another build of the same ABI (kernel A/B tools only, tools/gpu_ab_lib.sh)
+LIB_PATH = os.environ.get("MPIV_LIB") or os.path.join(_HERE, "libmpiv.so")
 
 _c_i64p = ctypes.POINTER(ctypes.c_int64)
 _vp = ctypes.c_void_p

@@ -14,15 +14,6 @@ namespace mpiv {
 constexpr int kWave = 64;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// Packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32): two IEEE fp32 operations per
-// VALU issue slot, each rounded exactly like its scalar form (same rounding mode and
-// denormal mode), so pairing two independent lanes of the recipe -- (u, v), (x, y),
-// (r, g) / (b, a) -- halves their issue cost without changing a bit.  The 64-lane VALU
-// peak (157 TFLOP/s) is only reachable through these.
-__device__ __forceinline__ f32x2 splat2(float a) { return (f32x2){a, a}; }
-__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // 16-byte raw buffer load.  ROCm 7.2's __builtin_amdgcn_raw_buffer_load_b128 lowers to
 // a 4-byte buffer_load_dword (observed in the .s; the other 12 bytes are garbage), so
@@ -148,27 +139,6 @@ __device__ __forceinline__ void divide_safe2(float u, float v, float w, float& q
     }
 }
 
-// Packed div_const for (x / c.x, y / c.y): q = RN(q*rc), two residual corrections.
-__device__ __forceinline__ f32x2 div_const2(f32x2 x, f32x2 c, f32x2 rc) {
-    const f32x2 q = x * rc;
-    const f32x2 r = fma2(-c, q, x);
-    return fma2(r, rc, q);
-}
-
-// div2_fast with the (u, v) pair packed: one shared reciprocal of w, then div_core on
-// both numerators as pk ops.  Valid wherever div2_safe(u, v, w) holds.
-__device__ __forceinline__ f32x2 div2_fast_pk(f32x2 uv, float w) {
-    float y = __builtin_amdgcn_rcpf(w);
-    const float e = __builtin_fmaf(-w, y, 1.0f);
-    y = __builtin_fmaf(e, y, y);
-    const f32x2 yy = splat2(y), nw = splat2(-w);
-    f32x2 q = uv * yy;
-    f32x2 r = fma2(nw, q, uv);
-    q = fma2(r, yy, q);
-    r = fma2(nw, q, uv);
-    return fma2(r, yy, q);
-}
-
 // grid value g in [-1, 1] -> source pixel, align_corners=False (ATen CPU vectorised
 // grid sampler: (g + 1) * (size / 2) - 0.5, contracted to one FMA).
 __device__ __forceinline__ float unnormalize(float g, float half_size) {
@@ -250,23 +220,6 @@ struct TapSet {
     float nw, ne, sw, se;
 };
 
-// ATen's bilinear weights, nw = (1-wy)(1-wx), ne = (1-wy)wx, sw = wy(1-wx), se = wy*wx
-// with wx = px - floor(px), as five packed ops: (wx, wy) = p - floor(p); the pairs
-// X = (1 - wx, wx) and Y = (1 - wy, wy) are each one pk_fma(w, (-1, 1), (1, 0))
-// (fma(w, -1, 1) rounds like 1 - w; w + 0 == w since w = p - floor(p) is never -0);
-// (nw, ne) = Y.x * X, (sw, se) = Y.y * X.
-__device__ __forceinline__ void bilinear_weights(float px, float py, float fx0, float fy0, TapSet& t) {
-    const f32x2 f = (f32x2){px, py} - (f32x2){fx0, fy0};
-    const f32x2 m1p1 = (f32x2){-1.0f, 1.0f}, one0 = (f32x2){1.0f, 0.0f};
-    const f32x2 X = fma2(splat2(f.x), m1p1, one0);
-    const f32x2 Y = fma2(splat2(f.y), m1p1, one0);
-    const f32x2 n = splat2(Y.x) * X, s = splat2(Y.y) * X;
-    t.nw = n.x;
-    t.ne = n.y;
-    t.sw = s.x;
-    t.se = s.y;
-}
-
 // Issue the four tap loads of one sample of one packed plane.  Taps outside the
 // plane (and every tap when `live` is false) get the out-of-range offset, so the
 // buffer unit returns 0 for them without a memory access: grid_sample's zeros
@@ -274,7 +227,12 @@ __device__ __forceinline__ void bilinear_weights(float px, float py, float fx0, 
 __device__ __forceinline__ void issue_taps(__amdgpu_buffer_rsrc_t r, int W, int H, float px, float py, bool live,
                                            TapSet& t) {
     const float fx0 = floorf(px), fy0 = floorf(py);
-    bilinear_weights(px, py, fx0, fy0, t);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
     // clamp to [-2, W] / [-2, H] so the int conversion is defined and every tap index
     // outside [0, W) / [0, H) stays outside; unsigned compares then test the range
     const unsigned ux = (unsigned)(int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)W);
@@ -304,7 +262,12 @@ constexpr int kPad = 2;
 __device__ __forceinline__ void issue_taps_padded(__amdgpu_buffer_rsrc_t r, int W, int H, int Wp, int org,
                                                   int row, float px, float py, TapSet& t) {
     const float fx0 = floorf(px), fy0 = floorf(py);
-    bilinear_weights(px, py, fx0, fy0, t);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
     // med3 also maps NaN to a bound, so the index is always defined (the NaN weights
     // still make the sample NaN, as in the reference)
     const int cx = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)W);
@@ -316,18 +279,17 @@ __device__ __forceinline__ void issue_taps_padded(__amdgpu_buffer_rsrc_t r, int 
     t.d = llvm_raw_buffer_load_v4f32(r, off + 16, row, 0);
 }
 
-// per channel: a*nw, then fma(b, ne), fma(c, sw), fma(d, se) (ATen's order); the
-// channel pairs (r, g) and (b, a) run as packed ops: 8 VALU issues instead of 16
 __device__ __forceinline__ f32x4 blend_taps(const TapSet& t) {
-    const f32x2 nw = splat2(t.nw), ne = splat2(t.ne), sw = splat2(t.sw), se = splat2(t.se);
-    f32x2 lo = t.a.xy * nw, hi = t.a.zw * nw;
-    lo = fma2(t.b.xy, ne, lo);
-    hi = fma2(t.b.zw, ne, hi);
-    lo = fma2(t.c.xy, sw, lo);
-    hi = fma2(t.c.zw, sw, hi);
-    lo = fma2(t.d.xy, se, lo);
-    hi = fma2(t.d.zw, se, hi);
-    return (f32x4){lo.x, lo.y, hi.x, hi.y};
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float acc = t.a[k] * t.nw;
+        acc = __builtin_fmaf(t.b[k], t.ne, acc);
+        acc = __builtin_fmaf(t.c[k], t.sw, acc);
+        acc = __builtin_fmaf(t.d[k], t.se, acc);
+        o[k] = acc;
+    }
+    return o;
 }
 
 // ---------------------------------------------------------------------------
@@ -372,9 +334,13 @@ __device__ __forceinline__ LdsBox make_lds_box(int xl, int yl, int rows, int pit
 __device__ __forceinline__ bool lds_issue(const float4* __restrict__ tex, const LdsBox& b, float px, float py,
                                           TapSet& t) {
     const float fx0 = floorf(px), fy0 = floorf(py);
-    bilinear_weights(px, py, fx0, fy0, t);
-    const f32x2 rr = (f32x2){fx0, fy0} - (f32x2){b.xl, b.yl};  // exact wherever the origin can be staged
-    const float rx = rr.x, ry = rr.y;
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
+    const float rx = fx0 - b.xl, ry = fy0 - b.yl;  // exact wherever the origin can be staged
     const float ix = __builtin_amdgcn_fmed3f(rx, 0.0f, b.xspan);
     const float iy = __builtin_amdgcn_fmed3f(ry, 0.0f, b.yspan);
     const float4* st = tex + (int)__builtin_fmaf(iy, (float)b.pitch, ix);  // < rows * pitch: exact

@@ -71,9 +71,7 @@ __device__ __forceinline__ void render_pos(const float* __restrict__ h, float fx
     }
 }
 
-// render_pos<true> with the (x, y) pair of the recipe as packed fp32 ops (bit-identical:
-// mpiv_common.hpp f32x2).  GUARD: divide_safe2's per-sample range test; without it the
-// caller has proven the fast division for the whole tile (div2_rect_safe).
+// one plane's homography, held in SGPRs (wave-uniform scalar loads)
 struct Hom9 {
     float h[9];
 };
@@ -85,36 +83,23 @@ __device__ __forceinline__ Hom9 load_hom(const float* __restrict__ h) {
     return r;
 }
 
-// (u, v) and w of pixel (x, y) through a row-major homography (transform_points_torch,
-// utils.py:69-88, in MKL's order), (u, v) as one packed pair
-__device__ __forceinline__ void hom_uvw_pk(const float* __restrict__ h, float fx, float fy, f32x2& uv, float& w) {
-    uv = fma2((f32x2){h[1], h[4]}, splat2(fy), (f32x2){h[0], h[3]} * splat2(fx)) + (f32x2){h[2], h[5]};
-    w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
-}
-
-// (u/w, v/w) -> sample position: SWAPPED x / (H-1), y / (W-1) (utils.py:188), then
-// -1 + 2c (utils.py:127) and grid_sample's unnormalise, as packed pairs
-__device__ __forceinline__ f32x2 grid_pos_pk(f32x2 q, const RenderGeom& g) {
-    const f32x2 c = div_const2(q, (f32x2){g.hm1, g.wm1}, (f32x2){g.rc_hm1, g.rc_wm1});
-    const f32x2 gr = fma2(splat2(2.0f), c, splat2(-1.0f));
-    return fma2(gr + 1.0f, (f32x2){g.half_w, g.half_h}, splat2(-0.5f));
-}
-
+// render_pos<true>; GUARD: divide_safe2's per-sample range test; without it the caller
+// has proven the fast division for the whole tile (div2_rect_safe).
 template <bool GUARD>
-__device__ __forceinline__ f32x2 render_pos_pk(const float* __restrict__ h, float fx, float fy,
-                                               const RenderGeom& g) {
-    f32x2 uv;
-    float w;
-    hom_uvw_pk(h, fx, fy, uv, w);
-    f32x2 q;
-    if (!GUARD || __builtin_expect(div2_safe(uv.x, uv.y, w), 1)) {
-        q = div2_fast_pk(uv, w);
-    } else {
-        float qu, qv;
-        divide_safe2(uv.x, uv.y, w, qu, qv);  // utils.py:35-39
-        q = (f32x2){qu, qv};
-    }
-    return grid_pos_pk(q, g);
+__device__ __forceinline__ void render_pos_fast(const float* __restrict__ h, float fx, float fy,
+                                                const RenderGeom& g, float& px, float& py) {
+    const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
+    const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
+    const float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+    float qu, qv;
+    if (GUARD)
+        divide_safe2(u, v, w, qu, qv);  // divide_safe_torch, utils.py:35-39
+    else
+        div2_fast(u, v, w, qu, qv);
+    const float cx = div_const(qu, g.hm1, g.rc_hm1);  // SWAPPED x / (H-1), utils.py:188
+    const float cy = div_const(qv, g.wm1, g.rc_wm1);  //         y / (W-1)
+    px = unnormalize(to_grid(cx), g.half_w);
+    py = unnormalize(to_grid(cy), g.half_h);
 }
 
 // True when div2_safe(u, v, w) holds for every pixel of [x0, x1] x [y0, y1] (integer
@@ -165,8 +150,8 @@ __device__ __forceinline__ int xcd_logical_block(int b, int nblocks) {
 //             (Cf, Tf) o (Cb, Tb) = (Cf + Tf*Cb, Tf*Tb)  (SURVEY.md §8e).
 // One work-item = one output pixel of one view.  Plane p+1's four tap loads are
 // issued before plane p is blended, so every wave keeps 8 x 16 B in flight.
-// MODE 0: scalar recipe (H or W < 2); 1: packed recipe with the per-sample division
-// guard; 2: packed recipe, fast division proven for the block's tile and every plane.
+// MODE 0: generic recipe (H or W < 2); 1: fast recipe with the per-sample division
+// guard; 2: fast recipe, fast division proven for the block's tile and every plane.
 template <bool CT, int MODE>
 __device__ __forceinline__ void render_packed_pixel(const float4* __restrict__ planes, int64_t plane_stride,
                                                     const RenderGeom& g, int p_begin, int p_end, int back,
@@ -176,8 +161,7 @@ __device__ __forceinline__ void render_packed_pixel(const float4* __restrict__ p
     // The reference's plane 0 replaces the background: with alpha forced to 1 and the
     // colour started at -0.0, `out = rgb*1 + (-0)*(1-1)` returns rgb bit for bit (x + -0
     // == x for every x, signed zeros included), so every plane runs the same code.
-    f32x2 crg = splat2(-0.0f);
-    float cb = -0.0f, t = 1.0f;
+    float cr = -0.0f, cg = -0.0f, cb = -0.0f, t = 1.0f;
     const bool replace_first = !CT || back;
     const int last = p_end - 1;
     // plane p's taps; past the range the last plane is re-issued (L2-hot, result
@@ -189,22 +173,19 @@ __device__ __forceinline__ void render_packed_pixel(const float4* __restrict__ p
     auto issue = [&](int p, const Hom9& h, TapSet& ts) {
         const int q = p < last ? p : last;
         float px, py;
-        if (MODE == 0) {
+        if (MODE == 0)
             render_pos<false>(h.h, fx, fy, g, px, py);
-        } else {
-            const f32x2 pp = render_pos_pk<MODE == 1>(h.h, fx, fy, g);
-            px = pp.x;
-            py = pp.y;
-        }
+        else
+            render_pos_fast<MODE == 1>(h.h, fx, fy, g, px, py);
         issue_taps_padded(make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes), g.W, g.H, g.Wp, g.org,
                           g.row, px, py, ts);
     };
-    // over (utils.py:155-156) unfused, with the (r, g) pair packed
     auto consume = [&](const TapSet& ts, bool first) {
         const f32x4 s = blend_taps(ts);
         const float a = first ? 1.0f : s[3];
         const float om = 1.0f - a;
-        crg = s.xy * splat2(a) + crg * splat2(om);
+        cr = over(s[0], a, om, cr);
+        cg = over(s[1], a, om, cg);
         cb = over(s[2], a, om, cb);
         if (CT) t = t * om;
     };
@@ -230,10 +211,10 @@ __device__ __forceinline__ void render_packed_pixel(const float4* __restrict__ p
     }
     if (p < p_end) consume(A, replace_first && p == p_begin);
     if (CT) {
-        *reinterpret_cast<float4*>(out_px) = make_float4(crg.x, crg.y, cb, t);
+        *reinterpret_cast<float4*>(out_px) = make_float4(cr, cg, cb, t);
     } else {
-        out_px[0] = crg.x;
-        out_px[1] = crg.y;
+        out_px[0] = cr;
+        out_px[1] = cg;
         out_px[2] = cb;
     }
 }

@@ -90,13 +90,7 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
         const float* h = homs + ((int64_t)v * g.P + pl) * 9;
         float px, py;
         render_pos<true>(h, fx, fy, g, px, py);
-        const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
-        const float v2 = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
         float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
-        // u, v, w are affine over the tile: corner values a factor 2 inside div2_safe's
-        // range (room for rounding) prove the fast division for every pixel and view
-        int fastv = __builtin_fabsf(w) >= 0x1p-59f && __builtin_fabsf(w) <= 0x1p59f &&
-                    __builtin_fmaxf(__builtin_fabsf(u), __builtin_fabsf(v2)) <= 0x1p59f;
         w = (w == 0.0f) ? w + 1e-8f : w;
         const bool fin = __builtin_isfinite(px) && __builtin_isfinite(py) && __builtin_fabsf(px) < 1e7f &&
                          __builtin_fabsf(py) < 1e7f;
@@ -110,7 +104,6 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
             ymax = fmaxf(ymax, __shfl_xor(ymax, m));
             pos &= __shfl_xor(pos, m);
             neg &= __shfl_xor(neg, m);
-            fastv &= __shfl_xor(fastv, m);
         }
         if (live && (q & (kMI - 1)) == 0) {
             const bool ok = pos || neg;
@@ -121,7 +114,7 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
             const int width = xh - xl + 1, rows = yh - yl + 1;
             const bool staged = ok && width >= 2 && rows >= 2 && width <= kMMaxPitch && rows <= kMCap &&
                                 width * rows <= kMCap;
-            s_box[q / kMI] = make_int4(xl, yl, rows, (staged ? 1 : 0) | (fastv ? 2 : 0));
+            s_box[q / kMI] = make_int4(xl, yl, rows, staged ? 1 : 0);
             if (staged) atomicMax(&s_pitch, width);
         }
     }
@@ -142,7 +135,7 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
         return make_int4(__builtin_amdgcn_readfirstlane(b.x), __builtin_amdgcn_readfirstlane(b.y),
                          __builtin_amdgcn_readfirstlane(b.z), __builtin_amdgcn_readfirstlane(b.w));
     };
-    auto staged = [&](const int4& b) { return (b.w & 1) != 0 && b.z * pitch <= kMCap; };
+    auto staged = [&](const int4& b) { return b.w != 0 && b.z * pitch <= kMCap; };
 
     // register staging (render_lds.hip says why not LDS-DMA); texels past the box are
     // loaded too (real memory or the buffer's zero range) and never read
@@ -173,19 +166,20 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
     };
 
     const float fx = (float)x, fy = (float)y;
-    f32x2 crg[kMVB];
-    float cb[kMVB], tt[kMVB];
+    float cr[kMVB], cg[kMVB], cb[kMVB], tt[kMVB];
 #pragma unroll
     for (int j = 0; j < kMVB; ++j) {
-        crg[j] = splat2(-0.0f);  // plane p_begin replaces it exactly (render.hip)
+        cr[j] = -0.0f;  // plane p_begin replaces it exactly (render.hip)
+        cg[j] = -0.0f;
         cb[j] = -0.0f;
         tt[j] = 1.0f;
     }
     const bool replace_first = !CT || back;
-    auto consume = [&](int j, const f32x4& s, bool first) {  // over, (r, g) packed
+    auto consume = [&](int j, const f32x4& s, bool first) {
         const float a = first ? 1.0f : s[3];
         const float om = 1.0f - a;
-        crg[j] = s.xy * splat2(a) + crg[j] * splat2(om);
+        cr[j] = over(s[0], a, om, cr[j]);
+        cg[j] = over(s[1], a, om, cg[j]);
         cb[j] = over(s[2], a, om, cb[j]);
         if (CT) tt[j] = tt[j] * om;
     };
@@ -212,7 +206,6 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
             const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)p * plane_stride, g.plane_bytes);
             if (staged(bx)) {
                 const LdsBox lbx = make_lds_box(bx.x, bx.y, bx.z, pitch, g.W, g.H);
-                const bool plane_fast = (bx.w & 2) != 0;  // division fast path proven for the tile
                 const float4* tex = s_tex[buf];
                 // kMG views at a time, phase by phase (positions, tap reads, blends), with
                 // the rare fix-ups behind wave-uniform tests: their LDS reads are in flight
@@ -220,27 +213,25 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
 #pragma unroll
                 for (int j0 = 0; j0 < kMVB; j0 += kMG) {
                     if (j0 < nv) {
-                        f32x2 q[kMG];
+                        float qu[kMG], qv[kMG];
                         bool fast = true;
 #pragma unroll
                         for (int jj = 0; jj < kMG; ++jj) {
-                            f32x2 uv;
-                            float w;
-                            hom_uvw_pk(s_hom[buf][j0 + jj], fx, fy, uv, w);
-                            if (!plane_fast) fast = fast && div2_safe(uv.x, uv.y, w);
-                            q[jj] = div2_fast_pk(uv, w);
+                            const float* h = s_hom[buf][j0 + jj];
+                            const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
+                            const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
+                            const float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+                            fast = fast && div2_safe(u, v, w);
+                            div2_fast(u, v, w, qu[jj], qv[jj]);
                         }
                         if (__builtin_amdgcn_ballot_w64(!fast)) {  // rare: divide_safe2's slow path
 #pragma unroll
                             for (int jj = 0; jj < kMG; ++jj) {
-                                f32x2 uv;
-                                float w;
-                                hom_uvw_pk(s_hom[buf][j0 + jj], fx, fy, uv, w);
-                                if (!div2_safe(uv.x, uv.y, w)) {
-                                    float qu, qv;
-                                    divide_safe2(uv.x, uv.y, w, qu, qv);
-                                    q[jj] = (f32x2){qu, qv};
-                                }
+                                const float* h = s_hom[buf][j0 + jj];
+                                const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
+                                const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
+                                const float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+                                if (!div2_safe(u, v, w)) divide_safe2(u, v, w, qu[jj], qv[jj]);
                             }
                         }
                         float px[kMG], py[kMG];
@@ -248,9 +239,10 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
                         bool ok = true;
 #pragma unroll
                         for (int jj = 0; jj < kMG; ++jj) {
-                            const f32x2 pp = grid_pos_pk(q[jj], g);
-                            px[jj] = pp.x;
-                            py[jj] = pp.y;
+                            const float cx = div_const(qu[jj], g.hm1, g.rc_hm1);  // SWAPPED x / (H-1), utils.py:188
+                            const float cy = div_const(qv[jj], g.wm1, g.rc_wm1);  //         y / (W-1)
+                            px[jj] = unnormalize(to_grid(cx), g.half_w);
+                            py[jj] = unnormalize(to_grid(cy), g.half_h);
                             ok = lds_issue(tex, lbx, px[jj], py[jj], ts[jj]) && ok;
                         }
                         f32x4 sm[kMG];
@@ -295,10 +287,10 @@ __global__ __launch_bounds__(kMThreads) void render_mv_kernel(const float4* __re
         if (j < nv) {
             const int64_t o = ((int64_t)(vg0 + j) * g.H + y) * g.W + x;
             if (CT) {
-                reinterpret_cast<float4*>(out)[o] = make_float4(crg[j].x, crg[j].y, cb[j], tt[j]);
+                reinterpret_cast<float4*>(out)[o] = make_float4(cr[j], cg[j], cb[j], tt[j]);
             } else {
-                out[o * 3 + 0] = crg[j].x;
-                out[o * 3 + 1] = crg[j].y;
+                out[o * 3 + 0] = cr[j];
+                out[o * 3 + 1] = cg[j];
                 out[o * 3 + 2] = cb[j];
             }
         }
