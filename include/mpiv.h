@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 3
+#define MPIV_ABI_VERSION 4
 
 enum {
     MPIV_OK = 0,
@@ -99,6 +99,33 @@ size_t mpiv_render_backward_workspace_size(int H, int W, int P);
 int mpiv_render_backward(const float *packed, int H, int W, int P, const float *homs, int V,
                          const float *dout, float *dmpi, const int64_t dmpi_strides[5], void *workspace,
                          size_t workspace_bytes, void *stream);
+
+/* ---- MPI assembly from the network output ------------------------------- */
+
+/* mpi_from_net_output (fast-torch-stereo-vision.ipynb cell 10 L79-111): the network's
+ * channels-first prediction pred [B, 2P+3, H, W] (element strides pred_strides[4];
+ * channels 0..P-1 blend weights, P..2P-1 alphas, 2P..2P+2 background rgb, tanh domain)
+ * and the reference image fg [B,H,W,3] (fg_strides[4]) -> the MPI
+ *   rgba[b,y,x,p] = (w*fg + (1-w)*bg, (pred[P+p]+1)/2),  w = (pred[p]+1)/2,
+ * rounded like the notebook's ATen ops (bit-exact).  rgba: [B,H,W,P,4] contiguous,
+ * 16-B aligned. */
+int mpiv_assemble_mpi(const float *pred, const int64_t pred_strides[4], const float *fg,
+                      const int64_t fg_strides[4], int B, int H, int W, int P, float *rgba, void *stream);
+
+/* The same for batch element b, written straight into the render's packed layout
+ * (mpiv_pack_planes: [P][H+4][W+4][4] with a zero border): assembly + pack in one
+ * pass, no [B,H,W,P,4] tensor. */
+int mpiv_assemble_mpi_packed(const float *pred, const int64_t pred_strides[4], const float *fg,
+                             const int64_t fg_strides[4], int b, int H, int W, int P, float *packed,
+                             void *stream);
+
+/* Backward of mpiv_assemble_mpi w.r.t. pred (the notebook trains through it, cell 12
+ * L5-15): drgba [B,H,W,P,4] (drgba_strides[5]) -> dpred [B,2P+3,H,W] contiguous
+ * (written, not accumulated).  Per plane dw = (sum_c g*fg - sum_c g*bg)/2,
+ * dalpha = g_a/2; d bg = sum over planes (last to first) of g*(1-w). */
+int mpiv_assemble_mpi_backward(const float *drgba, const int64_t drgba_strides[5], const float *pred,
+                               const int64_t pred_strides[4], const float *fg, const int64_t fg_strides[4],
+                               int B, int H, int W, int P, float *dpred, void *stream);
 
 /* ---- plane sweep -------------------------------------------------------- */
 

@@ -45,9 +45,12 @@ _SIGS = {
     "mpiv_render_backward": [_vp, _int, _int, _int, _vp, _int, _vp, _vp, _c_i64p, _vp, ctypes.c_size_t, _vp],
     "mpiv_plane_sweep_padded_into": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,
                                      _vp],
+    "mpiv_assemble_mpi": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
+    "mpiv_assemble_mpi_packed": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
+    "mpiv_assemble_mpi_backward": [_vp, _c_i64p, _vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib = None
 
@@ -272,6 +275,70 @@ class RenderFunction(torch.autograd.Function):
         (rgba_layers,) = ctx.saved_tensors
         grad = render_backward(rgba_layers, ctx.homs, dout) if ctx.needs_input_grad[0] else None
         return grad, None
+
+
+# ---------------------------------------------------------------------------
+# MPI assembly from the network output (notebook mpi_from_net_output)
+# ---------------------------------------------------------------------------
+
+def _net_args(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int):
+    dev = _dev(mpi_pred, fg)
+    if mpi_pred.dim() != 4 or mpi_pred.shape[1] != 2 * P + 3:
+        raise RuntimeError(f"mpi_pred must be [B, 2*{P}+3, H, W], got {tuple(mpi_pred.shape)}")
+    B, _, H, W = mpi_pred.shape
+    if tuple(fg.shape) != (B, H, W, 3):
+        raise RuntimeError(f"ref_img must be [{B},{H},{W},3], got {tuple(fg.shape)}")
+    return dev, B, H, W
+
+
+def assemble_mpi(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int) -> torch.Tensor:
+    """[B,2P+3,H,W] prediction + [B,H,W,3] reference image -> MPI [B,H,W,P,4]."""
+    dev, B, H, W = _net_args(mpi_pred, fg, P)
+    out = torch.empty((B, H, W, P, 4), device=dev, dtype=torch.float32)
+    _call("mpiv_assemble_mpi", mpi_pred, _strides(mpi_pred), fg, _strides(fg), B, H, W, P, out, _stream(dev))
+    return out
+
+
+def assemble_mpi_packed(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int, b: int,
+                        out: torch.Tensor | None = None) -> torch.Tensor:
+    """Batch element b of the assembled MPI, straight into the packed layout [P,H+4,W+4,4]."""
+    dev, B, H, W = _net_args(mpi_pred, fg, P)
+    if not 0 <= b < B:
+        raise IndexError(f"batch index {b} out of range for {B}")
+    packed = torch.empty(packed_shape(H, W, P), device=dev, dtype=torch.float32) if out is None else out
+    _call("mpiv_assemble_mpi_packed", mpi_pred, _strides(mpi_pred), fg, _strides(fg), b, H, W, P, packed,
+          _stream(dev))
+    return packed
+
+
+def assemble_mpi_backward(drgba: torch.Tensor, mpi_pred: torch.Tensor, fg: torch.Tensor, P: int) -> torch.Tensor:
+    dev, B, H, W = _net_args(mpi_pred, fg, P)
+    _dev(drgba)
+    if tuple(drgba.shape) != (B, H, W, P, 4):
+        raise RuntimeError(f"grad must be [{B},{H},{W},{P},4], got {tuple(drgba.shape)}")
+    dpred = torch.empty((B, 2 * P + 3, H, W), device=dev, dtype=torch.float32)
+    _call("mpiv_assemble_mpi_backward", drgba, _strides(drgba), mpi_pred, _strides(mpi_pred), fg, _strides(fg),
+          B, H, W, P, dpred, _stream(dev))
+    return dpred
+
+
+class AssembleFunction(torch.autograd.Function):
+    """Autograd node of the assembly: gradient w.r.t. the network prediction (the
+    reference image is data, as in the notebook's training)."""
+
+    @staticmethod
+    def forward(ctx, mpi_pred, fg, P):
+        ctx.save_for_backward(mpi_pred, fg)
+        ctx.P = P
+        return assemble_mpi(mpi_pred, fg, P)
+
+    @staticmethod
+    def backward(ctx, drgba):
+        mpi_pred, fg = ctx.saved_tensors
+        if ctx.needs_input_grad[1]:
+            raise RuntimeError("mpi_from_net_output: no gradient w.r.t. the reference image (data, not a parameter)")
+        d = assemble_mpi_backward(drgba, mpi_pred, fg, ctx.P) if ctx.needs_input_grad[0] else None
+        return d, None, None
 
 
 # ---------------------------------------------------------------------------

@@ -15,6 +15,7 @@
 #include "render_bwd.hip"
 #include "sweep.hip"
 #include "geometry.hip"
+#include "assemble.hip"
 
 namespace {
 
@@ -485,6 +486,55 @@ int mpiv_deprocess_u8(const float* in, int64_t n, uint8_t* out, void* stream) {
     if (n <= 0) return fail(MPIV_ERR_ARG, "mpiv_deprocess_u8: bad size");
     deprocess_u8_kernel<<<blocks(n, 256), 256, 0, S(stream)>>>(in, n, out);
     return launched("mpiv_deprocess_u8");
+}
+
+// ---- MPI assembly from the network output (ipynb cell 10 L79-111) ----------------
+
+static int check_net(const char* nm, const float* pred, const int64_t ps[4], const float* fg, const int64_t fs[4],
+                     int B, int H, int W, int P) {
+    if (!pred || !ps || !fg || !fs) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (B <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    if ((int64_t)H * W >= (1ll << 31) || B > kMaxGridYZ) return fail(MPIV_ERR_ARG, "%s: too large", nm);
+    return MPIV_OK;
+}
+
+int mpiv_assemble_mpi(const float* pred, const int64_t ps[4], const float* fg, const int64_t fs[4], int B, int H,
+                      int W, int P, float* rgba, void* stream) {
+    if (int rc = check_net("mpiv_assemble_mpi", pred, ps, fg, fs, B, H, W, P)) return rc;
+    if (!rgba || !aligned16(rgba)) return fail(MPIV_ERR_ARG, "mpiv_assemble_mpi: rgba null or not 16-byte aligned");
+    if (blocks(P, kAsmPl) > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_assemble_mpi: too many planes");
+    const NetStrides s{ps[0], ps[1], ps[2], ps[3], fs[0], fs[1], fs[2], fs[3]};
+    const dim3 grid(blocks((int64_t)H * W, kAsmPix), blocks(P, kAsmPl), B);
+    assemble_native_kernel<<<grid, 256, 0, S(stream)>>>(pred, fg, s, H, W, P, make_fastdiv((unsigned)W),
+                                                        reinterpret_cast<float4*>(rgba));
+    return launched("mpiv_assemble_mpi");
+}
+
+int mpiv_assemble_mpi_packed(const float* pred, const int64_t ps[4], const float* fg, const int64_t fs[4], int b,
+                             int H, int W, int P, float* packed, void* stream) {
+    if (int rc = check_net("mpiv_assemble_mpi_packed", pred, ps, fg, fs, b + 1, H, W, P)) return rc;
+    if (b < 0) return fail(MPIV_ERR_ARG, "mpiv_assemble_mpi_packed: bad batch index");
+    if (!packed || !aligned16(packed))
+        return fail(MPIV_ERR_ARG, "mpiv_assemble_mpi_packed: packed null or not 16-byte aligned");
+    if ((int64_t)(H + 2 * kPad) * (W + 2 * kPad) * 16 >= (int64_t)kOOB || P > kMaxGridYZ)
+        return fail(MPIV_ERR_ARG, "mpiv_assemble_mpi_packed: padded plane larger than 2 GiB or too many planes");
+    const NetStrides s{ps[0], ps[1], ps[2], ps[3], fs[0], fs[1], fs[2], fs[3]};
+    const int64_t npix = (int64_t)(H + 2 * kPad) * (W + 2 * kPad);
+    assemble_packed_kernel<<<dim3(blocks(npix, 256), P), 256, 0, S(stream)>>>(
+        pred, fg, s, H, W, P, b, make_fastdiv((unsigned)(W + 2 * kPad)), reinterpret_cast<float4*>(packed), npix);
+    return launched("mpiv_assemble_mpi_packed");
+}
+
+int mpiv_assemble_mpi_backward(const float* drgba, const int64_t gs[5], const float* pred, const int64_t ps[4],
+                               const float* fg, const int64_t fs[4], int B, int H, int W, int P, float* dpred,
+                               void* stream) {
+    if (int rc = check_net("mpiv_assemble_mpi_backward", pred, ps, fg, fs, B, H, W, P)) return rc;
+    if (!drgba || !gs || !dpred) return fail(MPIV_ERR_ARG, "mpiv_assemble_mpi_backward: null pointer");
+    const NetStrides s{ps[0], ps[1], ps[2], ps[3], fs[0], fs[1], fs[2], fs[3]};
+    const NativeStrides g{gs[0], gs[1], gs[2], gs[3], gs[4]};
+    assemble_backward_kernel<<<dim3(blocks((int64_t)H * W, 256), B), 256, 0, S(stream)>>>(
+        drgba, g, pred, fg, s, H, W, P, make_fastdiv((unsigned)W), dpred);
+    return launched("mpiv_assemble_mpi_backward");
 }
 
 int mpiv_selftest_div_const(int divisor, unsigned long long* mismatches, void* stream) {

@@ -154,6 +154,40 @@ def mpi_render_view_torch(rgba_layers, tgt_pose, planes, intrinsics):
     return _lib.render(rgba_layers, homs)
 
 
+def mpi_from_net_output(mpi_pred, dep):
+    """The notebook's MPI assembly (fast-torch-stereo-vision.ipynb cell 10 L79-111):
+    the network output [B, 2P+3, H, W] (P blend weights, P alphas, background rgb) and
+    dep['ref_img'] [B, H, W, 3] -> rgba_layers [B, H, W, P, 4], P = dep['mpi_planes'].shape[1].
+    One HIP pass (assemble.hip) instead of the notebook's P-step torch.cat loop, bit-exact;
+    differentiable w.r.t. mpi_pred (HIP backward) when it requires grad."""
+    num_mpi_planes = dep['mpi_planes'].shape[1]
+    fg_rgb = dep['ref_img'].to(mpi_pred.device)
+    if torch.is_grad_enabled() and (mpi_pred.requires_grad or fg_rgb.requires_grad):
+        return _lib.AssembleFunction.apply(mpi_pred, fg_rgb, num_mpi_planes)
+    return _lib.assemble_mpi(mpi_pred, fg_rgb, num_mpi_planes)
+
+
+def mpi_render_net_output_torch(mpi_pred, ref_img, tgt_pose, planes, intrinsics):
+    """mpi_render_view_torch(mpi_from_net_output(mpi_pred, ...), tgt_pose, planes, intrinsics)
+    without the [B, H, W, P, 4] tensor: each view's MPI is assembled straight into the
+    render's packed plane layout and rendered (inference / viewer path, no autograd).
+    Bit-identical to the two-step form."""
+    batch_size = tgt_pose.shape[0]
+    n_planes = len(planes)
+    depths = planes.reshape([n_planes, 1])
+    homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
+    fg = ref_img.to(mpi_pred.device)
+    dev = mpi_pred.device
+    B, _, H, W = mpi_pred.shape
+    out = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32)
+    packed = torch.empty(_lib.packed_shape(H, W, n_planes), device=dev, dtype=torch.float32)
+    h = homs.reshape(B, n_planes, 9)
+    for b in range(B):
+        _lib.assemble_mpi_packed(mpi_pred, fg, n_planes, b, out=packed)
+        _lib.render_packed(packed, h[b:b + 1], out=out[b:b + 1])
+    return out
+
+
 def pixel2cam_torch(depth, pixel_coords, intrinsics, is_homogeneous=True):
     """Back-project pixels to camera space (utils.py:356-375)."""
     return _lib.pixel2cam(depth, pixel_coords, intrinsics, is_homogeneous)

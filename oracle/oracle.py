@@ -145,3 +145,42 @@ def over_composite(layers: np.ndarray) -> np.ndarray:
     out = np.empty(layers.shape[1:-1] + (3,), np.float32)
     lib().oracle_over_composite(_fp(layers), P, n, _fp(out))
     return out
+
+
+# ---------------------------------------------------------------------------
+# MPI assembly (the notebook's mpi_from_net_output, ipynb cell 10 L79-111): pure
+# elementwise fp32 arithmetic, so numpy float32 ops round exactly like ATen's CPU
+# kernels: (x + 1) / 2, w * fg, 1 - w, (1 - w) * bg, the sum -- each rounded once.
+# ---------------------------------------------------------------------------
+
+def assemble_mpi(pred: np.ndarray, fg: np.ndarray, P: int) -> np.ndarray:
+    """pred [B,2P+3,H,W] + fg [B,H,W,3] -> rgba [B,H,W,P,4]."""
+    one, two = np.float32(1), np.float32(2)
+    p = np.transpose(pred.astype(np.float32), (0, 2, 3, 1))               # mpi_pred.permute(0, 2, 3, 1)
+    w = (p[..., :P] + one) / two                                          # blend weights
+    a = (p[..., P:2 * P] + one) / two                                     # alphas
+    bg = p[..., -3:]
+    rgb = w[..., :, None] * fg[..., None, :] + (one - w)[..., :, None] * bg[..., None, :]
+    return np.concatenate([rgb, a[..., None]], axis=-1).astype(np.float32)
+
+
+def assemble_mpi_backward(drgba: np.ndarray, pred: np.ndarray, fg: np.ndarray, P: int) -> np.ndarray:
+    """d pred for d rgba, in autograd's order: per plane dw = (sum_c g*fg + -(sum_c g*bg)) / 2
+    (channel sums left to right), dalpha = g_a / 2, and d bg accumulated from the last
+    plane to the first (the engine runs the planes' nodes in reverse creation order)."""
+    one, two = np.float32(1), np.float32(2)
+    p = np.transpose(pred.astype(np.float32), (0, 2, 3, 1))
+    w = (p[..., :P] + one) / two
+    bg = p[..., -3:]
+    g = drgba.astype(np.float32)
+    gc = g[..., :3]
+    sf = (gc[..., 0] * fg[..., None, 0] + gc[..., 1] * fg[..., None, 1]) + gc[..., 2] * fg[..., None, 2]
+    sb = (gc[..., 0] * bg[..., None, 0] + gc[..., 1] * bg[..., None, 1]) + gc[..., 2] * bg[..., None, 2]
+    dw = (sf + -sb) / two
+    da = g[..., 3] / two
+    contrib = gc * (one - w)[..., None]                                   # [B,H,W,P,3]
+    dbg = contrib[..., P - 1, :].copy()
+    for i in range(P - 2, -1, -1):
+        dbg = dbg + contrib[..., i, :]
+    d = np.concatenate([dw, da, dbg], axis=-1)                            # [B,H,W,2P+3]
+    return np.ascontiguousarray(np.transpose(d, (0, 3, 1, 2))).astype(np.float32)

@@ -129,3 +129,20 @@ def test_training_loss_gradient(grad, dev):
     loss.backward()
     np.testing.assert_allclose(loss.item(), float(grad["loss_value"]), rtol=1e-6)
     np.testing.assert_allclose(pred.grad.cpu().numpy(), grad["loss_grad"], rtol=0, atol=1e-6)
+
+
+def test_training_loss_gradient_hip_assembly(grad, dev):
+    """The same training loss with the MPI assembled by the HIP drop-in
+    (mv.mpi_from_net_output, assemble.hip) instead of torch ops: loss and gradient
+    through assembly + render + MSE against the reference's CPU autograd."""
+    pred = torch.tensor(grad["loss_pred"]).to(dev).requires_grad_(True)
+    P = grad["loss_planes"].shape[0]
+    dep = {"mpi_planes": torch.zeros((pred.shape[0], P), device=dev),
+           "ref_img": torch.tensor(grad["loss_ref"]).to(dev)}
+    rgba = mv.mpi_from_net_output(pred, dep)
+    img = mv.mpi_render_view_torch(rgba, torch.tensor(grad["loss_pose"]).to(dev),
+                                   torch.tensor(grad["loss_planes"]).to(dev), torch.tensor(grad["loss_K"]).to(dev))
+    loss = torch.nn.functional.mse_loss(img, torch.tensor(grad["loss_tgt"]).to(dev))
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), float(grad["loss_value"]), rtol=1e-6)
+    np.testing.assert_allclose(pred.grad.cpu().numpy(), grad["loss_grad"], rtol=0, atol=1e-6)

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Golden fixtures for the MPI assembly: the notebook's own
+`mpi_from_net_output` (fast-torch-stereo-vision.ipynb cell 10 L79-111), run here on
+CPU with torch 2.10 autograd.  The function lives in a notebook cell, not in utils.py,
+so it is taken from the notebook JSON at generation time (ast: the def node of that
+cell) and executed with `device = cpu`; nothing of it is copied into this repository.
+Test tooling only; writes tests/golden/netout.npz:
+
+    <case>_pred [B,2P+3,H,W], <case>_ref [B,H,W,3], <case>_P, <case>_rgba [B,H,W,P,4],
+    <case>_drgba (random upstream gradient), <case>_dpred (autograd d rgba . drgba / d pred)
+
+Usage:  python tools/gen_goldens_netout.py
+"""
+from __future__ import annotations
+
+import ast
+import glob
+import json
+import os
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden", "netout.npz")
+
+
+def load_notebook_function(name="mpi_from_net_output"):
+    nb = json.load(open(glob.glob(os.path.join(REF, "*.ipynb"))[0]))
+    for cell in nb["cells"]:
+        src = "".join(cell["source"])
+        if f"def {name}(" not in src:
+            continue
+        tree = ast.parse(src)
+        for node in tree.body:
+            if isinstance(node, ast.FunctionDef) and node.name == name:
+                ns = {"torch": torch, "device": torch.device("cpu")}
+                exec(compile(ast.Module(body=[node], type_ignores=[]), f"<notebook:{name}>", "exec"), ns)
+                return ns[name]
+    raise RuntimeError(f"{name} not found in the notebook")
+
+
+def main():
+    fn = load_notebook_function()
+    g = torch.Generator().manual_seed(2024)
+    out = {}
+
+    def case(name, B, H, W, P, scale=1.0):
+        pred = ((torch.rand((B, 2 * P + 3, H, W), generator=g) * 2 - 1) * scale).requires_grad_(True)
+        ref = torch.rand((B, H, W, 3), generator=g) * 2 - 1
+        dep = {"mpi_planes": torch.zeros((B, P)), "ref_img": ref}
+        rgba = fn(pred, dep)
+        drgba = torch.rand(rgba.shape, generator=g) * 2 - 1
+        rgba.backward(drgba)
+        out.update({f"{name}_pred": pred.detach().numpy(), f"{name}_ref": ref.numpy(),
+                    f"{name}_P": np.array(P, np.int32), f"{name}_rgba": rgba.detach().numpy(),
+                    f"{name}_drgba": drgba.numpy(), f"{name}_dpred": pred.grad.numpy()})
+
+    case("na", 2, 24, 40, 6)
+    case("nb", 1, 17, 29, 32)          # odd sizes, a Stereo-Mag plane count
+    case("nc", 3, 8, 72, 3, scale=1.5)  # values outside the tanh range too
+    np.savez_compressed(OUT, **out)
+    print("wrote", OUT, {k: v.shape for k, v in out.items() if k.endswith("rgba")})
+
+
+if __name__ == "__main__":
+    main()
