@@ -4,7 +4,7 @@ headline config 4).  One JSON line per measurement: kernel time from HIP events
 on the launching stream (median of --iters after --warmup), throughput and the
 achieved fraction of the 8 TB/s HBM roofline on ALGORITHMIC bytes.
 
-    python tools/bench_configs.py [--iters 20] [--only c1,c2,c3,c4,c5]
+    python tools/bench_configs.py [--iters 20] [--only c1,c2,c3,c4,c5,bwd,net]
 """
 from __future__ import annotations
 
@@ -213,11 +213,60 @@ def bwd(dev, it, wu):
                P * H * W * 32, H * W / 1e6, extra={"workspace_GB": round(ws / 1e9, 3)})
 
 
+def _notebook_assembly(mpi_pred, ref_img, P):
+    """The notebook's mpi_from_net_output op sequence (ipynb cell 10 L79-111: P-step
+    torch.cat loop) on torch's GPU ops -- the reference path on this GPU, for comparison."""
+    B, _, H, W = mpi_pred.shape
+    p = mpi_pred.permute(0, 2, 3, 1)
+    bw = (p[..., :P] + 1.) / 2.
+    al = (p[..., P:2 * P] + 1.) / 2.
+    bg = p[..., -3:]
+    layers = None
+    for i in range(P):
+        w = bw[..., i:i + 1]
+        cur = torch.cat([w * ref_img + (1 - w) * bg, al[..., i:i + 1]], dim=3)
+        layers = cur if layers is None else torch.cat([layers, cur], dim=3)
+    return layers.reshape(B, H, W, P, 4)
+
+
+def net(dev, it, wu):
+    """MPI assembly from the network output at the config-2 size (Stereo-Mag 1024x576x32,
+    one view): bytes = prediction (2P+3)*4 + reference image 12 read + the MPI written
+    (P*16 per pixel); packed layout writes the padded planes."""
+    c = configs.config2()
+    H, W, P = c["H"], c["W"], c["P"]
+    g = torch.Generator(device=dev).manual_seed(3)
+    pred = torch.rand((1, 2 * P + 3, H, W), generator=g, device=dev) * 2 - 1
+    ref = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    alg = H * W * ((2 * P + 3) * 4 + 12 + P * 16)
+    ms, mn = timed(lambda: _lib.assemble_mpi(pred, ref, P), it, wu)
+    report(f"net assemble {W}x{H}x{P} -> [1,H,W,P,4] (HIP)", ms, mn, alg, H * W / 1e6)
+    packed = torch.empty(_lib.packed_shape(H, W, P), device=dev)
+    ms, mn = timed(lambda: _lib.assemble_mpi_packed(pred, ref, P, 0, out=packed), it, wu)
+    report(f"net assemble {W}x{H}x{P} -> packed planes (HIP)", ms, mn,
+           H * W * ((2 * P + 3) * 4 + 12) + (H + 4) * (W + 4) * P * 16, H * W / 1e6)
+    ms, mn = timed(lambda: _notebook_assembly(pred, ref, P), max(3, it // 4), 1)
+    report(f"net assemble {W}x{H}x{P}: the notebook's torch.cat loop on torch GPU ops", ms, mn, alg, H * W / 1e6)
+    drgba = torch.rand((1, H, W, P, 4), generator=g, device=dev) * 2 - 1
+    ms, mn = timed(lambda: _lib.assemble_mpi_backward(drgba, pred, ref, P), it, wu)
+    report(f"net assemble backward {W}x{H}x{P} (HIP)", ms, mn, H * W * (P * 16 + (2 * P + 3) * 8 + 12), H * W / 1e6)
+    K = configs.f32([c["K"]]).to(dev)
+    pose = configs.f32(c["poses"][:1]).to(dev)
+    planes = configs.f32(c["depths"]).to(dev)
+    ms, mn = timed(lambda: mv.mpi_render_net_output_torch(pred, ref, pose, planes, K), it, wu)
+    report(f"net output -> rendered view {W}x{H}x{P}, fused (assemble to packed + render)", ms, mn,
+           alg + P * H * W * 16 + H * W * 12, H * W / 1e6)
+    dep = {"mpi_planes": torch.zeros((1, P), device=dev), "ref_img": ref}
+    ms, mn = timed(lambda: mv.mpi_render_view_torch(mv.mpi_from_net_output(pred, dep), pose, planes, K), it, wu)
+    report(f"net output -> rendered view {W}x{H}x{P}, two-step drop-ins", ms, mn,
+           alg + P * H * W * 16 + H * W * 12, H * W / 1e6)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--only", default="c1,c2,c3,c4,c5,bwd")
+    ap.add_argument("--only", default="c1,c2,c3,c4,c5,bwd,net")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     for name in a.only.split(","):
