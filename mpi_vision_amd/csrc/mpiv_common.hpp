@@ -351,6 +351,48 @@ __device__ __forceinline__ bool lds_issue(const float4* __restrict__ tex, const 
     return (__builtin_amdgcn_fmed3f(rx, b.gxl, b.gxh) == rx) & (__builtin_amdgcn_fmed3f(ry, b.gyl, b.gyh) == ry);
 }
 
+// lds_issue for C = 3 texels: the tap reads are ds_read_b96 (the padding channel is
+// never read), 12 VGPRs per tap instead of 16.
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+struct TapSet3 {
+    f32x3 a, b, c, d;
+    float nw, ne, sw, se;
+};
+
+__device__ __forceinline__ bool lds_issue3(const float4* __restrict__ tex, const LdsBox& b, float px, float py,
+                                           TapSet3& t) {
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
+    const float rx = fx0 - b.xl, ry = fy0 - b.yl;
+    const float ix = __builtin_amdgcn_fmed3f(rx, 0.0f, b.xspan);
+    const float iy = __builtin_amdgcn_fmed3f(ry, 0.0f, b.yspan);
+    const float4* st = tex + (int)__builtin_fmaf(iy, (float)b.pitch, ix);
+    t.a = *reinterpret_cast<const f32x3*>(st);
+    t.b = *reinterpret_cast<const f32x3*>(st + 1);
+    t.c = *reinterpret_cast<const f32x3*>(st + b.pitch);
+    t.d = *reinterpret_cast<const f32x3*>(st + b.pitch + 1);
+    return (__builtin_amdgcn_fmed3f(rx, b.gxl, b.gxh) == rx) & (__builtin_amdgcn_fmed3f(ry, b.gyl, b.gyh) == ry);
+}
+
+__device__ __forceinline__ f32x4 blend_taps3(const TapSet3& t) {
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float acc = t.a[k] * t.nw;
+        acc = __builtin_fmaf(t.b[k], t.ne, acc);
+        acc = __builtin_fmaf(t.c[k], t.sw, acc);
+        acc = __builtin_fmaf(t.d[k], t.se, acc);
+        o[k] = acc;
+    }
+    o[3] = 0.0f;
+    return o;
+}
+
 // One bilinear sample from the staged box, with the weights and fma chain of
 // issue_taps_padded + blend_taps.  Returns false when the tap origin is not staged
 // (see LdsBox; NaN included): its result is then meaningless and the caller gathers

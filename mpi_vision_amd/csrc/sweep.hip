@@ -515,7 +515,13 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
         }
         f32x4 s[kSweepDG];
         bool staged = pitch > 0;
-        if (staged) {
+        if (staged && C == 3) {  // RGB: 12-B tap reads, 3-channel blends
+            TapSet3 ts[kSweepDG];
+#pragma unroll
+            for (int j = 0; j < kSweepDG; ++j) staged = lds_issue3(s_src, lbx, px[j], py[j], ts[j]) && staged;
+#pragma unroll
+            for (int j = 0; j < kSweepDG; ++j) s[j] = blend_taps3(ts[j]);
+        } else if (staged) {
             TapSet ts[kSweepDG];
 #pragma unroll
             for (int j = 0; j < kSweepDG; ++j) staged = lds_issue(s_src, lbx, px[j], py[j], ts[j]) && staged;
