@@ -234,6 +234,9 @@ int mpiv_render_backward(const float* packed, int H, int W, int P, const float* 
     const int64_t nq = (int64_t)P * HW;
     const unsigned nb = (unsigned)((nk + kScanTile - 1) / kScanTile);
     const GradOut so{st[1], st[2], st[3], st[4]};
+    // dense [H,W,P,4] view gradients take the LDS-transposed gather
+    const bool dense = so.c == 1 && so.p == 4 && so.x == (int64_t)P * 4 && so.y == (int64_t)W * P * 4 &&
+                       (int64_t)H * W <= kMaxGridX && blocks(P, kGatherPl) <= kMaxGridYZ;
     hipStream_t q = S(stream);
     if (hipMemsetAsync(ws.count, 0, (size_t)nk * 4, q) != hipSuccess)
         return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
@@ -250,7 +253,12 @@ int mpiv_render_backward(const float* packed, int H, int W, int P, const float* 
         scan_apply_kernel<<<nb, kScanBlock, 0, q>>>(ws.count, nk, ws.bsum, ws.offs);
         bucket_fill_kernel<<<blocks(nq, 256), 256, 0, q>>>(P, HW, K, ws);
         bucket_sort_kernel<<<blocks(nk, 256), 256, 0, q>>>(nk, ws);
-        render_bwd_gather_kernel<<<blocks(nq, 256), 256, 0, q>>>(H, W, P, ws, dmpi + (int64_t)v * st[0], so);
+        float* gv = dmpi + (int64_t)v * st[0];
+        if (dense && aligned16(gv))
+            render_bwd_gather_dense_kernel<<<dim3(blocks((int64_t)H * W, kWave), blocks(P, kGatherPl)),
+                                             kGatherPl * kWave, 0, q>>>(H, W, P, ws, reinterpret_cast<float4*>(gv));
+        else
+            render_bwd_gather_kernel<<<blocks(nq, 256), 256, 0, q>>>(H, W, P, ws, gv, so);
     }
     return launched(nm);
 }

@@ -214,12 +214,9 @@ __device__ __forceinline__ unsigned order_key(int pix, int corner) {
     return ((unsigned)(pix / kGridVec) << 5) | ((unsigned)corner << 3) | (unsigned)(pix % kGridVec);
 }
 
-__global__ __launch_bounds__(256) void render_bwd_gather_kernel(int H, int W, int P, BwdWs ws,
-                                                                float* __restrict__ dmpi, GradOut so) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Sum of the gradient contributions of texel t of plane p, in the reference's order.
+__device__ __forceinline__ float4 gather_texel(int H, int W, int p, int t, const BwdWs& ws) {
     const int HW = H * W;
-    if (q >= (int64_t)P * HW) return;
-    const int p = (int)(q / HW), t = (int)(q - (int64_t)p * HW);
     const int ty = t / W, tx = t - ty * W;
     const int K1 = W + 1;
     const int64_t base = (int64_t)p * (H + 1) * K1;
@@ -266,11 +263,41 @@ __global__ __launch_bounds__(256) void render_bwd_gather_kernel(int H, int W, in
         a2 = a2 + w * d.z;
         a3 = a3 + w * d.w;
     }
+    return make_float4(a0, a1, a2, a3);
+}
+
+// Generic output strides: one work-item per (plane, texel), planes outermost.
+__global__ __launch_bounds__(256) void render_bwd_gather_kernel(int H, int W, int P, BwdWs ws,
+                                                                float* __restrict__ dmpi, GradOut so) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int HW = H * W;
+    if (q >= (int64_t)P * HW) return;
+    const int p = (int)(q / HW), t = (int)(q - (int64_t)p * HW);
+    const int ty = t / W, tx = t - ty * W;
+    const float4 a = gather_texel(H, W, p, t, ws);
     float* o = dmpi + ty * so.y + tx * so.x + p * so.p;
-    o[0] = a0;
-    o[so.c] = a1;
-    o[2 * so.c] = a2;
-    o[3 * so.c] = a3;
+    o[0] = a.x;
+    o[so.c] = a.y;
+    o[2 * so.c] = a.z;
+    o[3 * so.c] = a.w;
+}
+
+// Dense output ([H,W,P,4] contiguous, 16-B aligned): a block gathers 64 texels x 8
+// planes (wave = plane: the workspace reads stay coalesced) and writes them through
+// LDS as one 128-B run per texel (8 planes x 16 B) -- the direct form writes 4-B pieces
+// at a P*16-B lane stride.
+constexpr int kGatherPl = 8;
+__global__ __launch_bounds__(kGatherPl * 64) void render_bwd_gather_dense_kernel(int H, int W, int P, BwdWs ws,
+                                                                              float4* __restrict__ dmpi) {
+    __shared__ float4 tile[kGatherPl][kWave + 1];
+    const int HW = H * W;
+    const int t0 = blockIdx.x * kWave, p0 = blockIdx.y * kGatherPl;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
+    const int t = t0 + lane, p = p0 + w;
+    if (t < HW && p < P) tile[w][lane] = gather_texel(H, W, p, t, ws);
+    __syncthreads();
+    const int i = threadIdx.x / kGatherPl, j = threadIdx.x % kGatherPl;  // texel, plane (plane fastest)
+    if (t0 + i < HW && p0 + j < P) dmpi[(int64_t)(t0 + i) * P + p0 + j] = tile[j][i];
 }
 
 }  // namespace mpiv
