@@ -132,9 +132,18 @@ __global__ __launch_bounds__(kScanBlock) void scan_tile_sums_kernel(const int* _
     __shared__ int s_tmp[kScanBlock];
     const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
     int sum = 0;
+    if (base + kScanItems <= n) {  // whole item run in range: 16-B loads (base is 64-B aligned)
+        const int4* v4 = reinterpret_cast<const int4*>(in + base);
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i)
-        if (base + i < n) sum += in[base + i];
+        for (int i = 0; i < kScanItems / 4; ++i) {
+            const int4 v = v4[i];
+            sum += v.x + v.y + v.z + v.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kScanItems; ++i)
+            if (base + i < n) sum += in[base + i];
+    }
     int total;
     block_exclusive_scan(sum, s_tmp, total);
     if (threadIdx.x == 0) bsum[blockIdx.x] = total;
@@ -161,17 +170,39 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const int* __res
     const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
     int v[kScanItems];
     int sum = 0;
+    const bool full = base + kScanItems <= n;  // whole run in range: 16-B loads and stores
+    if (full) {
+        const int4* v4 = reinterpret_cast<const int4*>(in + base);
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-        v[i] = base + i < n ? in[base + i] : 0;
-        sum += v[i];
+        for (int i = 0; i < kScanItems / 4; ++i) {
+            const int4 q = v4[i];
+            v[4 * i] = q.x; v[4 * i + 1] = q.y; v[4 * i + 2] = q.z; v[4 * i + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kScanItems; ++i) v[i] = base + i < n ? in[base + i] : 0;
     }
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) sum += v[i];
     int total;
     int run = bsum[blockIdx.x] + block_exclusive_scan(sum, s_tmp, total);
+    if (full) {  // out = offs + 0: 16-B aligned like in
+        int4* o4 = reinterpret_cast<int4*>(out + base);
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-        if (base + i < n) out[base + i] = run;
-        run += v[i];
+        for (int i = 0; i < kScanItems / 4; ++i) {
+            int4 q;
+            q.x = run; run += v[4 * i];
+            q.y = run; run += v[4 * i + 1];
+            q.z = run; run += v[4 * i + 2];
+            q.w = run; run += v[4 * i + 3];
+            o4[i] = q;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kScanItems; ++i) {
+            if (base + i < n) out[base + i] = run;
+            run += v[i];
+        }
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanBlock - 1) out[n] = run;  // grand total
 }
