@@ -63,16 +63,23 @@ __global__ __launch_bounds__(256) void render_bwd_chain_kernel(const float4* __r
     const float fx = (float)x, fy = (float)y;
 
     float cr = -0.0f, cg = -0.0f, cb = -0.0f;  // plane 0 replaces it exactly (render.hip)
-    for (int p = 0; p < g.P; ++p) {
-        float px, py;
-        render_pos<FAST>(homs + (int64_t)p * 9, fx, fy, g, px, py);
+    // plane p's sample: position, then its four taps in flight (the last plane is
+    // re-issued past the end so every iteration issues; render.hip's ping-pong)
+    struct Sample {
         TapSet ts;
-        issue_taps_padded(make_rsrc(planes + (int64_t)p * plane_stride, g.plane_bytes), g.W, g.H, g.Wp, g.org,
-                          g.row, px, py, ts);
-        const f32x4 s = blend_taps(ts);
-        const float fx0 = floorf(px), fy0 = floorf(py);
+        float px, py;
+    };
+    auto issue = [&](int p, Sample& sm) {
+        const int pc = p < g.P ? p : g.P - 1;
+        render_pos<FAST>(homs + (int64_t)pc * 9, fx, fy, g, sm.px, sm.py);
+        issue_taps_padded(make_rsrc(planes + (int64_t)pc * plane_stride, g.plane_bytes), g.W, g.H, g.Wp, g.org,
+                          g.row, sm.px, sm.py, sm.ts);
+    };
+    auto consume = [&](int p, const Sample& sm) {
+        const f32x4 s = blend_taps(sm.ts);
+        const float fx0 = floorf(sm.px), fy0 = floorf(sm.py);
         const int64_t q = (int64_t)p * HW + pix;
-        ws.fw[q] = make_float2(px - fx0, py - fy0);
+        ws.fw[q] = make_float2(sm.px - fx0, sm.py - fy0);
         // some tap of this sample lies in the image iff the nw tap is in [-1, W-1] x [-1, H-1]
         // (float compares: NaN positions have no taps, as in the reference's masks)
         const bool in = fx0 >= -1.0f && fx0 <= (float)(g.W - 1) && fy0 >= -1.0f && fy0 <= (float)(g.H - 1);
@@ -86,7 +93,19 @@ __global__ __launch_bounds__(256) void render_bwd_chain_kernel(const float4* __r
         cr = over(s[0], a, om, cr);
         cg = over(s[1], a, om, cg);
         cb = over(s[2], a, om, cb);
+    };
+    Sample A, B;
+    issue(0, A);
+    int p = 0;
+    for (; p + 1 < g.P; p += 2) {
+        issue(p + 1, B);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(p, A);
+        issue(p + 2, A);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(p + 1, B);
     }
+    if (p < g.P) consume(p, A);
     // over_composite backward (utils.py:149-156 under autograd), front to back
     const float* d = dout + (int64_t)pix * 3;
     float g0 = d[0], g1 = d[1], g2 = d[2];
