@@ -540,8 +540,14 @@ int mpiv_assemble_mpi_backward(const float* drgba, const int64_t gs[5], const fl
     if (!drgba || !gs || !dpred) return fail(MPIV_ERR_ARG, "mpiv_assemble_mpi_backward: null pointer");
     const NetStrides s{ps[0], ps[1], ps[2], ps[3], fs[0], fs[1], fs[2], fs[3]};
     const NativeStrides g{gs[0], gs[1], gs[2], gs[3], gs[4]};
-    assemble_backward_kernel<<<dim3(blocks((int64_t)H * W, 256), B), 256, 0, S(stream)>>>(
-        drgba, g, pred, fg, s, H, W, P, make_fastdiv((unsigned)W), dpred);
+    const bool dense = g.c == 1 && g.p == 4 && g.x == (int64_t)P * 4 && g.y == (int64_t)W * P * 4 &&
+                       g.b == (int64_t)H * W * P * 4 && aligned16(drgba);
+    if (dense)
+        assemble_backward_dense_kernel<<<dim3(blocks((int64_t)H * W, kAbPix), B), kAbPix, 0, S(stream)>>>(
+            reinterpret_cast<const float4*>(drgba), pred, fg, s, H, W, P, make_fastdiv((unsigned)W), dpred);
+    else
+        assemble_backward_kernel<<<dim3(blocks((int64_t)H * W, 256), B), 256, 0, S(stream)>>>(
+            drgba, g, pred, fg, s, H, W, P, make_fastdiv((unsigned)W), dpred);
     return launched("mpiv_assemble_mpi_backward");
 }
 

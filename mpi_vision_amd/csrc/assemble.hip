@@ -132,4 +132,65 @@ __global__ __launch_bounds__(256) void assemble_backward_kernel(const float* __r
     dp[(int64_t)(2 * P + 2) * npix] = db2;
 }
 
+// The same for a dense d rgba ([B,H,W,P,4] contiguous): 256 pixels per block; the
+// gradient runs are staged through LDS 8 planes at a time (each pixel's 8 x 16 B read
+// as one 128-B segment) instead of each lane walking its own P*16-B run.
+constexpr int kAbPix = 256;
+constexpr int kAbPl = 8;
+
+__global__ __launch_bounds__(kAbPix) void assemble_backward_dense_kernel(const float4* __restrict__ grad,
+                                                                        const float* __restrict__ pred,
+                                                                        const float* __restrict__ fg, NetStrides s,
+                                                                        int H, int W, int P, FastDiv w_div,
+                                                                        float* __restrict__ dpred) {
+    __shared__ float4 tile[kAbPix][kAbPl + 1];
+    const int64_t npix = (int64_t)H * W;
+    const int64_t pix0 = (int64_t)blockIdx.x * kAbPix;
+    const int b = blockIdx.y;
+    const int64_t pix = pix0 + threadIdx.x;
+    const bool live = pix < npix;
+    const int y = live ? (int)fast_div((unsigned)pix, w_div) : 0, x = live ? (int)pix - y * W : 0;
+    const float* pp = pred + (int64_t)b * s.pb + (int64_t)y * s.py + (int64_t)x * s.px;
+    const float* fp = fg + (int64_t)b * s.fb + (int64_t)y * s.fy + (int64_t)x * s.fx;
+    float f0 = 0.f, f1 = 0.f, f2 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f;
+    if (live) {
+        f0 = fp[0]; f1 = fp[s.fc]; f2 = fp[2 * s.fc];
+        b0 = pp[(int64_t)(2 * P) * s.pc]; b1 = pp[(int64_t)(2 * P + 1) * s.pc]; b2 = pp[(int64_t)(2 * P + 2) * s.pc];
+    }
+    const float4* gb = grad + (int64_t)b * npix * P;
+    float* dp = dpred + (int64_t)b * (2 * P + 3) * npix + pix;
+    float db0 = 0.f, db1 = 0.f, db2 = 0.f;
+    const int nch = (P + kAbPl - 1) / kAbPl;
+    for (int ch = nch - 1; ch >= 0; --ch) {  // planes last to first, as autograd runs them
+        const int p0 = ch * kAbPl, np = min(kAbPl, P - p0);
+        __syncthreads();  // the previous chunk's reads of the tile are done
+        for (int k = threadIdx.x; k < kAbPix * kAbPl; k += kAbPix) {
+            const int i = k / kAbPl, j = k % kAbPl;
+            if (pix0 + i < npix && j < np) tile[i][j] = gb[(pix0 + i) * P + p0 + j];
+        }
+        __syncthreads();
+        if (!live) continue;
+        for (int j = np - 1; j >= 0; --j) {
+            const int p = p0 + j;
+            const float4 g = tile[threadIdx.x][j];
+            const float w = (pp[(int64_t)p * s.pc] + 1.0f) / 2.0f;
+            const float om = 1.0f - w;
+            const float sf = (g.x * f0 + g.y * f1) + g.z * f2;
+            const float sb = (g.x * b0 + g.y * b1) + g.z * b2;
+            dp[(int64_t)p * npix] = (sf + -sb) / 2.0f;
+            dp[(int64_t)(P + p) * npix] = g.w / 2.0f;
+            const float c0 = g.x * om, c1 = g.y * om, c2 = g.z * om;
+            if (p == P - 1) {
+                db0 = c0; db1 = c1; db2 = c2;
+            } else {
+                db0 = db0 + c0; db1 = db1 + c1; db2 = db2 + c2;
+            }
+        }
+    }
+    if (!live) return;
+    dp[(int64_t)(2 * P) * npix] = db0;
+    dp[(int64_t)(2 * P + 1) * npix] = db1;
+    dp[(int64_t)(2 * P + 2) * npix] = db2;
+}
+
 }  // namespace mpiv

@@ -63,10 +63,15 @@ def test_assemble_strided_inputs(dev):
     rgba = _lib.assemble_mpi(pred, fg, P)
     drgba = torch.rand((B, H, W, P, 4), generator=g) * 2 - 1
     dpred = _lib.assemble_mpi_backward(drgba.to(dev), pred, fg, P)
+    # a non-dense upstream gradient takes the generic (per-lane run) backward kernel
+    dwide = torch.rand((B, H, W, P + 2, 4), generator=g) * 2 - 1
+    dpred_s = _lib.assemble_mpi_backward(dwide.to(dev)[:, :, :, 1:P + 1], pred, fg, P)
     torch.cuda.synchronize()
     pn, fn = nhwc.permute(0, 3, 1, 2).contiguous().numpy(), wide[..., 1:4].contiguous().numpy()
     assert_bits(rgba.cpu().numpy(), oracle.assemble_mpi(pn, fn, P), "strided forward")
-    assert_bits(dpred.cpu().numpy(), oracle.assemble_mpi_backward(drgba.numpy(), pn, fn, P), "strided backward")
+    assert_bits(dpred.cpu().numpy(), oracle.assemble_mpi_backward(drgba.numpy(), pn, fn, P), "dense backward")
+    assert_bits(dpred_s.cpu().numpy(), oracle.assemble_mpi_backward(dwide[:, :, :, 1:P + 1].contiguous().numpy(),
+                                                                    pn, fn, P), "strided backward")
 
 
 def test_assemble_packed_equals_pack_of_assembled(net, dev):
