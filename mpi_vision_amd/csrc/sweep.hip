@@ -345,6 +345,7 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
     __shared__ int4 s_box;              // x_lo, y_lo, rows, pitch (0: gather from global memory)
     __shared__ int s_fast;              // every sample of the tile is in div2_rn's fast range
     __shared__ __attribute__((aligned(16))) float4 s_out[kWaves][kWave * C];  // per wave: its run
+
     const int segs = (sp.Wt + kSLP - 1) / kSLP;
     const int b = blockIdx.y;
     const int ty = blockIdx.x / segs;

@@ -125,7 +125,7 @@ def test_plane_sweep_many_depths_vs_oracle(dev):
     assert_bits(out.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("C", [1, 4])
+@pytest.mark.parametrize("C", [1, 2, 3, 4])
 @pytest.mark.parametrize("shrink", ["0", "3"])
 def test_plane_sweep_lds_vs_oracle(C, shrink, dev, monkeypatch):
     """The LDS-staged sweep with C = 1 and 4, a target size whose rows end in a partial
