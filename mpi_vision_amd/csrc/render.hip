@@ -255,6 +255,173 @@ __global__ __launch_bounds__(256) void render_packed_kernel(const float4* __rest
 }
 
 // ---------------------------------------------------------------------------
+// two horizontally adjacent pixels per work-item (render_pair_kernel)
+// ---------------------------------------------------------------------------
+//
+// What bounds render_packed_kernel on a camera path is the texture path: four 16-B
+// gathers per sample at ~64 B/clk/CU.  Where the sample of pixel x+1 has its north-west
+// tap exactly one texel east of pixel x's (floor(px) advanced by one on the same row --
+// almost every pair at magnifications near 1), pixel x+1's west taps ARE pixel x's east
+// taps, already in registers.  A work-item owns the pair (x, x+1): it always gathers
+// pixel x's four taps and pixel x+1's two east taps, and pixel x+1's two west taps only
+// when some lane of the wave has a pair that does not share (a wave-uniform branch;
+// lanes that share get the buffer's zero range there).  The sharing test compares the
+// two tap offsets, so a shared texel is the same memory word: the result is
+// bit-identical to the one-pixel kernel.  A wave covers 128 pixels of one row.
+constexpr int kPairX = 128;
+
+struct PairTaps {
+    f32x4 a0, b0, c0, d0;  // pixel x:   NW, NE, SW, SE
+    f32x4 a1, b1, c1, d1;  // pixel x+1: NW (unless shared), NE, SW (unless shared), SE
+    float w0[4], w1[4];    // bilinear weights nw, ne, sw, se
+    bool share;            // pixel x+1's west taps are pixel x's east taps
+};
+
+// floor, weights and the padded-plane byte offset of the north-west tap (issue_taps_padded)
+__device__ __forceinline__ int tap_origin(const RenderGeom& g, float px, float py, float* w) {
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    w[0] = sy * ex;
+    w[1] = sy * wx;
+    w[2] = wy * ex;
+    w[3] = wy * wx;
+    const int cx = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)g.W);
+    const int cy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)g.H);
+    return (__mul24(cy, g.Wp) + cx) * 16 + g.org;
+}
+
+__device__ __forceinline__ f32x4 blend4w(f32x4 a, f32x4 b, f32x4 c, f32x4 d, const float* w) {
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float acc = a[k] * w[0];
+        acc = __builtin_fmaf(b[k], w[1], acc);
+        acc = __builtin_fmaf(c[k], w[2], acc);
+        acc = __builtin_fmaf(d[k], w[3], acc);
+        o[k] = acc;
+    }
+    return o;
+}
+
+template <bool CT, bool GUARD>
+__device__ __forceinline__ void render_pair_pixels(const float4* __restrict__ planes, int64_t plane_stride,
+                                                   const RenderGeom& g, int p_begin, int p_end, int back,
+                                                   const float* __restrict__ hv, int x, int y, bool second,
+                                                   float* __restrict__ out0) {
+    const float fx = (float)x, fx1 = (float)(x + 1), fy = (float)y;
+    float c0r = -0.0f, c0g = -0.0f, c0b = -0.0f, t0 = 1.0f;  // render_packed_pixel: plane 0 replaces
+    float c1r = -0.0f, c1g = -0.0f, c1b = -0.0f, t1 = 1.0f;
+    const bool replace_first = !CT || back;
+    const int last = p_end - 1;
+    auto hom = [&](int p) { return load_hom(hv + (int64_t)(p < last ? p : last) * 9); };
+    auto issue = [&](int p, const Hom9& h, PairTaps& ts) {
+        const int q = p < last ? p : last;
+        float px0, py0, px1, py1;
+        render_pos_fast<GUARD>(h.h, fx, fy, g, px0, py0);
+        render_pos_fast<GUARD>(h.h, fx1, fy, g, px1, py1);
+        const int off0 = tap_origin(g, px0, py0, ts.w0);
+        const int off1 = tap_origin(g, px1, py1, ts.w1);
+        ts.share = off1 == off0 + 16;
+        const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes);
+        if (__builtin_amdgcn_ballot_w64(!ts.share)) {  // wave-uniform: some pair does not share
+            const int o = ts.share ? kOOB : off1;
+            ts.a1 = llvm_raw_buffer_load_v4f32(r, o, 0, 0);
+            ts.c1 = llvm_raw_buffer_load_v4f32(r, o, g.row, 0);
+        }
+        ts.a0 = llvm_raw_buffer_load_v4f32(r, off0, 0, 0);
+        ts.b0 = llvm_raw_buffer_load_v4f32(r, off0 + 16, 0, 0);
+        ts.c0 = llvm_raw_buffer_load_v4f32(r, off0, g.row, 0);
+        ts.d0 = llvm_raw_buffer_load_v4f32(r, off0 + 16, g.row, 0);
+        ts.b1 = llvm_raw_buffer_load_v4f32(r, off1 + 16, 0, 0);
+        ts.d1 = llvm_raw_buffer_load_v4f32(r, off1 + 16, g.row, 0);
+    };
+    auto consume = [&](const PairTaps& ts, bool first) {
+        const f32x4 s0 = blend4w(ts.a0, ts.b0, ts.c0, ts.d0, ts.w0);
+        const f32x4 a1 = ts.share ? ts.b0 : ts.a1, c1 = ts.share ? ts.d0 : ts.c1;
+        const f32x4 s1 = blend4w(a1, ts.b1, c1, ts.d1, ts.w1);
+        const float a0 = first ? 1.0f : s0[3], om0 = 1.0f - a0;
+        const float aa1 = first ? 1.0f : s1[3], om1 = 1.0f - aa1;
+        c0r = over(s0[0], a0, om0, c0r);
+        c0g = over(s0[1], a0, om0, c0g);
+        c0b = over(s0[2], a0, om0, c0b);
+        c1r = over(s1[0], aa1, om1, c1r);
+        c1g = over(s1[1], aa1, om1, c1g);
+        c1b = over(s1[2], aa1, om1, c1b);
+        if (CT) {
+            t0 = t0 * om0;
+            t1 = t1 * om1;
+        }
+    };
+    PairTaps A, B;
+    Hom9 hA = hom(p_begin), hB = hom(p_begin + 1);
+    issue(p_begin, hA, A);
+    hA = hom(p_begin + 2);
+    int p = p_begin;
+    for (; p + 1 < p_end; p += 2) {  // A holds plane p, B will hold p + 1
+        issue(p + 1, hB, B);
+        hB = hom(p + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(A, replace_first && p == p_begin);
+        issue(p + 2, hA, A);
+        hA = hom(p + 4);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(B, false);
+    }
+    if (p < p_end) consume(A, replace_first && p == p_begin);
+    if (CT) {
+        float4* o = reinterpret_cast<float4*>(out0);
+        o[0] = make_float4(c0r, c0g, c0b, t0);
+        if (second) o[1] = make_float4(c1r, c1g, c1b, t1);
+    } else {
+        out0[0] = c0r;
+        out0[1] = c0g;
+        out0[2] = c0b;
+        if (second) {
+            out0[3] = c1r;
+            out0[4] = c1g;
+            out0[5] = c1b;
+        }
+    }
+}
+
+// render_packed_kernel's contract (FAST recipe: H, W >= 2); 256 threads = 4 rows x 128
+// pixels, XCD-aware (tile, view) order, tile-level division proof.
+template <bool CT>
+__global__ __launch_bounds__(256) void render_pair_kernel(const float4* __restrict__ planes, int64_t plane_stride,
+                                                          RenderGeom g, int V, int p_begin, int p_end, int back,
+                                                          const float* __restrict__ homs, float* __restrict__ out) {
+    const int tiles_x = (g.W + kPairX - 1) / kPairX;
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int v = lb % V;
+    const int tile = lb / V;
+    const int tx0 = (tile % tiles_x) * kPairX, ty0 = (tile / tiles_x) * kTileY;
+    const int x = tx0 + 2 * (threadIdx.x & (kWave - 1));
+    const int y = ty0 + (threadIdx.x >> 6);
+    const float* hv = homs + (int64_t)v * g.P * 9;
+    bool ok = true;
+    {
+        const float x0 = (float)tx0, x1 = (float)min(tx0 + kPairX - 1, g.W - 1);
+        const float y0 = (float)ty0, y1 = (float)min(ty0 + kTileY - 1, g.H - 1);
+        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256)
+            ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, y0, y1);
+    }
+    const bool proven = __syncthreads_and(ok);
+    if (x >= g.W || y >= g.H) return;
+    const int64_t o = ((int64_t)v * g.H + y) * g.W + x;
+    float* out0 = CT ? out + o * 4 : out + o * 3;
+    const bool second = x + 1 < g.W;
+    if (proven) {
+        render_pair_pixels<CT, false>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y, second, out0);
+    } else {  // rare (w near 0 over the tile): the guarded one-pixel recipe, pixel by pixel
+        render_packed_pixel<CT, 1>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y, out0);
+        if (second)
+            render_packed_pixel<CT, 1>(planes, plane_stride, g, p_begin, p_end, back, hv, x + 1, y,
+                                       out0 + (CT ? 4 : 3));
+    }
+}
+
+// ---------------------------------------------------------------------------
 // native [B,H,W,P,C=4] layout, arbitrary element strides
 // ---------------------------------------------------------------------------
 

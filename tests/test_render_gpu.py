@@ -231,12 +231,36 @@ def test_multiview_kernel_bit_exact(shrink, dev, monkeypatch):
     assert_bits(_lib.render_packed(packed, homs).cpu().numpy(), want, "direct")
 
 
-@pytest.mark.parametrize("mv", ["0", "1"])
+def _variant_env(monkeypatch, mv):
+    """mv "0" / "1": direct / multi-view LDS kernel; "pair": pixel-pair kernel (A/B)."""
+    monkeypatch.setenv("MPIV_RENDER_MV", "0" if mv == "pair" else mv)
+    monkeypatch.setenv("MPIV_RENDER_PAIR", "1" if mv == "pair" else "0")
+
+
+def test_pair_kernel_odd_width_and_extreme_poses(dev, monkeypatch):
+    """The pixel-pair kernel on an odd width (the last pair has no second pixel), a
+    partial 128-pixel tile and strongly minifying / magnifying views (pairs that do not
+    share their taps): bit-exact vs the oracle."""
+    monkeypatch.setenv("MPIV_RENDER_PAIR", "1")
+    from mpi_vision_amd import _host
+    H, W, P, V = 37, 203, 7, 3
+    mpi = configs.synthetic_mpi(1, H, W, P, 12)
+    K = configs.f32([configs.intrinsics_matrix(90.0, 85.0, W / 2.0, H / 2.0)] * V)
+    poses = configs.f32([configs.pose_from(configs.rot_y(12.0), (0.3, -0.1, 0.6)),
+                         configs.pose_from(configs.rot_y(-3.0), (0.02, 0.01, -0.7)),
+                         configs.pose_from(configs.rot_y(0.5), (0.01, 0.0, 0.0))])
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(1, 100, P)), K, V)
+    want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.numpy())
+    got = _lib.render_packed(_lib.pack_planes(mpi[0].to(dev)), homs)
+    assert_bits(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("mv", ["0", "1", "pair"])
 def test_multiview_camera_path_many_views(mv, dev, monkeypatch):
     """A config-4-style sway path (40 consecutive poses of the 1000-pose path, 24 planes,
     viewer camera) rendered in one launch by the direct and the multi-view kernel:
     bit-exact."""
-    monkeypatch.setenv("MPIV_RENDER_MV", mv)
+    _variant_env(monkeypatch, mv)
     from mpi_vision_amd import _host
     H, W, P, V = 96, 160, 24, 40
     mpi = configs.synthetic_mpi(1, H, W, P, 9)
@@ -249,11 +273,11 @@ def test_multiview_camera_path_many_views(mv, dev, monkeypatch):
     assert_bits(got.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("mv", ["0", "1"])
+@pytest.mark.parametrize("mv", ["0", "1", "pair"])
 def test_multiview_ct_partials(mv, dev, monkeypatch):
     """Plane-range (C, T) partials of 6 views (direct and multi-view kernel) equal the
     oracle's bit for bit, and their ordered combine equals the sequential render (1e-5)."""
-    monkeypatch.setenv("MPIV_RENDER_MV", mv)
+    _variant_env(monkeypatch, mv)
     mpi, homs = _multiview_case(6, seed=3)
     V, P = homs.shape[0], homs.shape[1]
     H, W = mpi.shape[1], mpi.shape[2]
