@@ -43,6 +43,7 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 // A/B and test hooks read from the environment (never needed in production use):
 //   MPIV_RENDER_MV=1      launches of >= 4 views use the multi-view LDS kernel (render_mv.hip)
 //   MPIV_RENDER_PAIR=1    the direct render takes pixel pairs sharing taps (render_pair_kernel)
+//   MPIV_RENDER_DPP=1     the direct render reads shared east taps across lanes (render_dpp_kernel)
 //   MPIV_SWEEP_TILE=1     the sweep uses the tile kernel; MPIV_SWEEP_STORE=k the grouped one
 //   MPIV_BOX_SHRINK=k     LDS-staged kernels stage boxes k texels narrower per side, which
 //                         forces their per-sample global fallback (tests)
@@ -136,15 +137,29 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             render_mv_kernel<false><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, shrink, homs, out);
         return launched(nm);
     }
-    // pixel pairs sharing their common taps (render.hip render_pair_kernel): opt-in A/B,
-    // 20 % fewer gathers but 117 VGPRs (4 waves/SIMD), measured 3 % slower (DESIGN.md §8)
-    if (fast && env_int("MPIV_RENDER_PAIR", 0)) {
-        const int64_t nb = (int64_t)blocks(W, kPairX) * blocks(H, kTileY) * V;
+    // east taps read from the neighbouring lane (render.hip render_dpp_kernel): A/B
+    if (fast && env_int("MPIV_RENDER_DPP", 0)) {
+        const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
         if (ct)
-            render_pair_kernel<true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
+            render_dpp_kernel<true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
         else
-            render_pair_kernel<false><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
+            render_dpp_kernel<false><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
+        return launched(nm);
+    }
+    // pixel pairs sharing their common taps (render.hip render_pair_kernel): opt-in A/B,
+    // 20 % fewer gathers but 117 VGPRs (4 waves/SIMD), measured 3 % slower (DESIGN.md §8)
+    if (const int pair = fast ? env_int("MPIV_RENDER_PAIR", 0) : 0) {  // 1: two planes in flight, 2: one
+        const int64_t nb = (int64_t)blocks(W, kPairX) * blocks(H, kTileY) * V;
+        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+        if (ct && pair == 1)
+            render_pair_kernel<true, true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
+        else if (ct)
+            render_pair_kernel<true, false><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
+        else if (pair == 1)
+            render_pair_kernel<false, true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
+        else
+            render_pair_kernel<false, false><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
         return launched(nm);
     }
     const int64_t nblocks = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;

@@ -43,6 +43,12 @@ def _world(group):
     return dist.get_world_size(group), dist.get_rank(group)
 
 
+def _staged(t: torch.Tensor, group) -> bool:
+    """gloo collectives take host tensors: device tensors are staged through host memory
+    (a rehearsal of the multi-rank path on one device; RCCL moves device tensors directly)."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def exchange_bands(ct: torch.Tensor, group=None) -> torch.Tensor:
     """all_to_all of row bands.
 
@@ -56,8 +62,14 @@ def exchange_bands(ct: torch.Tensor, group=None) -> torch.Tensor:
     send = ct.new_zeros((G, V, bh, W, C))
     for k, (b, e) in enumerate(bands):
         send[k, :, : e - b] = ct[:, b:e]
-    recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send, group=group)
+    if _staged(send, group):
+        send_h = send.cpu()
+        recv_h = torch.empty_like(send_h)
+        dist.all_to_all_single(recv_h, send_h, group=group)
+        recv = recv_h.to(send.device)
+    else:
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=group)
     b, e = bands[rank]
     return recv[:, :, : e - b]
 
@@ -70,11 +82,14 @@ def gather_frames(band: torch.Tensor, height: int, group=None, dst: int = 0) -> 
     V, h, W, C = band.shape
     padded = band.new_zeros((V, bh, W, C))
     padded[:, :h] = band
+    dev = padded.device
+    if _staged(padded, group):
+        padded = padded.cpu()
     gathered = [torch.empty_like(padded) for _ in range(G)] if rank == dst else None
     dist.gather(padded, gathered, dst=dst, group=group)
     if rank != dst:
         return None
-    return torch.cat([g[:, : e - b] for g, (b, e) in zip(gathered, bands)], dim=1)
+    return torch.cat([g[:, : e - b] for g, (b, e) in zip(gathered, bands)], dim=1).to(dev)
 
 
 def combine_partials(parts: torch.Tensor,

@@ -232,16 +232,19 @@ def test_multiview_kernel_bit_exact(shrink, dev, monkeypatch):
 
 
 def _variant_env(monkeypatch, mv):
-    """mv "0" / "1": direct / multi-view LDS kernel; "pair": pixel-pair kernel (A/B)."""
-    monkeypatch.setenv("MPIV_RENDER_MV", "0" if mv == "pair" else mv)
-    monkeypatch.setenv("MPIV_RENDER_PAIR", "1" if mv == "pair" else "0")
+    """mv "0" / "1": direct / multi-view LDS kernel; "pair" / "pair1" / "dpp": the
+    pixel-pair (two / one planes in flight) and lane-neighbour tap-sharing kernels (A/B)."""
+    monkeypatch.setenv("MPIV_RENDER_MV", mv if mv in ("0", "1") else "0")
+    monkeypatch.setenv("MPIV_RENDER_PAIR", {"pair": "1", "pair1": "2"}.get(mv, "0"))
+    monkeypatch.setenv("MPIV_RENDER_DPP", "1" if mv == "dpp" else "0")
 
 
-def test_pair_kernel_odd_width_and_extreme_poses(dev, monkeypatch):
-    """The pixel-pair kernel on an odd width (the last pair has no second pixel), a
-    partial 128-pixel tile and strongly minifying / magnifying views (pairs that do not
-    share their taps): bit-exact vs the oracle."""
-    monkeypatch.setenv("MPIV_RENDER_PAIR", "1")
+@pytest.mark.parametrize("variant", ["pair", "pair1", "dpp"])
+def test_sharing_kernels_odd_width_and_extreme_poses(variant, dev, monkeypatch):
+    """The tap-sharing kernels on an odd width (the last pair has no second pixel; a
+    partial wave), a partial tile and strongly minifying / magnifying views (neighbours
+    that do not share their taps): bit-exact vs the oracle."""
+    _variant_env(monkeypatch, variant)
     from mpi_vision_amd import _host
     H, W, P, V = 37, 203, 7, 3
     mpi = configs.synthetic_mpi(1, H, W, P, 12)
@@ -255,7 +258,7 @@ def test_pair_kernel_odd_width_and_extreme_poses(dev, monkeypatch):
     assert_bits(got.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("mv", ["0", "1", "pair"])
+@pytest.mark.parametrize("mv", ["0", "1", "pair", "pair1", "dpp"])
 def test_multiview_camera_path_many_views(mv, dev, monkeypatch):
     """A config-4-style sway path (40 consecutive poses of the 1000-pose path, 24 planes,
     viewer camera) rendered in one launch by the direct and the multi-view kernel:
@@ -273,7 +276,7 @@ def test_multiview_camera_path_many_views(mv, dev, monkeypatch):
     assert_bits(got.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("mv", ["0", "1", "pair"])
+@pytest.mark.parametrize("mv", ["0", "1", "pair", "pair1", "dpp"])
 def test_multiview_ct_partials(mv, dev, monkeypatch):
     """Plane-range (C, T) partials of 6 views (direct and multi-view kernel) equal the
     oracle's bit for bit, and their ordered combine equals the sequential render (1e-5)."""

@@ -26,6 +26,8 @@ if a.variant == "mv":
     os.environ["MPIV_RENDER_MV"] = "1"
 if a.variant == "pair":  # pixel pairs sharing taps (render_pair_kernel, A/B)
     os.environ["MPIV_RENDER_PAIR"] = "1"
+if a.variant == "dpp":  # east taps from the neighbouring lane (render_dpp_kernel, A/B)
+    os.environ["MPIV_RENDER_DPP"] = "1"
 dev = torch.device("cuda:0")
 c = configs.config4()
 H, W, P, V = c["H"], c["W"], c["P"], a.views
