@@ -323,7 +323,7 @@ __device__ __forceinline__ void sweep_pos_fast(const float* __restrict__ m, floa
 constexpr int kSLP = 64;                           // target pixels per tile row
 constexpr int kSLR = 4;                            // target rows per tile
 constexpr int kSLThreads = 512;                    // 8 waves
-constexpr int kSLCap = 2560;                       // staged source texels (40 KiB)
+constexpr int kSLCap = 3072;                       // staged source texels (48 KiB; 2 blocks per CU)
 constexpr int kSLFill = kSLCap / kSLThreads;       // staged texels per thread
 
 // wave-scope LDS ordering: every lane's LDS stores before any lane's later loads
@@ -416,10 +416,23 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
         if (lane == 0) {
             const bool ok = pos || neg;
             s_fast = ok && fin && fastv;
-            const int xl = ok ? max((int)xmin - 1 + shrink, -2) : 0;
-            const int xh = ok ? min((int)xmax + 2 - shrink, sp.Ws + 1) : 0;
-            const int yl = ok ? max((int)ymin - 1 + shrink, -2) : 0;
-            const int yh = ok ? min((int)ymax + 2 - shrink, sp.Hs + 1) : 0;
+            int xl = ok ? max((int)xmin - 1 + shrink, -2) : 0;
+            int xh = ok ? min((int)xmax + 2 - shrink, sp.Ws + 1) : 0;
+            int yl = ok ? max((int)ymin - 1 + shrink, -2) : 0;
+            int yh = ok ? min((int)ymax + 2 - shrink, sp.Hs + 1) : 0;
+            // A footprint wholly beyond one side of the image (the reference's swapped
+            // x / H normalisation sends every sample past x = 3W/4 out of a landscape
+            // source) stages the 3 columns (rows) at that edge: origins past the edge are
+            // then read exactly as the border's zeros (LdsBox's open border edges), so
+            // these tiles stay on the LDS path instead of gathering zeros from memory.
+            if (ok && xl > xh) {
+                xl = xh == sp.Ws + 1 ? sp.Ws - 1 : -2;
+                xh = xl + 2;
+            }
+            if (ok && yl > yh) {
+                yl = yh == sp.Hs + 1 ? sp.Hs - 1 : -2;
+                yh = yl + 2;
+            }
             const int width = xh - xl + 1, rows = yh - yl + 1;
             const bool fits = ok && width >= 2 && rows >= 2 && width <= kSLCap && rows <= kSLCap &&
                               width * rows <= kSLCap;
