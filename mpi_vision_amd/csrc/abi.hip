@@ -377,9 +377,10 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
         if (tiles > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: too large");
         const dim3 lgrid((unsigned)tiles, B, 1);
         const int shrink = env_int("MPIV_BOX_SHRINK", 0);
+        const FastDiv fd_b = make_fastdiv((unsigned)(16 * NG));
 #define MPIV_LDS(CC)                                                                                          \
-    plane_sweep_lds_kernel<CC><<<lgrid, kSLThreads, 0, q>>>(im, sp, pg, rc_hs, rc_ws, fd_g, ki, proj, depths, out, \
-                                                     out_bstride, out_pstride, (int)vec, shrink)
+    plane_sweep_lds_kernel<CC><<<lgrid, kSLThreads, 0, q>>>(im, sp, pg, rc_hs, rc_ws, fd_g, fd_b, ki, proj, depths, \
+                                                     out, out_bstride, out_pstride, (int)vec, shrink)
         switch (C) {
             case 1: MPIV_LDS(1); break;
             case 2: MPIV_LDS(2); break;

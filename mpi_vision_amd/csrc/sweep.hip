@@ -336,7 +336,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 template <int C>
 __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
     const float4* __restrict__ img4, SweepParams sp, PadGeom pg, float rc_hs, float rc_ws, FastDiv fd_g,
-    const float* __restrict__ ki, const float* __restrict__ proj, const float* __restrict__ depths,
+    FastDiv fd_b, const float* __restrict__ ki, const float* __restrict__ proj, const float* __restrict__ depths,
     float* __restrict__ out, int64_t out_bstride, int64_t out_pstride, int vec, int shrink) {
     constexpr int kWaves = kSLThreads / kWave;
     __shared__ __attribute__((aligned(16))) float4 s_src[kSLCap];
@@ -472,13 +472,35 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
     // every group complete and pixels packed: each tile row's output is one dense run
     const bool d4 = sp.D % kSweepDG == 0;  // whole depth groups: one 16-B LDS read per group
     const bool dense = vec && d4 && out_pstride == (int64_t)sp.D * C;
+    // Pixel-interleaved order (when the tile row splits into whole 16-pixel blocks and
+    // the depth groups into fours): a wave takes 16 consecutive pixels x 4 consecutive
+    // depth groups, pixel fastest, so each 8-lane phase of a tap read touches ~8
+    // consecutive staged texels (one depth, neighbouring pixels) instead of 8 points
+    // along one pixel's epipolar line -- no LDS bank conflicts.  Each pixel's 4 groups are
+    // one 16C-float piece of its run, so the wave's output is 16 whole 64-B-aligned pieces.
+    const bool pix16 = np % 16 == 0 && NG % 4 == 0;
+    const int nb16 = 16 * NG;  // groups per 16-pixel block
+    int lane_off[C];           // dense pixel-interleaved stores: float4 offsets of this lane's
+#pragma unroll                 // k-th store in the wave's 16 pieces
+    for (int k = 0; k < C; ++k) {
+        const int f = k * kWave + lane;
+        const int pc = f / (4 * C), qc = f - pc * 4 * C;
+        lane_off[k] = pc * (sp.D * C / 4) + qc;
+    }
     for (int gi = threadIdx.x; gi < ngr; gi += kSLThreads) {
         int tr = 0;  // tile row of group gi
 #pragma unroll
         for (int k = 1; k < kSLR; ++k) tr += gi >= k * nrow ? 1 : 0;
         const int gr = gi - tr * nrow;
-        const unsigned pl = fast_div((unsigned)gr, fd_g);
-        const int dg = gr - (int)pl * NG;
+        int pl, dg;
+        if (pix16) {
+            const int blk = (int)fast_div((unsigned)gr, fd_b), rem = gr - blk * nb16;
+            dg = rem >> 4;
+            pl = blk * 16 + (rem & 15);
+        } else {
+            pl = (int)fast_div((unsigned)gr, fd_g);
+            dg = gr - pl * NG;
+        }
         float* ob = out + (int64_t)b * out_bstride + ((int64_t)(y0 + tr) * sp.Wt + x0) * out_pstride;
         float rx, ry, rz;
         ray(k9, (float)(x0 + (int)pl), (float)(y0 + tr), rx, ry, rz);  // pixel2cam_torch, utils.py:370
@@ -568,7 +590,20 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
         int g0 = gw;
 #pragma unroll
         for (int k = 1; k < kSLR; ++k) g0 -= gw >= k * nrow ? nrow : 0;
-        if (dense && g0 + kWave <= nrow) {  // all 64 groups in one tile row
+        if (pix16 && dense) {  // 16 pixels x 4 groups: 16 pieces of 16C floats
+            float4* so = s_out[wave];
+            wave_lds_sync();  // the previous iteration's reads of the slot are done
+            const int pq = lane & 15, dq = lane >> 4;
+#pragma unroll
+            for (int k = 0; k < C; ++k)
+                so[pq * 4 * C + dq * C + k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+            wave_lds_sync();
+            const int blk0 = g0 / nb16, dg0 = (g0 - blk0 * nb16) >> 4;  // wave-uniform
+            f32x4* base = reinterpret_cast<f32x4*>(ob + (int64_t)blk0 * 16 * out_pstride) + dg0 * C;
+            const f32x4* sn = reinterpret_cast<const f32x4*>(so);
+#pragma unroll
+            for (int k = 0; k < C; ++k) __builtin_nontemporal_store(sn[k * kWave + lane], base + lane_off[k]);
+        } else if (dense && g0 + kWave <= nrow) {  // all 64 groups in one tile row
             // the wave's 64 pieces are the contiguous run ob[g0*4C .. (g0+64)*4C): through
             // LDS, then lane-contiguous 16-B stores
             float4* so = s_out[wave];
