@@ -344,6 +344,7 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
     __shared__ float s_ext[3][kWaves];  // per wave: min depth, max depth, non-finite depth seen
     __shared__ int4 s_box;              // x_lo, y_lo, rows, pitch (0: gather from global memory)
     __shared__ int s_fast;              // every sample of the tile is in div2_rn's fast range
+    __shared__ int s_zero;              // every tap of the tile lies outside the source image
     __shared__ __attribute__((aligned(16))) float4 s_out[kWaves][kWave * C];  // per wave: its run
 
     const int segs = (sp.Wt + kSLP - 1) / kSLP;
@@ -437,9 +438,33 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
             const bool fits = ok && width >= 2 && rows >= 2 && width <= kSLCap && rows <= kSLCap &&
                               width * rows <= kSLCap;
             s_box = make_int4(xl, yl, rows, fits ? width : 0);
+            // Every tap of every sample outside the image: each sample is a blend of four
+            // zero texels with finite non-negative weights, i.e. exactly +0.  Interior
+            // samples lie in the hull of the 8 vertex positions (the box argument above) up
+            // to rounding far below the one-texel margin while |coordinates| < 2^16.
+            const bool small = xmin > -65536.0f && xmax < 65536.0f && ymin > -65536.0f && ymax < 65536.0f;
+            s_zero = ok && small && shrink == 0 &&
+                     ((int)xmin - 1 >= sp.Ws || (int)xmax + 2 <= -1 || (int)ymin - 1 >= sp.Hs || (int)ymax + 2 <= -1);
         }
     }
     __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(s_zero)) {  // the tile's output is all +0: store it
+        const int64_t run = (int64_t)np * sp.D * C;
+        for (int tr = 0; tr < nr; ++tr) {
+            float* ob = out + (int64_t)b * out_bstride + ((int64_t)(y0 + tr) * sp.Wt + x0) * out_pstride;
+            if (vec && out_pstride == (int64_t)sp.D * C && run % 4 == 0) {  // one dense 16-B-aligned run
+                f32x4* o4 = reinterpret_cast<f32x4*>(ob);
+                const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                for (int64_t i = threadIdx.x; i < run / 4; i += kSLThreads) __builtin_nontemporal_store(z, o4 + i);
+            } else {
+                for (int64_t i = threadIdx.x; i < run; i += kSLThreads) {
+                    const int pxl = (int)(i / (sp.D * C)), e = (int)(i - (int64_t)pxl * sp.D * C);
+                    ob[(int64_t)pxl * out_pstride + e] = 0.0f;
+                }
+            }
+        }
+        return;
+    }
     const int xl = __builtin_amdgcn_readfirstlane(s_box.x), yl = __builtin_amdgcn_readfirstlane(s_box.y);
     const int rows = __builtin_amdgcn_readfirstlane(s_box.z), pitch = __builtin_amdgcn_readfirstlane(s_box.w);
     const bool all_fast = __builtin_amdgcn_readfirstlane(s_fast) != 0;
