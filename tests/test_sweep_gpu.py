@@ -161,3 +161,27 @@ def test_plane_sweep_more_depths_than_lds_table(dev):
     ki, proj = _host.psv_matrices(K, K, pose)
     want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, 9, 13)
     assert_bits(_lib.plane_sweep(img.to(dev), depths, ki, proj, 9, 13).cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("C", [3, 4])
+def test_plane_sweep_off_image_tiles(C, dev):
+    """Landscape sources (the swapped x / H normalisation pushes every sample past x = 3W/4
+    off the image), a strong sideways baseline and a source looking away: many tiles have
+    footprints wholly off the image (zero-tile stores and border-collapsed boxes), others
+    straddle the edge; bit-exact to the oracle, output zeros included (+0.0)."""
+    from mpi_vision_amd import _host, _lib
+    from oracle import oracle
+    g = torch.Generator().manual_seed(77 + C)
+    B, Hs, Ws, D = 3, 60, 160, 16
+    img = torch.rand((B, Hs, Ws, C), generator=g) + 0.5
+    K = configs.f32([configs.intrinsics_matrix(150.0, 150.0, 80.0, 30.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(0.5), (0.1, 0.01, 0.0)),
+                         configs.pose_from(configs.rot_y(-20.0), (1.5, 0.2, 0.1)),
+                         configs.pose_from(configs.rot_y(40.0), (-2.0, -0.5, 0.3))])
+    depths = configs.inv_depths(1, 50, D)
+    ki, proj = _host.psv_matrices(K, K, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Hs, Ws)
+    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Hs, Ws)
+    got = out.cpu().numpy()
+    assert_bits(got, want, f"C={C}")
+    assert (want == 0).mean() > 0.2  # the case does exercise off-image samples
