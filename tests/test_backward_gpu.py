@@ -101,19 +101,15 @@ def test_backward_deterministic(grad, dev):
 
 
 def _mpi_from_net_output(mpi_pred, ref_img, num_mpi_planes):
-    """The notebook's mpi_from_net_output (ipynb cell 10 L79-111), same ops as
-    tools/gen_goldens_grad.py."""
-    batch_size, _, img_height, img_width = mpi_pred.shape
-    mpi_pred = mpi_pred.permute(0, 2, 3, 1)
-    blend_weights = (mpi_pred[:, :, :, :num_mpi_planes] + 1.) / 2.
-    alphas = (mpi_pred[:, :, :, num_mpi_planes:num_mpi_planes * 2] + 1.) / 2.
-    bg_rgb = mpi_pred[:, :, :, -3:]
-    layers = []
-    for i in range(num_mpi_planes):
-        curr_alpha = torch.unsqueeze(alphas[:, :, :, i], -1)
-        w = torch.unsqueeze(blend_weights[:, :, :, i], -1)
-        layers.append(torch.cat([w * ref_img + (1 - w) * bg_rgb, curr_alpha], dim=3))
-    return torch.reshape(torch.cat(layers, dim=3), [batch_size, img_height, img_width, num_mpi_planes, 4])
+    """The notebook's MPI assembly (ipynb cell 10 L79-111) as broadcast torch ops on the
+    GPU (same elementwise ops, so the same forward bits; autograd sums the background's
+    gradient over planes in its own order, hence the 1e-6 tolerance below)."""
+    p = mpi_pred.permute(0, 2, 3, 1)
+    P = num_mpi_planes
+    w = ((p[..., :P] + 1.) / 2.).unsqueeze(-1)
+    alpha = ((p[..., P:2 * P] + 1.) / 2.).unsqueeze(-1)
+    rgb = w * ref_img.unsqueeze(3) + (1 - w) * p[..., -3:].unsqueeze(3)
+    return torch.cat([rgb, alpha], dim=-1)
 
 
 def test_training_loss_gradient(grad, dev):

@@ -7,9 +7,8 @@ grid_sampler_2d_backward, utils.py:128).  Test tooling only (see gen_goldens.py 
 how the reference is imported); writes tests/golden/grad.npz.
 
 Also records the notebook's training-loss use (`test_loss`, ipynb cell 12 L5-15):
-mpi_from_net_output (ipynb cell 10 L79-111, restated below: it lives in the
-notebook, not in utils.py) -> render -> MSE, differentiated w.r.t. the network
-output.
+mpi_from_net_output (ipynb cell 10 L79-111, loaded from the notebook: it lives
+there, not in utils.py) -> render -> MSE, differentiated w.r.t. the network output.
 
 Usage:  python tools/gen_goldens_grad.py
 """
@@ -30,25 +29,12 @@ from mpi_vision_amd import configs  # noqa: E402
 
 
 def mpi_from_net_output(mpi_pred, ref_img, num_mpi_planes):
-    """Restatement of the notebook's mpi_from_net_output (ipynb cell 10 L79-111),
-    same op sequence: blend weights / alphas rescaled from the tanh domain, rgb of
-    plane i = w*fg + (1-w)*bg, planes concatenated then reshaped to [B,H,W,P,4]."""
-    batch_size, _, img_height, img_width = mpi_pred.shape
-    mpi_pred = mpi_pred.permute(0, 2, 3, 1)
-    blend_weights = (mpi_pred[:, :, :, :num_mpi_planes] + 1.) / 2.
-    alphas = (mpi_pred[:, :, :, num_mpi_planes:num_mpi_planes * 2] + 1.) / 2.
-    bg_rgb = mpi_pred[:, :, :, -3:]
-    fg_rgb = ref_img
-    for i in range(num_mpi_planes):
-        curr_alpha = torch.unsqueeze(alphas[:, :, :, i], -1)
-        w = torch.unsqueeze(blend_weights[:, :, :, i], -1)
-        curr_rgb = w * fg_rgb + (1 - w) * bg_rgb
-        curr_rgba = torch.cat([curr_rgb, curr_alpha], dim=3)
-        if i == 0:
-            rgba_layers = curr_rgba
-        else:
-            rgba_layers = torch.cat([rgba_layers, curr_rgba], dim=3)
-    return torch.reshape(rgba_layers, [batch_size, img_height, img_width, num_mpi_planes, 4])
+    """The notebook's own mpi_from_net_output (ipynb cell 10 L79-111), taken from the
+    notebook at generation time (gen_goldens_netout.load_notebook_function)."""
+    from gen_goldens_netout import load_notebook_function
+    fn = load_notebook_function()
+    B = mpi_pred.shape[0]
+    return fn(mpi_pred, {"mpi_planes": torch.zeros((B, num_mpi_planes)), "ref_img": ref_img})
 
 
 def main():
