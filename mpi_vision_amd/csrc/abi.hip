@@ -44,6 +44,7 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //   MPIV_RENDER_MV=1      launches of >= 4 views use the multi-view LDS kernel (render_mv.hip)
 //   MPIV_RENDER_PAIR=1    the direct render takes pixel pairs sharing taps (render_pair_kernel)
 //   MPIV_RENDER_DPP=1     the direct render reads shared east taps across lanes (render_dpp_kernel)
+//   MPIV_RENDER_NATIVE_LDS=0  mpiv_render gathers directly from the [B,H,W,P,4] tensor
 //   MPIV_SWEEP_TILE=1     the sweep uses the tile kernel; MPIV_SWEEP_STORE=k the grouped one
 //   MPIV_BOX_SHRINK=k     LDS-staged kernels stage boxes k texels narrower per side, which
 //                         forces their per-sample global fallback (tests)
@@ -53,6 +54,7 @@ int env_int(const char* name, int dflt) {
 }
 
 constexpr int64_t kMaxGridYZ = 65535;
+constexpr int kNativeLdsMaxP = 16;
 constexpr int64_t kMaxGridX = 2147483647;
 
 }  // namespace
@@ -76,6 +78,15 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
     const bool vec = s.c == 1 && aligned16(mpi) && s.b % 4 == 0 && s.y % 4 == 0 && s.x % 4 == 0 && s.p % 4 == 0;
     const bool fast = H >= 2 && W >= 2;
     hipStream_t q = S(stream);
+    // footprints staged through LDS, read in place (render_lds.hip render_lds_native_kernel):
+    // measured faster for few planes (P = 10: 0.031 vs 0.039 ms), slower for many (P = 128:
+    // 2.78 vs 1.86 ms, the fills' 64-B segments no longer serve the next planes)
+    if (vec && fast && P <= kNativeLdsMaxP && env_int("MPIV_RENDER_NATIVE_LDS", 1)) {
+        const int64_t nb = (int64_t)blocks(W, kLTX) * blocks(H, kLTY) * B;
+        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_render: too many blocks");
+        render_lds_native_kernel<true><<<(unsigned)nb, kLThreads, 0, q>>>(mpi, s, g, B, homs, out);
+        return launched("mpiv_render");
+    }
     if (vec && fast) render_native_kernel<true, true><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
     else if (vec) render_native_kernel<true, false><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
     else if (fast) render_native_kernel<false, true><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);

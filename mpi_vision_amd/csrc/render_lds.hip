@@ -218,4 +218,182 @@ __global__ __launch_bounds__(kLThreads, 8) void render_lds_kernel(const float4* 
     }
 }
 
+// The same LDS-staged render reading the reference's own [B,H,W,P,4] tensor in place
+// (mpi_render_view_torch without a pack pass; 16-B texels, any element strides with
+// contiguous channels).  In that layout a plane's texels are P*16 B apart, so the direct
+// kernel gathers one 64-B segment per tap; here each block fetches the footprint of its
+// tile once per plane (texels outside the image staged as zeros, the packed layout's
+// border made implicit) and the taps are ds_read_b128s.  The 64-B segments a fill
+// touches also hold the next 3 planes' texels, which the following fills find in L2 /
+// the Infinity Cache.  Planes whose footprint does not fit gather directly.
+template <bool FAST>
+__global__ __launch_bounds__(kLThreads, 8) void render_lds_native_kernel(const float* __restrict__ mpi,
+                                                                         NativeStrides s, RenderGeom g, int V,
+                                                                         const float* __restrict__ homs,
+                                                                         float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float4 s_tex[2][kLCap];
+    __shared__ int4 s_box[kLMaxP];  // per plane: x_lo, y_lo, rows, mode
+    __shared__ int s_pitch;
+
+    const int tiles_x = (g.W + kLTX - 1) / kLTX;
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int v = lb % V;
+    const int tile = lb / V;
+    const int tx0 = (tile % tiles_x) * kLTX, ty0 = (tile / tiles_x) * kLTY;
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+    const int x = tx0 + lane, y = ty0 + wave;
+    const bool active = x < g.W && y < g.H;
+    const float* hv = homs + (int64_t)v * g.P * 9;
+    const float* img = mpi + (int64_t)v * s.b;
+    const int np = g.P;
+
+    if (threadIdx.x == 0) s_pitch = 0;
+    __syncthreads();
+
+    // ---- footprint boxes (render_lds_kernel's prologue)
+    const int cx1 = min(tx0 + kLTX - 1, g.W - 1), cy1 = min(ty0 + kLTY - 1, g.H - 1);
+    for (int q0 = 0; q0 < 4 * np; q0 += kLThreads) {
+        const int q = q0 + threadIdx.x;
+        const bool live = q < 4 * np;
+        const int pl = live ? (q >> 2) : 0;
+        const int corner = q & 3;
+        const float fx = (float)((corner & 1) ? cx1 : tx0), fy = (float)((corner & 2) ? cy1 : ty0);
+        const float* h = hv + (int64_t)pl * 9;
+        float px, py;
+        render_pos<FAST>(h, fx, fy, g, px, py);
+        float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+        w = (w == 0.0f) ? w + 1e-8f : w;
+        const bool fin = __builtin_isfinite(px) && __builtin_isfinite(py) && __builtin_fabsf(px) < 1e7f &&
+                         __builtin_fabsf(py) < 1e7f;
+        float xmin = floorf(px), xmax = xmin, ymin = floorf(py), ymax = ymin;
+        int pos = fin && w > 0.0f, neg = fin && w < 0.0f;
+#pragma unroll
+        for (int m = 1; m <= 2; m <<= 1) {
+            xmin = fminf(xmin, __shfl_xor(xmin, m));
+            xmax = fmaxf(xmax, __shfl_xor(xmax, m));
+            ymin = fminf(ymin, __shfl_xor(ymin, m));
+            ymax = fmaxf(ymax, __shfl_xor(ymax, m));
+            pos &= __shfl_xor(pos, m);
+            neg &= __shfl_xor(neg, m);
+        }
+        if (live && corner == 0) {
+            int4 bx;
+            const bool ok = pos || neg;
+            const int xl = ok ? max((int)xmin - 1, -2) : 0, xh = ok ? min((int)xmax + 2, g.W + 1) : 0;
+            const int yl = ok ? max((int)ymin - 1, -2) : 0, yh = ok ? min((int)ymax + 2, g.H + 1) : 0;
+            const int width = xh - xl + 1, rows = yh - yl + 1;
+            bx.x = xl;
+            bx.y = yl;
+            bx.z = rows;
+            bx.w = (!ok || width < 2 || rows < 2 || width > kLMaxPitch || width * rows > kLCap) ? kLDirect : 0;
+            s_box[q >> 2] = bx;
+            if (bx.w == 0) atomicMax(&s_pitch, width);
+        }
+    }
+    __syncthreads();
+    const int pitch = s_pitch;
+
+    int row_j[2], col_j[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int idx = (wave + kLTY * j) * kWave + lane;
+        row_j[j] = pitch > 0 ? idx / pitch : 0;
+        col_j[j] = idx - row_j[j] * pitch;
+    }
+    auto lds_mode = [&](const int4& bx) { return bx.w == 0 && bx.z * pitch <= kLCap; };
+
+    f32x4 stg[2];
+    auto fetch = [&](int pl, const int4& bx) {
+        const float* plane = img + (int64_t)pl * s.p;
+        const int nfp = bx.z * pitch;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int base = (wave + kLTY * j) * kWave;  // wave-uniform
+            if (base < nfp) {
+                const int tx = bx.x + col_j[j], ty = bx.y + row_j[j];
+                const bool in = (unsigned)tx < (unsigned)g.W && (unsigned)ty < (unsigned)g.H;
+                const int cx = min(max(tx, 0), g.W - 1), cy = min(max(ty, 0), g.H - 1);
+                const f32x4 t = *reinterpret_cast<const f32x4*>(plane + (int64_t)cy * s.y + (int64_t)cx * s.x);
+                const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                stg[j] = in ? t : z;
+            }
+        }
+    };
+    auto commit = [&](int buf, const int4& bx) {
+        const int nfp = bx.z * pitch;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int base = (wave + kLTY * j) * kWave;
+            if (base < nfp) *reinterpret_cast<f32x4*>(&s_tex[buf][base + lane]) = stg[j];
+        }
+    };
+
+    const float fx = (float)x, fy = (float)y;
+    float cr = -0.0f, cg = -0.0f, cb = -0.0f;  // plane 0 replaces it exactly (render.hip)
+
+    int4 bx_next = s_box[0];
+    if (lds_mode(bx_next)) {
+        fetch(0, bx_next);
+        commit(0, bx_next);
+    }
+    __syncthreads();
+    for (int p = 0; p < np; ++p) {
+        const int buf = p & 1;
+        const int4 bx = bx_next;
+        const bool more = p + 1 < np;
+        if (more) {
+            bx_next = s_box[p + 1];
+            if (lds_mode(bx_next)) fetch(p + 1, bx_next);
+        }
+        if (active) {
+            float px, py;
+            render_pos<FAST>(hv + (int64_t)p * 9, fx, fy, g, px, py);
+            f32x4 sm;
+            if (lds_mode(bx)) {
+                const float fx0 = floorf(px), fy0 = floorf(py);
+                const float wx = px - fx0, ex = 1.0f - wx;
+                const float wy = py - fy0, sy = 1.0f - wy;
+                TapSet ts;
+                ts.nw = sy * ex;
+                ts.ne = sy * wx;
+                ts.sw = wy * ex;
+                ts.se = wy * wx;
+                const float ix = __builtin_amdgcn_fmed3f(fx0, (float)bx.x, (float)min(bx.x + pitch - 2, g.W));
+                const float iy = __builtin_amdgcn_fmed3f(fy0, (float)bx.y, (float)(bx.y + bx.z - 2));
+                const int li = (int)(__builtin_fmaf(iy, (float)pitch, ix) - (float)(bx.y * pitch + bx.x));
+                const float4* st = &s_tex[buf][li];
+                ts.a = *reinterpret_cast<const f32x4*>(st);
+                ts.b = *reinterpret_cast<const f32x4*>(st + 1);
+                ts.c = *reinterpret_cast<const f32x4*>(st + pitch);
+                ts.d = *reinterpret_cast<const f32x4*>(st + pitch + 1);
+                sm = blend_taps(ts);
+                asm volatile("" : "+v"(sm));
+            } else {  // the direct native gather (render_native_kernel)
+                const Bilinear b = bilinear_setup(px, py, g.W, g.H);
+                const float* pl = img + (int64_t)p * s.p;
+                TapSet t;
+                t.nw = b.nw; t.ne = b.ne; t.sw = b.sw; t.se = b.se;
+                t.a = ld_texel<true>(pl, s, g.W, g.H, b.ix, b.iy, b.x0 && b.y0);
+                t.b = ld_texel<true>(pl, s, g.W, g.H, b.ix + 1, b.iy, b.x1 && b.y0);
+                t.c = ld_texel<true>(pl, s, g.W, g.H, b.ix, b.iy + 1, b.x0 && b.y1);
+                t.d = ld_texel<true>(pl, s, g.W, g.H, b.ix + 1, b.iy + 1, b.x1 && b.y1);
+                sm = blend_taps(t);
+                asm volatile("" : "+v"(sm));
+            }
+            const float a = p == 0 ? 1.0f : sm[3];
+            const float om = 1.0f - a;
+            cr = over(sm[0], a, om, cr);
+            cg = over(sm[1], a, om, cg);
+            cb = over(sm[2], a, om, cb);
+        }
+        if (more && lds_mode(bx_next)) commit(buf ^ 1, bx_next);
+        __syncthreads();
+    }
+    if (!active) return;
+    const int64_t o = (((int64_t)v * g.H + y) * g.W + x) * 3;
+    out[o + 0] = cr;
+    out[o + 1] = cg;
+    out[o + 2] = cb;
+}
+
 }  // namespace mpiv

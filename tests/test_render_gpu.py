@@ -31,8 +31,11 @@ def test_render_matches_reference(name, small, meta, dev):
 
 
 @pytest.mark.parametrize("name", RENDER_CASES)
-def test_native_and_packed_kernels_agree_with_oracle(name, small, meta, dev):
-    """Both texel layouts, driven with the reference's own H bits."""
+@pytest.mark.parametrize("native_lds", ["0", "1"])
+def test_native_and_packed_kernels_agree_with_oracle(name, native_lds, small, meta, dev, monkeypatch):
+    """Both texel layouts (the in-place one through its direct and its LDS-staged kernel),
+    driven with the reference's own H bits."""
+    monkeypatch.setenv("MPIV_RENDER_NATIVE_LDS", native_lds)
     mpi = render_case_inputs(meta["small"], name)
     B, H, W, P, _ = mpi.shape
     homs = torch.tensor(small[f"{name}_H"]).permute(1, 0, 2, 3).reshape(B, P, 9).contiguous()
