@@ -321,9 +321,15 @@ __device__ __forceinline__ void sweep_pos_fast(const float* __restrict__ m, floa
 // So a wave whose 64 groups are complete and dense passes its pieces through a per-wave
 // LDS slot and stores the run with lane-contiguous 16-B stores.
 constexpr int kSLP = 64;                           // target pixels per tile row
-constexpr int kSLR = 4;                            // target rows per tile
+#ifndef MPIV_SLR
+#define MPIV_SLR 4
+#endif
+#ifndef MPIV_SLCAP
+#define MPIV_SLCAP 3072
+#endif
+constexpr int kSLR = MPIV_SLR;                     // target rows per tile
 constexpr int kSLThreads = 512;                    // 8 waves
-constexpr int kSLCap = 3072;                       // staged source texels (48 KiB; 2 blocks per CU)
+constexpr int kSLCap = MPIV_SLCAP;                 // staged source texels (48 KiB; 2 blocks per CU)
 constexpr int kSLFill = kSLCap / kSLThreads;       // staged texels per thread
 
 // wave-scope LDS ordering: every lane's LDS stores before any lane's later loads
