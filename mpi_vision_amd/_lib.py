@@ -345,11 +345,19 @@ class AssembleFunction(torch.autograd.Function):
 # plane sweep / inverse warp
 # ---------------------------------------------------------------------------
 
+def _require_depths(depth_planes) -> None:
+    # the reference concatenates one slice per depth (utils.py:466-470): no depths is
+    # torch.cat.s ValueError, raised here before anything is launched
+    if len(depth_planes) == 0:
+        raise ValueError("torch.cat(): expected a non-empty list of Tensors")
+
+
 def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.Tensor, tgt_h: int,
                 tgt_w: int) -> torch.Tensor:
     """[B,Hs,Ws,C] -> PSV [B,tgt_h,tgt_w,D*C].  C <= 4: the source is padded once to
     16-B texels with a zero border (B*(Hs+4)*(Ws+4)*16 bytes) and swept by the
     buffer-load kernel; otherwise the generic strided kernel."""
+    _require_depths(depth_planes)
     dev = _dev(img)
     B, Hs, Ws, C = img.shape
     d = torch.tensor([float(x) for x in depth_planes], dtype=torch.float32)
@@ -399,6 +407,8 @@ def network_input(ref_image, psv_src_images, rel_poses, depth_planes, intrinsics
     """format_network_input_torch: [B,H,W,3] ref + S PSVs of the 3-channel slices of
     psv_src_images, each swept directly into its channel range of one output."""
     from ._host import psv_matrices
+    if len(rel_poses):
+        _require_depths(depth_planes)
     dev = _dev(ref_image, psv_src_images)
     B, H, W, _ = ref_image.shape
     S = len(rel_poses)

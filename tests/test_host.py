@@ -105,3 +105,12 @@ def test_configs():
     assert c4["depths"][0] == 100 and c4["depths"][-1] == 1
     c1 = configs.config1_camera()
     assert abs(c1["K"][0][0] - 554.2562584220408) < 1e-9
+
+
+def test_plane_sweep_no_depths_raises_value_error():
+    """No depth planes: the reference's torch.cat raises ValueError (utils.py:470); the
+    drop-in raises it before touching a device (so also for a CPU tensor)."""
+    import mpi_vision_amd as mv
+    K = torch.tensor([[[40.0, 0, 26], [0, 41.0, 14], [0, 0, 1]]])
+    with pytest.raises(ValueError, match="non-empty list"):
+        mv.plane_sweep_torch(torch.rand(1, 12, 16, 3), [], torch.eye(4)[None], K)

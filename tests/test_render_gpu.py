@@ -142,6 +142,14 @@ def test_render_errors(dev):
         mv.mpi_render_view_torch(mpi.double(), pose, torch.tensor([2.0, 1.0], device=dev), K)
     with pytest.raises(RuntimeError):  # batch mismatch
         mv.mpi_render_view_torch(mpi, pose.expand(2, 4, 4), torch.tensor([2.0, 1.0], device=dev), K.expand(2, 3, 3))
+    # empty inputs: the reference raises RuntimeError for an empty batch, image or plane
+    # stack (its reshapes / grid_sampler's non-empty check; measured), and so does the drop-in
+    planes = torch.tensor([2.0, 1.0], device=dev)
+    for bad in (lambda: mv.mpi_render_view_torch(mpi[:0], pose[:0], planes, K[:0]),
+                lambda: mv.mpi_render_view_torch(mpi[:, :0], pose, planes, K),
+                lambda: mv.mpi_render_view_torch(mpi[..., :0, :], pose, planes[:0], K)):
+        with pytest.raises(RuntimeError):
+            bad()
 
 
 @pytest.mark.parametrize("divisor", [1, 2, 3, 7, 36, 39, 47, 48, 63, 64, 71, 95, 96, 127, 159, 255, 399, 400,

@@ -185,3 +185,38 @@ def test_plane_sweep_off_image_tiles(C, dev):
     got = out.cpu().numpy()
     assert_bits(got, want, f"C={C}")
     assert (want == 0).mean() > 0.2  # the case does exercise off-image samples
+
+
+@pytest.mark.parametrize("C", [5, 7])
+def test_plane_sweep_wide_channels_vs_oracle(C, dev):
+    """C > 4 (the reference sweeps any channel count, e.g. stacked sources): the generic
+    strided kernel, bit-exact to the oracle, through the plane_sweep_torch drop-in."""
+    from mpi_vision_amd import _host
+    from oracle import oracle
+    g = torch.Generator().manual_seed(70 + C)
+    B, H, W, D = 2, 29, 53, 6
+    img = torch.rand((B, H, W, C), generator=g)
+    K = configs.f32([configs.intrinsics_matrix(40.0, 41.0, 26.0, 14.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(2.0 * k - 1.0), (0.1 * k - 0.05, 0.02, 0.0))
+                         for k in range(B)])
+    depths = configs.inv_depths(1.0, 30, D)
+    ki, proj = _host.psv_matrices(K, K, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, H, W)
+    out = mv.plane_sweep_torch(img.to(dev), depths, poses.to(dev), K.to(dev))
+    assert out.shape == (B, H, W, D * C)
+    assert_bits(out.cpu().numpy(), want, f"C={C}")
+
+
+def test_plane_sweep_empty_inputs_raise_like_reference(dev):
+    """The reference raises on every empty input (measured: ValueError from torch.cat for
+    no depths, RuntimeError from its reshapes for an empty batch or image); so does the
+    drop-in, before any launch."""
+    K = configs.f32([configs.intrinsics_matrix(40.0, 41.0, 26.0, 14.0)])
+    pose = configs.f32([configs.pose_from(configs.rot_y(1.0), (0.05, 0.0, 0.0))])
+    img = torch.rand((1, 12, 16, 3), device=dev)
+    with pytest.raises(ValueError, match="non-empty list"):
+        mv.plane_sweep_torch(img, [], pose.to(dev), K.to(dev))
+    with pytest.raises(RuntimeError):
+        mv.plane_sweep_torch(img[:0], [1.0, 2.0], pose[:0].to(dev), K[:0].to(dev))
+    with pytest.raises(RuntimeError):
+        mv.plane_sweep_torch(img[:, :0], [1.0, 2.0], pose.to(dev), K.to(dev))
