@@ -518,6 +518,19 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
         const int pc = f / (4 * C), qc = f - pc * 4 * C;
         lane_off[k] = pc * (sp.D * C / 4) + qc;
     }
+    // The per-wave slot in that order: lane (pixel pq, group dq) writes its k-th float4 at
+    // pq*4C + dq*C + k and lane l reads float4 k*64 + l.  ds_*_b128 serve 16 lanes per pass
+    // over 16 16-B bank slots, and the writes of one pass (pq = 0..15) fall on 4 slots (C = 1,
+    // 3) or 1 (C = 4): up to 16-way conflicts.  Rotating each 16-float4 row a of the slot by
+    // G(a) (a / 3 for C = 3, a otherwise; a bijection within the row) makes both the write
+    // and the read passes conflict-free (checked for C = 1..4 by enumeration).
+    auto swz = [](int L) { return (L & ~15) | ((L + (C == 3 ? (L >> 4) / 3 : (L >> 4))) & 15); };
+    int so_w[C], so_r[C];  // lane constants: swizzled write / read slots
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+        so_w[k] = swz((lane & 15) * 4 * C + (lane >> 4) * C + k);
+        so_r[k] = swz(k * kWave + lane);
+    }
     for (int gi = threadIdx.x; gi < ngr; gi += kSLThreads) {
         int tr = 0;  // tile row of group gi
 #pragma unroll
@@ -624,16 +637,15 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
         if (pix16 && dense) {  // 16 pixels x 4 groups: 16 pieces of 16C floats
             float4* so = s_out[wave];
             wave_lds_sync();  // the previous iteration's reads of the slot are done
-            const int pq = lane & 15, dq = lane >> 4;
 #pragma unroll
             for (int k = 0; k < C; ++k)
-                so[pq * 4 * C + dq * C + k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+                so[so_w[k]] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
             wave_lds_sync();
             const int blk0 = g0 / nb16, dg0 = (g0 - blk0 * nb16) >> 4;  // wave-uniform
             f32x4* base = reinterpret_cast<f32x4*>(ob + (int64_t)blk0 * 16 * out_pstride) + dg0 * C;
             const f32x4* sn = reinterpret_cast<const f32x4*>(so);
 #pragma unroll
-            for (int k = 0; k < C; ++k) __builtin_nontemporal_store(sn[k * kWave + lane], base + lane_off[k]);
+            for (int k = 0; k < C; ++k) __builtin_nontemporal_store(sn[so_r[k]], base + lane_off[k]);
         } else if (dense && g0 + kWave <= nrow) {  // all 64 groups in one tile row
             // the wave's 64 pieces are the contiguous run ob[g0*4C .. (g0+64)*4C): through
             // LDS, then lane-contiguous 16-B stores
