@@ -121,9 +121,34 @@ def view_shard(n_views: int, rank: int, world: int) -> slice:
     return slice(b, e)
 
 
-def render_view_sharded(packed: torch.Tensor, homs_all: torch.Tensor, group=None) -> torch.Tensor:
-    """This rank's frames of a view-sharded camera path (no collective)."""
+def gather_view_frames(frames: torch.Tensor, n_views: int, group=None, dst: int = 0) -> Optional[torch.Tensor]:
+    """The view-sharded path's one optional collective (SURVEY.md §8e "final frame
+    gather"): rank k's frames [v_k, H, W, 3] of poses view_shard(n_views, k, G) -> the
+    whole camera path [n_views, H, W, 3] on dst (None elsewhere).  Shards may be uneven
+    (n_views % G != 0): each is padded to the largest for one gather and trimmed."""
+    G, rank = _world(group)
+    sizes = [e - b for b, e in (shard_range(n_views, k, G) for k in range(G))]
+    if frames.shape[0] != sizes[rank]:
+        raise RuntimeError(f"gather_view_frames: rank {rank} holds {frames.shape[0]} views, "
+                           f"its shard has {sizes[rank]}")
+    padded = frames.new_zeros((max(sizes),) + tuple(frames.shape[1:]))
+    padded[: sizes[rank]] = frames
+    dev = padded.device
+    if _staged(padded, group):
+        padded = padded.cpu()
+    gathered = [torch.empty_like(padded) for _ in range(G)] if rank == dst else None
+    dist.gather(padded, gathered, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([g[:n] for g, n in zip(gathered, sizes)], dim=0).to(dev)
+
+
+def render_view_sharded(packed: torch.Tensor, homs_all: torch.Tensor, group=None, gather: bool = False,
+                        dst: int = 0) -> Optional[torch.Tensor]:
+    """This rank's frames of a view-sharded camera path (no collective); with `gather`,
+    the whole path's frames on dst (gather_view_frames) and None elsewhere."""
     from . import _lib
     G, rank = _world(group)
     sl = view_shard(homs_all.shape[0], rank, G)
-    return _lib.render_packed(packed, homs_all[sl])
+    frames = _lib.render_packed(packed, homs_all[sl])
+    return gather_view_frames(frames, homs_all.shape[0], group, dst) if gather else frames
