@@ -220,3 +220,24 @@ def test_plane_sweep_empty_inputs_raise_like_reference(dev):
         mv.plane_sweep_torch(img[:0], [1.0, 2.0], pose[:0].to(dev), K[:0].to(dev))
     with pytest.raises(RuntimeError):
         mv.plane_sweep_torch(img[:, :0], [1.0, 2.0], pose.to(dev), K.to(dev))
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 4])
+def test_plane_sweep_pixel_interleaved_store_all_channels(C, dev):
+    """Whole 16-pixel blocks and whole sets of 4 depth groups (Wt % 64 == 0, D % 16 == 0):
+    the LDS kernel's pixel-interleaved order and its swizzled per-wave store slot (a
+    different row rotation for C = 3 than for C = 1, 2, 4), bit-exact to the oracle."""
+    from mpi_vision_amd import _host, _lib
+    from oracle import oracle
+    g = torch.Generator().manual_seed(90 + C)
+    B, Hs, Ws, D, Ht, Wt = 2, 40, 96, 32, 12, 128
+    img = torch.rand((B, Hs, Ws, C), generator=g)
+    Ks = configs.f32([configs.intrinsics_matrix(60.0, 61.0, 48.0, 20.0)] * B)
+    Kt = configs.f32([configs.intrinsics_matrix(80.0, 79.0, 64.0, 6.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(2.0 * k - 1.0), (0.1 * k - 0.05, 0.02, 0.0))
+                         for k in range(B)])
+    depths = configs.inv_depths(1.0, 40, D)
+    ki, proj = _host.psv_matrices(Ks, Kt, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Ht, Wt)
+    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Ht, Wt)
+    assert_bits(out.cpu().numpy(), want, f"C={C}")
