@@ -347,7 +347,6 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
     constexpr int kWaves = kSLThreads / kWave;
     __shared__ __attribute__((aligned(16))) float4 s_src[kSLCap];
     __shared__ __attribute__((aligned(16))) float s_dep[kSweepMaxLdsD];
-    __shared__ float s_ext[3][kWaves];  // per wave: min depth, max depth, non-finite depth seen
     __shared__ int4 s_box;              // x_lo, y_lo, rows, pitch (0: gather from global memory)
     __shared__ int s_fast;              // every sample of the tile is in div2_rn's fast range
     __shared__ int s_zero;              // every tap of the tile lies outside the source image
@@ -363,34 +362,22 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
     const float* m = proj + (int64_t)b * 16;
     const __amdgpu_buffer_rsrc_t r = make_rsrc(img4 + (int64_t)b * (pg.plane_bytes / 16), pg.plane_bytes);
 
-    // depths -> LDS, with their range
-    float dlo = __builtin_inff(), dhi = -__builtin_inff(), bad = 0.0f;
-    for (int i = threadIdx.x; i < sp.D; i += kSLThreads) {
-        const float d = depths[i];
-        s_dep[i] = d;
-        dlo = fminf(dlo, d);
-        dhi = fmaxf(dhi, d);
-        bad = __builtin_isfinite(d) ? bad : 1.0f;
-    }
-#pragma unroll
-    for (int k = 1; k < kWave; k <<= 1) {
-        dlo = fminf(dlo, __shfl_xor(dlo, k));
-        dhi = fmaxf(dhi, __shfl_xor(dhi, k));
-        bad = fmaxf(bad, __shfl_xor(bad, k));
-    }
-    if (lane == 0) {
-        s_ext[0][wave] = dlo;
-        s_ext[1][wave] = dhi;
-        s_ext[2][wave] = bad;
-    }
-    __syncthreads();
+    // depths -> LDS (all threads); wave 0 also reduces their range itself, so the box
+    // prologue needs no block barrier before the vertex computation
+    for (int i = threadIdx.x; i < sp.D; i += kSLThreads) s_dep[i] = depths[i];
     if (wave == 0) {  // vertex = lane % 8: (first | last pixel) x (first | last row) x (min | max depth)
-        float dmin = s_ext[0][0], dmax = s_ext[1][0], dbad = s_ext[2][0];
+        float dmin = __builtin_inff(), dmax = -__builtin_inff(), dbad = 0.0f;
+        for (int i = lane; i < sp.D; i += kWave) {
+            const float d = depths[i];
+            dmin = fminf(dmin, d);
+            dmax = fmaxf(dmax, d);
+            dbad = __builtin_isfinite(d) ? dbad : 1.0f;
+        }
 #pragma unroll
-        for (int w = 1; w < kWaves; ++w) {
-            dmin = fminf(dmin, s_ext[0][w]);
-            dmax = fmaxf(dmax, s_ext[1][w]);
-            dbad = fmaxf(dbad, s_ext[2][w]);
+        for (int k = 1; k < kWave; k <<= 1) {
+            dmin = fminf(dmin, __shfl_xor(dmin, k));
+            dmax = fmaxf(dmax, __shfl_xor(dmax, k));
+            dbad = fmaxf(dbad, __shfl_xor(dbad, k));
         }
         const int vtx = lane & 7;
         float rx, ry, rz;
