@@ -125,7 +125,7 @@ def cpu_baseline(mpi_dev: torch.Tensor, homs_all: torch.Tensor, budget_s: float,
 def main():
     args = parse()
     if args.kernel == "packed_mv":
-        os.environ["MPIV_RENDER_MV"] = "1"  # read by libmpiv's dispatch (A/B hook)
+        _lib.load().mpiv_debug_set(b"render_mv", 1)  # libmpiv's debug option (A/B)
     world, rank, dev = dist_setup(args)
     torch.cuda.set_device(dev)
     c4 = configs.config4()

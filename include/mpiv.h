@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 4
+#define MPIV_ABI_VERSION 5
 
 enum {
     MPIV_OK = 0,
@@ -40,6 +40,17 @@ enum {
 
 int mpiv_abi_version(void);
 const char *mpiv_last_error(void);
+
+/* First 16 hex digits of the sha256 of the sources the library was built from
+ * (mpi_vision_amd/csrc/SOURCES, in order); the Python binding refuses a library
+ * whose id does not match the sources next to it (a stale build). */
+const char *mpiv_build_id(void);
+
+/* Debug / A/B hook, never needed in production: selects a non-default kernel variant
+ * by name ("render_mv", "render_pair", "render_native_lds", "sweep_tile",
+ * "sweep_store", "box_shrink"; "reset" restores every default).  Process-wide;
+ * returns MPIV_ERR_ARG for an unknown name. */
+int mpiv_debug_set(const char *name, int value);
 
 /* ---- MPI render -------------------------------------------------------- */
 
@@ -119,13 +130,14 @@ int mpiv_assemble_mpi_packed(const float *pred, const int64_t pred_strides[4], c
                              const int64_t fg_strides[4], int b, int H, int W, int P, float *packed,
                              void *stream);
 
-/* Backward of mpiv_assemble_mpi w.r.t. pred (the notebook trains through it, cell 12
- * L5-15): drgba [B,H,W,P,4] (drgba_strides[5]) -> dpred [B,2P+3,H,W] contiguous
- * (written, not accumulated).  Per plane dw = (sum_c g*fg - sum_c g*bg)/2,
- * dalpha = g_a/2; d bg = sum over planes (last to first) of g*(1-w). */
+/* Backward of mpiv_assemble_mpi (the notebook trains through it, cell 12 L5-15):
+ * drgba [B,H,W,P,4] (drgba_strides[5]) -> dpred [B,2P+3,H,W] contiguous and, when dfg is
+ * not NULL, d fg [B,H,W,3] contiguous (both written, not accumulated).  Per plane
+ * dw = (sum_c g*fg - sum_c g*bg)/2, dalpha = g_a/2; d bg = sum over planes (last to
+ * first) of g*(1-w); d fg = the same sum of g*w (autograd's order, bit-exact). */
 int mpiv_assemble_mpi_backward(const float *drgba, const int64_t drgba_strides[5], const float *pred,
                                const int64_t pred_strides[4], const float *fg, const int64_t fg_strides[4],
-                               int B, int H, int W, int P, float *dpred, void *stream);
+                               int B, int H, int W, int P, float *dpred, float *dfg, void *stream);
 
 /* ---- plane sweep -------------------------------------------------------- */
 

@@ -6,14 +6,19 @@ without the built library these functions raise.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import hashlib
 import os
 
 import torch
+from torch.autograd.function import once_differentiable
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# MPIV_LIB: another build of the same ABI (kernel A/B tools only, tools/gpu_ab_lib.sh)
+# MPIV_LIB: another build of the same ABI (kernel A/B tools only, tools/gpu_ab_lib.sh);
+# its build id is not checked against the sources in this tree
 LIB_PATH = os.environ.get("MPIV_LIB") or os.path.join(_HERE, "libmpiv.so")
+_CSRC = os.path.join(_HERE, "csrc")
 
 _c_i64p = ctypes.POINTER(ctypes.c_int64)
 _vp = ctypes.c_void_p
@@ -47,10 +52,12 @@ _SIGS = {
                                      _vp],
     "mpiv_assemble_mpi": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_assemble_mpi_packed": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
-    "mpiv_assemble_mpi_backward": [_vp, _c_i64p, _vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
+    "mpiv_assemble_mpi_backward": [_vp, _c_i64p, _vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp,
+                                   _vp],
 }
-EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size")
-ABI_VERSION = 4
+EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
+                          "mpiv_build_id", "mpiv_debug_set")
+ABI_VERSION = 5
 
 _lib = None
 
@@ -59,14 +66,38 @@ _lib = None
 RENDER_POLICY = "auto"
 
 
+def source_hash() -> str | None:
+    """sha256 (first 16 hex digits) of the library sources listed in csrc/SOURCES, in order
+    -- the id the Makefile compiles into libmpiv.so; None when the sources are absent."""
+    try:
+        with open(os.path.join(_CSRC, "SOURCES")) as f:
+            names = f.read().split()
+        h = hashlib.sha256()
+        for n in names:
+            with open(os.path.join(_CSRC, n), "rb") as f:
+                h.update(f.read())
+        return h.hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def load():
-    """Load libmpiv.so (raises if it has not been built)."""
+    """Load libmpiv.so (raises if it has not been built, or was built from other sources
+    than the ones in this tree)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"mpi_vision_amd: {LIB_PATH} is missing -- build it first "
                                "(python -c 'import __graft_entry__ as g; g.build()')")
         L = ctypes.CDLL(LIB_PATH)
+        L.mpiv_build_id.restype = ctypes.c_char_p
+        want = source_hash()
+        if not os.environ.get("MPIV_LIB") and want is not None and L.mpiv_build_id().decode() != want:
+            raise RuntimeError(f"mpi_vision_amd: {LIB_PATH} was built from other sources (build id "
+                               f"{L.mpiv_build_id().decode()}, sources {want}) -- rebuild it "
+                               "(python -c 'import __graft_entry__ as g; g.build()')")
+        L.mpiv_debug_set.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        L.mpiv_debug_set.restype = ctypes.c_int
         for name, args in _SIGS.items():
             fn = getattr(L, name)
             fn.argtypes = args
@@ -90,6 +121,21 @@ def _call(name, *args):
     rc = getattr(L, name)(*cargs)
     if rc != 0:
         raise RuntimeError(f"{name} failed ({rc}): {L.mpiv_last_error().decode()}")
+
+
+@contextlib.contextmanager
+def debug(**opts):
+    """Select non-default kernel variants for the duration of the block (tests and A/B
+    tools only; mpiv_debug_set): e.g. ``with _lib.debug(render_mv=1, box_shrink=2): ...``.
+    Every option is restored to its production default on exit."""
+    L = load()
+    try:
+        for k, v in opts.items():
+            if L.mpiv_debug_set(k.encode(), int(v)) != 0:
+                raise ValueError(L.mpiv_last_error().decode())
+        yield
+    finally:
+        L.mpiv_debug_set(b"reset", 0)
 
 
 def _strides(t: torch.Tensor, dims=None):
@@ -128,6 +174,17 @@ def _p(t: torch.Tensor):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _check_out(out: torch.Tensor, shape, dev, what: str) -> torch.Tensor:
+    """A caller-supplied output must be a contiguous fp32 tensor of exactly `shape` on
+    `dev` (the kernels write it densely; anything else would be out-of-bounds writes)."""
+    if (not isinstance(out, torch.Tensor) or tuple(out.shape) != tuple(shape) or not out.is_contiguous()
+            or out.dtype != torch.float32 or out.device != dev):
+        got = (tuple(out.shape), out.dtype, out.device, out.is_contiguous()) if isinstance(out, torch.Tensor) \
+            else type(out).__name__
+        raise RuntimeError(f"{what}: out must be a contiguous float32 {tuple(shape)} tensor on {dev}, got {got}")
+    return out
+
+
 # ---------------------------------------------------------------------------
 # render
 # ---------------------------------------------------------------------------
@@ -153,7 +210,8 @@ def pack_planes(view: torch.Tensor, out: torch.Tensor | None = None) -> torch.Te
     H, W, P, C = view.shape
     if C != 4:
         raise RuntimeError(f"MPI texels must have 4 channels (RGBA), got {C}")
-    packed = torch.empty(packed_shape(H, W, P), device=dev, dtype=torch.float32) if out is None else out
+    packed = torch.empty(packed_shape(H, W, P), device=dev, dtype=torch.float32) if out is None else \
+        _check_out(out, packed_shape(H, W, P), dev, "pack_planes")
     _call("mpiv_pack_planes", view, _strides(view), H, W, P, packed, _stream(dev))
     return packed
 
@@ -172,6 +230,10 @@ def render_packed(packed: torch.Tensor, homs: torch.Tensor, out: torch.Tensor | 
     h = _up(homs.reshape(V, P, 9), dev)
     if out is None:
         out = torch.empty((V, H, W, 3), device=dev, dtype=torch.float32)
+    else:
+        _check_out(out, (V, H, W, 3), dev, "render_packed")
+    if V == 0:
+        return out
     _call("mpiv_render_packed", packed, H, W, P, h, V, out, _stream(dev))
     return out
 
@@ -186,6 +248,8 @@ def render_packed_ct(packed: torch.Tensor, homs: torch.Tensor, back: bool, p_beg
     h = _up(homs.reshape(V, P, 9), dev)
     if out is None:
         out = torch.empty((V, H, W, 4), device=dev, dtype=torch.float32)
+    else:
+        _check_out(out, (V, H, W, 4), dev, "render_packed_ct")
     _call("mpiv_render_packed_ct", packed, H, W, P, p_begin, p_end, int(back), h, V, out,
           _stream(dev))
     return out
@@ -271,6 +335,7 @@ class RenderFunction(torch.autograd.Function):
         return render(rgba_layers, homs)
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, dout):
         (rgba_layers,) = ctx.saved_tensors
         grad = render_backward(rgba_layers, ctx.homs, dout) if ctx.needs_input_grad[0] else None
@@ -305,26 +370,30 @@ def assemble_mpi_packed(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int, b: int
     dev, B, H, W = _net_args(mpi_pred, fg, P)
     if not 0 <= b < B:
         raise IndexError(f"batch index {b} out of range for {B}")
-    packed = torch.empty(packed_shape(H, W, P), device=dev, dtype=torch.float32) if out is None else out
+    packed = torch.empty(packed_shape(H, W, P), device=dev, dtype=torch.float32) if out is None else \
+        _check_out(out, packed_shape(H, W, P), dev, "assemble_mpi_packed")
     _call("mpiv_assemble_mpi_packed", mpi_pred, _strides(mpi_pred), fg, _strides(fg), b, H, W, P, packed,
           _stream(dev))
     return packed
 
 
-def assemble_mpi_backward(drgba: torch.Tensor, mpi_pred: torch.Tensor, fg: torch.Tensor, P: int) -> torch.Tensor:
+def assemble_mpi_backward(drgba: torch.Tensor, mpi_pred: torch.Tensor, fg: torch.Tensor, P: int,
+                          want_dfg: bool = False):
+    """d pred [B,2P+3,H,W] (and, with want_dfg, (d pred, d fg [B,H,W,3])) for d rgba."""
     dev, B, H, W = _net_args(mpi_pred, fg, P)
     _dev(drgba)
     if tuple(drgba.shape) != (B, H, W, P, 4):
         raise RuntimeError(f"grad must be [{B},{H},{W},{P},4], got {tuple(drgba.shape)}")
     dpred = torch.empty((B, 2 * P + 3, H, W), device=dev, dtype=torch.float32)
+    dfg = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32) if want_dfg else None
     _call("mpiv_assemble_mpi_backward", drgba, _strides(drgba), mpi_pred, _strides(mpi_pred), fg, _strides(fg),
-          B, H, W, P, dpred, _stream(dev))
-    return dpred
+          B, H, W, P, dpred, dfg, _stream(dev))
+    return (dpred, dfg) if want_dfg else dpred
 
 
 class AssembleFunction(torch.autograd.Function):
-    """Autograd node of the assembly: gradient w.r.t. the network prediction (the
-    reference image is data, as in the notebook's training)."""
+    """Autograd node of the assembly: gradients w.r.t. the network prediction and, when
+    it requires grad, the reference image (both bit-exact to the notebook's autograd)."""
 
     @staticmethod
     def forward(ctx, mpi_pred, fg, P):
@@ -333,12 +402,13 @@ class AssembleFunction(torch.autograd.Function):
         return assemble_mpi(mpi_pred, fg, P)
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, drgba):
         mpi_pred, fg = ctx.saved_tensors
-        if ctx.needs_input_grad[1]:
-            raise RuntimeError("mpi_from_net_output: no gradient w.r.t. the reference image (data, not a parameter)")
-        d = assemble_mpi_backward(drgba, mpi_pred, fg, ctx.P) if ctx.needs_input_grad[0] else None
-        return d, None, None
+        if not (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]):
+            return None, None, None
+        dpred, dfg = assemble_mpi_backward(drgba, mpi_pred, fg, ctx.P, want_dfg=ctx.needs_input_grad[1])
+        return (dpred if ctx.needs_input_grad[0] else None), dfg, None
 
 
 # ---------------------------------------------------------------------------

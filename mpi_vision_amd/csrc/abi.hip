@@ -40,18 +40,23 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
-// A/B and test hooks read from the environment (never needed in production use):
-//   MPIV_RENDER_MV=1      launches of >= 4 views use the multi-view LDS kernel (render_mv.hip)
-//   MPIV_RENDER_PAIR=1    the direct render takes pixel pairs sharing taps (render_pair_kernel)
-//   MPIV_RENDER_DPP=1     the direct render reads shared east taps across lanes (render_dpp_kernel)
-//   MPIV_RENDER_NATIVE_LDS=0  mpiv_render gathers directly from the [B,H,W,P,4] tensor
-//   MPIV_SWEEP_TILE=1     the sweep uses the tile kernel; MPIV_SWEEP_STORE=k the grouped one
-//   MPIV_BOX_SHRINK=k     LDS-staged kernels stage boxes k texels narrower per side, which
-//                         forces their per-sample global fallback (tests)
-int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return (e && *e) ? atoi(e) : dflt;
-}
+// Debug / A/B options (mpiv_debug_set; the defaults are the production dispatch and
+// production callers never set them):
+//   render_mv=1        launches of >= 4 views use the multi-view LDS kernel (render_mv.hip)
+//   render_pair=1|2    the direct render takes pixel pairs sharing taps (render_pair_kernel)
+//   render_native_lds=0  mpiv_render gathers directly from the [B,H,W,P,4] tensor
+//   sweep_tile=1       the sweep uses the tile kernel; sweep_store=k (k >= 0) the grouped one
+//   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
+//                      forces their per-sample global fallback (tests)
+// Relaxed atomics: a launch reads each option once; setting options while another thread
+// launches is a test-harness race on which kernel runs, never on memory.
+enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink, kNumOpts };
+const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
+                                         "sweep_tile", "sweep_store", "box_shrink"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0};
+
+int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
 constexpr int64_t kMaxGridYZ = 65535;
 constexpr int kNativeLdsMaxP = 16;
@@ -65,6 +70,26 @@ extern "C" {
 
 int mpiv_abi_version(void) { return MPIV_ABI_VERSION; }
 const char* mpiv_last_error(void) { return g_err; }
+
+#ifndef MPIV_SRC_HASH
+#define MPIV_SRC_HASH "unknown"
+#endif
+const char* mpiv_build_id(void) { return MPIV_SRC_HASH; }
+
+int mpiv_debug_set(const char* name, int value) {
+    if (!name) return fail(MPIV_ERR_ARG, "mpiv_debug_set: null name");
+    for (int i = 0; i < kNumOpts; ++i) {
+        if (strcmp(name, kOptNames[i]) == 0) {
+            __atomic_store_n(&g_opts[i], value, __ATOMIC_RELAXED);
+            return MPIV_OK;
+        }
+    }
+    if (strcmp(name, "reset") == 0) {
+        for (int i = 0; i < kNumOpts; ++i) __atomic_store_n(&g_opts[i], kOptDefaults[i], __ATOMIC_RELAXED);
+        return MPIV_OK;
+    }
+    return fail(MPIV_ERR_ARG, "mpiv_debug_set: unknown option '%s'", name);
+}
 
 int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int P, const float* homs,
                 float* out, void* stream) {
@@ -81,7 +106,7 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
     // footprints staged through LDS, read in place (render_lds.hip render_lds_native_kernel):
     // measured faster for few planes (P = 10: 0.031 vs 0.039 ms), slower for many (P = 128:
     // 2.78 vs 1.86 ms, the fills' 64-B segments no longer serve the next planes)
-    if (vec && fast && P <= kNativeLdsMaxP && env_int("MPIV_RENDER_NATIVE_LDS", 1)) {
+    if (vec && fast && P <= kNativeLdsMaxP && opt(kOptNativeLds)) {
         const int64_t nb = (int64_t)blocks(W, kLTX) * blocks(H, kLTY) * B;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_render: too many blocks");
         render_lds_native_kernel<true><<<(unsigned)nb, kLThreads, 0, q>>>(mpi, s, g, B, homs, out);
@@ -137,10 +162,10 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     }
     // several views of one MPI: the multi-view LDS-staged kernel (render_mv.hip) on request
     // (A/B: it ties the direct kernel on a camera path)
-    if (variant == 0 && fast && V >= kMMinViews && p_end - p_begin <= kMMaxP && env_int("MPIV_RENDER_MV", 0)) {
+    if (variant == 0 && fast && V >= kMMinViews && p_end - p_begin <= kMMaxP && opt(kOptRenderMv)) {
         const int64_t nb = (int64_t)blocks(W, kMTX) * blocks(H, kMTY) * ((V + kMVB - 1) / kMVB);
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
-        const int shrink = env_int("MPIV_BOX_SHRINK", 0);
+        const int shrink = opt(kOptBoxShrink);
         const dim3 grid((unsigned)nb), blk(kMThreads);
         if (ct)
             render_mv_kernel<true><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, shrink, homs, out);
@@ -148,19 +173,9 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             render_mv_kernel<false><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, shrink, homs, out);
         return launched(nm);
     }
-    // east taps read from the neighbouring lane (render.hip render_dpp_kernel): A/B
-    if (fast && env_int("MPIV_RENDER_DPP", 0)) {
-        const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;
-        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
-        if (ct)
-            render_dpp_kernel<true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
-        else
-            render_dpp_kernel<false><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
-        return launched(nm);
-    }
     // pixel pairs sharing their common taps (render.hip render_pair_kernel): opt-in A/B,
     // 20 % fewer gathers but 117 VGPRs (4 waves/SIMD), measured 3 % slower
-    if (const int pair = fast ? env_int("MPIV_RENDER_PAIR", 0) : 0) {  // 1: two planes in flight, 2: one
+    if (const int pair = fast ? opt(kOptRenderPair) : 0) {  // 1: two planes in flight, 2: one
         const int64_t nb = (int64_t)blocks(W, kPairX) * blocks(H, kTileY) * V;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
         if (ct && pair == 1)
@@ -227,6 +242,7 @@ size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
     char* offs = take((nk + 1) * 4);
     char* ids = take(n * 4);
     char* bsum = take(nb * 4);
+    char* big = take((n / (kSmallBucket + 1) + 2) * 4);
     if (ws) {
         ws->prev = reinterpret_cast<float4*>(prev);
         ws->ds = reinterpret_cast<float4*>(ds);
@@ -236,6 +252,7 @@ size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
         ws->offs = reinterpret_cast<int*>(offs);
         ws->ids = reinterpret_cast<int*>(ids);
         ws->bsum = reinterpret_cast<int*>(bsum);
+        ws->big = reinterpret_cast<int*>(big);
     }
     return off;
 }
@@ -290,7 +307,9 @@ int mpiv_render_backward(const float* packed, int H, int W, int P, const float* 
         scan_tile_offsets_kernel<<<1, kScanBlock, 0, q>>>(ws.bsum, (int)nb);
         scan_apply_kernel<<<nb, kScanBlock, 0, q>>>(ws.count, nk, ws.bsum, ws.offs);
         bucket_fill_kernel<<<blocks(nq, 256), 256, 0, q>>>(P, HW, K, ws);
+        if (hipMemsetAsync(ws.big, 0, 4, q) != hipSuccess) return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
         bucket_sort_kernel<<<blocks(nk, 256), 256, 0, q>>>(nk, ws);
+        big_bucket_sort_kernel<<<256, 256, 0, q>>>(ws);
         float* gv = dmpi + (int64_t)v * st[0];
         if (dense && aligned16(gv))
             render_bwd_gather_dense_kernel<<<dim3(blocks((int64_t)H * W, kWave), blocks(P, kGatherPl)),
@@ -378,16 +397,17 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
     const bool vec = aligned16(out) && out_pstride % 4 == 0 && out_bstride % 4 == 0;
     const bool dense = vec && out_pstride == (int64_t)NG * kSweepDG * C;
     int store = dense ? 2 : vec ? 1 : 0;
-    const char* e_store = getenv("MPIV_SWEEP_STORE");  // A/B only: the grouped kernel's store modes
-    const bool tile = !e_store && (env_int("MPIV_SWEEP_TILE", 0) || D > kSweepMaxLdsD);
-    if (e_store) store = min(store, atoi(e_store));
+    const int o_store = opt(kOptSweepStore);  // A/B only: the grouped kernel's store modes
+    const bool grouped = o_store >= 0;
+    const bool tile = !grouped && (opt(kOptSweepTile) || D > kSweepMaxLdsD);
+    if (grouped) store = min(store, o_store);
     hipStream_t q = S(stream);
-    if (!e_store && !tile) {
+    if (!grouped && !tile) {
         // default: source footprint staged in LDS (plane_sweep_lds_kernel)
         const int64_t tiles = (int64_t)((Wt + kSLP - 1) / kSLP) * ((Ht + kSLR - 1) / kSLR);
         if (tiles > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: too large");
         const dim3 lgrid((unsigned)tiles, B, 1);
-        const int shrink = env_int("MPIV_BOX_SHRINK", 0);
+        const int shrink = opt(kOptBoxShrink);
         const FastDiv fd_b = make_fastdiv((unsigned)(16 * NG));
 #define MPIV_LDS(CC)                                                                                          \
     plane_sweep_lds_kernel<CC><<<lgrid, kSLThreads, 0, q>>>(im, sp, pg, rc_hs, rc_ws, fd_g, fd_b, ki, proj, depths, \
@@ -574,7 +594,7 @@ int mpiv_assemble_mpi_packed(const float* pred, const int64_t ps[4], const float
 
 int mpiv_assemble_mpi_backward(const float* drgba, const int64_t gs[5], const float* pred, const int64_t ps[4],
                                const float* fg, const int64_t fs[4], int B, int H, int W, int P, float* dpred,
-                               void* stream) {
+                               float* dfg, void* stream) {
     if (int rc = check_net("mpiv_assemble_mpi_backward", pred, ps, fg, fs, B, H, W, P)) return rc;
     if (!drgba || !gs || !dpred) return fail(MPIV_ERR_ARG, "mpiv_assemble_mpi_backward: null pointer");
     const NetStrides s{ps[0], ps[1], ps[2], ps[3], fs[0], fs[1], fs[2], fs[3]};
@@ -583,10 +603,10 @@ int mpiv_assemble_mpi_backward(const float* drgba, const int64_t gs[5], const fl
                        g.b == (int64_t)H * W * P * 4 && aligned16(drgba);
     if (dense)
         assemble_backward_dense_kernel<<<dim3(blocks((int64_t)H * W, kAbPix), B), kAbPix, 0, S(stream)>>>(
-            reinterpret_cast<const float4*>(drgba), pred, fg, s, H, W, P, make_fastdiv((unsigned)W), dpred);
+            reinterpret_cast<const float4*>(drgba), pred, fg, s, H, W, P, make_fastdiv((unsigned)W), dpred, dfg);
     else
         assemble_backward_kernel<<<dim3(blocks((int64_t)H * W, 256), B), 256, 0, S(stream)>>>(
-            drgba, g, pred, fg, s, H, W, P, make_fastdiv((unsigned)W), dpred);
+            drgba, g, pred, fg, s, H, W, P, make_fastdiv((unsigned)W), dpred, dfg);
     return launched("mpiv_assemble_mpi_backward");
 }
 

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void assemble_backward_kernel(const float* __r
                                                                 NativeStrides gs, const float* __restrict__ pred,
                                                                 const float* __restrict__ fg, NetStrides s, int H,
                                                                 int W, int P, FastDiv w_div,
-                                                                float* __restrict__ dpred) {
+                                                                float* __restrict__ dpred, float* __restrict__ dfg) {
     const int64_t npix = (int64_t)H * W;
     const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void assemble_backward_kernel(const float* __r
                 b2 = pp[(int64_t)(2 * P + 2) * s.pc];
     const float* g0 = grad + (int64_t)b * gs.b + (int64_t)y * gs.y + (int64_t)x * gs.x;
     float* dp = dpred + (int64_t)b * (2 * P + 3) * npix + pix;
-    float db0 = 0.f, db1 = 0.f, db2 = 0.f;
+    float db0 = 0.f, db1 = 0.f, db2 = 0.f, df0 = 0.f, df1 = 0.f, df2 = 0.f;
     for (int p = P - 1; p >= 0; --p) {  // autograd runs the planes' nodes last to first
         const float* g = g0 + (int64_t)p * gs.p;
         const float gr = g[0], gg = g[gs.c], gb = g[2 * gs.c], ga = g[3 * gs.c];
@@ -121,15 +121,22 @@ __global__ __launch_bounds__(256) void assemble_backward_kernel(const float* __r
         dp[(int64_t)p * npix] = dw / 2.0f;            // DivBackward
         dp[(int64_t)(P + p) * npix] = ga / 2.0f;
         const float c0 = gr * om, c1 = gg * om, c2 = gb * om;
+        const float e0 = gr * w, e1 = gg * w, e2 = gb * w;  // MulBackward of w * fg w.r.t. fg
         if (p == P - 1) {
             db0 = c0; db1 = c1; db2 = c2;
+            df0 = e0; df1 = e1; df2 = e2;
         } else {
             db0 = db0 + c0; db1 = db1 + c1; db2 = db2 + c2;
+            df0 = df0 + e0; df1 = df1 + e1; df2 = df2 + e2;
         }
     }
     dp[(int64_t)(2 * P) * npix] = db0;
     dp[(int64_t)(2 * P + 1) * npix] = db1;
     dp[(int64_t)(2 * P + 2) * npix] = db2;
+    if (dfg) {
+        float* o = dfg + ((int64_t)b * npix + pix) * 3;
+        o[0] = df0; o[1] = df1; o[2] = df2;
+    }
 }
 
 // The same for a dense d rgba ([B,H,W,P,4] contiguous): 256 pixels per block; the
@@ -142,7 +149,8 @@ __global__ __launch_bounds__(kAbPix) void assemble_backward_dense_kernel(const f
                                                                         const float* __restrict__ pred,
                                                                         const float* __restrict__ fg, NetStrides s,
                                                                         int H, int W, int P, FastDiv w_div,
-                                                                        float* __restrict__ dpred) {
+                                                                        float* __restrict__ dpred,
+                                                                        float* __restrict__ dfg) {
     __shared__ float4 tile[kAbPix][kAbPl + 1];
     const int64_t npix = (int64_t)H * W;
     const int64_t pix0 = (int64_t)blockIdx.x * kAbPix;
@@ -159,7 +167,7 @@ __global__ __launch_bounds__(kAbPix) void assemble_backward_dense_kernel(const f
     }
     const float4* gb = grad + (int64_t)b * npix * P;
     float* dp = dpred + (int64_t)b * (2 * P + 3) * npix + pix;
-    float db0 = 0.f, db1 = 0.f, db2 = 0.f;
+    float db0 = 0.f, db1 = 0.f, db2 = 0.f, df0 = 0.f, df1 = 0.f, df2 = 0.f;
     const int nch = (P + kAbPl - 1) / kAbPl;
     for (int ch = nch - 1; ch >= 0; --ch) {  // planes last to first, as autograd runs them
         const int p0 = ch * kAbPl, np = min(kAbPl, P - p0);
@@ -180,10 +188,13 @@ __global__ __launch_bounds__(kAbPix) void assemble_backward_dense_kernel(const f
             dp[(int64_t)p * npix] = (sf + -sb) / 2.0f;
             dp[(int64_t)(P + p) * npix] = g.w / 2.0f;
             const float c0 = g.x * om, c1 = g.y * om, c2 = g.z * om;
+            const float e0 = g.x * w, e1 = g.y * w, e2 = g.z * w;
             if (p == P - 1) {
                 db0 = c0; db1 = c1; db2 = c2;
+                df0 = e0; df1 = e1; df2 = e2;
             } else {
                 db0 = db0 + c0; db1 = db1 + c1; db2 = db2 + c2;
+                df0 = df0 + e0; df1 = df1 + e1; df2 = df2 + e2;
             }
         }
     }
@@ -191,6 +202,10 @@ __global__ __launch_bounds__(kAbPix) void assemble_backward_dense_kernel(const f
     dp[(int64_t)(2 * P) * npix] = db0;
     dp[(int64_t)(2 * P + 1) * npix] = db1;
     dp[(int64_t)(2 * P + 2) * npix] = db2;
+    if (dfg) {
+        float* o = dfg + ((int64_t)b * npix + pix) * 3;
+        o[0] = df0; o[1] = df1; o[2] = df2;
+    }
 }
 
 }  // namespace mpiv

@@ -432,125 +432,6 @@ __global__ __launch_bounds__(256) void render_pair_kernel(const float4* __restri
 }
 
 // ---------------------------------------------------------------------------
-// east taps from the neighbouring lane (render_dpp_kernel, A/B)
-// ---------------------------------------------------------------------------
-//
-// A wave renders 64 consecutive pixels of a row.  Where lane i+1's north-west tap is one
-// texel east of lane i's (the offsets are compared: same memory word), lane i's NE / SE
-// taps are lane i+1's NW / SW, read across lanes (DPP wave_shl:1, full EXEC) instead of
-// gathered; only the lanes that do not share -- always lane 63 -- gather their east taps,
-// under an EXEC mask.  Every lane of the wave runs the loop (no early exit), because a
-// DPP read from a disabled lane is not its register.
-__device__ __forceinline__ float lane_next(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130 /* wave_shl:1 */, 0xF, 0xF, true));
-}
-__device__ __forceinline__ int lane_next_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, true);
-}
-
-template <bool CT, bool GUARD>
-__device__ __forceinline__ void render_dpp_pixel(const float4* __restrict__ planes, int64_t plane_stride,
-                                                 const RenderGeom& g, int p_begin, int p_end, int back,
-                                                 const float* __restrict__ hv, int x, int y, bool store,
-                                                 float* __restrict__ out_px) {
-    const float fx = (float)x, fy = (float)y;
-    float cr = -0.0f, cg = -0.0f, cb = -0.0f, t = 1.0f;  // render_packed_pixel: plane 0 replaces
-    const bool replace_first = !CT || back;
-    const int last = p_end - 1;
-    struct Taps {
-        TapSet ts;
-        bool share;
-    };
-    auto hom = [&](int p) { return load_hom(hv + (int64_t)(p < last ? p : last) * 9); };
-    auto issue = [&](int p, const Hom9& h, Taps& tt) {
-        const int q = p < last ? p : last;
-        float px, py;
-        render_pos_fast<GUARD>(h.h, fx, fy, g, px, py);
-        const int off = tap_origin(g, px, py, &tt.ts.nw);
-        tt.share = lane_next_i(off) == off + 16;  // lane 63 reads 0: never shares
-        const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes);
-        tt.ts.a = llvm_raw_buffer_load_v4f32(r, off, 0, 0);
-        tt.ts.c = llvm_raw_buffer_load_v4f32(r, off, g.row, 0);
-        if (!tt.share) {  // EXEC-masked east gathers
-            tt.ts.b = llvm_raw_buffer_load_v4f32(r, off + 16, 0, 0);
-            tt.ts.d = llvm_raw_buffer_load_v4f32(r, off + 16, g.row, 0);
-        }
-    };
-    auto consume = [&](Taps& tt, bool first) {
-        TapSet& ts = tt.ts;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {  // full EXEC here: every lane's NW / SW is readable
-            const float nb = lane_next(ts.a[k]), nd = lane_next(ts.c[k]);
-            ts.b[k] = tt.share ? nb : ts.b[k];
-            ts.d[k] = tt.share ? nd : ts.d[k];
-        }
-        const f32x4 s = blend_taps(ts);
-        const float a = first ? 1.0f : s[3];
-        const float om = 1.0f - a;
-        cr = over(s[0], a, om, cr);
-        cg = over(s[1], a, om, cg);
-        cb = over(s[2], a, om, cb);
-        if (CT) t = t * om;
-    };
-    Taps A, B;
-    Hom9 hA = hom(p_begin), hB = hom(p_begin + 1);
-    issue(p_begin, hA, A);
-    hA = hom(p_begin + 2);
-    int p = p_begin;
-    for (; p + 1 < p_end; p += 2) {
-        issue(p + 1, hB, B);
-        hB = hom(p + 3);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(A, replace_first && p == p_begin);
-        issue(p + 2, hA, A);
-        hA = hom(p + 4);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(B, false);
-    }
-    if (p < p_end) consume(A, replace_first && p == p_begin);
-    if (!store) return;
-    if (CT) {
-        *reinterpret_cast<float4*>(out_px) = make_float4(cr, cg, cb, t);
-    } else {
-        out_px[0] = cr;
-        out_px[1] = cg;
-        out_px[2] = cb;
-    }
-}
-
-template <bool CT>
-__global__ __launch_bounds__(256) void render_dpp_kernel(const float4* __restrict__ planes, int64_t plane_stride,
-                                                         RenderGeom g, int V, int p_begin, int p_end, int back,
-                                                         const float* __restrict__ homs, float* __restrict__ out) {
-    const int tiles_x = (g.W + kTileX - 1) / kTileX;
-    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
-    const int v = lb % V;
-    const int tile = lb / V;
-    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * kTileY;
-    const int x = tx0 + (threadIdx.x & (kWave - 1));
-    const int y = ty0 + (threadIdx.x >> 6);
-    const float* hv = homs + (int64_t)v * g.P * 9;
-    bool ok = true;
-    {
-        const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
-        const float y0 = (float)ty0, y1 = (float)min(ty0 + kTileY - 1, g.H - 1);
-        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256)
-            ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, y0, y1);
-    }
-    const bool proven = __syncthreads_and(ok);
-    // lanes past the image edge run the loop on a clamped pixel (their neighbours' DPP
-    // reads need them) and store nothing
-    const bool store = x < g.W && y < g.H;
-    const int xc = min(x, g.W - 1), yc = min(y, g.H - 1);
-    const int64_t o = ((int64_t)v * g.H + yc) * g.W + xc;
-    float* out_px = CT ? out + o * 4 : out + o * 3;
-    if (proven)
-        render_dpp_pixel<CT, false>(planes, plane_stride, g, p_begin, p_end, back, hv, xc, yc, store, out_px);
-    else
-        render_dpp_pixel<CT, true>(planes, plane_stride, g, p_begin, p_end, back, hv, xc, yc, store, out_px);
-}
-
-// ---------------------------------------------------------------------------
 // native [B,H,W,P,C=4] layout, arbitrary element strides
 // ---------------------------------------------------------------------------
 

@@ -19,7 +19,10 @@
 //            and the bucket of its north-west tap; bucket sizes are counted.
 //  2. scan   exclusive prefix sum of the bucket sizes (3 kernels).
 //  3. bucket pixel ids into their buckets (atomic slot claim), then sort each
-//            bucket by pixel id (buckets hold ~1 pixel for non-minifying warps).
+//            bucket by pixel id: buckets of <= kSmallBucket ids (~1 pixel for
+//            non-minifying warps) by one thread, larger ones (minification, degenerate
+//            homographies: up to every pixel of a plane in one bucket) by a block-wide
+//            merge sort, so no bucket size costs O(n^2) on one lane.
 //  4. gather (one work-item per source texel): the texel is the nw tap of bucket
 //            (x, y), the ne tap of bucket (x-1, y), sw of (x, y-1), se of (x-1, y-1);
 //            the four sorted lists are merged by the reference's order key
@@ -35,15 +38,19 @@ constexpr int kScanItems = 16;    // items per thread in the bucket scan
 constexpr int kScanBlock = 256;
 constexpr int kScanTile = kScanItems * kScanBlock;
 
+constexpr int kSmallBucket = 32;  // larger buckets are sorted by a whole block
+
 struct BwdWs {
     float4* prev;  // [P][HW]  out_{p-1} (rgb, 0)
     float4* ds;    // [P][HW]  sample s_p, then d s_p = (d rgb, d a)
     float2* fw;    // [P][HW]  bilinear fractions (wx, wy)
-    int* key;      // [P][HW]  nw-tap bucket in the (H+1) x (W+1) grid, -1 = no tap in the image
+    int* key;      // [P][HW]  nw-tap bucket in the (H+1) x (W+1) grid, -1 = no tap in the image;
+                   //          after the fill: merge-sort scratch (same offsets as ids)
     int* count;    // [P*K]    bucket sizes; zero on entry and on exit of every view
     int* offs;     // [P*K+1]  exclusive scan of count
     int* ids;      // [P*HW]   pixel ids grouped by bucket
     int* bsum;     // scan block sums
+    int* big;      // [0] = number of large buckets, [1..] their indices (P*HW/(kSmallBucket+1) max)
 };
 
 // ---- 1. forward recompute + over-chain adjoint, one work-item per output pixel ----
@@ -243,7 +250,11 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(int64_t nbuckets, BwdW
     const int64_t pk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (pk >= nbuckets) return;
     const int b = ws.offs[pk], e = ws.offs[pk + 1];
-    for (int i = b + 1; i < e; ++i) {  // insertion sort (buckets are tiny)
+    if (e - b > kSmallBucket) {  // left to big_bucket_sort_kernel
+        ws.big[1 + atomicAdd(&ws.big[0], 1)] = (int)pk;
+        return;
+    }
+    for (int i = b + 1; i < e; ++i) {  // insertion sort (at most kSmallBucket ids)
         const int v = ws.ids[i];
         int j = i - 1;
         while (j >= b && ws.ids[j] > v) {
@@ -251,6 +262,46 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(int64_t nbuckets, BwdW
             --j;
         }
         ws.ids[j + 1] = v;
+    }
+}
+
+// Sorts the large buckets listed by bucket_sort_kernel: each block takes buckets
+// blockIdx.x, blockIdx.x + gridDim.x, ... and merge-sorts one at a time, all threads
+// together (runs of width w merged pairwise per pass; output element k of a pair found
+// by a merge-path binary search; ids within a bucket are distinct).  The scratch is the
+// bucket's range of `key` (dead after the fill).  O(n log^2 n / threads) per bucket.
+__global__ __launch_bounds__(256) void big_bucket_sort_kernel(BwdWs ws) {
+    const int nbig = ws.big[0];
+    for (int i = blockIdx.x; i < nbig; i += gridDim.x) {
+        const int pk = ws.big[1 + i];
+        const int b = ws.offs[pk], n = ws.offs[pk + 1] - b;
+        int* src = ws.ids + b;
+        int* dst = ws.key + b;
+        for (int w = 1; w < n; w <<= 1) {
+            for (int k0 = threadIdx.x; k0 < n; k0 += blockDim.x) {
+                const int s0 = (k0 / (2 * w)) * (2 * w);
+                const int m = min(s0 + w, n), e = min(s0 + 2 * w, n);
+                const int k = k0 - s0;
+                const int* A = src + s0;
+                const int* Bv = src + m;
+                const int la = m - s0, lb = e - m;
+                int lo = max(0, k - lb), hi = min(k, la);
+                while (lo < hi) {  // number of A's elements among the pair's first k outputs
+                    const int mid = (lo + hi) >> 1;
+                    if (A[mid] < Bv[k - 1 - mid]) lo = mid + 1;
+                    else hi = mid;
+                }
+                const int ib = k - lo;
+                dst[k0] = (lo < la && (ib >= lb || A[lo] < Bv[ib])) ? A[lo] : Bv[ib];
+            }
+            __syncthreads();
+            int* t = src;
+            src = dst;
+            dst = t;
+        }
+        if (src != ws.ids + b)
+            for (int k0 = threadIdx.x; k0 < n; k0 += blockDim.x) ws.ids[b + k0] = src[k0];
+        __syncthreads();
     }
 }
 

@@ -94,25 +94,44 @@ def gather_frames(band: torch.Tensor, height: int, group=None, dst: int = 0) -> 
 
 def combine_partials(parts: torch.Tensor,
                      combine: Optional[Callable[[torch.Tensor], torch.Tensor]] = None) -> torch.Tensor:
-    """Ordered back-to-front over-combine of [G, ...,4] partials -> [..., 3] (HIP kernel)."""
+    """Ordered back-to-front over-combine of [G, ...,4] partials -> [..., 3] (HIP kernel).
+    An empty band (a frame with fewer rows than ranks) combines to an empty band."""
+    if parts[0].numel() == 0:
+        return parts.new_empty(tuple(parts.shape[1:-1]) + (3,))
     if combine is None:
         from . import _lib
         combine = _lib.combine_ct
     return combine(parts)
 
 
+def identity_partial(views: int, height: int, width: int, like: torch.Tensor) -> torch.Tensor:
+    """The (C, T) partial of an empty plane range, (0, 1): the over-operator's identity, so a
+    rank that owns no planes (P < ranks) leaves the combined frame unchanged."""
+    ct = like.new_zeros((views, height, width, 4))
+    ct[..., 3] = 1.0
+    return ct
+
+
 def render_plane_sharded(packed_local: torch.Tensor, homs_local: torch.Tensor, height: int, group=None,
-                         dst: int = 0) -> Optional[torch.Tensor]:
+                         dst: int = 0, render_ct: Optional[Callable] = None,
+                         combine: Optional[Callable[[torch.Tensor], torch.Tensor]] = None) -> Optional[torch.Tensor]:
     """Plane-sharded render of V views.
 
     packed_local: this rank's planes, packed [P_local, H+4, W+4, 4] (_lib.pack_planes) (rank 0 holds the
     back-most range, which contains the reference's plane 0); homs_local
-    [V, P_local, 9].  Returns the final frames [V, H, W, 3] on dst, None elsewhere."""
+    [V, P_local, 9].  P_local may be 0 (more ranks than planes): that rank contributes the
+    identity partial.  Returns the final frames [V, H, W, 3] on dst, None elsewhere.
+    render_ct / combine replace the HIP kernels (CPU tests of the exchange logic only)."""
     from . import _lib
     G, rank = _world(group)
-    ct = _lib.render_packed_ct(packed_local, homs_local, back=(rank == 0))
+    V = homs_local.shape[0]
+    width = packed_local.shape[2] - 2 * _lib.PAD
+    if packed_local.shape[0] == 0:
+        ct = identity_partial(V, height, width, packed_local)
+    else:
+        ct = (render_ct or _lib.render_packed_ct)(packed_local, homs_local, back=(rank == 0))
     parts = exchange_bands(ct, group)
-    band = combine_partials(parts)
+    band = combine_partials(parts, combine)
     return gather_frames(band, height, group, dst)
 
 
@@ -144,11 +163,18 @@ def gather_view_frames(frames: torch.Tensor, n_views: int, group=None, dst: int 
 
 
 def render_view_sharded(packed: torch.Tensor, homs_all: torch.Tensor, group=None, gather: bool = False,
-                        dst: int = 0) -> Optional[torch.Tensor]:
+                        dst: int = 0, render: Optional[Callable] = None) -> Optional[torch.Tensor]:
     """This rank's frames of a view-sharded camera path (no collective); with `gather`,
-    the whole path's frames on dst (gather_view_frames) and None elsewhere."""
+    the whole path's frames on dst (gather_view_frames) and None elsewhere.  A rank whose
+    shard is empty (fewer views than ranks) renders nothing and still joins the gather.
+    render replaces the HIP kernel (CPU tests of the sharding logic only)."""
     from . import _lib
     G, rank = _world(group)
     sl = view_shard(homs_all.shape[0], rank, G)
-    frames = _lib.render_packed(packed, homs_all[sl])
+    hv = homs_all[sl]
+    if hv.shape[0] == 0:
+        H, W = packed.shape[1] - 2 * _lib.PAD, packed.shape[2] - 2 * _lib.PAD
+        frames = packed.new_empty((0, H, W, 3))
+    else:
+        frames = (render or _lib.render_packed)(packed, hv)
     return gather_view_frames(frames, homs_all.shape[0], group, dst) if gather else frames

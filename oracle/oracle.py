@@ -184,3 +184,16 @@ def assemble_mpi_backward(drgba: np.ndarray, pred: np.ndarray, fg: np.ndarray, P
         dbg = dbg + contrib[..., i, :]
     d = np.concatenate([dw, da, dbg], axis=-1)                            # [B,H,W,2P+3]
     return np.ascontiguousarray(np.transpose(d, (0, 3, 1, 2))).astype(np.float32)
+
+
+def assemble_mpi_backward_fg(drgba: np.ndarray, pred: np.ndarray, P: int) -> np.ndarray:
+    """d fg [B,H,W,3] for d rgba: MulBackward of w * fg per plane (g * w), accumulated from
+    the last plane to the first like d bg (the same engine order)."""
+    one, two = np.float32(1), np.float32(2)
+    p = np.transpose(pred.astype(np.float32), (0, 2, 3, 1))
+    w = (p[..., :P] + one) / two
+    contrib = drgba.astype(np.float32)[..., :3] * w[..., None]           # [B,H,W,P,3]
+    dfg = contrib[..., P - 1, :].copy()
+    for i in range(P - 2, -1, -1):
+        dfg = dfg + contrib[..., i, :]
+    return dfg.astype(np.float32)

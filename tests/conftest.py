@@ -45,6 +45,21 @@ def dev():
     return torch.device("cuda:0")
 
 
+@pytest.fixture
+def kopts():
+    """Select non-default kernel variants for one test (libmpiv's debug options,
+    mpiv_debug_set); every option is restored to its production default afterwards."""
+    from mpi_vision_amd import _lib
+    L = _lib.load()
+
+    def set_(**opts):
+        for k, v in opts.items():
+            assert L.mpiv_debug_set(k.encode(), int(v)) == 0, L.mpiv_last_error()
+
+    yield set_
+    L.mpiv_debug_set(b"reset", 0)
+
+
 def sha256(a) -> str:
     if isinstance(a, torch.Tensor):
         a = a.detach().cpu().contiguous().numpy()

@@ -61,3 +61,37 @@ def test_bad_shapes_rejected():
     assert b"plane range" in L.mpiv_last_error()
     assert L.mpiv_render_packed(ctypes.c_void_p(8), 4, 4, 2, p, 1, p, None) == -1
     assert b"alignment" in L.mpiv_last_error()
+
+
+def test_build_id_matches_sources():
+    """libmpiv.so carries the sha256 of the sources it was built from (csrc/SOURCES);
+    _lib.load() refuses a library whose id differs from the tree's sources."""
+    L = _lib.load()
+    assert L.mpiv_build_id().decode() == _lib.source_hash()
+
+
+def test_debug_options():
+    """Kernel A/B variants are selected only through the debug entry point (no getenv on
+    the launch path); unknown names are rejected; reset restores the defaults."""
+    L = _lib.load()
+    assert L.mpiv_debug_set(b"no_such_option", 1) == -1
+    assert b"unknown option" in L.mpiv_last_error()
+    with _lib.debug(render_mv=1, box_shrink=2):
+        pass
+    with pytest.raises(ValueError):
+        with _lib.debug(bogus=1):
+            pass
+
+
+def test_output_buffers_validated():
+    """Caller-supplied outputs of the packed render / pack must be dense fp32 tensors of the
+    exact shape on the same device, else a Python error (not out-of-bounds device writes)."""
+    import torch
+    good = torch.zeros(4)
+    with pytest.raises(RuntimeError, match="out must be"):
+        _lib._check_out(torch.zeros((2, 3)), (3, 2), good.device, "x")
+    with pytest.raises(RuntimeError, match="out must be"):
+        _lib._check_out(torch.zeros((3, 4))[:, :2], (3, 2), good.device, "x")
+    with pytest.raises(RuntimeError, match="out must be"):
+        _lib._check_out(torch.zeros((3, 2), dtype=torch.float64), (3, 2), good.device, "x")
+    assert _lib._check_out(torch.zeros((3, 2)), (3, 2), good.device, "x") is not None

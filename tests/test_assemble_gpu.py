@@ -51,6 +51,32 @@ def test_assemble_backward_vs_notebook_autograd(net, dev, c):
     assert_bits(pred.grad.cpu().numpy(), net[c + "_dpred"], f"d pred {c}")
 
 
+@pytest.mark.parametrize("c", CASES)
+def test_assemble_backward_ref_image_vs_notebook_autograd(net, dev, c):
+    """ref_img requiring grad too: d ref and d pred bit-exact to the notebook's
+    autograd (which accumulates the per-plane g*w terms from the last plane to the first)."""
+    pred = torch.tensor(net[c + "_pred"]).to(dev).requires_grad_(True)
+    dep = _dep(net, c, dev)
+    dep["ref_img"].requires_grad_(True)
+    mv.mpi_from_net_output(pred, dep).backward(torch.tensor(net[c + "_drgba"]).to(dev))
+    torch.cuda.synchronize()
+    assert_bits(dep["ref_img"].grad.cpu().numpy(), net[c + "_dref"], f"d ref {c}")
+    assert_bits(pred.grad.cpu().numpy(), net[c + "_dpred"], f"d pred {c}")
+
+
+def test_backward_is_once_differentiable(dev):
+    """Double backward through the HIP nodes raises instead of returning a graph-less
+    gradient."""
+    g = torch.Generator().manual_seed(3)
+    B, H, W, P = 1, 12, 16, 4
+    pred = (torch.rand((B, 2 * P + 3, H, W), generator=g) * 2 - 1).to(dev).requires_grad_(True)
+    dep = {"mpi_planes": torch.zeros((B, P), device=dev), "ref_img": torch.rand((B, H, W, 3)).to(dev)}
+    rgba = mv.mpi_from_net_output(pred, dep)
+    (gp,) = torch.autograd.grad(rgba.sum(), pred, create_graph=True)
+    with pytest.raises(RuntimeError):
+        gp.sum().backward()
+
+
 def test_assemble_strided_inputs(dev):
     """Non-contiguous prediction (a channels-last buffer viewed as NCHW) and reference
     image (a slice of a wider buffer): same bits as the oracle on dense copies."""
@@ -65,13 +91,15 @@ def test_assemble_strided_inputs(dev):
     dpred = _lib.assemble_mpi_backward(drgba.to(dev), pred, fg, P)
     # a non-dense upstream gradient takes the generic (per-lane run) backward kernel
     dwide = torch.rand((B, H, W, P + 2, 4), generator=g) * 2 - 1
-    dpred_s = _lib.assemble_mpi_backward(dwide.to(dev)[:, :, :, 1:P + 1], pred, fg, P)
+    dpred_s, dfg_s = _lib.assemble_mpi_backward(dwide.to(dev)[:, :, :, 1:P + 1], pred, fg, P, want_dfg=True)
     torch.cuda.synchronize()
     pn, fn = nhwc.permute(0, 3, 1, 2).contiguous().numpy(), wide[..., 1:4].contiguous().numpy()
     assert_bits(rgba.cpu().numpy(), oracle.assemble_mpi(pn, fn, P), "strided forward")
     assert_bits(dpred.cpu().numpy(), oracle.assemble_mpi_backward(drgba.numpy(), pn, fn, P), "dense backward")
     assert_bits(dpred_s.cpu().numpy(), oracle.assemble_mpi_backward(dwide[:, :, :, 1:P + 1].contiguous().numpy(),
                                                                     pn, fn, P), "strided backward")
+    assert_bits(dfg_s.cpu().numpy(), oracle.assemble_mpi_backward_fg(dwide[:, :, :, 1:P + 1].contiguous().numpy(),
+                                                                     pn, P), "strided backward d fg")
 
 
 def test_assemble_packed_equals_pack_of_assembled(net, dev):

@@ -42,6 +42,25 @@ def test_backward_matches_reference_autograd(name, grad, dev):
     assert_bits(leaf.grad, grad[f"{name}_grad"], f"{name} d rgba_layers")
 
 
+def test_backward_collapsing_homography_vs_oracle(dev):
+    """Homographies that send many target pixels to one source texel: plane 0
+    maps the whole frame to one point (one bucket holding every pixel), plane 1 minifies
+    ~16x (buckets of ~70 pixels), plane 2 is a mild warp.  The large buckets take the
+    block merge sort; the gradient stays bit-exact to the oracle's ordered scatter."""
+    g = torch.Generator().manual_seed(17)
+    H, W, P = 48, 80, 3
+    mpi = configs.synthetic_mpi(1, H, W, P, 21)
+    s = (H - 1) / (W - 1)  # the reference's swapped x / (H-1): undo it so the x step is 16 texels
+    homs = torch.tensor([[[0.0, 0.0, 12.3, 0.0, 0.0, 7.6, 0.0, 0.0, 1.0],
+                          [16.0 * s, 0.0, 0.5, 0.0, 16.0 / s, 0.25, 0.0, 0.0, 1.0],
+                          [1.01, 0.02, -0.7, -0.01, 0.99, 0.4, 1e-4, 0.0, 1.0]]], dtype=torch.float32)
+    dout = torch.rand((1, H, W, 3), generator=g) * 2 - 1
+    want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
+    got = _lib.render_backward(mpi.to(dev), homs, dout.to(dev))
+    assert_bits(got, want, "collapsing homographies")
+    assert np.abs(want[0, :, :, 0]).max() > 1.0  # plane 0's one texel gathered the whole frame
+
+
 def test_backward_broadcast_mpi(grad, dev):
     """Broadcast MPI (stride-0 batch): per-view gradients are bit-exact to the oracle;
     their sum (torch's expand backward on the GPU) matches the reference within 1e-6."""

@@ -24,10 +24,10 @@ def _free_port():
     return p
 
 
-def _case():
+def _case(H=37, W=53, P=11):
     sys.path.insert(0, REPO)
     from mpi_vision_amd import _host, configs
-    H, W, P, V = 37, 53, 11, 2
+    V = 2
     mpi = configs.synthetic_mpi(1, H, W, P, 5)
     K = configs.f32([configs.intrinsics_matrix(50.0, 52.0, 26.0, 18.0)] * V)
     poses = configs.f32([configs.pose_from(configs.rot_y(1.5), (0.05, -0.02, 0.03)),
@@ -68,6 +68,52 @@ def test_plane_sharded_exchange_matches_sequential(world, tmp_path):
     np.testing.assert_allclose(got, want, rtol=0, atol=1e-5)
 
 
+def _empty_shard_worker(rank, world, port, H, W, P, out_path):
+    """The product's render_plane_sharded / render_view_sharded with more ranks than planes,
+    rows or views (such a rank used to raise while the others waited in the
+    collective).  The per-rank kernels are replaced by the oracle (CPU tensors)."""
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mpi_vision_amd import _lib, parallel
+    from oracle import oracle
+    mpi, homs = _case(H, W, P)
+    V = mpi.shape[0]
+    p0, p1 = parallel.shard_range(P, rank, world)
+    packed = torch.zeros(_lib.packed_shape(H, W, p1 - p0))
+    packed[:, 2:2 + H, 2:2 + W] = torch.from_numpy(mpi[0, :, :, p0:p1]).permute(2, 0, 1, 3)
+    local = np.ascontiguousarray(mpi[:, :, :, p0:p1])
+    frame = parallel.render_plane_sharded(
+        packed, torch.from_numpy(np.ascontiguousarray(homs[:, p0:p1])), H,
+        render_ct=lambda pk, h, back: torch.from_numpy(oracle.render_ct(local, h.numpy(), 0, p1 - p0, back)),
+        combine=lambda x: torch.from_numpy(oracle.combine_ct(x.numpy())))
+    # view sharding with more ranks than views: 2 views over `world` ranks
+    full_pk = torch.zeros(_lib.packed_shape(H, W, P))
+    full_pk[:, 2:2 + H, 2:2 + W] = torch.from_numpy(mpi[0]).permute(2, 0, 1, 3)
+    views = parallel.render_view_sharded(
+        full_pk, torch.from_numpy(homs), gather=True,
+        render=lambda pk, h: torch.from_numpy(oracle.render(np.ascontiguousarray(mpi[:h.shape[0]]), h.numpy())))
+    if rank == 0:
+        np.save(out_path, frame.numpy())
+        np.save(out_path + ".views.npy", views.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,H,W,P", [(3, 9, 13, 2), (3, 2, 11, 5), (4, 3, 6, 2)])
+def test_more_ranks_than_planes_rows_views(world, H, W, P, tmp_path):
+    """Ranks with no planes contribute the identity partial, ranks with no rows an empty
+    band, ranks with no views an empty shard: the job completes and rank 0's frames match
+    the sequential render (1e-5 plane-sharded; views bit-exact up to the view order)."""
+    sys.path.insert(0, REPO)
+    from oracle import oracle
+    out = str(tmp_path / "frame.npy")
+    mp.spawn(_empty_shard_worker, args=(world, _free_port(), H, W, P, out), nprocs=world, join=True)
+    mpi, homs = _case(H, W, P)
+    want = oracle.render(mpi, homs)
+    np.testing.assert_allclose(np.load(out), want, rtol=0, atol=1e-5)
+    np.testing.assert_array_equal(np.load(out + ".views.npy"), want)
+
+
 def test_shard_ranges_cover_exactly():
     sys.path.insert(0, REPO)
     from mpi_vision_amd import parallel
@@ -94,7 +140,7 @@ def test_ct_partials_single_process_reassociation():
             assert np.array_equal(oracle.combine_ct(parts), want)
 
 
-def _plane_worker_gpu(rank, world, port, out_path):
+def _plane_worker_gpu(rank, world, port, out_path, shape=(37, 53, 11)):
     """One rank of the plane-sharded render with the HIP kernels (every rank on cuda:0,
     gloo collectives staged through host memory): packed local planes -> (C, T) partial
     (mpiv_render_packed_ct) -> band all-to-all -> ordered combine (mpiv_combine_ct) ->
@@ -104,10 +150,13 @@ def _plane_worker_gpu(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from mpi_vision_amd import _lib, parallel
     dev = torch.device("cuda:0")
-    mpi, homs = _case()
+    mpi, homs = _case(*shape)
     V, H, W, P, _ = mpi.shape
     p0, p1 = parallel.shard_range(P, rank, world)
-    packed = _lib.pack_planes(torch.from_numpy(np.ascontiguousarray(mpi[0, :, :, p0:p1])).to(dev))
+    if p1 > p0:
+        packed = _lib.pack_planes(torch.from_numpy(np.ascontiguousarray(mpi[0, :, :, p0:p1])).to(dev))
+    else:  # more ranks than planes: this rank owns none
+        packed = torch.zeros(_lib.packed_shape(H, W, 0), device=dev)
     homs_local = torch.from_numpy(np.ascontiguousarray(homs[:, p0:p1])).to(dev)
     frame = parallel.render_plane_sharded(packed, homs_local, H)
     if rank == 0:
@@ -116,17 +165,17 @@ def _plane_worker_gpu(rank, world, port, out_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_plane_sharded_hip_ranks_match_sequential(world, tmp_path):
+@pytest.mark.parametrize("world,shape", [(2, (37, 53, 11)), (3, (37, 53, 11)), (3, (2, 11, 5)), (4, (3, 6, 2))])
+def test_plane_sharded_hip_ranks_match_sequential(world, shape, tmp_path):
     """The whole plane-sharded path on the GPU kernels, world 2 and 3 (ranks share one
-    device; the driver's 8-GPU node runs the same code over RCCL): within 1e-5 of the
-    sequential oracle render."""
+    device; the driver's 8-GPU node runs the same code over RCCL), incl. more ranks than
+    planes / rows: within 1e-5 of the sequential oracle render."""
     sys.path.insert(0, REPO)
     from oracle import oracle
     out = str(tmp_path / "frame.npy")
-    mp.spawn(_plane_worker_gpu, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_plane_worker_gpu, args=(world, _free_port(), out, shape), nprocs=world, join=True)
     got = np.load(out)
-    mpi, homs = _case()
+    mpi, homs = _case(*shape)
     want = oracle.render(mpi, homs)
     np.testing.assert_allclose(got, want, rtol=0, atol=1e-5)
 

@@ -32,10 +32,10 @@ def test_render_matches_reference(name, small, meta, dev):
 
 @pytest.mark.parametrize("name", RENDER_CASES)
 @pytest.mark.parametrize("native_lds", ["0", "1"])
-def test_native_and_packed_kernels_agree_with_oracle(name, native_lds, small, meta, dev, monkeypatch):
+def test_native_and_packed_kernels_agree_with_oracle(name, native_lds, small, meta, dev, kopts):
     """Both texel layouts (the in-place one through its direct and its LDS-staged kernel),
     driven with the reference's own H bits."""
-    monkeypatch.setenv("MPIV_RENDER_NATIVE_LDS", native_lds)
+    kopts(render_native_lds=native_lds)
     mpi = render_case_inputs(meta["small"], name)
     B, H, W, P, _ = mpi.shape
     homs = torch.tensor(small[f"{name}_H"]).permute(1, 0, 2, 3).reshape(B, P, 9).contiguous()
@@ -225,37 +225,34 @@ def _multiview_case(V, seed=7):
 
 
 @pytest.mark.parametrize("shrink", ["0", "2"])
-def test_multiview_kernel_bit_exact(shrink, dev, monkeypatch):
-    """render_mv_kernel (MPIV_RENDER_MV=1, >= 4 views per launch): 11 views = a full group
-    of 8 + a partial one, bit-exact to the oracle and to the direct-gather kernel (the
-    default).  MPIV_BOX_SHRINK=2 stages every box 2 texels narrower per side than the
+def test_multiview_kernel_bit_exact(shrink, dev, kopts):
+    """render_mv_kernel (debug option render_mv=1, >= 4 views per launch): 11 views = a full
+    group of 8 + a partial one, bit-exact to the oracle and to the direct-gather kernel (the
+    default).  box_shrink=2 stages every box 2 texels narrower per side than the
     footprint, which forces the per-sample global fallback on most samples."""
-    monkeypatch.setenv("MPIV_BOX_SHRINK", shrink)
-    monkeypatch.setenv("MPIV_RENDER_MV", "1")
+    kopts(box_shrink=shrink, render_mv=1)
     mpi, homs = _multiview_case(11)
     V, P = homs.shape[0], homs.shape[1]
     H, W = mpi.shape[1], mpi.shape[2]
     want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.numpy())
     packed = _lib.pack_planes(mpi[0].to(dev))
     assert_bits(_lib.render_packed(packed, homs).cpu().numpy(), want, "multi-view")
-    monkeypatch.delenv("MPIV_RENDER_MV")
+    kopts(render_mv=0)
     assert_bits(_lib.render_packed(packed, homs).cpu().numpy(), want, "direct")
 
 
-def _variant_env(monkeypatch, mv):
-    """mv "0" / "1": direct / multi-view LDS kernel; "pair" / "pair1" / "dpp": the
-    pixel-pair (two / one planes in flight) and lane-neighbour tap-sharing kernels (A/B)."""
-    monkeypatch.setenv("MPIV_RENDER_MV", mv if mv in ("0", "1") else "0")
-    monkeypatch.setenv("MPIV_RENDER_PAIR", {"pair": "1", "pair1": "2"}.get(mv, "0"))
-    monkeypatch.setenv("MPIV_RENDER_DPP", "1" if mv == "dpp" else "0")
+def _variant_env(kopts, mv):
+    """mv "0" / "1": direct / multi-view LDS kernel; "pair" / "pair1": the pixel-pair
+    tap-sharing kernel with two / one planes in flight (A/B)."""
+    kopts(render_mv=1 if mv == "1" else 0, render_pair={"pair": 1, "pair1": 2}.get(mv, 0))
 
 
-@pytest.mark.parametrize("variant", ["pair", "pair1", "dpp"])
-def test_sharing_kernels_odd_width_and_extreme_poses(variant, dev, monkeypatch):
+@pytest.mark.parametrize("variant", ["pair", "pair1"])
+def test_sharing_kernels_odd_width_and_extreme_poses(variant, dev, kopts):
     """The tap-sharing kernels on an odd width (the last pair has no second pixel; a
     partial wave), a partial tile and strongly minifying / magnifying views (neighbours
     that do not share their taps): bit-exact vs the oracle."""
-    _variant_env(monkeypatch, variant)
+    _variant_env(kopts, variant)
     from mpi_vision_amd import _host
     H, W, P, V = 37, 203, 7, 3
     mpi = configs.synthetic_mpi(1, H, W, P, 12)
@@ -269,12 +266,12 @@ def test_sharing_kernels_odd_width_and_extreme_poses(variant, dev, monkeypatch):
     assert_bits(got.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("mv", ["0", "1", "pair", "pair1", "dpp"])
-def test_multiview_camera_path_many_views(mv, dev, monkeypatch):
+@pytest.mark.parametrize("mv", ["0", "1", "pair", "pair1"])
+def test_multiview_camera_path_many_views(mv, dev, kopts):
     """A config-4-style sway path (40 consecutive poses of the 1000-pose path, 24 planes,
     viewer camera) rendered in one launch by the direct and the multi-view kernel:
     bit-exact."""
-    _variant_env(monkeypatch, mv)
+    _variant_env(kopts, mv)
     from mpi_vision_amd import _host
     H, W, P, V = 96, 160, 24, 40
     mpi = configs.synthetic_mpi(1, H, W, P, 9)
@@ -287,11 +284,11 @@ def test_multiview_camera_path_many_views(mv, dev, monkeypatch):
     assert_bits(got.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("mv", ["0", "1", "pair", "pair1", "dpp"])
-def test_multiview_ct_partials(mv, dev, monkeypatch):
+@pytest.mark.parametrize("mv", ["0", "1", "pair", "pair1"])
+def test_multiview_ct_partials(mv, dev, kopts):
     """Plane-range (C, T) partials of 6 views (direct and multi-view kernel) equal the
     oracle's bit for bit, and their ordered combine equals the sequential render (1e-5)."""
-    _variant_env(monkeypatch, mv)
+    _variant_env(kopts, mv)
     mpi, homs = _multiview_case(6, seed=3)
     V, P = homs.shape[0], homs.shape[1]
     H, W = mpi.shape[1], mpi.shape[2]

@@ -82,17 +82,17 @@ def test_format_network_input(small, dev):
 
 
 @pytest.mark.parametrize("store", [None, "shrink", "tile", "0", "1", "2"])
-def test_plane_sweep_store_modes(store, small, meta, dev, monkeypatch):
+def test_plane_sweep_store_modes(store, small, meta, dev, kopts):
     """The LDS-staged sweep (default; "shrink" forces its per-sample global fallback),
     the tile kernel, and every output-store path of the grouped kernel (scalar, 16-B per
-    lane, LDS-staged dense run; MPIV_SWEEP_STORE selects it) give the reference bits,
+    lane, LDS-staged dense run; debug option sweep_store selects it) give the reference bits,
     incl. a partial last depth group (D = 6, 5)."""
     if store == "shrink":
-        monkeypatch.setenv("MPIV_BOX_SHRINK", "2")
+        kopts(box_shrink=2)
     elif store == "tile":
-        monkeypatch.setenv("MPIV_SWEEP_TILE", "1")
+        kopts(sweep_tile=1)
     elif store is not None:
-        monkeypatch.setenv("MPIV_SWEEP_STORE", store)
+        kopts(sweep_store=store)
     img = psv_case_input(meta["small"], "psv_a")
     out = mv.plane_sweep_torch(img.to(dev), list(small["psv_a_depths"]), _t(small, "psv_a_pose", dev),
                                _t(small, "psv_a_K", dev))
@@ -127,14 +127,14 @@ def test_plane_sweep_many_depths_vs_oracle(dev):
 
 @pytest.mark.parametrize("C", [1, 2, 3, 4])
 @pytest.mark.parametrize("shrink", ["0", "3"])
-def test_plane_sweep_lds_vs_oracle(C, shrink, dev, monkeypatch):
+def test_plane_sweep_lds_vs_oracle(C, shrink, dev, kopts):
     """The LDS-staged sweep with C = 1 and 4, a target size whose rows end in a partial
     64-pixel segment, separate source / target intrinsics and sizes (the _one2 geometry):
-    bit-exact to the oracle, also with every staged box shrunk (MPIV_BOX_SHRINK: most
+    bit-exact to the oracle, also with every staged box shrunk (box_shrink: most
     samples take the per-sample global fallback)."""
     from mpi_vision_amd import _host, _lib
     from oracle import oracle
-    monkeypatch.setenv("MPIV_BOX_SHRINK", shrink)
+    kopts(box_shrink=shrink)
     g = torch.Generator().manual_seed(31 + C)
     B, Hs, Ws, D, Ht, Wt = 2, 45, 97, 11, 38, 131
     img = torch.rand((B, Hs, Ws, C), generator=g)

@@ -87,11 +87,9 @@ def c2(dev, it, wu):
     packed = _lib.pack_planes(mpi[0])
     out = torch.empty((V, H, W, 3), device=dev)
     per_view = P * H * W * 16 + H * W * 12
-    for label, env in (("direct gathers (default)", {}), ("multi-view LDS kernel", {"MPIV_RENDER_MV": "1"})):
-        os.environ.update(env)
-        ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it, wu)
-        for k in env:
-            del os.environ[k]
+    for label, opts in (("direct gathers (default)", {}), ("multi-view LDS kernel", {"render_mv": 1})):
+        with _lib.debug(**opts):
+            ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it, wu)
         report(f"c2 1024x576x32, {V} views, packed, {label}", ms, mn, V * per_view, V * H * W / 1e6)
     ms, mn = timed(lambda: _lib.pack_planes(mpi[0]), it, wu)
     report("c2 pack (one-time per MPI)", ms, mn, 2 * P * H * W * 16)
@@ -125,13 +123,11 @@ def c3(dev, it, wu):
     ms, mn = timed(lambda: out.fill_(1.0), it, wu)
     report(f"c3 write-bandwidth reference: torch fill_ of the {S}x{H}x{W}x{D * 3} volume", ms, mn,
            S * D * H * W * 12)
-    for label, env in (("LDS-staged kernel (default)", {}), ("tile kernel", {"MPIV_SWEEP_TILE": "1"}),
-                       ("grouped kernel, store mode 1", {"MPIV_SWEEP_STORE": "1"}),
-                       ("grouped kernel, store mode 2", {"MPIV_SWEEP_STORE": "2"})):
-        os.environ.update(env)
-        ms, mn = timed(sweep, it, wu)
-        for k in env:
-            del os.environ[k]
+    for label, opts in (("LDS-staged kernel (default)", {}), ("tile kernel", {"sweep_tile": 1}),
+                        ("grouped kernel, store mode 1", {"sweep_store": 1}),
+                        ("grouped kernel, store mode 2", {"sweep_store": 2})):
+        with _lib.debug(**opts):
+            ms, mn = timed(sweep, it, wu)
         report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, {label}", ms, mn, alg,
                extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
     ms, mn = timed(lambda: (pad(), sweep()), it, wu)
@@ -150,11 +146,9 @@ def c4(dev, it, wu):
                                          configs.f32([c["K"]] * V), V).to(dev)
         out = torch.empty((V, H, W, 3), device=dev)
         n_it = it if V < 125 else max(3, it // 4)
-        for label, env in (("direct gathers (default)", {}), ("multi-view LDS kernel", {"MPIV_RENDER_MV": "1"})):
-            os.environ.update(env)
-            ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), n_it, 1)
-            for k in env:
-                del os.environ[k]
+        for label, opts in (("direct gathers (default)", {}), ("multi-view LDS kernel", {"render_mv": 1})):
+            with _lib.debug(**opts):
+                ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), n_it, 1)
             report(f"c4 1024^2x128 packed, {label}, {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
         ms, mn = timed(lambda: _lib._call("mpiv_render_packed_lds", packed, H, W, P, homs, V, out,
                                           _lib._stream(dev)), n_it, 1)

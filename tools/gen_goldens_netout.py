@@ -7,7 +7,8 @@ cell) and executed with `device = cpu`; nothing of it is copied into this reposi
 Test tooling only; writes tests/golden/netout.npz:
 
     <case>_pred [B,2P+3,H,W], <case>_ref [B,H,W,3], <case>_P, <case>_rgba [B,H,W,P,4],
-    <case>_drgba (random upstream gradient), <case>_dpred (autograd d rgba . drgba / d pred)
+    <case>_drgba (random upstream gradient), <case>_dpred (autograd d rgba . drgba / d pred),
+    <case>_dref (the same w.r.t. the reference image, run with ref_img requiring grad)
 
 Usage:  python tools/gen_goldens_netout.py
 """
@@ -53,9 +54,15 @@ def main():
         rgba = fn(pred, dep)
         drgba = torch.rand(rgba.shape, generator=g) * 2 - 1
         rgba.backward(drgba)
+        # the same with the reference image differentiable too: d ref (and d pred, unchanged)
+        ref2 = ref.clone().requires_grad_(True)
+        pred2 = pred.detach().clone().requires_grad_(True)
+        fn(pred2, {"mpi_planes": dep["mpi_planes"], "ref_img": ref2}).backward(drgba)
+        assert torch.equal(pred2.grad, pred.grad)
         out.update({f"{name}_pred": pred.detach().numpy(), f"{name}_ref": ref.numpy(),
                     f"{name}_P": np.array(P, np.int32), f"{name}_rgba": rgba.detach().numpy(),
-                    f"{name}_drgba": drgba.numpy(), f"{name}_dpred": pred.grad.numpy()})
+                    f"{name}_drgba": drgba.numpy(), f"{name}_dpred": pred.grad.numpy(),
+                    f"{name}_dref": ref2.grad.numpy()})
 
     case("na", 2, 24, 40, 6)
     case("nb", 1, 17, 29, 32)          # odd sizes, a Stereo-Mag plane count

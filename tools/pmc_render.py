@@ -4,8 +4,8 @@
     python tools/pmc_render.py --variant mv|direct|lds --views 8 --iters 3
 
 direct = the default direct-gather kernel, pair = pixel pairs sharing taps,
-mv = the multi-view LDS kernel
-(MPIV_RENDER_MV=1), lds = the single-view LDS variant.
+mv = the multi-view LDS kernel (debug option render_mv=1), lds = the single-view LDS
+variant.
 """
 import argparse
 import os
@@ -23,11 +23,9 @@ ap.add_argument("--views", type=int, default=8)
 ap.add_argument("--iters", type=int, default=3)
 a = ap.parse_args()
 if a.variant == "mv":
-    os.environ["MPIV_RENDER_MV"] = "1"
+    _lib.load().mpiv_debug_set(b"render_mv", 1)
 if a.variant == "pair":  # pixel pairs sharing taps (render_pair_kernel, A/B)
-    os.environ["MPIV_RENDER_PAIR"] = "1"
-if a.variant == "dpp":  # east taps from the neighbouring lane (render_dpp_kernel, A/B)
-    os.environ["MPIV_RENDER_DPP"] = "1"
+    _lib.load().mpiv_debug_set(b"render_pair", 1)
 dev = torch.device("cuda:0")
 c = configs.config4()
 H, W, P, V = c["H"], c["W"], c["P"], a.views

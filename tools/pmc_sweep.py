@@ -21,9 +21,9 @@ ap.add_argument("--store", default="lds")
 ap.add_argument("--iters", type=int, default=3)
 a = ap.parse_args()
 if a.store == "tile":
-    os.environ["MPIV_SWEEP_TILE"] = "1"
+    _lib.load().mpiv_debug_set(b"sweep_tile", 1)
 elif a.store != "lds":
-    os.environ["MPIV_SWEEP_STORE"] = a.store
+    _lib.load().mpiv_debug_set(b"sweep_store", int(a.store))
 dev = torch.device("cuda:0")
 c = configs.config3()
 S, H, W, D = c["S"], c["H"], c["W"], c["D"]
