@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Headline benchmark: rendered Mpix/s of the fused MPI warp + over-composite on
 BASELINE.json config 4 (128-plane 1024x1024 MPI, 1000-pose camera path,
-view-sharded), plus the dominant kernel's HBM roofline fraction and the CPU
-restatement timed on the same host.
+view-sharded), with the dominant kernel's roofline and the CPU restatement timed on
+the same host, plus a config-5 leg (256-plane 4096x2160 MPI, plane-sharded).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--views V]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--views V] [--no-config5]
 
 One process per GPU (torchrun for N > 1).  Each rank holds a full MPI replica in
 HBM (packed plane-major once, outside the timed region) and every step renders
@@ -15,10 +15,22 @@ is exactly the 1000-pose path.  There is no collective on the data path.
 Per step (inside the timed region): host-side homographies for the NEXT step
 (torch-CPU fp32, the reference's op order) overlap the current launch; then one
 render launch writes V frames [V,1024,1024,3] fp32 that stay in HBM.
+
+Roofline.  The V views of one launch share one MPI, so the texels
+they gather come from L2 (hit rate ~0.99): what bounds the kernel is the vector-memory
+("texture") path that serves the gathers, not HBM.  `roofline` therefore prices the
+launch against that path: algorithmic bytes = V*P*H*W*64 (four 16-B taps per
+plane-sample), peak = the gather rate the same device reaches with the render's access
+shape (mpiv_probe_gather, measured live).  HBM is reported separately, with fractions
+that cannot exceed 1: `hbm_traffic_frac` (PMC bytes actually moved per launch, from the
+committed rocprofv3 summary of this same command, only if its build id / kernel / shape
+match) and `single_view` (one view per launch: every texel is read once, so its
+algorithmic bytes P*H*W*16 + H*W*12 really cross HBM -- the north-star 0.60 bar).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -30,7 +42,7 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from mpi_vision_amd import _host, _lib, configs  # noqa: E402
+from mpi_vision_amd import _host, _lib, configs, parallel  # noqa: E402
 
 METRIC = "rendered Mpix/sec (node) + achieved HBM GB/s fraction, 1024²×128-plane MPI"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -43,6 +55,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--views", type=int, default=125, help="views rendered per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 plane-sharded leg")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="only the timed config-4 launches (rocprofv3 runs: tools/profile.sh), no frame check, "
+                         "single-view leg, gather probe or config-5 leg")
     ap.add_argument("--kernel", choices=["packed", "packed_mv", "packed_lds", "native"], default="packed",
                     help="packed: direct-gather kernel on the packed MPI (default); packed_mv: multi-view "
                          "LDS kernel (A/B); packed_lds: single-view LDS variant (A/B); native: reference "
@@ -83,18 +99,43 @@ def barrier(world):
         dist.barrier()
 
 
-def load_traffic(profile_dir: str, kernel: str, views: int):
-    """Per-launch HBM bytes of the render kernel from the committed rocprofv3 PMC
-    summary of this same bench command (tools/profile.sh), corrected as
-    MI355X_MICROARCH.md §HBM prescribes; None when no summary matches."""
+def load_pmc(profile_dir: str, kernel: str, views: int, shape):
+    """The committed rocprofv3 PMC summary of this bench command (tools/profile.sh ->
+    tools/parse_pmc.py -> profiles/render_pmc.json), or None unless it was taken from the
+    same library build (source hash), kernel, views per launch and MPI shape."""
     path = os.path.join(profile_dir, "render_pmc.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
-    if d.get("kernel") != kernel or d.get("views", views) != views:
+    want = {"build_id": _lib.load().mpiv_build_id().decode(), "kernel": kernel, "views": views,
+            "shape": list(shape)}
+    if any(d.get(k) != v for k, v in want.items()):
         return None
-    return d.get("hbm_bytes_per_launch")
+    return d
+
+
+def event_ms(fn, n, stream):
+    """Average device time of fn() over n calls, HIP events on the launch stream."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+
+def gather_peak_gbs(dev, stream):
+    """The texture path's gather ceiling on this device (mpiv_probe_gather: 16-B-per-lane
+    buffer loads with the render's access shape from an L1/L2-resident window)."""
+    window = torch.zeros(4096, device=dev)
+    sink = torch.zeros(4, device=dev)
+    blocks, iters = 2048, 2048
+    fn = lambda: _lib._call("mpiv_probe_gather", window, iters, blocks, sink, _lib._stream(dev))  # noqa: E731
+    fn()
+    ms = event_ms(fn, 5, stream)
+    return blocks * 256 * iters * 128 / (ms * 1e-3) / 1e9
 
 
 def cpu_baseline(mpi_dev: torch.Tensor, homs_all: torch.Tensor, budget_s: float, check_frames):
@@ -122,6 +163,67 @@ def cpu_baseline(mpi_dev: torch.Tensor, homs_all: torch.Tensor, budget_s: float,
             "gpu_frames_bit_exact_vs_cpu": mism == 0}
 
 
+def sha16(t: torch.Tensor) -> str:
+    return hashlib.sha256(t.detach().cpu().contiguous().numpy().tobytes()).hexdigest()[:16]
+
+
+def config5_leg(world, rank, dev, steps, warmup):
+    """BASELINE config 5: the 256-plane 4096x2160 MPI (36.2 GB), one pose, planes sharded
+    over the ranks.  Each rank generates its plane range on the device (counter-based
+    synth.hip, outside the timed region).  Step at N = 1: one render of all 256 planes;
+    at N > 1: render_plane_sharded -- the rank's (C, T) partial, one all-to-all of row
+    bands (RCCL point-to-point over xGMI), the ordered combine of its band, and the gather
+    of the RGB bands to rank 0.  Total work is fixed ("strong" scaling)."""
+    c = configs.config5()
+    H, W, P = c["H"], c["W"], c["P"]
+    homs = _host.render_homographies(configs.f32(c["poses"]), configs.f32(c["depths"]), configs.f32([c["K"]]), 1)
+    p0, p1 = parallel.shard_range(P, rank, world)
+    hl = homs[:, p0:p1].contiguous().to(dev)
+    stream = torch.cuda.current_stream(dev)
+    packed = _lib.synth_mpi_packed(c["seed"], H, W, p0, p1, dev)
+    if world == 1:
+        out = torch.empty((1, H, W, 3), device=dev)
+        launch = lambda: _lib._call("mpiv_render_packed", packed, H, W, p1 - p0, hl, 1, out,  # noqa: E731
+                                    _lib._stream(dev))
+
+        def step():
+            launch()
+            return out
+        shard_bytes = P * H * W * 16 + H * W * 12
+    else:
+        ct = torch.empty((1, H, W, 4), device=dev)
+        launch = lambda: _lib._call("mpiv_render_packed_ct", packed, H, W, p1 - p0, 0, p1 - p0,  # noqa: E731
+                                    int(rank == 0), hl, 1, ct, _lib._stream(dev))
+        step = lambda: parallel.render_plane_sharded(packed, hl, H)  # noqa: E731
+        shard_bytes = (p1 - p0) * H * W * 16 + H * W * 16
+    kern_ms = event_ms(launch, 3, stream)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        frame = step()
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    kern_ms = max_over_ranks(kern_ms, world, dev)
+    res = {"workload": "BASELINE config 5: 256-plane 4096x2160 MPI (36.2 GB), 1 pose, plane-sharded",
+           "value": round(steps * H * W / 1e6 / elapsed, 2), "unit": "Mpix/s", "n_gpus": world,
+           "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "scaling": "strong",
+           "data": "synthetic (counter-based per-shard generator, synth.hip, seed 0)",
+           "planes_per_gpu": p1 - p0, "shard_kernel_ms": round(kern_ms, 3),
+           "shard_alg_bytes": shard_bytes,
+           "shard_hbm_frac": round(shard_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "parallelism": "single GPU, sequential render" if world == 1 else
+           f"plane-sharded x{world}: (C,T) partials + band all-to-all + ordered combine + gather",
+           "frame_sha16": sha16(frame) if rank == 0 else None}
+    del packed
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     args = parse()
     if args.kernel == "packed_mv":
@@ -133,11 +235,15 @@ def main():
     V = args.views
     n_path = len(c4["poses"])
 
+    def make_view():
+        gen = torch.Generator(device=dev).manual_seed(c4["seed"])
+        v = torch.rand((H, W, P, 4), generator=gen, device=dev, dtype=torch.float32)
+        v[..., :3].mul_(2.0).sub_(1.0)
+        v[:, :, 0, 3] = 1.0
+        return v
+
     # --- resident inputs: one MPI replica per GPU (generated on device), packed once
-    gen = torch.Generator(device=dev).manual_seed(c4["seed"])
-    view = torch.rand((H, W, P, 4), generator=gen, device=dev, dtype=torch.float32)
-    view[..., :3].mul_(2.0).sub_(1.0)
-    view[:, :, 0, 3] = 1.0
+    view = make_view()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     packed = _lib.pack_planes(view) if args.kernel.startswith("packed") else None
@@ -146,7 +252,6 @@ def main():
     entry = "mpiv_render_packed_lds" if args.kernel == "packed_lds" else "mpiv_render_packed"
     torch.cuda.synchronize()
     pack_ms = (time.perf_counter() - t0) * 1e3
-    mpi5 = view.unsqueeze(0).expand(V, H, W, P, 4)
 
     poses = configs.f32(c4["poses"])
     K = configs.f32(c4["K"])
@@ -156,22 +261,21 @@ def main():
         base = (rank * V + s * world * V) % n_path
         return [(base + j) % n_path for j in range(V)]
 
-    def host_homs(s):
-        idx = step_indices(s)
-        return _host.render_homographies(poses[idx], depths, K.expand(V, 3, 3), V)
+    def host_homs(s, n=V):
+        idx = step_indices(s)[:n]
+        return _host.render_homographies(poses[idx], depths, K.expand(n, 3, 3), n)
 
     out = torch.empty((V, H, W, 3), device=dev, dtype=torch.float32)
     hbuf = [torch.empty((V, P, 9), dtype=torch.float32).pin_memory() for _ in range(2)]
     dbuf = [torch.empty((V, P, 9), device=dev, dtype=torch.float32) for _ in range(2)]
     stream = torch.cuda.current_stream(dev)
 
-    def launch(s, h_dev):
-        if args.kernel.startswith("packed"):
-            _lib._call(entry, packed, H, W, P, h_dev, V, out,
-                       _lib._stream(dev))
+    def launch(h_dev, n, o):
+        if packed is not None:
+            _lib._call(entry, packed, H, W, P, h_dev, n, o, _lib._stream(dev))
         else:
-            _lib._call("mpiv_render", mpi5, _lib._strides(mpi5), V, H, W, P, h_dev,
-                       out, _lib._stream(dev))
+            mpi5 = view.unsqueeze(0).expand(n, H, W, P, 4)
+            _lib._call("mpiv_render", mpi5, _lib._strides(mpi5), n, H, W, P, h_dev, o, _lib._stream(dev))
 
     copied = [None, None]  # event recorded after the last H2D copy out of each pinned slot
 
@@ -190,7 +294,7 @@ def main():
         for s in range(first, first + n_steps):
             if events is not None:
                 events[s - first][0].record(stream)
-            launch(s, dbuf[s % 2])
+            launch(dbuf[s % 2], V, out)
             if events is not None:
                 events[s - first][1].record(stream)
             if s + 1 < first + n_steps:
@@ -210,11 +314,35 @@ def main():
     elapsed = max_over_ranks(elapsed, world, dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
 
+    # --- after the timed region: the last timed launch's first frame against a one-view
+    # launch of the same pose (bit-exact), the single-view leg, the gather ceiling
+    last = args.warmup + args.steps - 1
+    one = torch.empty((1, H, W, 3), device=dev)
+    timed_frame_sha = one_sha = None
+    sv_ms, peak_gbs = float("nan"), float("nan")
+    if not args.no_extras:
+        timed_frame_sha = sha16(out[0])
+        h1 = host_homs(last, 1).to(dev)
+        launch(h1, 1, one)
+        torch.cuda.synchronize()
+        one_sha = sha16(one[0])
+        sv_ms = event_ms(lambda: launch(h1, 1, one), 20, stream)
+        peak_gbs = gather_peak_gbs(dev, stream)
+
     mpix_total = world * args.steps * V * H * W / 1e6
     value = mpix_total / elapsed
-    alg_bytes = V * (P * H * W * 16 + H * W * 12)
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(os.path.join(REPO, "profiles"), kernel_name, V)
+    tap_bytes = V * P * H * W * 64            # four 16-B taps per plane-sample
+    hbm_alg_bytes = V * (P * H * W * 16 + H * W * 12)  # every view reading its MPI once (§8d)
+    sv_bytes = P * H * W * 16 + H * W * 12
+    achieved = tap_bytes / (kern_ms * 1e-3) / 1e9
+    pmc = load_pmc(os.path.join(REPO, "profiles"), kernel_name, V, (H, W, P))
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+
+    del out
+    if packed is not None:
+        del view
+    torch.cuda.empty_cache()
+    c5 = None if (args.no_config5 or args.no_extras) else config5_leg(world, rank, dev, max(3, args.steps // 2), 1)
 
     if rank == 0:
         res = {
@@ -226,28 +354,37 @@ def main():
                        "H": H, "W": W, "planes": P, "views_per_gpu_per_step": V, "kernel": args.kernel,
                        "parallelism": f"view-sharded x{world} (replicas, no data-path collective)",
                        "views_per_s": round(value / (H * W / 1e6), 2), "pack_ms_once": round(pack_ms, 2)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": kernel_name,
-                         "kernel_ms_per_launch": round(kern_ms, 3),
-                         "alg_bytes_per_launch": alg_bytes,
-                         "note": "achieved = algorithmic bytes (P*H*W*16 + H*W*12 per view) / kernel time; "
-                                 "frac > 1 because the views of one launch re-read the same MPI texels from L2 "
-                                 "(traffic = HBM bytes actually moved, PMC); the kernel is bound by its texture "
-                                 "path and VALU issue, not HBM (DESIGN.md section 4)"},
+            "roofline": {
+                "bound": "texture", "achieved": round(achieved, 1),
+                "peak": round(peak_gbs, 1) if peak_gbs == peak_gbs else None, "unit": "GB/s",
+                "frac": round(achieved / peak_gbs, 4) if peak_gbs == peak_gbs else None, "traffic": traffic,
+                "kernel": kernel_name, "kernel_ms_per_launch": round(kern_ms, 3),
+                "alg_bytes_per_launch": tap_bytes,
+                "alg_bytes_def": "V*P*H*W*64: four 16-B bilinear taps per plane-sample through the vector-memory path",
+                "peak_def": "mpiv_probe_gather on this device: 16-B/lane buffer loads, render access shape, "
+                            "L1/L2-resident window (MI355X_MICROARCH.md L2: 34.5-36.9 TB/s)",
+                "ta_busy_frac": pmc.get("ta_busy_frac") if pmc else None,
+                "l2_hit_rate": pmc.get("l2_hit_rate") if pmc else None,
+                "hbm_traffic_frac": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                "mpi_reuse_per_launch": round(hbm_alg_bytes / traffic, 1) if traffic else None,
+                "single_view": None if args.no_extras else {
+                    "kernel_ms": round(sv_ms, 4), "alg_bytes": sv_bytes,
+                    "achieved_gbs": round(sv_bytes / (sv_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                    "frac": round(sv_bytes / (sv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bound": "hbm"},
+                "pmc_source": "profiles/render_pmc.json (same build id / kernel / views / shape)" if pmc else
+                              "no matching profiles/render_pmc.json for this build",
+            },
+            "timed_frame_check": {"frame": "view 0 of the last timed launch vs a 1-view launch of its pose",
+                                  "sha16": timed_frame_sha, "bit_exact": timed_frame_sha == one_sha},
             "cpu_baseline": None,
+            "config5_plane_sharded": c5,
         }
-        if world == 1 and args.cpu_seconds > 0:
-            # the GPU frames of the first views of step 0, to cross-check the CPU sample bit-exactly
+        if world == 1 and args.cpu_seconds > 0 and not args.no_extras:
+            # the GPU frame of the first view of step 0, to cross-check the CPU sample bit-exactly
             hs = host_homs(0)
-            _lib._call(entry if packed is not None else "mpiv_render",
-                       *([packed, H, W, P, hs[:1].to(dev), 1, out, _lib._stream(dev)]
-                         if packed is not None else
-                         [mpi5[:1], _lib._strides(mpi5[:1]), 1, H, W, P, hs[:1].to(dev),
-                          out, _lib._stream(dev)]))
+            launch(hs[:1].to(dev), 1, one)
             torch.cuda.synchronize()
-            frames = [out[:1].cpu().numpy()]
-            res["cpu_baseline"] = cpu_baseline(view, hs, args.cpu_seconds, frames)
+            res["cpu_baseline"] = cpu_baseline(make_view(), hs, args.cpu_seconds, [one.cpu().numpy()])
         print(json.dumps(res), flush=True)
     if world > 1:
         import torch.distributed as dist

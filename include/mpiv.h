@@ -227,7 +227,24 @@ int mpiv_preprocess(const float *in, int64_t n, float *out, void *stream);
  * CPU cast semantics (truncate to int32, keep the low byte; NaN / out of int32 -> 0) */
 int mpiv_deprocess_u8(const float *in, int64_t n, uint8_t *out, void *stream);
 
+/* ---- synthetic workloads ------------------------------------------------------ */
+
+/* Counter-based synthetic MPI (BASELINE config 5 is 36.2 GB: each GPU generates its
+ * plane shard in HBM).  Writes planes [p_begin, p_end) of the MPI defined by `seed`
+ * in the packed layout of mpiv_pack_planes: packed [p_end-p_begin][H+4][W+4][4] with
+ * the zero border.  Texel (p, y, x, c) depends only on (seed, p, y*W+x, c) -- plane
+ * indices are global, so shards generated separately equal the same planes of the
+ * whole MPI bit for bit: rgb U[-1,1), alpha U[0,1), plane 0 alpha 1 (synth.hip). */
+int mpiv_synth_mpi_packed(uint32_t seed, int H, int W, int p_begin, int p_end, float *packed, void *stream);
+
 /* ---- diagnostics ------------------------------------------------------------ */
+
+/* Gather-rate probe (bench.py's texture-path roofline): `blocks` x 256 work-items each
+ * issue iters x 8 16-B buffer loads (1 KiB per wave instruction, the render's tap shape)
+ * from a 16 KiB L1/L2-resident window (>= 16 KiB of zeros, device, 16-B aligned);
+ * bytes moved = blocks * 256 * iters * 128.  `sink` (>= 4 floats) is never written for a
+ * zero window. */
+int mpiv_probe_gather(const float *window, int iters, int blocks, float *sink, void *stream);
 
 /* Exhaustive self-check of the render's launch-constant division (x / (H-1),
  * x / (W-1) via a precomputed reciprocal + two residual corrections) against IEEE

@@ -43,6 +43,7 @@ _SIGS = {
     "mpiv_cam2pixel": [_vp, _vp, _int, _i64, _vp, _vp],
     "mpiv_plane_coords": [_vp, _int, _i64, _vp, _int, _int, _vp, _vp],
     "mpiv_selftest_div_const": [_int, _vp, _vp],
+    "mpiv_probe_gather": [_vp, _int, _int, _vp, _vp],
     "mpiv_pad_texels": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_plane_sweep_padded": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
     "mpiv_preprocess": [_vp, _i64, _vp, _vp],
@@ -52,6 +53,7 @@ _SIGS = {
                                      _vp],
     "mpiv_assemble_mpi": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_assemble_mpi_packed": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
+    "mpiv_synth_mpi_packed": [ctypes.c_uint32, _int, _int, _int, _int, _vp, _vp],
     "mpiv_assemble_mpi_backward": [_vp, _c_i64p, _vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp,
                                    _vp],
 }
@@ -213,6 +215,19 @@ def pack_planes(view: torch.Tensor, out: torch.Tensor | None = None) -> torch.Te
     packed = torch.empty(packed_shape(H, W, P), device=dev, dtype=torch.float32) if out is None else \
         _check_out(out, packed_shape(H, W, P), dev, "pack_planes")
     _call("mpiv_pack_planes", view, _strides(view), H, W, P, packed, _stream(dev))
+    return packed
+
+
+def synth_mpi_packed(seed: int, H: int, W: int, p_begin: int, p_end: int, device,
+                     out: torch.Tensor | None = None) -> torch.Tensor:
+    """Planes [p_begin, p_end) of the counter-based synthetic MPI `seed` (synth.hip),
+    generated on `device` straight into the packed layout [p_end-p_begin, H+4, W+4, 4]."""
+    dev = torch.device(device)
+    shape = packed_shape(H, W, p_end - p_begin)
+    packed = torch.empty(shape, device=dev, dtype=torch.float32) if out is None else \
+        _check_out(out, shape, dev, "synth_mpi_packed")
+    _dev(packed)
+    _call("mpiv_synth_mpi_packed", ctypes.c_uint32(seed & 0xFFFFFFFF), H, W, p_begin, p_end, packed, _stream(dev))
     return packed
 
 
@@ -407,7 +422,8 @@ class AssembleFunction(torch.autograd.Function):
         mpi_pred, fg = ctx.saved_tensors
         if not (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]):
             return None, None, None
-        dpred, dfg = assemble_mpi_backward(drgba, mpi_pred, fg, ctx.P, want_dfg=ctx.needs_input_grad[1])
+        res = assemble_mpi_backward(drgba, mpi_pred, fg, ctx.P, want_dfg=ctx.needs_input_grad[1])
+        dpred, dfg = res if ctx.needs_input_grad[1] else (res, None)
         return (dpred if ctx.needs_input_grad[0] else None), dfg, None
 
 

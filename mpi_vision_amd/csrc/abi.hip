@@ -16,6 +16,7 @@
 #include "sweep.hip"
 #include "geometry.hip"
 #include "assemble.hip"
+#include "synth.hip"
 
 namespace {
 
@@ -608,6 +609,28 @@ int mpiv_assemble_mpi_backward(const float* drgba, const int64_t gs[5], const fl
         assemble_backward_kernel<<<dim3(blocks((int64_t)H * W, 256), B), 256, 0, S(stream)>>>(
             drgba, g, pred, fg, s, H, W, P, make_fastdiv((unsigned)W), dpred, dfg);
     return launched("mpiv_assemble_mpi_backward");
+}
+
+int mpiv_synth_mpi_packed(uint32_t seed, int H, int W, int p_begin, int p_end, float* packed, void* stream) {
+    const char* nm = "mpiv_synth_mpi_packed";
+    if (!packed) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (H <= 0 || W <= 0 || p_begin < 0 || p_end <= p_begin) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    if (!aligned16(packed)) return fail(MPIV_ERR_ARG, "%s: packed must be 16-byte aligned", nm);
+    if ((int64_t)(H + 2 * kPad) * (W + 2 * kPad) * 16 >= (int64_t)kOOB || (int64_t)H * W >= (1ll << 31) ||
+        p_end - p_begin > kMaxGridYZ)
+        return fail(MPIV_ERR_ARG, "%s: padded plane larger than 2 GiB or too many planes", nm);
+    const int64_t npix = (int64_t)(H + 2 * kPad) * (W + 2 * kPad);
+    synth_packed_kernel<<<dim3(blocks(npix, 256), p_end - p_begin), 256, 0, S(stream)>>>(
+        seed, H, W, p_begin, make_fastdiv((unsigned)(W + 2 * kPad)), reinterpret_cast<float4*>(packed), npix);
+    return launched(nm);
+}
+
+int mpiv_probe_gather(const float* window, int iters, int blocks_, float* sink, void* stream) {
+    if (!window || !sink) return fail(MPIV_ERR_ARG, "mpiv_probe_gather: null pointer");
+    if (iters <= 0 || blocks_ <= 0) return fail(MPIV_ERR_ARG, "mpiv_probe_gather: bad size");
+    if (!aligned16(window)) return fail(MPIV_ERR_ARG, "mpiv_probe_gather: window must be 16-byte aligned");
+    probe_gather_kernel<<<blocks_, 256, 0, S(stream)>>>(reinterpret_cast<const float4*>(window), iters, sink);
+    return launched("mpiv_probe_gather");
 }
 
 int mpiv_selftest_div_const(int divisor, unsigned long long* mismatches, void* stream) {

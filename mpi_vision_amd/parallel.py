@@ -59,9 +59,12 @@ def exchange_bands(ct: torch.Tensor, group=None) -> torch.Tensor:
     V, H, W, C = ct.shape
     bands = band_bounds(H, G)
     bh = max(e - b for b, e in bands)
-    send = ct.new_zeros((G, V, bh, W, C))
-    for k, (b, e) in enumerate(bands):
-        send[k, :, : e - b] = ct[:, b:e]
+    if V == 1 and H % G == 0 and ct.is_contiguous():
+        send = ct.view(G, 1, bh, W, C)  # the bands are already consecutive row ranges: no copy
+    else:
+        send = ct.new_zeros((G, V, bh, W, C))
+        for k, (b, e) in enumerate(bands):
+            send[k, :, : e - b] = ct[:, b:e]
     if _staged(send, group):
         send_h = send.cpu()
         recv_h = torch.empty_like(send_h)
@@ -80,8 +83,11 @@ def gather_frames(band: torch.Tensor, height: int, group=None, dst: int = 0) -> 
     bands = band_bounds(height, G)
     bh = max(e - b for b, e in bands)
     V, h, W, C = band.shape
-    padded = band.new_zeros((V, bh, W, C))
-    padded[:, :h] = band
+    if h == bh and band.is_contiguous():
+        padded = band
+    else:
+        padded = band.new_zeros((V, bh, W, C))
+        padded[:, :h] = band
     dev = padded.device
     if _staged(padded, group):
         padded = padded.cpu()

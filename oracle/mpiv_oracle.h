@@ -27,6 +27,12 @@ void oracle_render_backward(const float *mpi, const int64_t st[5], int B, int H,
                             const float *homs, const float *dout, float *dmpi, int vec, int nthreads);
 /* layers [P][n][4] contiguous; out [n][3] */
 void oracle_over_composite(const float *layers, int P, int64_t n, float *out);
+/* counter-based synthetic MPI (synth.hip restated): planes [p0,p1) as [H][W][p1-p0][4] */
+void oracle_synth_mpi(uint32_t seed, int H, int W, int p0, int p1, float *out);
+/* rows [y0,y1) of one view of the synthetic MPI through planes [p0,p1), homs [P][9]:
+ * ct = 0 -> final render [y1-y0][W][3]; ct = 1 -> (C,T) partial [y1-y0][W][4] */
+void oracle_render_synth(uint32_t seed, int H, int W, int P, int p0, int p1, int back, int ct,
+                         const float *homs, int y0, int y1, float *out, int nthreads);
 #ifdef __cplusplus
 }
 #endif

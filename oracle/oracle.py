@@ -39,6 +39,9 @@ def lib():
         L.oracle_over_composite.argtypes = [_f, ctypes.c_int, ctypes.c_int64, _f]
         L.oracle_render_backward.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, _f, _f, ctypes.c_int,
                                                                              ctypes.c_int]
+        L.oracle_synth_mpi.argtypes = [ctypes.c_uint32] + [ctypes.c_int] * 4 + [_f]
+        L.oracle_render_synth.argtypes = [ctypes.c_uint32] + [ctypes.c_int] * 7 + [_f, ctypes.c_int, ctypes.c_int,
+                                                                                  _f, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -103,6 +106,28 @@ def combine_ct(parts: np.ndarray) -> np.ndarray:
         acc[..., :3] = np.float32(acc[..., 3:4] * b[..., :3] + acc[..., :3])
         acc[..., 3] = acc[..., 3] * b[..., 3]
     return acc[..., :3]
+
+
+def synth_mpi(seed: int, H: int, W: int, p0: int, p1: int) -> np.ndarray:
+    """Planes [p0, p1) of the counter-based synthetic MPI (mpi_vision_amd synth.hip,
+    restated) as [H, W, p1-p0, 4] float32."""
+    out = np.empty((H, W, p1 - p0, 4), np.float32)
+    lib().oracle_synth_mpi(seed & 0xFFFFFFFF, H, W, p0, p1, _fp(out))
+    return out
+
+
+def render_synth(seed: int, H: int, W: int, homs: np.ndarray, y0: int, y1: int, p0: int = 0, p1=None,
+                 back: bool = True, ct: bool = False, nthreads: int = 0) -> np.ndarray:
+    """Rows [y0, y1) of one view of the synthetic MPI rendered procedurally (no MPI in
+    memory): homs [P, 9] (one view); ct=False -> final colour [y1-y0, W, 3] (p0 = 0),
+    ct=True -> the (C, T) partial [y1-y0, W, 4] of planes [p0, p1)."""
+    homs = np.ascontiguousarray(homs, np.float32).reshape(-1, 9)
+    P = homs.shape[0]
+    p1 = P if p1 is None else p1
+    out = np.empty((y1 - y0, W, 4 if ct else 3), np.float32)
+    lib().oracle_render_synth(seed & 0xFFFFFFFF, H, W, P, p0, p1, int(back), int(ct), _fp(homs), y0, y1, _fp(out),
+                              _threads(nthreads))
+    return out
 
 
 def plane_sweep(img: np.ndarray, ki: np.ndarray, proj: np.ndarray, depths, tgt_h: int, tgt_w: int,

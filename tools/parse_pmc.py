@@ -7,6 +7,10 @@ bytes of wide (16 B/lane) coalesced reads, so the read side is doubled:
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
 The uncorrected figure is kept beside it.  FETCH_SIZE also counts Infinity-Cache
 (MALL) hits, so it is an upper bound on DRAM reads.
+
+The summary records the library build id (sha of the sources, mpiv_build_id), the
+kernel, views per launch and MPI shape; bench.py uses it only when all of them match
+the build it runs (load_pmc).  Run it in the tree whose sources were profiled.
 """
 import csv
 import glob
@@ -44,7 +48,11 @@ def main():
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(repo, "profiles")
     os.makedirs(prof, exist_ok=True)
-    res = {"kernel": KERNEL, "tag": tag, "views": views}
+    sys.path.insert(0, repo)
+    from mpi_vision_amd import _lib
+    res = {"kernel": KERNEL, "tag": tag, "views": views, "shape": [1024, 1024, 128],
+           "build_id": _lib.source_hash(),
+           "command": "python bench.py --steps 2 --warmup 1 --no-extras (tools/profile.sh)"}
     stats = glob.glob(os.path.join(out_dir, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
@@ -71,6 +79,11 @@ def main():
         cycles = sum(gui) / len(gui) / 8
         res["valu_insts_per_launch"] = sum(valu) / len(valu)
         res["valu_issue_frac"] = res["valu_insts_per_launch"] / (512 * cycles)
+    trows = rows(os.path.join(out_dir, "TA", "**", "*counter_collection.csv"))
+    ta, tgui = per_dispatch(trows, "TA_BUSY_avr"), per_dispatch(trows, "GRBM_GUI_ACTIVE")
+    if ta and tgui:
+        # TA_BUSY_avr: busy cycles averaged over the TA instances; GRBM_GUI_ACTIVE sums 8 XCDs
+        res["ta_busy_frac"] = (sum(ta) / len(ta)) / (sum(tgui) / len(tgui) / 8)
     for name in (f"{tag}_render_pmc.json", "render_pmc.json"):
         with open(os.path.join(prof, name), "w") as fh:
             json.dump(res, fh, indent=1)
