@@ -92,6 +92,14 @@ int mpiv_render_packed_ct(const float *packed, int H, int W, int P, int p_begin,
  * -> out [n][3].  (Cf,Tf) o (Cb,Tb) = (Cf + Tf*Cb, Tf*Tb). */
 int mpiv_combine_ct(const float *parts, int G, int64_t n, float *out, void *stream);
 
+/* HOST function (no device memory): the per-(view, plane) target->source homographies
+ * of mpi_render_view_torch (utils.py:278-285 -> 255-262 -> 225-229 -> inv_homography_torch
+ * 44-67), bit-identical to the reference's torch-CPU fp32 chain.
+ * pose [B][4][4], depths [P] (plane depths, far->near), K and Kinv = inverse(K) [B][3][3]
+ * (host, row-major) -> H [B][P][9]. */
+int mpiv_render_homographies(const float *pose, const float *depths, const float *K, const float *Kinv, int B,
+                             int P, float *H);
+
 /* ---- render backward ------------------------------------------------------ */
 
 /* Workspace bytes mpiv_render_backward needs for one H x W x P MPI (reused across

@@ -39,10 +39,52 @@ def inv_homography(k_s, k_t, rot, t, n_hat, a):
     return torch.matmul(torch.matmul(k_s, rot_t + divide_safe(numerator, denom)), k_t_inv)
 
 
+_KINV_CACHE: dict = {}
+
+
+def _inverse_cached(K: torch.Tensor) -> torch.Tensor:
+    """torch.inverse(K) for contiguous fp32 CPU K [B,3,3], memoised on K's exact bits
+    (intrinsics rarely change along a camera path; LAPACK is ~10 us of the host path).
+    Every batch element is inverted on its own, so the result equals the reference's
+    inverse of its [P,B,3,3] repeat element for element (tests/test_host.py)."""
+    key = K.numpy().tobytes()
+    kinv = _KINV_CACHE.get(key)
+    if kinv is None:
+        if len(_KINV_CACHE) >= 256:
+            _KINV_CACHE.clear()
+        kinv = torch.inverse(K).contiguous()
+        _KINV_CACHE[key] = kinv
+    return kinv
+
+
 def render_homographies(pose: torch.Tensor, depths: torch.Tensor, intrinsics: torch.Tensor,
-                        batch: int) -> torch.Tensor:
+                        batch: int, pin: bool = False) -> torch.Tensor:
     """Per-(view, plane) target->source homographies for mpi_render_view_torch
-    (utils.py:278-285 -> 255-262 -> 225-229 -> 44-67), as a [B, P, 9] fp32 CPU tensor.
+    (utils.py:278-285 -> 255-262 -> 225-229 -> 44-67), as a [B, P, 9] fp32 CPU tensor
+    (page-locked with pin=True, ready for an asynchronous upload).
+
+    The chain runs in libmpiv's host code (mpiv_render_homographies): torch's CPU matmul
+    of these tiny matrices is plain products summed in ascending k, which the library
+    restates exactly; only K^-1 comes from torch.inverse (LAPACK), as in the reference.
+    ~35 tiny torch ops (~0.2 ms of dispatch) become one call.  render_homographies_torch
+    keeps the op-by-op form (tests compare the two bit for bit)."""
+    from . import _lib
+    pose = _cpu32(pose).contiguous()
+    K = _cpu32(intrinsics).expand(batch, 3, 3).contiguous()
+    d = _cpu32(depths).reshape(-1).contiguous()
+    P = d.shape[0]
+    kinv = _inverse_cached(K)
+    H = torch.empty((batch, P, 9), dtype=_F32, pin_memory=pin)
+    rc = _lib.load().mpiv_render_homographies(pose.data_ptr(), d.data_ptr(), K.data_ptr(), kinv.data_ptr(),
+                                              batch, P, H.data_ptr())
+    if rc != 0:
+        raise RuntimeError(f"mpiv_render_homographies failed ({rc}): {_lib.load().mpiv_last_error().decode()}")
+    return H
+
+
+def render_homographies_torch(pose: torch.Tensor, depths: torch.Tensor, intrinsics: torch.Tensor,
+                              batch: int) -> torch.Tensor:
+    """render_homographies with the reference's torch ops, op for op.
 
     The reference materialises every camera tensor as a contiguous [P, B, ...]
     repeat before the matmul chain (utils.py:225-228, 258).  That matters: on

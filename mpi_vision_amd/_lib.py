@@ -53,6 +53,7 @@ _SIGS = {
                                      _vp],
     "mpiv_assemble_mpi": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_assemble_mpi_packed": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
+    "mpiv_render_homographies": [_vp, _vp, _vp, _vp, _int, _int, _vp],
     "mpiv_synth_mpi_packed": [ctypes.c_uint32, _int, _int, _int, _int, _vp, _vp],
     "mpiv_assemble_mpi_backward": [_vp, _c_i64p, _vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp,
                                    _vp],
@@ -168,7 +169,11 @@ def _stream(dev):
 
 
 def _up(x: torch.Tensor, dev) -> torch.Tensor:
-    """Upload a small host-computed matrix buffer (contiguous fp32)."""
+    """Upload a small host-computed matrix buffer (contiguous fp32).  A page-locked host
+    buffer is copied asynchronously on the current stream (torch's pinned allocator keeps
+    it alive until that copy has run)."""
+    if x.device.type == "cpu" and x.is_pinned() and x.dtype == torch.float32 and x.is_contiguous():
+        return x.to(device=dev, non_blocking=True)
     return x.to(device=dev, dtype=torch.float32).contiguous()
 
 

@@ -59,6 +59,18 @@ int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
+// C = A (M x K) @ B (K x N), row-major, sum in ascending k, no fused multiply-add
+// (mpiv_render_homographies: torch's CPU matmul of tiny matrices rounds this way)
+template <int M, int K, int N>
+inline void mm(const float* A, const float* B, float* C) {
+    for (int i = 0; i < M; ++i)
+        for (int j = 0; j < N; ++j) {
+            float s = A[i * K] * B[j];
+            for (int k = 1; k < K; ++k) s = s + A[i * K + k] * B[k * N + j];
+            C[i * N + j] = s;
+        }
+}
+
 constexpr int64_t kMaxGridYZ = 65535;
 constexpr int kNativeLdsMaxP = 16;
 constexpr int64_t kMaxGridX = 2147483647;
@@ -609,6 +621,47 @@ int mpiv_assemble_mpi_backward(const float* drgba, const int64_t gs[5], const fl
         assemble_backward_kernel<<<dim3(blocks((int64_t)H * W, 256), B), 256, 0, S(stream)>>>(
             drgba, g, pred, fg, s, H, W, P, make_fastdiv((unsigned)W), dpred, dfg);
     return launched("mpiv_assemble_mpi_backward");
+}
+
+// ---- host-side homographies (inv_homography_torch chain, utils.py:44-67) -------------
+// The reference evaluates the chain with torch-CPU ops on materialised [P,B,...] tensors;
+// torch's CPU matmul of these tiny matrices rounds as plain products summed in ascending
+// k (no FMA; checked against torch for every shape of the chain, batch 1..1280), and the
+// rest is elementwise IEEE arithmetic, so the chain is restated here exactly (the library
+// builds with -ffp-contract=off, host code included).  Kinv = torch.inverse(K) comes from
+// the caller (LAPACK).  Pinned bit-exact by tests/test_host.py against the reference's H.
+int mpiv_render_homographies(const float* pose, const float* depths, const float* K, const float* Kinv, int B,
+                             int P, float* H) {
+    if (!pose || !depths || !K || !Kinv || !H) return fail(MPIV_ERR_ARG, "mpiv_render_homographies: null pointer");
+    if (B <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "mpiv_render_homographies: bad shape");
+    const float n_hat[3] = {0.0f, 0.0f, 1.0f};
+    for (int b = 0; b < B; ++b) {
+        const float* T = pose + (int64_t)b * 16;
+        float rt[9], t[3];  // rot^T (transpose_torch, exact) and t = pose[:3, 3:]
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) rt[i * 3 + j] = T[j * 4 + i];
+            t[i] = T[i * 4 + 3];
+        }
+        float nr[3], c, rtt[3], num0[9], num[9];
+        mm<1, 3, 3>(n_hat, rt, nr);       // n_hat @ rot^T
+        mm<1, 3, 1>(nr, t, &c);           // (n_hat @ rot^T) @ t
+        mm<3, 3, 1>(rt, t, rtt);          // rot^T @ t
+        mm<3, 1, 3>(rtt, n_hat, num0);    // (rot^T @ t) @ n_hat
+        mm<3, 3, 3>(num0, rt, num);       // ... @ rot^T
+        const float* Kb = K + (int64_t)b * 9;
+        const float* Ki = Kinv + (int64_t)b * 9;
+        for (int p = 0; p < P; ++p) {
+            const float a = -depths[p];
+            float den = a - c;
+            den = den + (den == 0.0f ? 1e-8f : 0.0f);  // divide_safe_torch, utils.py:38
+            float m[9], km[9];
+            for (int e = 0; e < 9; ++e) m[e] = rt[e] + num[e] / den;
+            mm<3, 3, 3>(Kb, m, km);                              // k_s @ (rot^T + num / den)
+            mm<3, 3, 3>(km, Ki, H + ((int64_t)b * P + p) * 9);   // ... @ inverse(k_t)
+        }
+    }
+    g_err[0] = '\0';
+    return MPIV_OK;
 }
 
 int mpiv_synth_mpi_packed(uint32_t seed, int H, int W, int p_begin, int p_end, float* packed, void* stream) {

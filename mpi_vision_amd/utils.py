@@ -146,7 +146,8 @@ def mpi_render_view_torch(rgba_layers, tgt_pose, planes, intrinsics):
     batch_size = tgt_pose.shape[0]
     n_planes = len(planes)
     depths = planes.reshape([n_planes, 1])  # AttributeError on a list, like the reference
-    homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
+    homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size,
+                                     pin=rgba_layers.is_cuda)
     if torch.is_grad_enabled() and rgba_layers.requires_grad:
         # training (ipynb cell 12): the adjoint runs in HIP too, bit-exact to the
         # reference's autograd (render_bwd.hip)

@@ -27,6 +27,11 @@ void oracle_render_backward(const float *mpi, const int64_t st[5], int B, int H,
                             const float *homs, const float *dout, float *dmpi, int vec, int nthreads);
 /* layers [P][n][4] contiguous; out [n][3] */
 void oracle_over_composite(const float *layers, int P, int64_t n, float *out);
+/* depth-map inverse warp: img [B,Hs,Ws,C] (strides), ki [B][9], proj [B][16],
+ * depth [B][Ht][Wt] contiguous -> out [B,Ht,Wt,C] */
+void oracle_inverse_warp(const float *img, const int64_t st[4], int B, int Hs, int Ws, int C,
+                         const float *ki, const float *proj, const float *depth, int Ht, int Wt,
+                         float *out, int nthreads);
 /* counter-based synthetic MPI (synth.hip restated): planes [p0,p1) as [H][W][p1-p0][4] */
 void oracle_synth_mpi(uint32_t seed, int H, int W, int p0, int p1, float *out);
 /* rows [y0,y1) of one view of the synthetic MPI through planes [p0,p1), homs [P][9]:

@@ -39,6 +39,8 @@ def lib():
         L.oracle_over_composite.argtypes = [_f, ctypes.c_int, ctypes.c_int64, _f]
         L.oracle_render_backward.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, _f, _f, ctypes.c_int,
                                                                              ctypes.c_int]
+        L.oracle_inverse_warp.argtypes = [_f, _i64] + [ctypes.c_int] * 4 + [_f, _f, _f, ctypes.c_int, ctypes.c_int,
+                                                                          _f, ctypes.c_int]
         L.oracle_synth_mpi.argtypes = [ctypes.c_uint32] + [ctypes.c_int] * 4 + [_f]
         L.oracle_render_synth.argtypes = [ctypes.c_uint32] + [ctypes.c_int] * 7 + [_f, ctypes.c_int, ctypes.c_int,
                                                                                   _f, ctypes.c_int]
@@ -142,6 +144,20 @@ def plane_sweep(img: np.ndarray, ki: np.ndarray, proj: np.ndarray, depths, tgt_h
     out = np.empty((B, tgt_h, tgt_w, D * C), np.float32)
     lib().oracle_plane_sweep(_fp(img), _strides(img), B, Hs, Ws, C, _fp(ki), _fp(proj), _fp(d), D,
                              tgt_h, tgt_w, _fp(out), _threads(nthreads))
+    return out
+
+
+def inverse_warp(img: np.ndarray, ki: np.ndarray, proj: np.ndarray, depth: np.ndarray, nthreads: int = 0):
+    """projective_inverse_warp_torch[2] with a depth map: img [B,Hs,Ws,C], ki [B,9], proj [B,16],
+    depth [B,Ht,Wt] -> [B,Ht,Wt,C]."""
+    B, Hs, Ws, C = img.shape
+    ki = np.ascontiguousarray(ki, np.float32).reshape(B, 9)
+    proj = np.ascontiguousarray(proj, np.float32).reshape(B, 16)
+    depth = np.ascontiguousarray(depth, np.float32)
+    Ht, Wt = depth.shape[1], depth.shape[2]
+    out = np.empty((B, Ht, Wt, C), np.float32)
+    lib().oracle_inverse_warp(_fp(img), _strides(img), B, Hs, Ws, C, _fp(ki), _fp(proj), _fp(depth), Ht, Wt,
+                              _fp(out), _threads(nthreads))
     return out
 
 

@@ -29,6 +29,35 @@ def test_render_homographies_bit_exact(name, small):
     assert_bits(H.numpy(), small[f"{name}_H"].transpose(1, 0, 2, 3).reshape(B, P, 9), name)
 
 
+@pytest.mark.parametrize("name", RENDER_CASES)
+def test_native_homography_chain_equals_torch_ops(name, small):
+    """The library's host restatement of the chain (mpiv_render_homographies) equals the
+    op-by-op torch form on the same inputs, and both equal the reference's H."""
+    B = small[f"{name}_pose"].shape[0]
+    args = (torch.tensor(small[f"{name}_pose"]), torch.tensor(small[f"{name}_depths"]),
+            torch.tensor(small[f"{name}_K"]), B)
+    assert_bits(_host.render_homographies(*args).numpy(), _host.render_homographies_torch(*args).numpy(), name)
+
+
+def test_native_homography_chain_random_poses():
+    """Random poses / intrinsics / depths (incl. a plane through the camera centre, where
+    divide_safe's den == 0 branch fires): native chain == torch ops, bit for bit."""
+    g = torch.Generator().manual_seed(99)
+    B, P = 6, 40
+    poses = []
+    for k in range(B):
+        R = configs.rot_y(float(torch.rand(1, generator=g)) * 40 - 20)
+        poses.append(configs.pose_from(R, ((torch.rand(3, generator=g) - 0.5) * 3).tolist()))
+    poses[0] = configs.pose_from(configs.rot_y(0.0), (0.3, -0.2, -7.5))  # n R^T t = t_z exactly
+    pose = configs.f32(poses)
+    K = configs.f32([configs.intrinsics_matrix(*(torch.rand(4, generator=g) * 200 + 10).tolist()) for _ in range(B)])
+    d = (torch.rand(P, generator=g) * 50 + 0.1).sort(descending=True).values
+    d[5] = 7.5  # a - n R^T t = -7.5 - (-7.5) == 0 for view 0: the 1e-8 branch
+    H = _host.render_homographies_torch(pose, d, K, B)
+    assert torch.isfinite(H).all() and H.abs().max() > 1e6  # the branch fired (division by 1e-8)
+    assert_bits(_host.render_homographies(pose, d, K, B).numpy(), _host.render_homographies_torch(pose, d, K, B).numpy())
+
+
 def test_inv_homography_helper_bit_exact(small):
     K, pose, d = (torch.tensor(small[k]) for k in ("hom_K", "hom_pose", "hom_depths"))
     P, B = d.shape[0], K.shape[0]
