@@ -115,13 +115,32 @@ def load():
     return _lib
 
 
+# MPIV_ROCTX=1: every entry-point call is wrapped in a roctx range named after it, so
+# `rocprofv3 --marker-trace --kernel-trace` attributes each kernel to its drop-in call
+# (tracing only; off by default: no overhead on the launch path).
+_ROCTX = None
+if os.environ.get("MPIV_ROCTX") == "1":
+    try:
+        _ROCTX = ctypes.CDLL("/opt/rocm/lib/libroctx64.so")
+        _ROCTX.roctxRangePushA.argtypes = [ctypes.c_char_p]
+    except OSError:
+        _ROCTX = None
+
+
 def _call(name, *args):
     """Call an entry point.  Tensor arguments are passed as their device pointers and
     stay referenced (alive) for the duration of the call, so temporaries built inline
     cannot be freed and their memory reused by a later argument's allocation."""
     L = load()
     cargs = [ctypes.c_void_p(a.data_ptr()) if isinstance(a, torch.Tensor) else a for a in args]
-    rc = getattr(L, name)(*cargs)
+    if _ROCTX is not None:
+        _ROCTX.roctxRangePushA(name.encode())
+        try:
+            rc = getattr(L, name)(*cargs)
+        finally:
+            _ROCTX.roctxRangePop()
+    else:
+        rc = getattr(L, name)(*cargs)
     if rc != 0:
         raise RuntimeError(f"{name} failed ({rc}): {L.mpiv_last_error().decode()}")
 

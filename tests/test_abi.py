@@ -95,3 +95,19 @@ def test_output_buffers_validated():
     with pytest.raises(RuntimeError, match="out must be"):
         _lib._check_out(torch.zeros((3, 2), dtype=torch.float64), (3, 2), good.device, "x")
     assert _lib._check_out(torch.zeros((3, 2)), (3, 2), good.device, "x") is not None
+
+
+@pytest.mark.slow
+def test_host_asan_builds():
+    """Host AddressSanitizer + UBSan flavour (GPU ASan is not available on
+    this pool): an ASan-instrumented libmpiv driven through every argument-validation
+    path and the host homography chain, and the CPU oracle on small / degenerate inputs
+    (tools/asan/Makefile, built into /tmp)."""
+    import shutil
+    import subprocess
+    if shutil.which("/opt/rocm/bin/hipcc") is None or shutil.which("gcc") is None:
+        pytest.skip("needs hipcc and gcc")
+    r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tools", "asan"), "run"], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "abi_check: 0 failure(s)" in r.stdout and "oracle_check: ok" in r.stdout
