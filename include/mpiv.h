@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 5
+#define MPIV_ABI_VERSION 6
 
 enum {
     MPIV_OK = 0,
@@ -47,7 +47,7 @@ const char *mpiv_last_error(void);
 const char *mpiv_build_id(void);
 
 /* Debug / A/B hook, never needed in production: selects a non-default kernel variant
- * by name ("render_mv", "render_pair", "render_native_lds", "sweep_tile",
+ * by name ("render_mv", "render_pair", "render_native_lds", "render_chunk", "sweep_tile",
  * "sweep_store", "box_shrink"; "reset" restores every default).  Process-wide;
  * returns MPIV_ERR_ARG for an unknown name. */
 int mpiv_debug_set(const char *name, int value);
@@ -58,7 +58,10 @@ int mpiv_debug_set(const char *name, int value);
  * mpi:   [B,H,W,P,4] with element strides mpi_strides[5] (B may be stride 0)
  * homs:  [B][P][9] row-major target->source homographies
  *        (inv_homography_torch, utils.py:44-67, evaluated by the caller)
- * out:   [B,H,W,3] contiguous */
+ * out:   [B,H,W,3] contiguous
+ * Planes contiguous per pixel (strides[3] == 4, strides[4] == 1, 16-B texels) are read
+ * in place at full-line coalescing (render_chunk.hip); other layouts by a per-pixel
+ * gather kernel. */
 int mpiv_render(const float *mpi, const int64_t mpi_strides[5], int B, int H, int W, int P,
                 const float *homs, float *out, void *stream);
 
@@ -99,6 +102,12 @@ int mpiv_combine_ct(const float *parts, int G, int64_t n, float *out, void *stre
  * (host, row-major) -> H [B][P][9]. */
 int mpiv_render_homographies(const float *pose, const float *depths, const float *K, const float *Kinv, int B,
                              int P, float *H);
+
+/* The same chain evaluated on the device (all five pointers DEVICE memory), one
+ * work-item per (view, plane): bit-identical to mpiv_render_homographies, for callers
+ * whose poses and intrinsics live in HBM (no blocking device-to-host copies). */
+int mpiv_render_homographies_device(const float *pose, const float *depths, const float *K, const float *Kinv,
+                                    int B, int P, float *H, void *stream);
 
 /* ---- render backward ------------------------------------------------------ */
 

@@ -9,6 +9,8 @@ once per call (P*B*36 bytes).
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 _CPU = torch.device("cpu")
@@ -55,6 +57,50 @@ def _inverse_cached(K: torch.Tensor) -> torch.Tensor:
         kinv = torch.inverse(K).contiguous()
         _KINV_CACHE[key] = kinv
     return kinv
+
+
+_KINV_DEV: dict = {}
+
+
+def _kinv_device(intrinsics: torch.Tensor, batch: int, dev) -> torch.Tensor:
+    """inverse(K) [batch,3,3] on `dev` for a device-resident intrinsics tensor, memoised on
+    that tensor OBJECT and its version counter (an in-place update bumps it; a new tensor
+    is a new object), so a camera path that reuses one intrinsics tensor reads it back to
+    the host once.  On a miss: one device-to-host copy of K and LAPACK (torch.inverse, as
+    the reference), then the upload."""
+    try:
+        ver = intrinsics._version
+    except RuntimeError:  # inference tensors track no version: no memo
+        ver = None
+    ent = _KINV_DEV.get(id(intrinsics))
+    if (ver is not None and ent is not None and ent[0]() is intrinsics and ent[1] == ver and ent[2] == batch
+            and ent[3].device == dev):
+        return ent[3]
+    K = _cpu32(intrinsics).expand(batch, 3, 3).contiguous()
+    kinv = _inverse_cached(K).to(dev)
+    if ver is not None:
+        if len(_KINV_DEV) >= 64:
+            _KINV_DEV.clear()
+        _KINV_DEV[id(intrinsics)] = (weakref.ref(intrinsics), ver, batch, kinv)
+    return kinv
+
+
+def render_homographies_device(pose: torch.Tensor, depths: torch.Tensor, intrinsics: torch.Tensor,
+                               batch: int) -> torch.Tensor:
+    """render_homographies for a pose batch that lives on a ROCm device: the same chain
+    evaluated there (mpiv_render_homographies_device, bit-identical to the host entry),
+    so the render path issues no blocking device-to-host copy of the poses.  Returns a
+    [B, P, 9] fp32 tensor on the pose's device."""
+    from . import _lib
+    dev = pose.device
+    pose_d = pose.to(dtype=_F32).contiguous()
+    d = depths.to(device=dev, dtype=_F32).reshape(-1).contiguous()
+    K = intrinsics.to(device=dev, dtype=_F32).expand(batch, 3, 3).contiguous()
+    kinv = _kinv_device(intrinsics, batch, dev)
+    P = d.shape[0]
+    H = torch.empty((batch, P, 9), dtype=_F32, device=dev)
+    _lib._call("mpiv_render_homographies_device", pose_d, d, K, kinv, batch, P, H, _lib._stream(dev))
+    return H
 
 
 def render_homographies(pose: torch.Tensor, depths: torch.Tensor, intrinsics: torch.Tensor,

@@ -54,19 +54,39 @@ _SIGS = {
     "mpiv_assemble_mpi": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_assemble_mpi_packed": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_render_homographies": [_vp, _vp, _vp, _vp, _int, _int, _vp],
+    "mpiv_render_homographies_device": [_vp, _vp, _vp, _vp, _int, _int, _vp, _vp],
     "mpiv_synth_mpi_packed": [ctypes.c_uint32, _int, _int, _int, _int, _vp, _vp],
     "mpiv_assemble_mpi_backward": [_vp, _c_i64p, _vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp,
                                    _vp],
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
                           "mpiv_build_id", "mpiv_debug_set")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lib = None
 
-# How mpi_render_view_torch renders a non-broadcast MPI batch: "auto" (pack per view
-# when P >= 8, else read in place), "pack", or "native" (the in-place kernel).
+# How mpi_render_view_torch renders a non-broadcast MPI batch: "auto" (the in-place
+# chunked kernel when the layout allows it, else pack per view when P >= 8, else read in
+# place), "pack", or "native" (mpiv_render, which picks its in-place kernel itself).
 RENDER_POLICY = "auto"
+
+_KOOB = 0x7FFFFF00
+_CHUNK_LDS = 65536
+
+
+def chunk_layout_ok(rgba_layers: torch.Tensor) -> bool:
+    """True when mpiv_render reads this [B,H,W,P,4] tensor with render_chunk_kernel
+    (abi.hip: planes contiguous per pixel, 16-B texels, offsets below the buffer range)."""
+    B, H, W, P, C = rgba_layers.shape
+    st = rgba_layers.stride()
+    if C != 4 or H < 2 or W < 2 or st[4] != 1 or st[3] != 4 or any(s % 4 for s in st[:3]):
+        return False
+    if rgba_layers.data_ptr() % 16:
+        return False
+    CH = 4 if P <= 4 else 8
+    rec = ((H - 1) * st[1] + (W - 1) * st[2]) * 4 + CH * 16
+    return (rec < _KOOB and st[1] // 4 < (1 << 22) and st[2] // 4 < (1 << 22)
+            and 4 * 64 * CH * 16 + P * 36 <= _CHUNK_LDS)
 
 
 def source_hash() -> str | None:
@@ -321,6 +341,10 @@ def render(rgba_layers: torch.Tensor, homs: torch.Tensor) -> torch.Tensor:
         return render_packed(pack_planes(rgba_layers[0]), homs)
     h = _up(homs, dev)
     out = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32)
+    if RENDER_POLICY == "auto" and chunk_layout_ok(rgba_layers):
+        # in place, whole 128-B pixel lines per tap instruction (render_chunk.hip): no pack
+        _call("mpiv_render", rgba_layers, _strides(rgba_layers), B, H, W, P, h, out, _stream(dev))
+        return out
     if RENDER_POLICY == "pack" or (RENDER_POLICY == "auto" and P >= 8 and (H + 4) * (W + 4) * 16 < 0x7FFFFF00):
         # per view: pack its MPI plane-major (one coalesced transpose pass) and render
         # from the packed copy -- the gathers of the in-place layout touch one 128-B

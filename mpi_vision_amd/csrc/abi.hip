@@ -11,6 +11,7 @@
 #include "../../include/mpiv.h"
 #include "render.hip"
 #include "render_lds.hip"
+#include "render_chunk.hip"
 #include "render_mv.hip"
 #include "render_bwd.hip"
 #include "sweep.hip"
@@ -46,33 +47,25 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //   render_mv=1        launches of >= 4 views use the multi-view LDS kernel (render_mv.hip)
 //   render_pair=1|2    the direct render takes pixel pairs sharing taps (render_pair_kernel)
 //   render_native_lds=0  mpiv_render gathers directly from the [B,H,W,P,4] tensor
+//   render_chunk=-1|4|8  mpiv_render's in-place chunked kernel off, or CH planes per chunk
+//                      (default 0 = automatic: 8, or 4 for P <= 4)
 //   sweep_tile=1       the sweep uses the tile kernel; sweep_store=k (k >= 0) the grouped one
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
 //                      forces their per-sample global fallback (tests)
 // Relaxed atomics: a launch reads each option once; setting options while another thread
 // launches is a test-harness race on which kernel runs, never on memory.
-enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink, kNumOpts };
+enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
+                kOptRenderChunk, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
-                                         "sweep_tile", "sweep_store", "box_shrink"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0};
+                                         "sweep_tile", "sweep_store", "box_shrink", "render_chunk"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
-// C = A (M x K) @ B (K x N), row-major, sum in ascending k, no fused multiply-add
-// (mpiv_render_homographies: torch's CPU matmul of tiny matrices rounds this way)
-template <int M, int K, int N>
-inline void mm(const float* A, const float* B, float* C) {
-    for (int i = 0; i < M; ++i)
-        for (int j = 0; j < N; ++j) {
-            float s = A[i * K] * B[j];
-            for (int k = 1; k < K; ++k) s = s + A[i * K + k] * B[k * N + j];
-            C[i * N + j] = s;
-        }
-}
-
 constexpr int64_t kMaxGridYZ = 65535;
 constexpr int kNativeLdsMaxP = 16;
+constexpr int kChunkMaxLds = 65536;  // render_chunk_kernel: slots + P homographies, default LDS limit
 constexpr int64_t kMaxGridX = 2147483647;
 
 }  // namespace
@@ -116,6 +109,23 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
     const bool vec = s.c == 1 && aligned16(mpi) && s.b % 4 == 0 && s.y % 4 == 0 && s.x % 4 == 0 && s.p % 4 == 0;
     const bool fast = H >= 2 && W >= 2;
     hipStream_t q = S(stream);
+    // in place at full-line coalescing (render_chunk.hip): planes contiguous per pixel
+    // (s.p == 4), every offset from a chunk base below the buffer's out-of-range offset
+    const int ch_opt = opt(kOptRenderChunk);
+    const int CH = ch_opt ? ch_opt : (P <= 4 ? 4 : 8);
+    const int64_t rec = ((int64_t)(H - 1) * s.y + (int64_t)(W - 1) * s.x) * 4 + CH * 16;
+    const size_t ch_lds = (size_t)(CH == 8 ? chunk_slot_floats<8>() : chunk_slot_floats<4>()) * 4 + (size_t)P * 36;
+    if (vec && fast && s.p == 4 && ch_opt >= 0 && (CH == 4 || CH == 8) && rec < (int64_t)kOOB &&
+        s.y / 4 < (1 << 22) && s.x / 4 < (1 << 22) && ch_lds <= (size_t)kChunkMaxLds) {
+        const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * B;
+        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_render: too many blocks");
+        const ChunkGeom cg{(int)(s.y / 4), (int)(s.x / 4), (int)rec};
+        if (CH == 8)
+            render_chunk_kernel<8><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
+        else
+            render_chunk_kernel<4><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
+        return launched("mpiv_render");
+    }
     // footprints staged through LDS, read in place (render_lds.hip render_lds_native_kernel):
     // measured faster for few planes (P = 10: 0.031 vs 0.039 ms), slower for many (P = 128:
     // 2.78 vs 1.86 ms, the fills' 64-B segments no longer serve the next planes)
@@ -634,34 +644,24 @@ int mpiv_render_homographies(const float* pose, const float* depths, const float
                              int P, float* H) {
     if (!pose || !depths || !K || !Kinv || !H) return fail(MPIV_ERR_ARG, "mpiv_render_homographies: null pointer");
     if (B <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "mpiv_render_homographies: bad shape");
-    const float n_hat[3] = {0.0f, 0.0f, 1.0f};
-    for (int b = 0; b < B; ++b) {
-        const float* T = pose + (int64_t)b * 16;
-        float rt[9], t[3];  // rot^T (transpose_torch, exact) and t = pose[:3, 3:]
-        for (int i = 0; i < 3; ++i) {
-            for (int j = 0; j < 3; ++j) rt[i * 3 + j] = T[j * 4 + i];
-            t[i] = T[i * 4 + 3];
-        }
-        float nr[3], c, rtt[3], num0[9], num[9];
-        mm<1, 3, 3>(n_hat, rt, nr);       // n_hat @ rot^T
-        mm<1, 3, 1>(nr, t, &c);           // (n_hat @ rot^T) @ t
-        mm<3, 3, 1>(rt, t, rtt);          // rot^T @ t
-        mm<3, 1, 3>(rtt, n_hat, num0);    // (rot^T @ t) @ n_hat
-        mm<3, 3, 3>(num0, rt, num);       // ... @ rot^T
-        const float* Kb = K + (int64_t)b * 9;
-        const float* Ki = Kinv + (int64_t)b * 9;
-        for (int p = 0; p < P; ++p) {
-            const float a = -depths[p];
-            float den = a - c;
-            den = den + (den == 0.0f ? 1e-8f : 0.0f);  // divide_safe_torch, utils.py:38
-            float m[9], km[9];
-            for (int e = 0; e < 9; ++e) m[e] = rt[e] + num[e] / den;
-            mm<3, 3, 3>(Kb, m, km);                              // k_s @ (rot^T + num / den)
-            mm<3, 3, 3>(km, Ki, H + ((int64_t)b * P + p) * 9);   // ... @ inverse(k_t)
-        }
-    }
+    for (int b = 0; b < B; ++b)
+        for (int p = 0; p < P; ++p) render_hom_chain(pose + (int64_t)b * 16, depths[p], K + (int64_t)b * 9,
+                                                     Kinv + (int64_t)b * 9, H + ((int64_t)b * P + p) * 9);
     g_err[0] = '\0';
     return MPIV_OK;
+}
+
+// The same chain on the device, one work-item per (view, plane), for poses / intrinsics
+// that already live in HBM (no blocking device-to-host copies on the render path).
+// Same code as the host entry (render_hom_chain, IEEE fp32, no contraction, correctly
+// rounded division): bit-identical results (tests/test_host.py).
+int mpiv_render_homographies_device(const float* pose, const float* depths, const float* K, const float* Kinv,
+                                    int B, int P, float* H, void* stream) {
+    const char* nm = "mpiv_render_homographies_device";
+    if (!pose || !depths || !K || !Kinv || !H) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (B <= 0 || P <= 0 || (int64_t)B * P >= (1ll << 31)) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    render_homographies_kernel<<<blocks((int64_t)B * P, 256), 256, 0, S(stream)>>>(pose, depths, K, Kinv, B, P, H);
+    return launched(nm);
 }
 
 int mpiv_synth_mpi_packed(uint32_t seed, int H, int W, int p_begin, int p_end, float* packed, void* stream) {

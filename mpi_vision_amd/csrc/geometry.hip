@@ -136,4 +136,61 @@ __global__ __launch_bounds__(256) void div_const_selftest_kernel(float c, float 
     if (local) atomicAdd(bad, local);
 }
 
+// ---------------------------------------------------------------------------
+// per-(view, plane) render homographies: the inv_homography_torch chain (utils.py:44-67,
+// via :278-285 -> :255-262 -> :225-229).  The reference evaluates it with torch-CPU ops
+// on materialised [P,B,...] tensors; torch's CPU matmul of these tiny matrices rounds as
+// plain products summed in ascending k (no FMA; checked against torch for every shape
+// of the chain, batch 1..1280) and the rest is elementwise IEEE arithmetic, so the chain
+// is restated exactly.  Shared by the host entry and the device kernel (the library
+// builds with -ffp-contract=off on both sides; fp32 division is correctly rounded on
+// both).  Kinv = torch.inverse(K) comes from the caller (LAPACK).
+// ---------------------------------------------------------------------------
+
+// C = A (M x K) @ B (K x N), row-major, sum in ascending k, no fused multiply-add
+template <int M, int K, int N>
+__host__ __device__ inline void mm(const float* A, const float* B, float* C) {
+    for (int i = 0; i < M; ++i)
+        for (int j = 0; j < N; ++j) {
+            float s = A[i * K] * B[j];
+            for (int k = 1; k < K; ++k) s = s + A[i * K + k] * B[k * N + j];
+            C[i * N + j] = s;
+        }
+}
+
+// pose T [4x4] (row-major), plane depth, K and K^-1 [3x3] -> H [3x3]
+__host__ __device__ inline void render_hom_chain(const float* T, float depth, const float* Kb, const float* Ki,
+                                                 float* H) {
+    const float n_hat[3] = {0.0f, 0.0f, 1.0f};
+    float rt[9], t[3];  // rot^T (transpose_torch, exact) and t = pose[:3, 3:]
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) rt[i * 3 + j] = T[j * 4 + i];
+        t[i] = T[i * 4 + 3];
+    }
+    float nr[3], c, rtt[3], num0[9], num[9];
+    mm<1, 3, 3>(n_hat, rt, nr);     // n_hat @ rot^T
+    mm<1, 3, 1>(nr, t, &c);         // (n_hat @ rot^T) @ t
+    mm<3, 3, 1>(rt, t, rtt);        // rot^T @ t
+    mm<3, 1, 3>(rtt, n_hat, num0);  // (rot^T @ t) @ n_hat
+    mm<3, 3, 3>(num0, rt, num);     // ... @ rot^T
+    const float a = -depth;
+    float den = a - c;
+    den = den + (den == 0.0f ? 1e-8f : 0.0f);  // divide_safe_torch, utils.py:38
+    float m[9], km[9];
+    for (int e = 0; e < 9; ++e) m[e] = rt[e] + num[e] / den;
+    mm<3, 3, 3>(Kb, m, km);  // k_s @ (rot^T + num / den)
+    mm<3, 3, 3>(km, Ki, H);  // ... @ inverse(k_t)
+}
+
+__global__ __launch_bounds__(256) void render_homographies_kernel(const float* __restrict__ pose,
+                                                                  const float* __restrict__ depths,
+                                                                  const float* __restrict__ K,
+                                                                  const float* __restrict__ Kinv, int B, int P,
+                                                                  float* __restrict__ H) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)B * P) return;
+    const int b = (int)(i / P), p = (int)(i % P);
+    render_hom_chain(pose + (int64_t)b * 16, depths[p], K + (int64_t)b * 9, Kinv + (int64_t)b * 9, H + i * 9);
+}
+
 }  // namespace mpiv

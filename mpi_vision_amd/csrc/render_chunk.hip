@@ -1,0 +1,193 @@
+// render_chunk.hip -- mpi_render_view_torch (utils.py:267-294) reading the reference's
+// own [B,H,W,P,4] tensor IN PLACE at the packed kernel's coalescing, so the training
+// caller (non-broadcast MPI per view, ipynb cell 12 L42) pays no per-view pack.
+//
+// In that layout the P texels of one pixel are one contiguous P*16-B run, so a plane's
+// texels are P*16 B apart: render_native_kernel's one-pixel-per-lane gathers touch one
+// 128-B line per 16-B tap.  Here the lanes of a wave are (pixel, plane-in-chunk) pairs:
+// with CH planes per chunk, lane l samples plane  c*CH + l%CH  of pixel  l/CH  (+ the
+// sub-step's pixel base), so the CH lanes of one pixel read CH consecutive texels of one
+// pixel run -- a whole 128-B line for CH = 8 -- and one tap instruction covers 64/CH
+// pixels x CH planes, the same 1 KiB in 8 lines as a packed-layout wave row.
+//
+// Compositing must stay sequential per pixel (the unfused over-operator rounds in the
+// reference's order, back to front), so the blended samples go through a per-wave LDS
+// slot: after the CH sub-steps of a chunk the slot holds 64 pixels x CH planes, and lane
+// l re-reads pixel l's CH samples (one ds_read_b128 each) and composites them in order.
+// Slot rows are XOR-swizzled so both the sub-step writes and the per-pixel reads are
+// bank-conflict free.  The per-sample arithmetic is render_packed_kernel's recipe
+// (tile-level division proof, exact constant divisions, ATen weights, 4-tap fma chain),
+// so the output is bit-identical to the other render kernels; grid_sample's zero
+// padding is per tap: an out-of-image tap gets the buffer's out-of-range offset.
+#include "mpiv_common.hpp"
+
+namespace mpiv {
+
+// one sample position of render_packed_kernel's recipe for an arbitrary (per-lane) plane
+// homography held in VGPRs
+template <bool GUARD>
+__device__ __forceinline__ void chunk_pos(const float* h, float fx, float fy, const RenderGeom& g, float& px,
+                                          float& py) {
+    const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
+    const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
+    const float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+    float qu, qv;
+    if (GUARD)
+        divide_safe2(u, v, w, qu, qv);  // divide_safe_torch, utils.py:35-39
+    else
+        div2_fast(u, v, w, qu, qv);
+    const float cx = div_const(qu, g.hm1, g.rc_hm1);  // SWAPPED x / (H-1), utils.py:188
+    const float cy = div_const(qv, g.wm1, g.rc_wm1);  //         y / (W-1)
+    px = unnormalize(to_grid(cx), g.half_w);
+    py = unnormalize(to_grid(cy), g.half_h);
+}
+
+struct ChunkGeom {
+    int row_t, pix_t;  // texel (16-B) strides of a row and a pixel in the reference tensor
+    int rec_bytes;     // buffer range from a chunk's base: every live tap is below it
+};
+
+// Issue the four taps of one (pixel, plane) sample from the in-place tensor.  Tap origin
+// clamped into [-2, W] x [-2, H] (defined int conversion; NaN maps to a bound and its NaN
+// weights still poison the sample, as in the reference); a tap outside the image, or any
+// tap of a lane past the last plane, gets kOOB: the buffer unit returns 0 without an access.
+__device__ __forceinline__ void issue_taps_chunk(__amdgpu_buffer_rsrc_t r, const RenderGeom& g, const ChunkGeom& cg,
+                                                 int jt, bool live, float px, float py, TapSet& t) {
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
+    const int ix = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)g.W);
+    const int iy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)g.H);
+    const bool x0 = (unsigned)ix < (unsigned)g.W, x1 = (unsigned)(ix + 1) < (unsigned)g.W;
+    const bool y0 = live && (unsigned)iy < (unsigned)g.H, y1 = live && (unsigned)(iy + 1) < (unsigned)g.H;
+    // wrapping 32-bit arithmetic: the value is only used where every tap index is valid
+    const int off = (int)(((unsigned)__mul24(iy, cg.row_t) + (unsigned)__mul24(ix, cg.pix_t) + (unsigned)jt) * 16u);
+    const int pb = cg.pix_t * 16, rb = cg.row_t * 16;
+    t.a = llvm_raw_buffer_load_v4f32(r, (x0 && y0) ? off : kOOB, 0, 0);
+    t.b = llvm_raw_buffer_load_v4f32(r, (x1 && y0) ? off + pb : kOOB, 0, 0);
+    t.c = llvm_raw_buffer_load_v4f32(r, (x0 && y1) ? off + rb : kOOB, 0, 0);
+    t.d = llvm_raw_buffer_load_v4f32(r, (x1 && y1) ? off + rb + pb : kOOB, 0, 0);
+}
+
+// LDS: [4 waves][64 pixels][CH] float4 sample slots, then the view's P homographies
+// (9 floats each).  Slot of (pixel q, plane j): q*CH + (j ^ swz(q)).
+template <int CH>
+__device__ __forceinline__ int chunk_slot(int q, int j) {
+    // ds_read_b128 serves 16 lanes per LDS cycle; with q's row CH*16 B wide, the XOR
+    // spreads those lanes' reads over all 16 four-bank groups (MI355X_MICROARCH.md §LDS)
+    const int swz = CH == 8 ? ((q >> 1) & 7) : ((q >> 2) & 3);
+    return q * CH + (j ^ swz);
+}
+
+template <int CH>
+constexpr int chunk_slot_floats() {
+    return 4 * kWave * CH * 4;
+}
+
+template <int CH, bool GUARD>
+__device__ __forceinline__ void render_chunk_wave(const float* __restrict__ view, const RenderGeom& g,
+                                                  const ChunkGeom& cg, const float* __restrict__ hs,
+                                                  f32x4* __restrict__ slot, int tx0, int y, int lane,
+                                                  float& cr, float& cg_, float& cb) {
+    constexpr int PPS = kWave / CH;  // pixels per sub-step
+    const int j = lane % CH, i = lane / CH;
+    const float fy = (float)y;
+    const int nchunk = (g.P + CH - 1) / CH;
+    float h[9];
+    auto load_h = [&](int c, float* d) {
+        const int p = min(c * CH + j, g.P - 1);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) d[k] = hs[p * 9 + k];
+    };
+    auto rsrc = [&](int c) {
+        return make_rsrc(view + (int64_t)c * CH * 4, cg.rec_bytes);
+    };
+    // sub-step k of chunk c: pixel tx0 + k*PPS + i, plane c*CH + j
+    auto issue = [&](int c, int k, const float* hh, TapSet& ts) {
+        float px, py;
+        chunk_pos<GUARD>(hh, (float)(tx0 + k * PPS + i), fy, g, px, py);
+        issue_taps_chunk(rsrc(c), g, cg, j, c * CH + j < g.P, px, py, ts);
+    };
+    auto put = [&](int k, const TapSet& ts) { slot[chunk_slot<CH>(k * PPS + i, j)] = blend_taps(ts); };
+    TapSet A, B;
+    load_h(0, h);
+    issue(0, 0, h, A);
+    for (int c = 0; c < nchunk; ++c) {
+        const int cn = c + 1 < nchunk ? c + 1 : c;  // past the end: re-issue (cached, unused)
+#pragma unroll
+        for (int k = 0; k < CH; k += 2) {  // A holds sub-step k
+            issue(c, k + 1, h, B);
+            __builtin_amdgcn_sched_barrier(0);
+            put(k, A);
+            if (k + 2 < CH) {
+                issue(c, k + 2, h, A);
+            } else {
+                load_h(cn, h);  // the next chunk's homography (LDS) replaces this one's
+                issue(cn, 0, h, A);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            put(k + 1, B);
+        }
+        // composite: lane = pixel tx0 + lane, planes c*CH .. c*CH+CH-1 back to front
+#pragma unroll
+        for (int jj = 0; jj < CH; ++jj) {
+            const int p = c * CH + jj;
+            if (p < g.P) {
+                const f32x4 s = slot[chunk_slot<CH>(lane, jj)];
+                const float a = p == 0 ? 1.0f : s[3];  // plane 0 replaces (render_packed_pixel)
+                const float om = 1.0f - a;
+                cr = over(s[0], a, om, cr);
+                cg_ = over(s[1], a, om, cg_);
+                cb = over(s[2], a, om, cb);
+            }
+        }
+    }
+}
+
+// One block = 4 waves = a 64x4 output tile of one view; blocks in render_packed_kernel's
+// XCD-aware (tile, view) order.  Dynamic LDS: chunk_slot_floats<CH>() + P*9 floats.
+template <int CH>
+__global__ __launch_bounds__(256) void render_chunk_kernel(const float* __restrict__ mpi, int64_t view_stride,
+                                                           RenderGeom g, ChunkGeom cg, int V,
+                                                           const float* __restrict__ homs,
+                                                           float* __restrict__ out) {
+    extern __shared__ float4 chunk_lds[];
+    f32x4* slots = reinterpret_cast<f32x4*>(chunk_lds);
+    float* hs = reinterpret_cast<float*>(chunk_lds) + chunk_slot_floats<CH>();
+    const int tiles_x = (g.W + kTileX - 1) / kTileX;
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int v = lb % V;
+    const int tile = lb / V;
+    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * kTileY;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+    const float* hv = homs + (int64_t)v * g.P * 9;
+    for (int k = threadIdx.x; k < g.P * 9; k += 256) hs[k] = hv[k];
+    // block prologue: prove the fast division for the tile, all planes at once
+    const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
+    const float y0 = (float)ty0, y1 = (float)min(ty0 + kTileY - 1, g.H - 1);
+    bool ok = true;
+    for (int p = (int)threadIdx.x; p < g.P; p += 256) ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, y0, y1);
+    const bool proven = __syncthreads_and(ok);  // also publishes hs
+    const int y = ty0 + wave;
+    if (y >= g.H) return;  // whole wave; no barrier follows
+    const float* view = mpi + (int64_t)v * view_stride;
+    f32x4* slot = slots + wave * kWave * CH;
+    float cr = -0.0f, cgr = -0.0f, cb = -0.0f;
+    if (proven)
+        render_chunk_wave<CH, false>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb);
+    else
+        render_chunk_wave<CH, true>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb);
+    const int x = tx0 + lane;
+    if (x < g.W) {
+        float* o = out + (((int64_t)v * g.H + y) * g.W + x) * 3;
+        o[0] = cr;
+        o[1] = cgr;
+        o[2] = cb;
+    }
+}
+
+}  // namespace mpiv

@@ -146,8 +146,11 @@ def mpi_render_view_torch(rgba_layers, tgt_pose, planes, intrinsics):
     batch_size = tgt_pose.shape[0]
     n_planes = len(planes)
     depths = planes.reshape([n_planes, 1])  # AttributeError on a list, like the reference
-    homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size,
-                                     pin=rgba_layers.is_cuda)
+    if tgt_pose.is_cuda and rgba_layers.is_cuda:  # poses in HBM: the chain runs there too
+        homs = _host.render_homographies_device(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
+    else:
+        homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size,
+                                         pin=rgba_layers.is_cuda)
     if torch.is_grad_enabled() and rgba_layers.requires_grad:
         # training (ipynb cell 12): the adjoint runs in HIP too, bit-exact to the
         # reference's autograd (render_bwd.hip)
@@ -176,7 +179,10 @@ def mpi_render_net_output_torch(mpi_pred, ref_img, tgt_pose, planes, intrinsics)
     batch_size = tgt_pose.shape[0]
     n_planes = len(planes)
     depths = planes.reshape([n_planes, 1])
-    homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
+    if tgt_pose.is_cuda:
+        homs = _host.render_homographies_device(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
+    else:
+        homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
     fg = ref_img.to(mpi_pred.device)
     dev = mpi_pred.device
     B, _, H, W = mpi_pred.shape

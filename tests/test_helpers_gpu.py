@@ -79,3 +79,30 @@ def test_meshgrid(dev):
     assert g.shape == (2, 3, 3, 4)
     assert torch.equal(g[1, 0, 2], torch.arange(4.0)) and torch.equal(g[0, 1, :, 1], torch.arange(3.0))
     assert torch.all(g[:, 2] == 1)
+
+
+def test_device_homographies_bit_exact(dev):
+    """mpiv_render_homographies_device (the chain on the GPU, used when poses live in HBM)
+    equals the host chain bit for bit: random rotations / translations, a pose whose
+    den == 0 branch fires, several batch sizes; and the K^-1 memo follows in-place edits."""
+    from mpi_vision_amd import configs
+    from mpi_vision_amd import _host
+    g = torch.Generator().manual_seed(17)
+    for B, P in ((1, 10), (7, 33), (64, 128)):
+        poses = []
+        for k in range(B):
+            t = ((torch.rand(3, generator=g) - 0.5) * (0.3 + k)).tolist()
+            poses.append(configs.pose_from(configs.rot_y(float(torch.rand(1, generator=g)) * 40 - 20), t))
+        if B > 1:
+            poses[1] = configs.pose_from(configs.rot_y(0.0), (0.0, 0.0, 2.0))  # a - c == 0 at depth 2
+        pose = configs.f32(poses)
+        depths = configs.f32(configs.inv_depths(1, 100, P) if B != 7 else [2.0] + configs.inv_depths(1, 100, P - 1))
+        K = configs.f32([configs.intrinsics_matrix(500.0 + k, 480.0, 320.0, 200.0 + k) for k in range(B)])
+        want = _host.render_homographies(pose, depths, K, B).numpy()
+        Kd = K.to(dev)
+        got = _host.render_homographies_device(pose.to(dev), depths.to(dev), Kd, B)
+        assert_bits(got.cpu().numpy(), want, f"B={B}")
+        Kd.mul_(1.5)  # in place: the memoised inverse must not be reused
+        want2 = _host.render_homographies(pose, depths, K * 1.5, B).numpy()
+        got2 = _host.render_homographies_device(pose.to(dev), depths.to(dev), Kd, B)
+        assert_bits(got2.cpu().numpy(), want2, f"B={B} after in-place K update")

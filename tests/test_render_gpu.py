@@ -30,12 +30,18 @@ def test_render_matches_reference(name, small, meta, dev):
     assert_bits(out.cpu().numpy(), small[f"{name}_out"])
 
 
+# in-place ([B,H,W,P,4]) kernels behind mpiv_render, selected by libmpiv's debug options
+NATIVE_KERNELS = {"chunk8": dict(render_chunk=8), "chunk4": dict(render_chunk=4),
+                  "lds": dict(render_chunk=-1, render_native_lds=1),
+                  "direct": dict(render_chunk=-1, render_native_lds=0)}
+
+
 @pytest.mark.parametrize("name", RENDER_CASES)
-@pytest.mark.parametrize("native_lds", ["0", "1"])
-def test_native_and_packed_kernels_agree_with_oracle(name, native_lds, small, meta, dev, kopts):
-    """Both texel layouts (the in-place one through its direct and its LDS-staged kernel),
-    driven with the reference's own H bits."""
-    kopts(render_native_lds=native_lds)
+@pytest.mark.parametrize("native", list(NATIVE_KERNELS))
+def test_native_and_packed_kernels_agree_with_oracle(name, native, small, meta, dev, kopts):
+    """Both texel layouts (the in-place one through its chunked, direct and LDS-staged
+    kernels), driven with the reference's own H bits."""
+    kopts(**NATIVE_KERNELS[native])
     mpi = render_case_inputs(meta["small"], name)
     B, H, W, P, _ = mpi.shape
     homs = torch.tensor(small[f"{name}_H"]).permute(1, 0, 2, 3).reshape(B, P, 9).contiguous()
@@ -302,3 +308,48 @@ def test_multiview_ct_partials(mv, dev, kopts):
         parts.append(ct)
     got = _lib.combine_ct(torch.stack(parts)).cpu().numpy()
     np.testing.assert_allclose(got, oracle.render(full, homs.numpy()), rtol=0, atol=1e-5)
+
+
+def _chunk_case(H, W, P, V, seed):
+    """V views of V different MPIs (non-broadcast, the training caller's layout) from large
+    rotations / translations (planes partly behind the camera, taps far off the image)."""
+    from mpi_vision_amd import _host
+    g = torch.Generator().manual_seed(seed)
+    mpi = configs.synthetic_mpi(V, H, W, P, seed)
+    poses = [configs.pose_from(configs.rot_y(0.2), (0.01, 0.0, 0.0))]
+    for k in range(V - 1):
+        t = ((torch.rand(3, generator=g) - 0.5) * (0.4 + k)).tolist()
+        poses.append(configs.pose_from(configs.rot_y((k - 2) * 11.0), t))
+    K = configs.f32([configs.intrinsics_matrix(90.0, 85.0, W / 2.0, H / 2.0)] * V)
+    homs = _host.render_homographies(configs.f32(poses), configs.f32(configs.inv_depths(0.5, 50, P)), K, V)
+    return mpi, homs
+
+
+@pytest.mark.parametrize("ch", [4, 8])
+@pytest.mark.parametrize("shape", [(37, 203, 13), (70, 150, 9), (33, 64, 8), (21, 70, 3), (5, 130, 21)])
+def test_chunk_kernel_odd_shapes_extreme_poses(ch, shape, dev, kopts):
+    """render_chunk_kernel: plane counts that leave a partial last chunk, partial tiles in
+    x and y, non-broadcast batches and extreme views: bit-exact vs the oracle."""
+    kopts(render_chunk=ch)
+    H, W, P = shape
+    mpi, homs = _chunk_case(H, W, P, 5, seed=H + W + P)
+    want = oracle.render(mpi.numpy(), homs.numpy())
+    dmpi = mpi.to(dev)
+    out = torch.empty((5, H, W, 3), device=dev)
+    _lib._call("mpiv_render", dmpi, _lib._strides(dmpi), 5, H, W, P, homs.to(dev), out, _lib._stream(dev))
+    assert_bits(out.cpu().numpy(), want)
+
+
+def test_chunk_kernel_plane_and_pixel_strides(dev):
+    """The drop-in on a plane-sliced / cropped view of a larger tensor (planes still
+    contiguous per pixel, pixel and row strides larger than P*4): the chunked kernel reads
+    it in place, bit-exact vs the oracle on the same values."""
+    H, W, P = 40, 72, 11
+    big = configs.synthetic_mpi(2, H + 3, W + 5, P + 6, 21)
+    view = big.to(dev)[:, 1:1 + H, 2:2 + W, 3:3 + P, :]
+    assert _lib.chunk_layout_ok(view) and not view.is_contiguous()
+    _, homs = _chunk_case(H, W, P, 2, seed=5)
+    want = oracle.render(big[:, 1:1 + H, 2:2 + W, 3:3 + P, :].contiguous().numpy(), homs.numpy())
+    out = torch.empty((2, H, W, 3), device=dev)
+    _lib._call("mpiv_render", view, _lib._strides(view), 2, H, W, P, homs.to(dev), out, _lib._stream(dev))
+    assert_bits(out.cpu().numpy(), want)

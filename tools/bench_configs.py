@@ -157,13 +157,16 @@ def c4(dev, it, wu):
     homs = _host.render_homographies(configs.f32(c["poses"][:1]), configs.f32(c["depths"]),
                                      configs.f32([c["K"]]), 1).to(dev)
     out = torch.empty((1, H, W, 3), device=dev)
-    ms, mn = timed(lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out,
-                                      _lib._stream(dev)), it, wu)
-    report("c4 native kernel (reference layout in place), 1 view", ms, mn, per_view, H * W / 1e6)
+    for label, opts in (("chunked CH=8 (default)", {}), ("chunked CH=4", {"render_chunk": 4}),
+                        ("one pixel per lane", {"render_chunk": -1})):
+        with _lib.debug(**opts):
+            ms, mn = timed(lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out,
+                                              _lib._stream(dev)), it, wu)
+        report(f"c4 in-place kernel (reference layout), {label}, 1 view", ms, mn, per_view, H * W / 1e6)
     pose = configs.f32(c["poses"][:1]).to(dev)
     K = configs.f32([c["K"]]).to(dev)
     d = configs.f32(c["depths"]).to(dev)
-    for policy in ("pack", "native"):
+    for policy in ("auto", "pack"):
         _lib.RENDER_POLICY = policy
         ms, mn = timed(lambda: mv.mpi_render_view_torch(mpi, pose, d, K), it, wu)
         report(f"c4 mpi_render_view_torch end-to-end, 1 view, policy={policy}", ms, mn, per_view, H * W / 1e6)
