@@ -47,8 +47,8 @@ const char *mpiv_last_error(void);
 const char *mpiv_build_id(void);
 
 /* Debug / A/B hook, never needed in production: selects a non-default kernel variant
- * by name ("render_mv", "render_pair", "render_native_lds", "render_chunk", "sweep_tile",
- * "sweep_store", "box_shrink"; "reset" restores every default).  Process-wide;
+ * by name ("render_mv", "render_pair", "render_native_lds", "render_chunk", "render_ring",
+ * "render_tile", "sweep_tile", "sweep_store", "box_shrink"; "reset" restores every default).  Process-wide;
  * returns MPIV_ERR_ARG for an unknown name. */
 int mpiv_debug_set(const char *name, int value);
 
@@ -76,7 +76,8 @@ int mpiv_pack_planes(const float *mpi_view, const int64_t strides[4], int H, int
                      float *packed, void *stream);
 
 /* mpi_render_view_torch on a packed MPI (mpiv_pack_planes layout) for V views at once.
- * homs [V][P][9]; out [V,H,W,3] contiguous. */
+ * homs [V][P][9]; out [V,H,W,3] contiguous.  Direct bilinear gathers, blocks ordered so
+ * the views of one output tile share an XCD's L2 (render.hip). */
 int mpiv_render_packed(const float *packed, int H, int W, int P, const float *homs, int V,
                        float *out, void *stream);
 

@@ -86,7 +86,7 @@ def chunk_layout_ok(rgba_layers: torch.Tensor) -> bool:
     CH = 4 if P <= 4 else 8
     rec = ((H - 1) * st[1] + (W - 1) * st[2]) * 4 + CH * 16
     return (rec < _KOOB and st[1] // 4 < (1 << 22) and st[2] // 4 < (1 << 22)
-            and 4 * 64 * CH * 16 + P * 36 <= _CHUNK_LDS)
+            and 4 * 64 * (CH + 1) * 16 + P * 36 <= _CHUNK_LDS)
 
 
 def source_hash() -> str | None:

@@ -12,6 +12,7 @@
 #include "render.hip"
 #include "render_lds.hip"
 #include "render_chunk.hip"
+#include "render_ring.hip"
 #include "render_mv.hip"
 #include "render_bwd.hip"
 #include "sweep.hip"
@@ -47,25 +48,32 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //   render_mv=1        launches of >= 4 views use the multi-view LDS kernel (render_mv.hip)
 //   render_pair=1|2    the direct render takes pixel pairs sharing taps (render_pair_kernel)
 //   render_native_lds=0  mpiv_render gathers directly from the [B,H,W,P,4] tensor
-//   render_chunk=-1|4|8  mpiv_render's in-place chunked kernel off, or CH planes per chunk
-//                      (default 0 = automatic: 8, or 4 for P <= 4)
+//   render_chunk=-1|4|8|104|108  mpiv_render's in-place chunked kernel off, or CH planes per
+//                      chunk (+100: two composite phases per chunk); default 0 = automatic
+//                      (8, or 4 for P <= 4)
+//   render_ring=-1|0|1..6  packed render through the LDS-DMA ring kernel (render_ring.hip):
+//                      off / automatic / forced with geometry k (kRingGeo: waves, rows per
+//                      lane, slots, fills per wave and plane)
+//   render_tile=0|2|4|8  direct packed render with R rows per work-item (render_rows_kernel)
 //   sweep_tile=1       the sweep uses the tile kernel; sweep_store=k (k >= 0) the grouped one
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
 //                      forces their per-sample global fallback (tests)
 // Relaxed atomics: a launch reads each option once; setting options while another thread
 // launches is a test-harness race on which kernel runs, never on memory.
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
-                kOptRenderChunk, kNumOpts };
+                kOptRenderChunk, kOptRenderRing, kOptRenderTile, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
-                                         "sweep_tile", "sweep_store", "box_shrink", "render_chunk"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0};
+                                         "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
+                                         "render_tile"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
 constexpr int64_t kMaxGridYZ = 65535;
 constexpr int kNativeLdsMaxP = 16;
 constexpr int kChunkMaxLds = 65536;  // render_chunk_kernel: slots + P homographies, default LDS limit
+constexpr int kChunkSplit = 1;       // composite phases per chunk (render_chunk.hip SPLIT)
 constexpr int64_t kMaxGridX = 2147483647;
 
 }  // namespace
@@ -112,18 +120,23 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
     // in place at full-line coalescing (render_chunk.hip): planes contiguous per pixel
     // (s.p == 4), every offset from a chunk base below the buffer's out-of-range offset
     const int ch_opt = opt(kOptRenderChunk);
-    const int CH = ch_opt ? ch_opt : (P <= 4 ? 4 : 8);
+    const int CH = ch_opt > 0 ? ch_opt % 100 : (P <= 4 ? 4 : 8);
+    const int SPLIT = ch_opt > 0 ? (ch_opt >= 100 ? 2 : 1) : kChunkSplit;
     const int64_t rec = ((int64_t)(H - 1) * s.y + (int64_t)(W - 1) * s.x) * 4 + CH * 16;
-    const size_t ch_lds = (size_t)(CH == 8 ? chunk_slot_floats<8>() : chunk_slot_floats<4>()) * 4 + (size_t)P * 36;
+    const size_t ch_lds = (size_t)4 * (kWave / SPLIT) * (CH + 1) * 16 + (size_t)P * 36;
     if (vec && fast && s.p == 4 && ch_opt >= 0 && (CH == 4 || CH == 8) && rec < (int64_t)kOOB &&
         s.y / 4 < (1 << 22) && s.x / 4 < (1 << 22) && ch_lds <= (size_t)kChunkMaxLds) {
         const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * B;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_render: too many blocks");
         const ChunkGeom cg{(int)(s.y / 4), (int)(s.x / 4), (int)rec};
-        if (CH == 8)
-            render_chunk_kernel<8><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
+        if (CH == 8 && SPLIT == 2)
+            render_chunk_kernel<8, 2><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
+        else if (CH == 8)
+            render_chunk_kernel<8, 1><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
+        else if (SPLIT == 2)
+            render_chunk_kernel<4, 2><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
         else
-            render_chunk_kernel<4><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
+            render_chunk_kernel<4, 1><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
         return launched("mpiv_render");
     }
     // footprints staged through LDS, read in place (render_lds.hip render_lds_native_kernel):
@@ -196,6 +209,39 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             render_mv_kernel<false><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, shrink, homs, out);
         return launched(nm);
     }
+    // LDS-DMA ring (render_ring.hip): footprints streamed into LDS several planes ahead
+    // opt-in A/B only: measured back to back, the ring ties the direct kernel on single views
+    // (0.47 ms both) and loses on multi-view launches and stretched footprints
+    if (const int ring = (variant == 0 && fast && p_end - p_begin <= kRMaxP) ? opt(kOptRenderRing) : -1;
+        ring > 0) {
+        // ring geometry: {waves, rows per lane, slots, fills per wave and plane}
+        static const int kRingGeo[][4] = {{4, 2, 4, 4}, {4, 4, 3, 5}, {4, 2, 3, 4}, {8, 1, 2, 2},
+                                          {8, 1, 3, 2}, {8, 1, 4, 2}, {8, 2, 2, 3}, {16, 1, 2, 2}};
+        if (ring > 8) return fail(MPIV_ERR_ARG, "%s: unknown ring geometry %d", nm, ring);
+        const int* geo = kRingGeo[ring - 1];
+        const int ty = geo[0] * geo[1];
+        const int64_t nb = (int64_t)blocks(W, kRTX) * blocks(H, ty) * V;
+        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+#define MPIV_RING(NW, RPL, NS, F)                                                                                \
+    if (ct)                                                                                                     \
+        render_ring_kernel<true, NW, RPL, NS, F><<<(unsigned)nb, NW * 64, 0, st>>>(pk, ps, g, V, p_begin, p_end, \
+                                                                                   back, homs, out);           \
+    else                                                                                                        \
+        render_ring_kernel<false, NW, RPL, NS, F><<<(unsigned)nb, NW * 64, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, \
+                                                                                    homs, out)
+        switch (ring) {
+            case 1: MPIV_RING(4, 2, 4, 4); break;
+            case 2: MPIV_RING(4, 4, 3, 5); break;
+            case 3: MPIV_RING(4, 2, 3, 4); break;
+            case 4: MPIV_RING(8, 1, 2, 2); break;
+            case 5: MPIV_RING(8, 1, 3, 2); break;
+            case 6: MPIV_RING(8, 1, 4, 2); break;
+            case 7: MPIV_RING(8, 2, 2, 3); break;
+            default: MPIV_RING(16, 1, 2, 2); break;
+        }
+#undef MPIV_RING
+        return launched(nm);
+    }
     // pixel pairs sharing their common taps (render.hip render_pair_kernel): opt-in A/B,
     // 20 % fewer gathers but 117 VGPRs (4 waves/SIMD), measured 3 % slower
     if (const int pair = fast ? opt(kOptRenderPair) : 0) {  // 1: two planes in flight, 2: one
@@ -209,6 +255,21 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             render_pair_kernel<false, true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
         else
             render_pair_kernel<false, false><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
+        return launched(nm);
+    }
+    // R rows per work-item, planes outermost (render.hip render_rows_kernel)
+    if (const int rows = fast ? opt(kOptRenderTile) : 0; rows == 2 || rows == 4 || rows == 8) {
+        const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * rows) * V;
+        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+#define MPIV_ROWS(R)                                                                                               \
+    if (ct)                                                                                                       \
+        render_rows_kernel<true, R><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out); \
+    else                                                                                                          \
+        render_rows_kernel<false, R><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out)
+        if (rows == 2) MPIV_ROWS(2);
+        else if (rows == 4) MPIV_ROWS(4);
+        else MPIV_ROWS(8);
+#undef MPIV_ROWS
         return launched(nm);
     }
     const int64_t nblocks = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;

@@ -255,6 +255,115 @@ __global__ __launch_bounds__(256) void render_packed_kernel(const float4* __rest
 }
 
 // ---------------------------------------------------------------------------
+// R vertically adjacent pixels per work-item, planes outermost (render_rows_kernel)
+// ---------------------------------------------------------------------------
+//
+// With one view per launch every texel crosses HBM about once, plus the halo its
+// neighbouring tiles re-read: a 64x4 tile's footprint is ~66x6 texels per plane, and
+// those re-reads come back from HBM/MALL whenever the neighbour reaches the plane
+// later than the L2 can hold it.  Here a lane renders rows y .. y+R-1 of its column
+// and the plane loop is outside the row loop, so row k+1's north taps are row k's
+// south taps fetched moments earlier by the same wave (an L1/L2 hit): a block tile of
+// 64 x 4R re-reads only its outer halo.  Same per-sample recipe as
+// render_packed_pixel, two samples in flight (ping-pong across rows and planes).
+template <bool CT, bool GUARD, int R>
+__device__ __forceinline__ void render_rows_pixels(const float4* __restrict__ planes, int64_t plane_stride,
+                                                   const RenderGeom& g, int p_begin, int p_end, int back,
+                                                   const float* __restrict__ hv, int x, int y0,
+                                                   float* cr, float* cg, float* cb, float* tt) {
+    static_assert(R % 2 == 0, "R must be even");
+    const float fx = (float)x;
+    const bool replace_first = !CT || back;
+    const int last = p_end - 1;
+    auto hom = [&](int p) { return load_hom(hv + (int64_t)(p < last ? p : last) * 9); };
+    auto issue = [&](int p, int k, const Hom9& h, TapSet& ts) {
+        const int q = p < last ? p : last;
+        float px, py;
+        render_pos_fast<GUARD>(h.h, fx, (float)(y0 + k), g, px, py);
+        issue_taps_padded(make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes), g.W, g.H, g.Wp, g.org,
+                          g.row, px, py, ts);
+    };
+    auto consume = [&](const TapSet& ts, int k, bool first) {
+        const f32x4 s = blend_taps(ts);
+        const float a = first ? 1.0f : s[3];
+        const float om = 1.0f - a;
+        cr[k] = over(s[0], a, om, cr[k]);
+        cg[k] = over(s[1], a, om, cg[k]);
+        cb[k] = over(s[2], a, om, cb[k]);
+        if (CT) tt[k] = tt[k] * om;
+    };
+    TapSet A, B;
+    Hom9 h = hom(p_begin), hn = hom(p_begin + 1);
+    issue(p_begin, 0, h, A);
+    for (int p = p_begin; p < p_end; ++p) {
+        const bool first = replace_first && p == p_begin;
+#pragma unroll
+        for (int k = 0; k < R; k += 2) {  // A holds (p, k)
+            issue(p, k + 1, h, B);
+            __builtin_amdgcn_sched_barrier(0);
+            consume(A, k, first);
+            if (k + 2 < R)
+                issue(p, k + 2, h, A);
+            else
+                issue(p + 1, 0, hn, A);  // past the end: the last plane again (cached, unused)
+            __builtin_amdgcn_sched_barrier(0);
+            consume(B, k + 1, first);
+        }
+        h = hn;
+        hn = hom(p + 2);
+    }
+}
+
+// render_packed_kernel's contract (FAST recipe: H, W >= 2); a 256-thread block = 64 x 4R
+// tile, wave w owns rows w*R .. w*R+R-1; XCD-aware (tile, view) order, tile-level
+// division proof.
+template <bool CT, int R>
+__global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restrict__ planes, int64_t plane_stride,
+                                                          RenderGeom g, int V, int p_begin, int p_end, int back,
+                                                          const float* __restrict__ homs, float* __restrict__ out) {
+    constexpr int TY = 4 * R;
+    const int tiles_x = (g.W + kTileX - 1) / kTileX;
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int v = lb % V;
+    const int tile = lb / V;
+    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * TY;
+    const int x = tx0 + (int)(threadIdx.x & (kWave - 1));
+    const int y0 = ty0 + (int)(threadIdx.x >> 6) * R;
+    const float* hv = homs + (int64_t)v * g.P * 9;
+    bool ok = true;
+    {
+        const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
+        const float fy0 = (float)ty0, fy1 = (float)min(ty0 + TY - 1, g.H - 1);
+        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256)
+            ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, fy0, fy1);
+    }
+    const bool proven = __syncthreads_and(ok);
+    if (x >= g.W || y0 >= g.H) return;  // rows past H inside [y0, y0+R) are computed, not stored
+    float cr[R], cg[R], cb[R], tt[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        cr[k] = -0.0f; cg[k] = -0.0f; cb[k] = -0.0f; tt[k] = 1.0f;  // render_packed_pixel: plane 0 replaces
+    }
+    if (proven)
+        render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
+    else
+        render_rows_pixels<CT, true, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int y = y0 + k;
+        if (y >= g.H) break;
+        const int64_t o = ((int64_t)v * g.H + y) * g.W + x;
+        if (CT) {
+            reinterpret_cast<float4*>(out)[o] = make_float4(cr[k], cg[k], cb[k], tt[k]);
+        } else {
+            out[o * 3 + 0] = cr[k];
+            out[o * 3 + 1] = cg[k];
+            out[o * 3 + 2] = cb[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // two horizontally adjacent pixels per work-item (render_pair_kernel)
 // ---------------------------------------------------------------------------
 //

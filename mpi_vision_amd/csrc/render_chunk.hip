@@ -47,19 +47,38 @@ struct ChunkGeom {
     int rec_bytes;     // buffer range from a chunk's base: every live tap is below it
 };
 
+// One sample in flight: four taps + the fractional offsets; the bilinear weights are
+// formed when the taps are blended (the same products as issue_taps_padded's, so the
+// result is identical) -- two VGPRs fewer per sample in flight.
+struct ChunkTaps {
+    f32x4 a, b, c, d;  // NW, NE, SW, SE
+    float wx, wy;
+};
+
+__device__ __forceinline__ f32x4 blend_chunk(const ChunkTaps& t) {
+    const float ex = 1.0f - t.wx, sy = 1.0f - t.wy;
+    const float nw = sy * ex, ne = sy * t.wx, sw = t.wy * ex, se = t.wy * t.wx;
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float acc = t.a[k] * nw;
+        acc = __builtin_fmaf(t.b[k], ne, acc);
+        acc = __builtin_fmaf(t.c[k], sw, acc);
+        acc = __builtin_fmaf(t.d[k], se, acc);
+        o[k] = acc;
+    }
+    return o;
+}
+
 // Issue the four taps of one (pixel, plane) sample from the in-place tensor.  Tap origin
 // clamped into [-2, W] x [-2, H] (defined int conversion; NaN maps to a bound and its NaN
 // weights still poison the sample, as in the reference); a tap outside the image, or any
 // tap of a lane past the last plane, gets kOOB: the buffer unit returns 0 without an access.
 __device__ __forceinline__ void issue_taps_chunk(__amdgpu_buffer_rsrc_t r, const RenderGeom& g, const ChunkGeom& cg,
-                                                 int jt, bool live, float px, float py, TapSet& t) {
+                                                 int jt, bool live, float px, float py, ChunkTaps& t) {
     const float fx0 = floorf(px), fy0 = floorf(py);
-    const float wx = px - fx0, ex = 1.0f - wx;
-    const float wy = py - fy0, sy = 1.0f - wy;
-    t.nw = sy * ex;
-    t.ne = sy * wx;
-    t.sw = wy * ex;
-    t.se = wy * wx;
+    t.wx = px - fx0;
+    t.wy = py - fy0;
     const int ix = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)g.W);
     const int iy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)g.H);
     const bool x0 = (unsigned)ix < (unsigned)g.W, x1 = (unsigned)(ix + 1) < (unsigned)g.W;
@@ -73,22 +92,18 @@ __device__ __forceinline__ void issue_taps_chunk(__amdgpu_buffer_rsrc_t r, const
     t.d = llvm_raw_buffer_load_v4f32(r, (x1 && y1) ? off + rb + pb : kOOB, 0, 0);
 }
 
-// LDS: [4 waves][64 pixels][CH] float4 sample slots, then the view's P homographies
-// (9 floats each).  Slot of (pixel q, plane j): q*CH + (j ^ swz(q)).
-template <int CH>
-__device__ __forceinline__ int chunk_slot(int q, int j) {
-    // ds_read_b128 serves 16 lanes per LDS cycle; with q's row CH*16 B wide, the XOR
-    // spreads those lanes' reads over all 16 four-bank groups (MI355X_MICROARCH.md §LDS)
-    const int swz = CH == 8 ? ((q >> 1) & 7) : ((q >> 2) & 3);
-    return q * CH + (j ^ swz);
-}
-
-template <int CH>
+// LDS: [4 waves][64 / SPLIT pixels][CH + 1] float4 sample slots (one pad texel per pixel
+// row), then the view's P homographies (9 floats each).  The pad makes both access shapes
+// bank-conflict free with IMMEDIATE offsets: a sub-step's ds_write_b128 covers CH
+// contiguous texels per pixel row, and the composite's per-plane ds_read_b128 has its 16
+// lanes of an LDS cycle on rows (CH+1)*16 B apart = 16 distinct four-bank groups
+// (MI355X_MICROARCH.md §LDS; checked for CH = 4 and 8).
+template <int CH, int SPLIT>
 constexpr int chunk_slot_floats() {
-    return 4 * kWave * CH * 4;
+    return 4 * (kWave / SPLIT) * (CH + 1) * 4;
 }
 
-template <int CH, bool GUARD>
+template <int CH, int SPLIT, bool GUARD>
 __device__ __forceinline__ void render_chunk_wave(const float* __restrict__ view, const RenderGeom& g,
                                                   const ChunkGeom& cg, const float* __restrict__ hs,
                                                   f32x4* __restrict__ slot, int tx0, int y, int lane,
@@ -107,13 +122,41 @@ __device__ __forceinline__ void render_chunk_wave(const float* __restrict__ view
         return make_rsrc(view + (int64_t)c * CH * 4, cg.rec_bytes);
     };
     // sub-step k of chunk c: pixel tx0 + k*PPS + i, plane c*CH + j
-    auto issue = [&](int c, int k, const float* hh, TapSet& ts) {
+    auto issue = [&](int c, int k, const float* hh, ChunkTaps& ts) {
         float px, py;
         chunk_pos<GUARD>(hh, (float)(tx0 + k * PPS + i), fy, g, px, py);
         issue_taps_chunk(rsrc(c), g, cg, j, c * CH + j < g.P, px, py, ts);
     };
-    auto put = [&](int k, const TapSet& ts) { slot[chunk_slot<CH>(k * PPS + i, j)] = blend_taps(ts); };
-    TapSet A, B;
+    constexpr int QP = kWave / SPLIT;  // pixels per composite phase
+    constexpr int KP = CH / SPLIT;     // sub-steps per composite phase
+    auto put = [&](int k, const ChunkTaps& ts) { slot[((k * PPS + i) % QP) * (CH + 1) + j] = blend_chunk(ts); };
+    // composite phase h: lane = pixel tx0 + lane (lanes of that phase only), planes
+    // c*CH .. c*CH+CH-1 back to front
+    auto over_px = [&](const f32x4& s, bool first) {
+        const float a = first ? 1.0f : s[3];  // plane 0 replaces (render_packed_pixel)
+        const float om = 1.0f - a;
+        cr = over(s[0], a, om, cr);
+        cg_ = over(s[1], a, om, cg_);
+        cb = over(s[2], a, om, cb);
+    };
+    auto composite = [&](int c, int h) {
+        if (SPLIT == 1 || lane / QP == h) {
+            const f32x4* row = slot + (lane % QP) * (CH + 1);
+            if (c * CH + CH <= g.P) {  // full chunk: reads in flight 4 at a time, no branches
+#pragma unroll
+                for (int j0 = 0; j0 < CH; j0 += 4) {
+                    f32x4 s[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) s[jj] = row[j0 + jj];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) over_px(s[jj], c == 0 && j0 + jj == 0);
+                }
+            } else {
+                for (int jj = 0; c * CH + jj < g.P; ++jj) over_px(row[jj], c * CH + jj == 0);
+            }
+        }
+    };
+    ChunkTaps A, B;
     load_h(0, h);
     issue(0, 0, h, A);
     for (int c = 0; c < nchunk; ++c) {
@@ -131,33 +174,21 @@ __device__ __forceinline__ void render_chunk_wave(const float* __restrict__ view
             }
             __builtin_amdgcn_sched_barrier(0);
             put(k + 1, B);
-        }
-        // composite: lane = pixel tx0 + lane, planes c*CH .. c*CH+CH-1 back to front
-#pragma unroll
-        for (int jj = 0; jj < CH; ++jj) {
-            const int p = c * CH + jj;
-            if (p < g.P) {
-                const f32x4 s = slot[chunk_slot<CH>(lane, jj)];
-                const float a = p == 0 ? 1.0f : s[3];  // plane 0 replaces (render_packed_pixel)
-                const float om = 1.0f - a;
-                cr = over(s[0], a, om, cr);
-                cg_ = over(s[1], a, om, cg_);
-                cb = over(s[2], a, om, cb);
-            }
+            if ((k + 2) % KP == 0) composite(c, (k + 1) / KP);
         }
     }
 }
 
 // One block = 4 waves = a 64x4 output tile of one view; blocks in render_packed_kernel's
-// XCD-aware (tile, view) order.  Dynamic LDS: chunk_slot_floats<CH>() + P*9 floats.
-template <int CH>
-__global__ __launch_bounds__(256) void render_chunk_kernel(const float* __restrict__ mpi, int64_t view_stride,
+// XCD-aware (tile, view) order.  Dynamic LDS: chunk_slot_floats<CH, SPLIT>() + P*9 floats.
+template <int CH, int SPLIT>
+__global__ __launch_bounds__(256, SPLIT == 2 ? 6 : 1) void render_chunk_kernel(const float* __restrict__ mpi, int64_t view_stride,
                                                            RenderGeom g, ChunkGeom cg, int V,
                                                            const float* __restrict__ homs,
                                                            float* __restrict__ out) {
     extern __shared__ float4 chunk_lds[];
     f32x4* slots = reinterpret_cast<f32x4*>(chunk_lds);
-    float* hs = reinterpret_cast<float*>(chunk_lds) + chunk_slot_floats<CH>();
+    float* hs = reinterpret_cast<float*>(chunk_lds) + chunk_slot_floats<CH, SPLIT>();
     const int tiles_x = (g.W + kTileX - 1) / kTileX;
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
     const int v = lb % V;
@@ -175,12 +206,12 @@ __global__ __launch_bounds__(256) void render_chunk_kernel(const float* __restri
     const int y = ty0 + wave;
     if (y >= g.H) return;  // whole wave; no barrier follows
     const float* view = mpi + (int64_t)v * view_stride;
-    f32x4* slot = slots + wave * kWave * CH;
+    f32x4* slot = slots + wave * (kWave / SPLIT) * (CH + 1);
     float cr = -0.0f, cgr = -0.0f, cb = -0.0f;
     if (proven)
-        render_chunk_wave<CH, false>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb);
+        render_chunk_wave<CH, SPLIT, false>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb);
     else
-        render_chunk_wave<CH, true>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb);
+        render_chunk_wave<CH, SPLIT, true>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb);
     const int x = tx0 + lane;
     if (x < g.W) {
         float* o = out + (((int64_t)v * g.H + y) * g.W + x) * 3;

@@ -249,11 +249,17 @@ def test_multiview_kernel_bit_exact(shrink, dev, kopts):
 
 def _variant_env(kopts, mv):
     """mv "0" / "1": direct / multi-view LDS kernel; "pair" / "pair1": the pixel-pair
-    tap-sharing kernel with two / one planes in flight (A/B)."""
-    kopts(render_mv=1 if mv == "1" else 0, render_pair={"pair": 1, "pair1": 2}.get(mv, 0))
+    tap-sharing kernel with two / one planes in flight (A/B); "ring<k>": the LDS-DMA ring
+    kernel with tile geometry k (render_ring.hip)."""
+    kopts(render_mv=1 if mv == "1" else 0, render_pair={"pair": 1, "pair1": 2}.get(mv, 0),
+          render_ring=int(mv[4:]) if mv.startswith("ring") else -1,
+          render_tile=int(mv[4:]) if mv.startswith("tile") else 0)
 
 
-@pytest.mark.parametrize("variant", ["pair", "pair1"])
+RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8"]
+
+
+@pytest.mark.parametrize("variant", ["pair", "pair1"] + RING)
 def test_sharing_kernels_odd_width_and_extreme_poses(variant, dev, kopts):
     """The tap-sharing kernels on an odd width (the last pair has no second pixel; a
     partial wave), a partial tile and strongly minifying / magnifying views (neighbours
@@ -272,7 +278,7 @@ def test_sharing_kernels_odd_width_and_extreme_poses(variant, dev, kopts):
     assert_bits(got.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("mv", ["0", "1", "pair", "pair1"])
+@pytest.mark.parametrize("mv", ["0", "1", "pair", "pair1"] + RING)
 def test_multiview_camera_path_many_views(mv, dev, kopts):
     """A config-4-style sway path (40 consecutive poses of the 1000-pose path, 24 planes,
     viewer camera) rendered in one launch by the direct and the multi-view kernel:
@@ -290,7 +296,7 @@ def test_multiview_camera_path_many_views(mv, dev, kopts):
     assert_bits(got.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("mv", ["0", "1", "pair", "pair1"])
+@pytest.mark.parametrize("mv", ["0", "1", "pair", "pair1"] + RING)
 def test_multiview_ct_partials(mv, dev, kopts):
     """Plane-range (C, T) partials of 6 views (direct and multi-view kernel) equal the
     oracle's bit for bit, and their ordered combine equals the sequential render (1e-5)."""
@@ -353,3 +359,23 @@ def test_chunk_kernel_plane_and_pixel_strides(dev):
     out = torch.empty((2, H, W, 3), device=dev)
     _lib._call("mpiv_render", view, _lib._strides(view), 2, H, W, P, homs.to(dev), out, _lib._stream(dev))
     assert_bits(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("ring", RING)
+@pytest.mark.parametrize("name", RENDER_CASES)
+def test_ring_kernel_golden_cases(ring, name, small, meta, dev, kopts):
+    """The LDS-DMA ring render on the reference golden cases (incl. 'render_big': planes
+    whose footprints do not fit a slot render direct) and on extreme views: bit-exact."""
+    _variant_env(kopts, ring)
+    mpi = render_case_inputs(meta["small"], name)
+    B, H, W, P, _ = mpi.shape
+    homs = torch.tensor(small[f"{name}_H"]).permute(1, 0, 2, 3).reshape(B, P, 9).contiguous()
+    for b in range(B):
+        packed = _lib.pack_planes(mpi[b].contiguous().to(dev))
+        got = _lib.render_packed(packed, homs[b:b + 1])
+        assert_bits(got.cpu().numpy(), small[f"{name}_out"][b:b + 1], f"{name}[{b}]")
+    mpi, homs = _multiview_case(6, seed=11)
+    V, P = homs.shape[0], homs.shape[1]
+    H, W = mpi.shape[1], mpi.shape[2]
+    want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.numpy())
+    assert_bits(_lib.render_packed(_lib.pack_planes(mpi[0].to(dev)), homs).cpu().numpy(), want, "extreme views")

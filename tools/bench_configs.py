@@ -146,7 +146,15 @@ def c4(dev, it, wu):
                                          configs.f32([c["K"]] * V), V).to(dev)
         out = torch.empty((V, H, W, 3), device=dev)
         n_it = it if V < 125 else max(3, it // 4)
-        for label, opts in (("direct gathers (default)", {}), ("multi-view LDS kernel", {"render_mv": 1})):
+        for label, opts in (("default routing", {}), ("direct gathers", {"render_ring": -1}),
+                            ("multi-view LDS kernel", {"render_mv": 1, "render_ring": -1}),
+                            ("LDS-DMA ring 64x8/4", {"render_ring": 1}), ("LDS-DMA ring 64x16/3", {"render_ring": 2}),
+                            ("LDS-DMA ring 64x8/3", {"render_ring": 3}),
+                            ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("LDS-DMA ring 8w 64x8/3", {"render_ring": 5}),
+                            ("LDS-DMA ring 8w 64x8/4", {"render_ring": 6}), ("LDS-DMA ring 8w 64x16/2", {"render_ring": 7}),
+                            ("LDS-DMA ring 16w 64x16/2", {"render_ring": 8})):
+            if V == 125 and "ring" in label:
+                continue
             with _lib.debug(**opts):
                 ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), n_it, 1)
             report(f"c4 1024^2x128 packed, {label}, {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
@@ -173,6 +181,28 @@ def c4(dev, it, wu):
     _lib.RENDER_POLICY = "auto"
 
 
+def c4n(dev, it, wu):
+    """Config 4 through the in-place (reference layout) kernels only: chunked variants
+    (render_chunk = CH, +100 = two composite phases per chunk) and the drop-in."""
+    c = configs.config4()
+    H, W, P = c["H"], c["W"], c["P"]
+    mpi = gen_mpi(H, W, P, 0, dev)
+    per_view = P * H * W * 16 + H * W * 12
+    homs = _host.render_homographies(configs.f32(c["poses"][:1]), configs.f32(c["depths"]),
+                                     configs.f32([c["K"]]), 1).to(dev)
+    out = torch.empty((1, H, W, 3), device=dev)
+    for opt in (0, 8, 108, 4, 104):
+        with _lib.debug(render_chunk=opt):
+            ms, mn = timed(lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out,
+                                              _lib._stream(dev)), it, wu)
+        report(f"c4 in-place kernel, render_chunk={opt}, 1 view", ms, mn, per_view, H * W / 1e6)
+    pose = configs.f32(c["poses"][:1]).to(dev)
+    K = configs.f32([c["K"]]).to(dev)
+    d = configs.f32(c["depths"]).to(dev)
+    ms, mn = timed(lambda: mv.mpi_render_view_torch(mpi, pose, d, K), it, wu)
+    report("c4 mpi_render_view_torch end-to-end, 1 view (default routing)", ms, mn, per_view, H * W / 1e6)
+
+
 def c5(dev, it, wu):
     """Per-GPU share of the 8-way plane-sharded 4096x2160x256 render + the combine."""
     c = configs.config5()
@@ -185,9 +215,16 @@ def c5(dev, it, wu):
     homs = _host.render_homographies(configs.f32(c["poses"]), configs.f32(c["depths"]), configs.f32([c["K"]]), 1)
     homs_local = homs[:, :PL].contiguous().to(dev)
     ct = torch.empty((1, H, W, 4), device=dev)
-    ms, mn = timed(lambda: _lib.render_packed_ct(packed, homs_local, back=True, out=ct), it, wu)
-    report(f"c5 plane shard: {PL} of {P} planes, 4096x2160 partial (C,T)", ms, mn, PL * H * W * 16 + H * W * 16,
-           H * W / 1e6)
+    for label, opts in (("default routing", {}), ("direct gathers", {"render_ring": -1}),
+                        ("LDS-DMA ring 64x8/4", {"render_ring": 1}), ("LDS-DMA ring 64x16/3", {"render_ring": 2}),
+                        ("LDS-DMA ring 64x8/3", {"render_ring": 3}),
+                        ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("LDS-DMA ring 8w 64x8/3", {"render_ring": 5}),
+                        ("LDS-DMA ring 8w 64x8/4", {"render_ring": 6}), ("LDS-DMA ring 8w 64x16/2", {"render_ring": 7}),
+                        ("LDS-DMA ring 16w 64x16/2", {"render_ring": 8})):
+        with _lib.debug(**opts):
+            ms, mn = timed(lambda: _lib.render_packed_ct(packed, homs_local, back=True, out=ct), it, wu)
+        report(f"c5 plane shard: {PL} of {P} planes, 4096x2160 partial (C,T), {label}", ms, mn,
+               PL * H * W * 16 + H * W * 16, H * W / 1e6)
     bh = H // G
     parts = torch.rand((G, 1, bh, W, 4), device=dev)
     ms, mn = timed(lambda: _lib.combine_ct(parts), it, wu)

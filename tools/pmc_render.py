@@ -5,7 +5,8 @@
 
 direct = the default direct-gather kernel, pair = pixel pairs sharing taps,
 mv = the multi-view LDS kernel (debug option render_mv=1), lds = the single-view LDS
-variant.
+variant; chunk<N> = mpiv_render on the reference [1,H,W,P,4] layout with debug option
+render_chunk=N (render_chunk.hip), native = the same layout, one pixel per lane.
 """
 import argparse
 import os
@@ -30,6 +31,17 @@ dev = torch.device("cuda:0")
 c = configs.config4()
 H, W, P, V = c["H"], c["W"], c["P"], a.views
 g = torch.Generator(device=dev).manual_seed(0)
+if a.variant.startswith("chunk") or a.variant == "native":
+    _lib.load().mpiv_debug_set(b"render_chunk", int(a.variant[5:]) if a.variant != "native" else -1)
+    mpi = torch.rand((V, H, W, P, 4), generator=g, device=dev)
+    homs = _host.render_homographies(configs.f32(c["poses"][:V]), configs.f32(c["depths"]),
+                                     configs.f32([c["K"]] * V), V).to(dev)
+    out = torch.empty((V, H, W, 3), device=dev)
+    for _ in range(a.iters):
+        _lib._call("mpiv_render", mpi, _lib._strides(mpi), V, H, W, P, homs, out, _lib._stream(dev))
+    torch.cuda.synchronize()
+    print("done", a.variant, V)
+    sys.exit(0)
 packed = torch.zeros(_lib.packed_shape(H, W, P), device=dev)
 packed[:, 2:2 + H, 2:2 + W].uniform_(generator=g)
 homs = _host.render_homographies(configs.f32(c["poses"][:V]), configs.f32(c["depths"]),
