@@ -247,7 +247,12 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     packed = _lib.pack_planes(view) if args.kernel.startswith("packed") else None
-    kernel_name = {"packed": "render_packed_kernel", "packed_lds": "render_lds_kernel", "native": "render_native_kernel",
+    # mpiv_render_packed's routing (abi.hip render_packed_impl): a near-square MPI at 1-2 or
+    # >= 32 views per launch goes to the R-rows-per-lane kernel, other view counts gather
+    # one row per work-item
+    rows = abs(W / (H - 1) - 1.0) <= 0.25 and (V <= 2 or V >= 32)
+    kernel_name = {"packed": "render_rows_kernel" if rows else "render_packed_kernel",
+                   "packed_lds": "render_lds_kernel", "native": "render_chunk_kernel",
                    "packed_mv": "render_mv_kernel" if V >= 4 else "render_packed_kernel"}[args.kernel]
     entry = "mpiv_render_packed_lds" if args.kernel == "packed_lds" else "mpiv_render_packed"
     torch.cuda.synchronize()

@@ -54,7 +54,9 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //   render_ring=-1|0|1..6  packed render through the LDS-DMA ring kernel (render_ring.hip):
 //                      off / automatic / forced with geometry k (kRingGeo: waves, rows per
 //                      lane, slots, fills per wave and plane)
-//   render_tile=0|2|4|8  direct packed render with R rows per work-item (render_rows_kernel)
+//   render_tile=-1|0|2|4|8|16|108|116|132  packed render with R rows per work-item
+//                      (render_rows_kernel; 100+R: state in LDS, render_rows_lds_kernel);
+//                      -1: off (one row per work-item), 0: automatic (R = 8 where it pays)
 //   sweep_tile=1       the sweep uses the tile kernel; sweep_store=k (k >= 0) the grouped one
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
 //                      forces their per-sample global fallback (tests)
@@ -257,8 +259,33 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             render_pair_kernel<false, false><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
         return launched(nm);
     }
-    // R rows per work-item, planes outermost (render.hip render_rows_kernel)
-    if (const int rows = fast ? opt(kOptRenderTile) : 0; rows == 2 || rows == 4 || rows == 8) {
+    // R rows per work-item, planes outermost (render.hip render_rows_kernel).  Automatic for a
+    // near-square MPI (the reference's swapped x/(H-1), y/(W-1) normalisation stretches the
+    // footprints by W/(H-1) and H/(W-1); stretched ones lose) at one or two
+    // views (single-view 0.435 vs 0.48-0.51 ms) and at >= 32 views per launch (camera-path
+    // launches: 30.7 vs 31.6 ms at 125 views); 8 views measured 2 % slower.
+    const float sxr = (float)W / (float)(H > 1 ? H - 1 : 1), syr = (float)H / (float)(W > 1 ? W - 1 : 1);
+    const bool square = sxr >= 0.8f && sxr <= 1.25f && syr >= 0.8f && syr <= 1.25f;
+    const int rows_opt = opt(kOptRenderTile);
+    const int rows_auto = (square && (V <= 2 || V >= 32) && !opt(kOptRenderMv) && !opt(kOptRenderPair)) ? 8 : 0;
+    const int rows_sel = fast ? (rows_opt ? rows_opt : rows_auto) : 0;
+    if (const int rows = rows_sel; rows == 108 || rows == 116 || rows == 132) {
+        // R rows with the compositing state in LDS (render_rows_lds_kernel)
+        const int R = rows - 100;
+        const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
+        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+#define MPIV_ROWSL(R)                                                                                                  \
+    if (ct)                                                                                                           \
+        render_rows_lds_kernel<true, R><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out); \
+    else                                                                                                              \
+        render_rows_lds_kernel<false, R><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out)
+        if (R == 8) MPIV_ROWSL(8);
+        else if (R == 16) MPIV_ROWSL(16);
+        else MPIV_ROWSL(32);
+#undef MPIV_ROWSL
+        return launched(nm);
+    }
+    if (const int rows = rows_sel; rows == 2 || rows == 4 || rows == 8 || rows == 16) {
         const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * rows) * V;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
 #define MPIV_ROWS(R)                                                                                               \
@@ -268,7 +295,8 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
         render_rows_kernel<false, R><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out)
         if (rows == 2) MPIV_ROWS(2);
         else if (rows == 4) MPIV_ROWS(4);
-        else MPIV_ROWS(8);
+        else if (rows == 8) MPIV_ROWS(8);
+        else MPIV_ROWS(16);
 #undef MPIV_ROWS
         return launched(nm);
     }

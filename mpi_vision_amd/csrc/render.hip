@@ -314,6 +314,103 @@ __device__ __forceinline__ void render_rows_pixels(const float4* __restrict__ pl
     }
 }
 
+// The same with the R rows' compositing state kept in LDS (rows loop not unrolled: the
+// register footprint of one sample in flight, so occupancy stays high for large R).
+// state: [R][256] float4 per block (cr, cg, cb, t).
+template <bool CT, bool GUARD, int R>
+__device__ __forceinline__ void render_rows_lds_pixels(const float4* __restrict__ planes, int64_t plane_stride,
+                                                       const RenderGeom& g, int p_begin, int p_end, int back,
+                                                       const float* __restrict__ hv, int x, int y0,
+                                                       float4* __restrict__ st) {
+    const float fx = (float)x;
+    const bool replace_first = !CT || back;
+    const int last = p_end - 1;
+    auto hom = [&](int p) { return load_hom(hv + (int64_t)(p < last ? p : last) * 9); };
+    auto issue = [&](int p, int k, const Hom9& h, TapSet& ts) {
+        const int q = p < last ? p : last;
+        float px, py;
+        render_pos_fast<GUARD>(h.h, fx, (float)(y0 + k), g, px, py);
+        issue_taps_padded(make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes), g.W, g.H, g.Wp, g.org,
+                          g.row, px, py, ts);
+    };
+    auto consume = [&](const TapSet& ts, int k, bool first) {
+        const f32x4 s = blend_taps(ts);
+        const float a = first ? 1.0f : s[3];
+        const float om = 1.0f - a;
+        float4 c = st[k * 256];
+        c.x = over(s[0], a, om, c.x);
+        c.y = over(s[1], a, om, c.y);
+        c.z = over(s[2], a, om, c.z);
+        if (CT) c.w = c.w * om;
+        st[k * 256] = c;
+    };
+    TapSet A, B;
+    Hom9 h = hom(p_begin), hn = hom(p_begin + 1);
+    issue(p_begin, 0, h, A);
+    for (int p = p_begin; p < p_end; ++p) {
+        const bool first = replace_first && p == p_begin;
+#pragma unroll 1
+        for (int k = 0; k < R; k += 2) {  // A holds (p, k)
+            issue(p, k + 1, h, B);
+            __builtin_amdgcn_sched_barrier(0);
+            consume(A, k, first);
+            if (k + 2 < R)
+                issue(p, k + 2, h, A);
+            else
+                issue(p + 1, 0, hn, A);
+            __builtin_amdgcn_sched_barrier(0);
+            consume(B, k + 1, first);
+        }
+        h = hn;
+        hn = hom(p + 2);
+    }
+}
+
+template <bool CT, int R>
+__global__ __launch_bounds__(256) void render_rows_lds_kernel(const float4* __restrict__ planes, int64_t plane_stride,
+                                                              RenderGeom g, int V, int p_begin, int p_end, int back,
+                                                              const float* __restrict__ homs,
+                                                              float* __restrict__ out) {
+    __shared__ float4 s_state[R * 256];
+    constexpr int TY = 4 * R;
+    const int tiles_x = (g.W + kTileX - 1) / kTileX;
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int v = lb % V;
+    const int tile = lb / V;
+    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * TY;
+    const int x = tx0 + (int)(threadIdx.x & (kWave - 1));
+    const int y0 = ty0 + (int)(threadIdx.x >> 6) * R;
+    const float* hv = homs + (int64_t)v * g.P * 9;
+    bool ok = true;
+    {
+        const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
+        const float fy0 = (float)ty0, fy1 = (float)min(ty0 + TY - 1, g.H - 1);
+        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256)
+            ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, fy0, fy1);
+    }
+    const bool proven = __syncthreads_and(ok);
+    if (x >= g.W || y0 >= g.H) return;
+    float4* st = s_state + threadIdx.x;  // this lane's row k at st[k * 256]
+    for (int k = 0; k < R; ++k) st[k * 256] = make_float4(-0.0f, -0.0f, -0.0f, 1.0f);  // plane 0 replaces
+    if (proven)
+        render_rows_lds_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, st);
+    else
+        render_rows_lds_pixels<CT, true, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, st);
+    for (int k = 0; k < R; ++k) {
+        const int y = y0 + k;
+        if (y >= g.H) break;
+        const float4 c = st[k * 256];
+        const int64_t o = ((int64_t)v * g.H + y) * g.W + x;
+        if (CT) {
+            reinterpret_cast<float4*>(out)[o] = c;
+        } else {
+            out[o * 3 + 0] = c.x;
+            out[o * 3 + 1] = c.y;
+            out[o * 3 + 2] = c.z;
+        }
+    }
+}
+
 // render_packed_kernel's contract (FAST recipe: H, W >= 2); a 256-thread block = 64 x 4R
 // tile, wave w owns rows w*R .. w*R+R-1; XCD-aware (tile, view) order, tile-level
 // division proof.
@@ -344,10 +441,15 @@ __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restri
     for (int k = 0; k < R; ++k) {
         cr[k] = -0.0f; cg[k] = -0.0f; cb[k] = -0.0f; tt[k] = 1.0f;  // render_packed_pixel: plane 0 replaces
     }
-    if (proven)
-        render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
-    else
-        render_rows_pixels<CT, true, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
+    if (!proven) {  // rare (w near 0 over the tile): the guarded one-pixel recipe, row by row
+        for (int k = 0; k < R && y0 + k < g.H; ++k) {
+            const int64_t o = ((int64_t)v * g.H + y0 + k) * g.W + x;
+            render_packed_pixel<CT, 1>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0 + k,
+                                       CT ? out + o * 4 : out + o * 3);
+        }
+        return;
+    }
+    render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const int y = y0 + k;

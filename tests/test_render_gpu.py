@@ -253,10 +253,10 @@ def _variant_env(kopts, mv):
     kernel with tile geometry k (render_ring.hip)."""
     kopts(render_mv=1 if mv == "1" else 0, render_pair={"pair": 1, "pair1": 2}.get(mv, 0),
           render_ring=int(mv[4:]) if mv.startswith("ring") else -1,
-          render_tile=int(mv[4:]) if mv.startswith("tile") else 0)
+          render_tile=int(mv[4:]) if mv.startswith("tile") else -1)
 
 
-RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8"]
+RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile16", "tile108", "tile116", "tile132"]
 
 
 @pytest.mark.parametrize("variant", ["pair", "pair1"] + RING)

@@ -146,14 +146,10 @@ def c4(dev, it, wu):
                                          configs.f32([c["K"]] * V), V).to(dev)
         out = torch.empty((V, H, W, 3), device=dev)
         n_it = it if V < 125 else max(3, it // 4)
-        for label, opts in (("default routing", {}), ("direct gathers", {"render_ring": -1}),
-                            ("multi-view LDS kernel", {"render_mv": 1, "render_ring": -1}),
-                            ("LDS-DMA ring 64x8/4", {"render_ring": 1}), ("LDS-DMA ring 64x16/3", {"render_ring": 2}),
-                            ("LDS-DMA ring 64x8/3", {"render_ring": 3}),
-                            ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("LDS-DMA ring 8w 64x8/3", {"render_ring": 5}),
-                            ("LDS-DMA ring 8w 64x8/4", {"render_ring": 6}), ("LDS-DMA ring 8w 64x16/2", {"render_ring": 7}),
-                            ("LDS-DMA ring 16w 64x16/2", {"render_ring": 8})):
-            if V == 125 and "ring" in label:
+        for label, opts in (("default routing", {}), ("direct gathers", {"render_tile": -1}),
+                            ("multi-view LDS kernel", {"render_mv": 1}),
+                            ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("rows x8 per lane", {"render_tile": 8}), ("rows x16 per lane", {"render_tile": 16})):
+            if V == 125 and ("ring" in label or "LDS kernel" in label):
                 continue
             with _lib.debug(**opts):
                 ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), n_it, 1)
@@ -215,12 +211,8 @@ def c5(dev, it, wu):
     homs = _host.render_homographies(configs.f32(c["poses"]), configs.f32(c["depths"]), configs.f32([c["K"]]), 1)
     homs_local = homs[:, :PL].contiguous().to(dev)
     ct = torch.empty((1, H, W, 4), device=dev)
-    for label, opts in (("default routing", {}), ("direct gathers", {"render_ring": -1}),
-                        ("LDS-DMA ring 64x8/4", {"render_ring": 1}), ("LDS-DMA ring 64x16/3", {"render_ring": 2}),
-                        ("LDS-DMA ring 64x8/3", {"render_ring": 3}),
-                        ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("LDS-DMA ring 8w 64x8/3", {"render_ring": 5}),
-                        ("LDS-DMA ring 8w 64x8/4", {"render_ring": 6}), ("LDS-DMA ring 8w 64x16/2", {"render_ring": 7}),
-                        ("LDS-DMA ring 16w 64x16/2", {"render_ring": 8})):
+    for label, opts in (("default routing", {}), ("direct gathers", {"render_tile": -1}),
+                        ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("rows x8 per lane", {"render_tile": 8}), ("rows x16 per lane", {"render_tile": 16})):
         with _lib.debug(**opts):
             ms, mn = timed(lambda: _lib.render_packed_ct(packed, homs_local, back=True, out=ct), it, wu)
         report(f"c5 plane shard: {PL} of {P} planes, 4096x2160 partial (C,T), {label}", ms, mn,

@@ -29,9 +29,9 @@ for k in [int(x) for x in a.poses.split(",")]:
     h = _host.render_homographies(configs.f32([c["poses"][k]]), configs.f32(c["depths"]),
                                   configs.f32([c["K"]]), 1).to(dev)
     row = {"pose": k}
-    for name, opts in (("direct", {"render_ring": -1}), ("ring4", {"render_ring": 4}), ("ring8", {"render_ring": 8}),
-                       ("rows2", {"render_ring": -1, "render_tile": 2}), ("rows4", {"render_ring": -1, "render_tile": 4}),
-                       ("rows8", {"render_ring": -1, "render_tile": 8}), ("lds", None)):
+    for name, opts in (("default", {}), ("direct", {"render_tile": -1}), ("ring4", {"render_ring": 4}),
+                       ("ring8", {"render_ring": 8}), ("rows4", {"render_tile": 4}), ("rows8", {"render_tile": 8}),
+                       ("rows16", {"render_tile": 16}), ("lds", None)):
         fn = (lambda: _lib._call("mpiv_render_packed_lds", packed, H, W, P, h, 1, out, _lib._stream(dev))) \
             if opts is None else (lambda: _lib._call("mpiv_render_packed", packed, H, W, P, h, 1, out, _lib._stream(dev)))
         with _lib.debug(**(opts or {})):
