@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 6
+#define MPIV_ABI_VERSION 7
 
 enum {
     MPIV_OK = 0,
@@ -254,6 +254,29 @@ int mpiv_deprocess_u8(const float *in, int64_t n, uint8_t *out, void *stream);
  * indices are global, so shards generated separately equal the same planes of the
  * whole MPI bit for bit: rgb U[-1,1), alpha U[0,1), plane 0 alpha 1 (synth.hip). */
 int mpiv_synth_mpi_packed(uint32_t seed, int H, int W, int p_begin, int p_end, float *packed, void *stream);
+
+/* ---- 8-bit RGBA MPIs (the reference's test MPI is uint8 PNG; utils.py:324-331 reads
+ * images as t.float() / 255) ------------------------------------------------------------ */
+
+/* One view [H,W,P,4] uint8 (element strides strides[4] = H,W,P,C) -> packed u8 planes
+ * [P][H+4][W+4] uint32 (RGBA bytes, R lowest; 4-B aligned) with a 2-texel zero border:
+ * mpiv_pack_planes' layout at 4 B per texel. */
+int mpiv_pack_planes_u8(const uint8_t *mpi_view, const int64_t strides[4], int H, int W, int P, uint32_t *packed,
+                        void *stream);
+
+/* mpiv_render_packed on a packed u8 MPI: out [V,H,W,3] fp32 equals mpiv_render_packed on
+ * the float MPI RN(u8 / 255) bit for bit (each texel channel is converted exactly before
+ * the reference's blend).  H, W >= 2. */
+int mpiv_render_packed_u8(const uint32_t *packed, int H, int W, int P, const float *homs, int V, float *out,
+                          void *stream);
+
+/* mpiv_render_packed_ct on a packed u8 MPI (plane-range partial (C, T) [V,H,W,4]). */
+int mpiv_render_packed_u8_ct(const uint32_t *packed, int H, int W, int P, int p_begin, int p_end, int back,
+                             const float *homs, int V, float *ct, void *stream);
+
+/* Counter-based synthetic u8 MPI (mpiv_synth_mpi_packed's hash, one byte per channel =
+ * the top 8 bits of its hash, plane 0 alpha 255) into the packed u8 layout. */
+int mpiv_synth_mpi_packed_u8(uint32_t seed, int H, int W, int p_begin, int p_end, uint32_t *packed, void *stream);
 
 /* ---- diagnostics ------------------------------------------------------------ */
 

@@ -7,5 +7,5 @@ from . import utils  # noqa: F401
 from .utils import *  # noqa: F401,F403
 
 __all__ = [n for n in dir(utils) if n.endswith("_torch") or n in (
-    "inv_depths", "over_composite", "mpi_from_net_output", "device", "read_file_lines", "parse_camera_lines",
+    "inv_depths", "over_composite", "mpi_from_net_output", "mpi_render_view_u8", "device", "read_file_lines", "parse_camera_lines",
     "make_intrinsics_matrix", "scale_intrinsics")]

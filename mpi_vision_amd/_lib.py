@@ -55,13 +55,17 @@ _SIGS = {
     "mpiv_assemble_mpi_packed": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_render_homographies": [_vp, _vp, _vp, _vp, _int, _int, _vp],
     "mpiv_render_homographies_device": [_vp, _vp, _vp, _vp, _int, _int, _vp, _vp],
+    "mpiv_pack_planes_u8": [_vp, _c_i64p, _int, _int, _int, _vp, _vp],
+    "mpiv_render_packed_u8": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
+    "mpiv_render_packed_u8_ct": [_vp, _int, _int, _int, _int, _int, _int, _vp, _int, _vp, _vp],
+    "mpiv_synth_mpi_packed_u8": [ctypes.c_uint32, _int, _int, _int, _int, _vp, _vp],
     "mpiv_synth_mpi_packed": [ctypes.c_uint32, _int, _int, _int, _int, _vp, _vp],
     "mpiv_assemble_mpi_backward": [_vp, _c_i64p, _vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp,
                                    _vp],
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
                           "mpiv_build_id", "mpiv_debug_set")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lib = None
 
@@ -273,6 +277,76 @@ def synth_mpi_packed(seed: int, H: int, W: int, p_begin: int, p_end: int, device
     _dev(packed)
     _call("mpiv_synth_mpi_packed", ctypes.c_uint32(seed & 0xFFFFFFFF), H, W, p_begin, p_end, packed, _stream(dev))
     return packed
+
+
+def pack_planes_u8(view: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """One 8-bit MPI view [H, W, P, 4] uint8 (any strides) -> packed u8 planes
+    [P, H+4, W+4] int32 (RGBA bytes of each texel, R lowest) with the zero border."""
+    if not isinstance(view, torch.Tensor) or view.dtype != torch.uint8:
+        raise RuntimeError("pack_planes_u8 expects a uint8 [H, W, P, 4] tensor")
+    if view.device.type != "cuda":
+        raise RuntimeError("mpi_vision_amd kernels need ROCm device tensors; there is no CPU path")
+    dev = view.device
+    H, W, P, C = view.shape
+    if C != 4:
+        raise RuntimeError(f"MPI texels must have 4 channels (RGBA), got {C}")
+    shape = (P, H + 2 * PAD, W + 2 * PAD)
+    if out is None:
+        packed = torch.empty(shape, device=dev, dtype=torch.int32)
+    elif tuple(out.shape) != shape or out.dtype != torch.int32 or not out.is_contiguous() or out.device != dev:
+        raise RuntimeError(f"pack_planes_u8: out must be a contiguous int32 {shape} tensor on {dev}")
+    else:
+        packed = out
+    _call("mpiv_pack_planes_u8", view, _strides(view), H, W, P, packed, _stream(dev))
+    return packed
+
+
+def synth_mpi_packed_u8(seed: int, H: int, W: int, p_begin: int, p_end: int, device) -> torch.Tensor:
+    """Planes [p_begin, p_end) of the counter-based synthetic u8 MPI `seed`, packed u8."""
+    dev = torch.device(device)
+    packed = torch.empty((p_end - p_begin, H + 2 * PAD, W + 2 * PAD), device=dev, dtype=torch.int32)
+    _call("mpiv_synth_mpi_packed_u8", ctypes.c_uint32(seed & 0xFFFFFFFF), H, W, p_begin, p_end, packed,
+          _stream(dev))
+    return packed
+
+
+def _u8_hw(packed: torch.Tensor):
+    if packed.dim() != 3 or packed.dtype != torch.int32 or not packed.is_contiguous() or packed.device.type != "cuda":
+        raise RuntimeError("packed u8 MPI must be a contiguous int32 [P, H+4, W+4] ROCm tensor")
+    return packed.shape[0], packed.shape[1] - 2 * PAD, packed.shape[2] - 2 * PAD
+
+
+def render_packed_u8(packed: torch.Tensor, homs: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """packed u8 [P,H+4,W+4] + homs [V,P,9] -> [V,H,W,3] fp32, bit-identical to rendering the
+    float MPI u8.float() / 255 (render_u8.hip)."""
+    P, H, W = _u8_hw(packed)
+    dev = packed.device
+    V = homs.shape[0]
+    h = _up(homs.reshape(V, P, 9), dev)
+    if out is None:
+        out = torch.empty((V, H, W, 3), device=dev, dtype=torch.float32)
+    else:
+        _check_out(out, (V, H, W, 3), dev, "render_packed_u8")
+    if V == 0:
+        return out
+    _call("mpiv_render_packed_u8", packed, H, W, P, h, V, out, _stream(dev))
+    return out
+
+
+def render_packed_u8_ct(packed: torch.Tensor, homs: torch.Tensor, back: bool, p_begin: int = 0,
+                        p_end: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Plane-range partial (C, T) [V,H,W,4] of a packed u8 MPI (plane sharding)."""
+    P, H, W = _u8_hw(packed)
+    dev = packed.device
+    p_end = P if p_end is None else p_end
+    V = homs.shape[0]
+    h = _up(homs.reshape(V, P, 9), dev)
+    if out is None:
+        out = torch.empty((V, H, W, 4), device=dev, dtype=torch.float32)
+    else:
+        _check_out(out, (V, H, W, 4), dev, "render_packed_u8_ct")
+    _call("mpiv_render_packed_u8_ct", packed, H, W, P, p_begin, p_end, int(back), h, V, out, _stream(dev))
+    return out
 
 
 def unpack_planes(packed: torch.Tensor) -> torch.Tensor:

@@ -19,6 +19,7 @@
 #include "geometry.hip"
 #include "assemble.hip"
 #include "synth.hip"
+#include "render_u8.hip"
 
 namespace {
 
@@ -765,6 +766,80 @@ int mpiv_synth_mpi_packed(uint32_t seed, int H, int W, int p_begin, int p_end, f
     synth_packed_kernel<<<dim3(blocks(npix, 256), p_end - p_begin), 256, 0, S(stream)>>>(
         seed, H, W, p_begin, make_fastdiv((unsigned)(W + 2 * kPad)), reinterpret_cast<float4*>(packed), npix);
     return launched(nm);
+}
+
+// ---- 8-bit RGBA MPI (render_u8.hip) -------------------------------------------------
+
+int mpiv_pack_planes_u8(const uint8_t* mpi, const int64_t st[4], int H, int W, int P, uint32_t* packed,
+                        void* stream) {
+    const char* nm = "mpiv_pack_planes_u8";
+    if (!mpi || !st || !packed) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    if (reinterpret_cast<uintptr_t>(packed) & 3) return fail(MPIV_ERR_ARG, "%s: packed must be 4-byte aligned", nm);
+    const int64_t npix = (int64_t)(H + 2 * kPad) * (W + 2 * kPad);
+    if (npix * 4 >= (int64_t)kOOB || blocks(P, kPackPl) > kMaxGridYZ)
+        return fail(MPIV_ERR_ARG, "%s: padded plane larger than 2 GiB or too many planes", nm);
+    const NativeStrides s{0, st[0], st[1], st[2], st[3]};
+    pack_planes_u8_kernel<<<dim3(blocks(npix, kPackPix), blocks(P, kPackPl)), 256, 0, S(stream)>>>(
+        mpi, s, H, W, P, make_fastdiv((unsigned)(W + 2 * kPad)), packed, npix);
+    return launched(nm);
+}
+
+int mpiv_synth_mpi_packed_u8(uint32_t seed, int H, int W, int p_begin, int p_end, uint32_t* packed, void* stream) {
+    const char* nm = "mpiv_synth_mpi_packed_u8";
+    if (!packed) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (H <= 0 || W <= 0 || p_begin < 0 || p_end <= p_begin) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    if (reinterpret_cast<uintptr_t>(packed) & 3) return fail(MPIV_ERR_ARG, "%s: packed must be 4-byte aligned", nm);
+    const int64_t npix = (int64_t)(H + 2 * kPad) * (W + 2 * kPad);
+    if (npix * 4 >= (int64_t)kOOB || (int64_t)H * W >= (1ll << 31) || p_end - p_begin > kMaxGridYZ)
+        return fail(MPIV_ERR_ARG, "%s: padded plane larger than 2 GiB or too many planes", nm);
+    synth_packed_u8_kernel<<<dim3(blocks(npix, 256), p_end - p_begin), 256, 0, S(stream)>>>(
+        seed, H, W, p_begin, make_fastdiv((unsigned)(W + 2 * kPad)), packed, npix);
+    return launched(nm);
+}
+
+static int render_u8_impl(const uint32_t* packed, int H, int W, int P, int p_begin, int p_end, int back,
+                          const float* homs, int V, float* out, bool ct, void* stream) {
+    const char* nm = ct ? "mpiv_render_packed_u8_ct" : "mpiv_render_packed_u8";
+    if (!packed || !homs || !out) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (V <= 0 || H < 2 || W < 2 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape (H, W >= 2)", nm);
+    if (p_begin < 0 || p_end > P || p_begin >= p_end) return fail(MPIV_ERR_ARG, "%s: bad plane range", nm);
+    if ((reinterpret_cast<uintptr_t>(packed) & 3) || (ct && !aligned16(out)))
+        return fail(MPIV_ERR_ARG, "%s: alignment (packed 4 B, ct 16 B)", nm);
+    const int64_t npix = (int64_t)(H + 2 * kPad) * (W + 2 * kPad);
+    if (npix * 4 >= (int64_t)kOOB || H >= (1 << 22) || W >= (1 << 22))
+        return fail(MPIV_ERR_ARG, "%s: padded plane larger than 2 GiB or a side >= 2^22", nm);
+    const RenderGeom g = make_geom(H, W, P);
+    U8Geom ug;
+    ug.row = g.Wp * 4;
+    ug.org = (kPad * g.Wp + kPad) * 4;
+    ug.plane_bytes = (int)(npix * 4);
+    // two rows per work-item: measured faster than 8 for u8 texels at 1, 8 and 125 views and
+    // on the config-5 shard (0.36 vs 0.44 ms single view); render_tile=8 A/B
+    const int R = opt(kOptRenderTile) == 8 ? 8 : 2;
+    const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
+    if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+    const unsigned* pk = reinterpret_cast<const unsigned*>(packed);
+    hipStream_t q = S(stream);
+#define MPIV_U8(CT, RR)                                                                                      \
+    render_u8_kernel<CT, RR><<<(unsigned)nb, 256, 0, q>>>(pk, npix, g, ug, V, p_begin, p_end, CT ? back : 1, \
+                                                          homs, out)
+    if (ct && R == 8) MPIV_U8(true, 8);
+    else if (ct) MPIV_U8(true, 2);
+    else if (R == 8) MPIV_U8(false, 8);
+    else MPIV_U8(false, 2);
+#undef MPIV_U8
+    return launched(nm);
+}
+
+int mpiv_render_packed_u8(const uint32_t* packed, int H, int W, int P, const float* homs, int V, float* out,
+                          void* stream) {
+    return render_u8_impl(packed, H, W, P, 0, P, 1, homs, V, out, false, stream);
+}
+
+int mpiv_render_packed_u8_ct(const uint32_t* packed, int H, int W, int P, int p_begin, int p_end, int back,
+                             const float* homs, int V, float* ct, void* stream) {
+    return render_u8_impl(packed, H, W, P, p_begin, p_end, back, homs, V, ct, true, stream);
 }
 
 int mpiv_probe_gather(const float* window, int iters, int blocks_, float* sink, void* stream) {

@@ -158,6 +158,35 @@ def mpi_render_view_torch(rgba_layers, tgt_pose, planes, intrinsics):
     return _lib.render(rgba_layers, homs)
 
 
+def mpi_render_view_u8(rgba_layers_u8, tgt_pose, planes, intrinsics):
+    """mpi_render_view_torch for an 8-bit MPI [B, H, W, P, 4] uint8 (the reference's own
+    test-MPI format, test/rgba_*.png): returns exactly
+    mpi_render_view_torch(rgba_layers_u8.float() / 255.0, tgt_pose, planes, intrinsics)
+    (the reference's image convention, utils.py:324-331) without the float copy: each
+    view is packed at 4 B per texel and rendered by render_u8.hip, which converts every
+    tap to RN(u8/255) exactly before the reference's blend.  Inference only (no autograd:
+    uint8 tensors carry no gradient).  An extension of the drop-in API."""
+    batch_size = tgt_pose.shape[0]
+    n_planes = len(planes)
+    depths = planes.reshape([n_planes, 1])
+    if tgt_pose.is_cuda:
+        homs = _host.render_homographies_device(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
+    else:
+        homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
+    B, H, W, P, _ = rgba_layers_u8.shape
+    if B != batch_size or P != n_planes:
+        raise RuntimeError(f"shape mismatch: MPI batch/planes {B}/{P} vs poses/planes {batch_size}/{n_planes}")
+    homs = homs.reshape(B, P, 9)
+    if B > 1 and rgba_layers_u8.stride(0) == 0:  # one MPI, many views: pack once
+        return _lib.render_packed_u8(_lib.pack_planes_u8(rgba_layers_u8[0]), homs)
+    out = torch.empty((B, H, W, 3), device=rgba_layers_u8.device, dtype=torch.float32)
+    packed = None
+    for b in range(B):
+        packed = _lib.pack_planes_u8(rgba_layers_u8[b], out=packed)
+        _lib.render_packed_u8(packed, homs[b:b + 1], out=out[b:b + 1])
+    return out
+
+
 def mpi_from_net_output(mpi_pred, dep):
     """The notebook's MPI assembly (fast-torch-stereo-vision.ipynb cell 10 L79-111):
     the network output [B, 2P+3, H, W] (P blend weights, P alphas, background rgb) and

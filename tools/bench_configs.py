@@ -199,6 +199,38 @@ def c4n(dev, it, wu):
     report("c4 mpi_render_view_torch end-to-end, 1 view (default routing)", ms, mn, per_view, H * W / 1e6)
 
 
+def u8(dev, it, wu):
+    """8-bit RGBA MPIs (render_u8.hip): config 4 at 1 / 8 / 125 views per launch and the
+    config-5 plane shard, u8 texels (4 B) vs the float path (16 B).  Bytes are the u8
+    algorithmic bytes P*H*W*4 + H*W*12 per view (shard: (P/G)*H*W*4 + H*W*16)."""
+    c = configs.config4()
+    H, W, P = c["H"], c["W"], c["P"]
+    packed = _lib.synth_mpi_packed_u8(0, H, W, 0, P, dev)
+    per_view = P * H * W * 4 + H * W * 12
+    for V in (1, 8, 125):
+        homs = _host.render_homographies(configs.f32(c["poses"][:V]), configs.f32(c["depths"]),
+                                         configs.f32([c["K"]] * V), V).to(dev)
+        out = torch.empty((V, H, W, 3), device=dev)
+        for label, opts in (("default routing", {}), ("2 rows per lane", {"render_tile": 2}),
+                            ("8 rows per lane", {"render_tile": 8})):
+            with _lib.debug(**opts):
+                ms, mn = timed(lambda: _lib.render_packed_u8(packed, homs, out), it if V < 125 else 3, 1)
+            report(f"u8 c4 1024^2x128 u8 texels, {label}, {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
+    del packed
+    c5c = configs.config5()
+    H, W, P = c5c["H"], c5c["W"], c5c["P"]
+    PL = P // 8
+    packed = _lib.synth_mpi_packed_u8(0, H, W, 0, PL, dev)
+    homs = _host.render_homographies(configs.f32(c5c["poses"]), configs.f32(c5c["depths"]),
+                                     configs.f32([c5c["K"]]), 1)[:, :PL].contiguous().to(dev)
+    ct = torch.empty((1, H, W, 4), device=dev)
+    for label, opts in (("default routing", {}), ("8 rows per lane", {"render_tile": 8})):
+        with _lib.debug(**opts):
+            ms, mn = timed(lambda: _lib.render_packed_u8_ct(packed, homs, back=True, out=ct), it, wu)
+        report(f"u8 c5 plane shard: {PL} of {P} planes, 4096x2160 u8 texels, (C,T), {label}", ms, mn,
+               PL * H * W * 4 + H * W * 16, H * W / 1e6)
+
+
 def c5(dev, it, wu):
     """Per-GPU share of the 8-way plane-sharded 4096x2160x256 render + the combine."""
     c = configs.config5()
@@ -292,7 +324,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--only", default="c1,c2,c3,c4,c5,bwd,net")
+    ap.add_argument("--only", default="c1,c2,c3,c4,c5,u8,bwd,net")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     for name in a.only.split(","):
