@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 7
+#define MPIV_ABI_VERSION 8
 
 enum {
     MPIV_OK = 0,
@@ -147,6 +147,15 @@ int mpiv_assemble_mpi(const float *pred, const int64_t pred_strides[4], const fl
 int mpiv_assemble_mpi_packed(const float *pred, const int64_t pred_strides[4], const float *fg,
                              const int64_t fg_strides[4], int b, int H, int W, int P, float *packed,
                              void *stream);
+
+/* mpi_render_view_torch(mpi_from_net_output(pred, fg), ...) in ONE kernel (inference /
+ * viewer path): homs [B][P][9] (the render's homographies, view b renders batch element
+ * b's MPI); out [B,H,W,3] contiguous.  Each plane's tile footprint is assembled from
+ * pred / fg straight into LDS; no MPI tensor is written.  Bit-identical to
+ * mpiv_assemble_mpi followed by mpiv_render.  2 <= H, W < 32764, P <= 512. */
+int mpiv_render_net_output(const float *pred, const int64_t pred_strides[4], const float *fg,
+                           const int64_t fg_strides[4], int B, int H, int W, int P, const float *homs, float *out,
+                           void *stream);
 
 /* Backward of mpiv_assemble_mpi (the notebook trains through it, cell 12 L5-15):
  * drgba [B,H,W,P,4] (drgba_strides[5]) -> dpred [B,2P+3,H,W] contiguous and, when dfg is

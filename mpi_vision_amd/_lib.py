@@ -56,6 +56,7 @@ _SIGS = {
     "mpiv_render_homographies": [_vp, _vp, _vp, _vp, _int, _int, _vp],
     "mpiv_render_homographies_device": [_vp, _vp, _vp, _vp, _int, _int, _vp, _vp],
     "mpiv_pack_planes_u8": [_vp, _c_i64p, _int, _int, _int, _vp, _vp],
+    "mpiv_render_net_output": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp],
     "mpiv_render_packed_u8": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_render_packed_u8_ct": [_vp, _int, _int, _int, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_synth_mpi_packed_u8": [ctypes.c_uint32, _int, _int, _int, _int, _vp, _vp],
@@ -65,7 +66,7 @@ _SIGS = {
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
                           "mpiv_build_id", "mpiv_debug_set")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lib = None
 
@@ -512,6 +513,18 @@ def assemble_mpi_packed(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int, b: int
     _call("mpiv_assemble_mpi_packed", mpi_pred, _strides(mpi_pred), fg, _strides(fg), b, H, W, P, packed,
           _stream(dev))
     return packed
+
+
+def render_net_output(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int, homs: torch.Tensor) -> torch.Tensor:
+    """Frames [B,H,W,3] of the MPIs assembled from [B,2P+3,H,W] + [B,H,W,3], view b from
+    batch element b with homs [B,P,9], in one kernel (render_netout_kernel); bit-identical
+    to render(assemble_mpi(...), homs)."""
+    dev, B, H, W = _net_args(mpi_pred, fg, P)
+    h = _up(homs.reshape(B, P, 9), dev)
+    out = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32)
+    _call("mpiv_render_net_output", mpi_pred, _strides(mpi_pred), fg, _strides(fg), B, H, W, P, h, out,
+          _stream(dev))
+    return out
 
 
 def assemble_mpi_backward(drgba: torch.Tensor, mpi_pred: torch.Tensor, fg: torch.Tensor, P: int,

@@ -723,6 +723,22 @@ int mpiv_assemble_mpi_backward(const float* drgba, const int64_t gs[5], const fl
     return launched("mpiv_assemble_mpi_backward");
 }
 
+// The assembly fused into the render (assemble.hip render_netout_kernel): pred/fg -> frames.
+int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* fg, const int64_t fs[4], int B, int H,
+                           int W, int P, const float* homs, float* out, void* stream) {
+    const char* nm = "mpiv_render_net_output";
+    if (int rc = check_net(nm, pred, ps, fg, fs, B, H, W, P)) return rc;
+    if (!homs || !out) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (H < 2 || W < 2 || H >= (1 << 15) - 4 || W >= (1 << 15) - 4 || P > kNMaxP)
+        return fail(MPIV_ERR_ARG, "%s: needs 2 <= H, W < 32764 and P <= %d", nm, kNMaxP);
+    const NetStrides s{ps[0], ps[1], ps[2], ps[3], fs[0], fs[1], fs[2], fs[3]};
+    const RenderGeom g = make_geom(H, W, P);
+    const int64_t nb = (int64_t)blocks(W, kNTX) * blocks(H, kNTY) * B;
+    if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+    render_netout_kernel<<<(unsigned)nb, kNThreads, 0, S(stream)>>>(pred, fg, s, g, B, homs, out);
+    return launched(nm);
+}
+
 // ---- host-side homographies (inv_homography_torch chain, utils.py:44-67) -------------
 // The reference evaluates the chain with torch-CPU ops on materialised [P,B,...] tensors;
 // torch's CPU matmul of these tiny matrices rounds as plain products summed in ascending

@@ -208,4 +208,217 @@ __global__ __launch_bounds__(kAbPix) void assemble_backward_dense_kernel(const f
     }
 }
 
+// ---------------------------------------------------------------------------
+// assembly fused into the render (inference / viewer: mpi_render_net_output_torch)
+// ---------------------------------------------------------------------------
+//
+// One launch from the network output to the rendered views: a 512-thread block owns a
+// 64x8 output tile of one view and walks the planes back to front; for each plane it
+// assembles the texels of the tile's footprint box (render_lds.hip's box argument:
+// corners through the exact recipe, one-texel margin, clipped to the 2-texel zero
+// border) straight from pred / fg into LDS -- assemble_texel's exact arithmetic, zeros
+// outside the image -- and the samples read their taps there.  The inputs of plane p+1's
+// box are loaded into registers while plane p is sampled (one barrier per plane).  No
+// MPI is written: per view the HBM traffic is the network output itself
+// ((2P+3)*4 + 12 B per pixel) instead of that plus a packed MPI written and read back
+// (P*16 B per pixel each way).  A sample whose tap origin is not staged, or a plane whose
+// box does not fit, assembles its four taps directly (the same texel function), so the
+// frame is bit-identical to assemble + render.
+constexpr int kNTX = 64, kNTY = 8;
+constexpr int kNThreads = kNTX * kNTY;
+constexpr int kNCap = 1024;   // texels per staged box (16 KiB)
+constexpr int kNMaxP = 512;   // planes in the box table
+constexpr int kNFill = kNCap / kNThreads;
+
+// one texel of plane p at image texel (tx, ty), zero outside the image (grid_sample's
+// zero padding of the packed border)
+__device__ __forceinline__ float4 net_texel(const float* __restrict__ pred, const float* __restrict__ fg,
+                                            const NetStrides& s, int H, int W, int P, int b, int p, int tx, int ty) {
+    if ((unsigned)tx >= (unsigned)W || (unsigned)ty >= (unsigned)H) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return assemble_texel(pred, fg, s, P, b, p, ty, tx);
+}
+
+// raw inputs of one texel (w, alpha, bg, fg), loaded ahead of the assembly
+struct NetRaw {
+    float w, a, b0, b1, b2, f0, f1, f2;
+    bool in;
+};
+
+__device__ __forceinline__ NetRaw net_load(const float* __restrict__ pred, const float* __restrict__ fg,
+                                           const NetStrides& s, int H, int W, int P, int b, int p, int tx, int ty) {
+    NetRaw r;
+    r.in = (unsigned)tx < (unsigned)W && (unsigned)ty < (unsigned)H;
+    const int cx = min(max(tx, 0), W - 1), cy = min(max(ty, 0), H - 1);  // always valid memory
+    const float* pp = pred + (int64_t)b * s.pb + (int64_t)cy * s.py + (int64_t)cx * s.px;
+    const float* fp = fg + (int64_t)b * s.fb + (int64_t)cy * s.fy + (int64_t)cx * s.fx;
+    r.w = pp[(int64_t)p * s.pc];
+    r.a = pp[(int64_t)(P + p) * s.pc];
+    r.b0 = pp[(int64_t)(2 * P + 0) * s.pc];
+    r.b1 = pp[(int64_t)(2 * P + 1) * s.pc];
+    r.b2 = pp[(int64_t)(2 * P + 2) * s.pc];
+    r.f0 = fp[0];
+    r.f1 = fp[s.fc];
+    r.f2 = fp[2 * s.fc];
+    return r;
+}
+
+// assemble_texel's arithmetic on preloaded inputs (bit-identical)
+__device__ __forceinline__ float4 net_assemble(const NetRaw& r) {
+    if (!r.in) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float w = (r.w + 1.0f) / 2.0f;
+    const float a = (r.a + 1.0f) / 2.0f;
+    const float om = 1.0f - w;
+    float4 t;
+    t.x = w * r.f0 + om * r.b0;
+    t.y = w * r.f1 + om * r.b1;
+    t.z = w * r.f2 + om * r.b2;
+    t.w = a;
+    return t;
+}
+
+__global__ __launch_bounds__(kNThreads) void render_netout_kernel(const float* __restrict__ pred,
+                                                                  const float* __restrict__ fg, NetStrides ns,
+                                                                  RenderGeom g, int V, const float* __restrict__ homs,
+                                                                  float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float4 s_tex[kNCap];
+    __shared__ int2 s_box[kNMaxP];  // per plane: (x_lo, y_lo), (rows, direct) as 16-bit pairs
+    __shared__ int s_pitch;
+    const int tiles_x = (g.W + kNTX - 1) / kNTX;
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int v = lb % V;
+    const int tile = lb / V;
+    const int tx0 = (tile % tiles_x) * kNTX, ty0 = (tile / tiles_x) * kNTY;
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+    const int x = tx0 + lane, y = ty0 + wave;
+    const bool active = x < g.W && y < g.H;
+    const float* hv = homs + (int64_t)v * g.P * 9;
+    const int P = g.P;
+    if (threadIdx.x == 0) s_pitch = 0;
+    __syncthreads();
+    // ---- footprint boxes (thread q -> plane q/4, corner q%4) + the tile's division proof
+    const int cx1 = min(tx0 + kNTX - 1, g.W - 1), cy1 = min(ty0 + kNTY - 1, g.H - 1);
+    bool ok_div = true;
+    for (int q0 = 0; q0 < 4 * P; q0 += kNThreads) {
+        const int q = q0 + (int)threadIdx.x;
+        const bool live = q < 4 * P;
+        const int pl = live ? (q >> 2) : 0;
+        const int corner = q & 3;
+        const float fx = (float)((corner & 1) ? cx1 : tx0), fy = (float)((corner & 2) ? cy1 : ty0);
+        const float* h = hv + (int64_t)pl * 9;
+        if (live && corner == 0) ok_div = ok_div && div2_rect_safe(h, (float)tx0, (float)cx1, (float)ty0, (float)cy1);
+        float px, py;
+        render_pos<true>(h, fx, fy, g, px, py);
+        float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+        w = (w == 0.0f) ? w + 1e-8f : w;
+        const bool fin = __builtin_isfinite(px) && __builtin_isfinite(py) && __builtin_fabsf(px) < 1e7f &&
+                         __builtin_fabsf(py) < 1e7f;
+        float xmin = floorf(px), xmax = xmin, ymin = floorf(py), ymax = ymin;
+        int pos = fin && w > 0.0f, neg = fin && w < 0.0f;
+#pragma unroll
+        for (int m = 1; m <= 2; m <<= 1) {
+            xmin = fminf(xmin, __shfl_xor(xmin, m));
+            xmax = fmaxf(xmax, __shfl_xor(xmax, m));
+            ymin = fminf(ymin, __shfl_xor(ymin, m));
+            ymax = fmaxf(ymax, __shfl_xor(ymax, m));
+            pos &= __shfl_xor(pos, m);
+            neg &= __shfl_xor(neg, m);
+        }
+        if (live && corner == 0) {
+            const bool ok = pos || neg;
+            const int xl = ok ? max((int)xmin - 1, -2) : 0, xh = ok ? min((int)xmax + 2, g.W + 1) : 0;
+            const int yl = ok ? max((int)ymin - 1, -2) : 0, yh = ok ? min((int)ymax + 2, g.H + 1) : 0;
+            const int width = xh - xl + 1, rows = yh - yl + 1;
+            const int direct = (!ok || width < 2 || rows < 2 || width > 256 || width * rows > kNCap) ? 1 : 0;
+            s_box[q >> 2] = make_int2((xl & 0xFFFF) | (yl << 16), rows | (direct << 16));
+            if (!direct) atomicMax(&s_pitch, width);
+        }
+    }
+    const bool proven = __syncthreads_and(ok_div);
+    const int pitch = s_pitch;
+    auto box_of = [&](int i) {
+        const int2 bb = s_box[i];
+        return make_int4((int)(short)(bb.x & 0xFFFF), bb.x >> 16, bb.y & 0xFFFF, bb.y >> 16);
+    };
+    auto staged = [&](const int4& bx) { return bx.w == 0 && bx.z * pitch <= kNCap; };
+    // this thread's box texels: idx = tid + 512*j -> (row, col) with the common pitch
+    int row_j[kNFill], col_j[kNFill];
+#pragma unroll
+    for (int j = 0; j < kNFill; ++j) {
+        const int idx = (int)threadIdx.x + kNThreads * j;
+        row_j[j] = pitch > 0 ? idx / pitch : 0;
+        col_j[j] = idx - row_j[j] * pitch;
+    }
+    NetRaw stg[kNFill];
+    auto fetch = [&](int p, const int4& bx) {
+        const int nfp = bx.z * pitch;
+#pragma unroll
+        for (int j = 0; j < kNFill; ++j)
+            if (kNThreads * j < nfp)  // block-uniform
+                stg[j] = net_load(pred, fg, ns, g.H, g.W, P, v, p, bx.x + col_j[j], bx.y + row_j[j]);
+    };
+    auto commit = [&](const int4& bx) {
+        const int nfp = bx.z * pitch;
+#pragma unroll
+        for (int j = 0; j < kNFill; ++j)
+            if ((int)threadIdx.x + kNThreads * j < nfp) s_tex[threadIdx.x + kNThreads * j] = net_assemble(stg[j]);
+    };
+    const float fx = (float)x, fy = (float)y;
+    float cr = -0.0f, cg = -0.0f, cb = -0.0f;  // plane 0 replaces it exactly (render.hip)
+    int4 bx_next = box_of(0);
+    if (staged(bx_next)) fetch(0, bx_next);
+    for (int p = 0; p < P; ++p) {
+        const int4 bx = bx_next;
+        if (staged(bx)) commit(bx);
+        __syncthreads();  // plane p's box is in LDS
+        if (p + 1 < P) {
+            bx_next = box_of(p + 1);
+            if (staged(bx_next)) fetch(p + 1, bx_next);  // in flight while plane p is sampled
+        }
+        if (active) {
+            float px, py;
+            if (proven)
+                render_pos_fast<false>(hv + (int64_t)p * 9, fx, fy, g, px, py);
+            else
+                render_pos<true>(hv + (int64_t)p * 9, fx, fy, g, px, py);
+            TapSet ts;
+            bool hit = false;
+            if (staged(bx)) {
+                const LdsBox box = make_lds_box(bx.x, bx.y, bx.z, pitch, g.W, g.H);
+                hit = lds_issue(s_tex, box, px, py, ts);
+            }
+            if (!hit) {  // assemble the four taps directly (rare)
+                const float fx0 = floorf(px), fy0 = floorf(py);
+                const float wx = px - fx0, ex = 1.0f - wx;
+                const float wy = py - fy0, sy = 1.0f - wy;
+                ts.nw = sy * ex;
+                ts.ne = sy * wx;
+                ts.sw = wy * ex;
+                ts.se = wy * wx;
+                const int ix = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)g.W);
+                const int iy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)g.H);
+                const float4 t0 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix, iy);
+                const float4 t1 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix + 1, iy);
+                const float4 t2 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix, iy + 1);
+                const float4 t3 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix + 1, iy + 1);
+                ts.a = {t0.x, t0.y, t0.z, t0.w};
+                ts.b = {t1.x, t1.y, t1.z, t1.w};
+                ts.c = {t2.x, t2.y, t2.z, t2.w};
+                ts.d = {t3.x, t3.y, t3.z, t3.w};
+            }
+            const f32x4 sm = blend_taps(ts);
+            const float a = p == 0 ? 1.0f : sm[3];
+            const float om = 1.0f - a;
+            cr = over(sm[0], a, om, cr);
+            cg = over(sm[1], a, om, cg);
+            cb = over(sm[2], a, om, cb);
+        }
+        __syncthreads();  // every sample of plane p has read the box
+    }
+    if (!active) return;
+    const int64_t o = (((int64_t)v * g.H + y) * g.W + x) * 3;
+    out[o + 0] = cr;
+    out[o + 1] = cg;
+    out[o + 2] = cb;
+}
+
 }  // namespace mpiv

@@ -202,9 +202,10 @@ def mpi_from_net_output(mpi_pred, dep):
 
 def mpi_render_net_output_torch(mpi_pred, ref_img, tgt_pose, planes, intrinsics):
     """mpi_render_view_torch(mpi_from_net_output(mpi_pred, ...), tgt_pose, planes, intrinsics)
-    without the [B, H, W, P, 4] tensor: each view's MPI is assembled straight into the
-    render's packed plane layout and rendered (inference / viewer path, no autograd).
-    Bit-identical to the two-step form."""
+    in ONE kernel (inference / viewer path, no autograd): each plane's tile footprint is
+    assembled from the network output straight into LDS and sampled there
+    (assemble.hip render_netout_kernel); no [B, H, W, P, 4] tensor and no packed MPI is
+    written.  Bit-identical to the two-step form."""
     batch_size = tgt_pose.shape[0]
     n_planes = len(planes)
     depths = planes.reshape([n_planes, 1])
@@ -213,15 +214,7 @@ def mpi_render_net_output_torch(mpi_pred, ref_img, tgt_pose, planes, intrinsics)
     else:
         homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
     fg = ref_img.to(mpi_pred.device)
-    dev = mpi_pred.device
-    B, _, H, W = mpi_pred.shape
-    out = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32)
-    packed = torch.empty(_lib.packed_shape(H, W, n_planes), device=dev, dtype=torch.float32)
-    h = homs.reshape(B, n_planes, 9)
-    for b in range(B):
-        _lib.assemble_mpi_packed(mpi_pred, fg, n_planes, b, out=packed)
-        _lib.render_packed(packed, h[b:b + 1], out=out[b:b + 1])
-    return out
+    return _lib.render_net_output(mpi_pred, fg, n_planes, homs)
 
 
 def pixel2cam_torch(depth, pixel_coords, intrinsics, is_homogeneous=True):

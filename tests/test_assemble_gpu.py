@@ -128,3 +128,35 @@ def test_fused_net_output_render(dev):
     got = mv.mpi_render_net_output_torch(pred, ref, poses, planes, K)
     torch.cuda.synchronize()
     assert_bits(got.cpu().numpy(), want.cpu().numpy(), "fused assemble + render")
+
+
+@pytest.mark.parametrize("case", ["odd", "extreme", "strided", "big"])
+def test_fused_net_output_render_cases(case, dev):
+    """The one-kernel assembly + render (render_netout_kernel) against the two-step drop-ins
+    (bit-exact, themselves pinned to the notebook / reference goldens): partial tiles, views
+    with planes behind the camera (taps assembled directly, boxes that do not fit), a
+    channel-strided prediction (a slice of a wider tensor) and a config-2-sized MPI."""
+    g = torch.Generator().manual_seed(len(case))
+    B, H, W, P = {"odd": (2, 37, 203, 7), "extreme": (4, 45, 70, 9), "strided": (2, 33, 64, 5),
+                  "big": (1, 576, 1024, 32)}[case]
+    pred = torch.rand((B, 2 * P + 3 + (4 if case == "strided" else 0), H, W), generator=g) * 2 - 1
+    if case == "strided":
+        pred = pred.to(dev)[:, 2:2 + 2 * P + 3]
+        assert not pred.is_contiguous()
+    else:
+        pred = pred.to(dev)
+    ref = (torch.rand((B, H, W, 3), generator=g) * 2 - 1).to(dev)
+    f = configs.focal_from_fov(W)
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * B).to(dev)
+    if case == "extreme":
+        poses = [configs.pose_from(configs.rot_y((i - 1.5) * 25.0), ((i - 1.5) * 0.6, 0.3, (i - 2) * 0.7))
+                 for i in range(B)]
+    else:
+        poses = [configs.pose_from(configs.rot_y(1.5 * (i - 1)), (0.03 * i, -0.02, 0.04)) for i in range(B)]
+    poses = configs.f32(poses).to(dev)
+    planes = configs.f32(mv.inv_depths(0.5 if case == "extreme" else 1, 100, P)).to(dev)
+    dep = {"mpi_planes": torch.zeros((B, P), device=dev), "ref_img": ref}
+    want = mv.mpi_render_view_torch(mv.mpi_from_net_output(pred, dep), poses, planes, K)
+    got = mv.mpi_render_net_output_torch(pred, ref, poses, planes, K)
+    torch.cuda.synchronize()
+    assert_bits(got.cpu().numpy(), want.cpu().numpy(), f"fused assemble + render ({case})")

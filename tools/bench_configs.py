@@ -312,7 +312,17 @@ def net(dev, it, wu):
     pose = configs.f32(c["poses"][:1]).to(dev)
     planes = configs.f32(c["depths"]).to(dev)
     ms, mn = timed(lambda: mv.mpi_render_net_output_torch(pred, ref, pose, planes, K), it, wu)
-    report(f"net output -> rendered view {W}x{H}x{P}, fused (assemble to packed + render)", ms, mn,
+    report(f"net output -> rendered view {W}x{H}x{P}, one kernel (drop-in end to end)", ms, mn,
+           H * W * ((2 * P + 3) * 4 + 12 + 12), H * W / 1e6)
+    homs = _host.render_homographies(pose, planes, K, 1).to(dev)
+    ms, mn = timed(lambda: _lib.render_net_output(pred, ref, P, homs), it, wu)
+    report(f"net output -> rendered view {W}x{H}x{P}, one kernel (render_netout_kernel only)", ms, mn,
+           H * W * ((2 * P + 3) * 4 + 12 + 12), H * W / 1e6)
+    pk = torch.empty(_lib.packed_shape(H, W, P), device=dev)
+    o1 = torch.empty((1, H, W, 3), device=dev)
+    ms, mn = timed(lambda: (_lib.assemble_mpi_packed(pred, ref, P, 0, out=pk), _lib.render_packed(pk, homs, out=o1)),
+                   it, wu)
+    report(f"net output -> rendered view {W}x{H}x{P}, two launches (assemble to packed + render)", ms, mn,
            alg + P * H * W * 16 + H * W * 12, H * W / 1e6)
     dep = {"mpi_planes": torch.zeros((1, P), device=dev), "ref_img": ref}
     ms, mn = timed(lambda: mv.mpi_render_view_torch(mv.mpi_from_net_output(pred, dep), pose, planes, K), it, wu)
