@@ -1,4 +1,4 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_assemble_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_asm.log 2>&1; rc=$?; tail -5 gpurun_out/t_asm.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/bench_configs.py --only net --iters 20 > gpurun_out/cfg_net.jsonl 2>&1; rc=$?; cut -c1-160 gpurun_out/cfg_net.jsonl; exit $rc
+TAG=r02b timeout -k 10 900 bash tools/profile.sh > gpurun_out/profile.log 2>&1; rc=$?; tail -3 gpurun_out/profile.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_r02d.json 2> gpurun_out/bench_r02d.err; rc=$?; tail -c 1500 gpurun_out/bench_r02d.json; exit $rc
