@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 8
+#define MPIV_ABI_VERSION 9
 
 enum {
     MPIV_OK = 0,
@@ -113,20 +113,24 @@ int mpiv_render_homographies_device(const float *pose, const float *depths, cons
 /* ---- render backward ------------------------------------------------------ */
 
 /* Workspace bytes mpiv_render_backward needs for one H x W x P MPI (reused across
- * views): ~60 B per plane-pixel + 8 B per plane-texel. */
+ * views): 16 B per plane-pixel of d samples + 2 B per plane-pixel of colour
+ * checkpoints + the fallback's bucket arrays (<= 16 B per plane-pixel of one plane
+ * chunk, chunks sized to at most 2^25 plane-pixels). */
 size_t mpiv_render_backward_workspace_size(int H, int W, int P);
 
 /* d(mpi_render_view_torch)/d(rgba_layers) (utils.py:267-294 under autograd), bit-exact
  * to the reference's CPU autograd: the over-composite adjoint followed by
  * grid_sampler_2d_backward's scatter, summed per texel in ATen's order.
- * packed:  the MPI in mpiv_pack_planes layout; homs [V][P][9] (the forward's);
- * dout:    [V,H,W,3] contiguous incoming gradient;
- * dmpi:    [V,H,W,P,4] with element strides dmpi_strides[5]: view v's gradient is
- *          written (not accumulated) to dmpi + v*dmpi_strides[0];
+ * mpi:     the forward's [V,H,W,P,4] rgba_layers IN PLACE, element strides mpi_strides[5]
+ *          with 16-byte aligned texels and planes contiguous per pixel (strides[3] == 4,
+ *          strides[4] == 1; a stride-0 broadcast batch is fine); P <= 796;
+ * homs:    [V][P][9] (the forward's); dout: [V,H,W,3] contiguous incoming gradient;
+ * dmpi:    [V,H,W,P,4] contiguous, 16-byte aligned: view v's gradient is written (not
+ *          accumulated);
  * workspace: >= mpiv_render_backward_workspace_size(H, W, P) bytes, 256-B aligned.
- * Deterministic (no float atomics); H*W < 2^26. */
-int mpiv_render_backward(const float *packed, int H, int W, int P, const float *homs, int V,
-                         const float *dout, float *dmpi, const int64_t dmpi_strides[5], void *workspace,
+ * Deterministic (no float atomics); H*W < 2^26, P*H*W < 2^31. */
+int mpiv_render_backward(const float *mpi, const int64_t mpi_strides[5], int V, int H, int W, int P,
+                         const float *homs, const float *dout, float *dmpi, void *workspace,
                          size_t workspace_bytes, void *stream);
 
 /* ---- MPI assembly from the network output ------------------------------- */

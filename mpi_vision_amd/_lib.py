@@ -48,7 +48,7 @@ _SIGS = {
     "mpiv_plane_sweep_padded": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
     "mpiv_preprocess": [_vp, _i64, _vp, _vp],
     "mpiv_deprocess_u8": [_vp, _i64, _vp, _vp],
-    "mpiv_render_backward": [_vp, _int, _int, _int, _vp, _int, _vp, _vp, _c_i64p, _vp, ctypes.c_size_t, _vp],
+    "mpiv_render_backward": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp],
     "mpiv_plane_sweep_padded_into": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,
                                      _vp],
     "mpiv_assemble_mpi": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
@@ -66,7 +66,7 @@ _SIGS = {
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
                           "mpiv_build_id", "mpiv_debug_set")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lib = None
 
@@ -433,9 +433,29 @@ def render(rgba_layers: torch.Tensor, homs: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.Tensor) -> torch.Tensor:
-    """d(mpi_render_view_torch)/d(rgba_layers): rgba_layers [B,H,W,P,4] (any strides, incl. a
-    stride-0 broadcast batch), homs [B,P,9] (the forward's), dout [B,H,W,3] ->
+def bwd_layout_ok(rgba_layers: torch.Tensor) -> bool:
+    """True when mpiv_render_backward reads this [B,H,W,P,4] tensor in place (abi.hip:
+    16-B texels with planes contiguous per pixel, one view below the buffer range)."""
+    B, H, W, P, C = rgba_layers.shape
+    st = rgba_layers.stride()
+    if C != 4 or st[4] != 1 or st[3] != 4 or any(s % 4 for s in st[:3]) or st[1] < 0 or st[2] < 0:
+        return False
+    rec = ((H - 1) * st[1] + (W - 1) * st[2]) * 4 + 8 * 16
+    return rgba_layers.data_ptr() % 16 == 0 and rec < _KOOB and st[1] // 4 < (1 << 22) and st[2] // 4 < (1 << 22)
+
+
+def bwd_flag_offset(H: int, W: int, P: int) -> int:
+    """Byte offset of the fallback flag in mpiv_render_backward's workspace (abi.hip
+    bwd_layout): 1 after a call whose last view went through the bucket fallback."""
+    a = lambda n: (n + 255) // 256 * 256  # noqa: E731
+    return a(P * H * W * 16) + a((P + 7) // 8 * H * W * 16) + a(P * 48) + 2 * a(64 * 8)
+
+
+def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.Tensor,
+                    workspace: torch.Tensor | None = None) -> torch.Tensor:
+    """d(mpi_render_view_torch)/d(rgba_layers): rgba_layers [B,H,W,P,4] (read in place when
+    its planes are contiguous per pixel, incl. a stride-0 broadcast batch; other layouts
+    are made contiguous first), homs [B,P,9] (the forward's), dout [B,H,W,3] ->
     [B,H,W,P,4] contiguous, one gradient per view (a broadcast input's views are summed
     by autograd's expand backward, as in the reference).  Bit-exact to the reference's
     CPU autograd (render_bwd.hip)."""
@@ -443,21 +463,16 @@ def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.T
     B, H, W, P, _ = rgba_layers.shape
     if tuple(dout.shape) != (B, H, W, 3):
         raise RuntimeError(f"grad_output must be [{B},{H},{W},3], got {tuple(dout.shape)}")
+    src = rgba_layers if bwd_layout_ok(rgba_layers) else rgba_layers.contiguous()
     L = load()
-    ws = torch.empty(L.mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    need = L.mpiv_render_backward_workspace_size(H, W, P)
+    ws = workspace if workspace is not None else torch.empty(need, dtype=torch.uint8, device=dev)
+    if ws.dtype != torch.uint8 or not ws.is_contiguous() or ws.numel() < need or ws.device != dev:
+        raise RuntimeError(f"workspace must be a contiguous uint8 tensor of >= {need} bytes on {dev}")
     grad = torch.empty((B, H, W, P, 4), device=dev, dtype=torch.float32)
     h = _up(homs.reshape(B, P, 9), dev)
     dout = dout.contiguous()
-    gst = _strides(grad)
-    if B > 1 and rgba_layers.stride(0) == 0:  # broadcast MPI: pack once, all views
-        packed = pack_planes(rgba_layers[0])
-        _call("mpiv_render_backward", packed, H, W, P, h, B, dout, grad, gst, ws, ws.numel(), _stream(dev))
-        return grad
-    packed = torch.empty(packed_shape(H, W, P), device=dev, dtype=torch.float32)
-    for b in range(B):
-        pack_planes(rgba_layers[b], out=packed)
-        _call("mpiv_render_backward", packed, H, W, P, h[b:b + 1], 1, dout[b:b + 1], grad[b:b + 1], gst, ws,
-              ws.numel(), _stream(dev))
+    _call("mpiv_render_backward", src, _strides(src), B, H, W, P, h, dout, grad, ws, ws.numel(), _stream(dev))
     return grad
 
 

@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <cstring>
 #include <cstdlib>
+#include <algorithm>
 
 #include "../../include/mpiv.h"
 #include "render.hip"
@@ -61,15 +62,20 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //   sweep_tile=1       the sweep uses the tile kernel; sweep_store=k (k >= 0) the grouped one
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
 //                      forces their per-sample global fallback (tests)
+//   bwd_fallback=1     mpiv_render_backward skips the tile gather and runs its bucket
+//                      fallback for every view (tests)
+//   bwd_margin=k       the tile gather's pixel-window margin in 1/64 pixel (default 16);
+//                      negative values make windows miss contributors, which the pair
+//                      count must catch (tests)
 // Relaxed atomics: a launch reads each option once; setting options while another thread
 // launches is a test-harness race on which kernel runs, never on memory.
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
-                kOptRenderChunk, kOptRenderRing, kOptRenderTile, kNumOpts };
+                kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
-                                         "render_tile"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0};
+                                         "render_tile", "bwd_fallback", "bwd_margin"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -336,30 +342,51 @@ namespace {
 
 inline size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
 
+// Planes per fallback chunk: all of them up to 2^25 plane-pixels, else the fewest equal
+// chunks below that (the bucket arrays are then <= 1/4 of the d-sample array).
+int bwd_fallback_planes(int H, int W, int P) {
+    const int64_t n = (int64_t)P * H * W, cap = (int64_t)1 << 25;
+    if (n <= cap) return P;
+    const int64_t chunks = (n + cap - 1) / cap;
+    return (int)(((int64_t)P + chunks - 1) / chunks);
+}
+
 // workspace carve-up for one view; returns the total size in bytes
 size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
-    const size_t n = (size_t)P * H * W;
-    const size_t nk = (size_t)P * (H + 1) * (W + 1);
+    const size_t hw = (size_t)H * W;
+    const int pc = bwd_fallback_planes(H, W, P);
+    const size_t nk = (size_t)pc * (H + 1) * (W + 1);
     const size_t nb = (nk + kScanTile - 1) / kScanTile;
+    const size_t nchunk = (size_t)(P + kBwdCH - 1) / kBwdCH;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         char* p = base ? base + off : nullptr;
         off += align256(bytes);
         return p;
     };
-    char* prev = take(n * 16);
-    char* ds = take(n * 16);
-    char* fw = take(n * 8);
-    char* key = take(n * 4);
+    char* ds = take((size_t)P * hw * 16);
+    char* ckpt = take(nchunk * hw * 16);
+    char* inv = take((size_t)P * 12 * 4);
+    char* truth = take(kCtrSlots * 8);
+    char* found = take(kCtrSlots * 8);
+    char* flag = take(4);
+    const size_t ntiles = (size_t)((W + kGTW - 1) / kGTW) * ((H + kGTH - 1) / kGTH);
+    char* box = take((size_t)P * ntiles * 16);
+    char* key = take((size_t)pc * hw * 4);
     char* count = take(nk * 4);
     char* offs = take((nk + 1) * 4);
-    char* ids = take(n * 4);
+    char* ids = take((size_t)pc * hw * 4);
     char* bsum = take(nb * 4);
-    char* big = take((n / (kSmallBucket + 1) + 2) * 4);
+    char* big = take(((size_t)pc * hw / (kSmallBucket + 1) + 2) * 4);
     if (ws) {
-        ws->prev = reinterpret_cast<float4*>(prev);
         ws->ds = reinterpret_cast<float4*>(ds);
-        ws->fw = reinterpret_cast<float2*>(fw);
+        ws->ckpt = reinterpret_cast<float4*>(ckpt);
+        ws->inv = reinterpret_cast<float*>(inv);
+        ws->truth = reinterpret_cast<unsigned long long*>(truth);
+        ws->found = reinterpret_cast<unsigned long long*>(found);
+        ws->flag = reinterpret_cast<int*>(flag);
+        ws->box = reinterpret_cast<int4*>(box);
+        ws->pc = pc;
         ws->key = reinterpret_cast<int*>(key);
         ws->count = reinterpret_cast<int*>(count);
         ws->offs = reinterpret_cast<int*>(offs);
@@ -370,6 +397,8 @@ size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
     return off;
 }
 
+inline unsigned fb_grid(int64_t n, int per) { return (unsigned)std::min<int64_t>(kFbGrid, std::max<int64_t>(1, (n + per - 1) / per)); }
+
 }  // namespace
 
 size_t mpiv_render_backward_workspace_size(int H, int W, int P) {
@@ -377,58 +406,81 @@ size_t mpiv_render_backward_workspace_size(int H, int W, int P) {
     return bwd_layout(H, W, P, nullptr, nullptr);
 }
 
-int mpiv_render_backward(const float* packed, int H, int W, int P, const float* homs, int V, const float* dout,
-                         float* dmpi, const int64_t st[5], void* workspace, size_t ws_bytes, void* stream) {
+int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, int W, int P, const float* homs,
+                         const float* dout, float* dmpi, void* workspace, size_t ws_bytes, void* stream) {
     const char* nm = "mpiv_render_backward";
-    if (!packed || !homs || !dout || !dmpi || !st || !workspace) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (!mpi || !st || !homs || !dout || !dmpi || !workspace) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
     if (V <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
-    if (!aligned16(packed) || (reinterpret_cast<uintptr_t>(workspace) & 255))
-        return fail(MPIV_ERR_ARG, "%s: packed must be 16-byte and workspace 256-byte aligned", nm);
-    if ((int64_t)(H + 2 * kPad) * (W + 2 * kPad) * 16 >= (int64_t)kOOB || H >= (1 << 22) || W >= (1 << 22))
-        return fail(MPIV_ERR_ARG, "%s: padded plane larger than 2 GiB or a side >= 2^22", nm);
-    // bucket / pixel ids and order keys are 32-bit: P*(H+1)*(W+1) + 1 < 2^31, H*W < 2^26
-    if ((int64_t)P * (H + 1) * (W + 1) + 1 >= ((int64_t)1 << 31) || (int64_t)H * W >= ((int64_t)1 << 26))
+    // in place: planes contiguous per pixel (16-B texels), every tap below the buffer range
+    const int64_t rec = ((int64_t)(H - 1) * st[1] + (int64_t)(W - 1) * st[2]) * 4 + kBwdCH * 16;
+    if (st[4] != 1 || st[3] != 4 || st[0] % 4 || st[1] % 4 || st[2] % 4 || !aligned16(mpi))
+        return fail(MPIV_ERR_ARG, "%s: rgba_layers must have 16-byte aligned texels with planes contiguous per pixel "
+                    "(strides[3] == 4, strides[4] == 1)", nm);
+    if (st[1] < 0 || st[2] < 0 || rec >= (int64_t)kOOB || st[1] / 4 >= (1 << 22) || st[2] / 4 >= (1 << 22))
+        return fail(MPIV_ERR_ARG, "%s: one view's MPI must span less than 2 GiB", nm);
+    const size_t chain_lds = (size_t)4 * kWave * (kBwdCH + 1) * 16 + (size_t)P * 36;
+    if (chain_lds > (size_t)kChunkMaxLds) return fail(MPIV_ERR_ARG, "%s: more than %d planes", nm,
+                                                      (int)((kChunkMaxLds - 4 * kWave * (kBwdCH + 1) * 16) / 36));
+    if (!aligned16(dmpi) || (reinterpret_cast<uintptr_t>(workspace) & 255))
+        return fail(MPIV_ERR_ARG, "%s: d rgba_layers must be 16-byte and workspace 256-byte aligned", nm);
+    // pixel ids, bucket ids and order keys are 32-bit
+    if ((int64_t)H * W >= ((int64_t)1 << 26) || (int64_t)P * H * W >= ((int64_t)1 << 31))
         return fail(MPIV_ERR_ARG, "%s: MPI too large for one backward launch", nm);
     BwdWs ws;
     const size_t need = bwd_layout(H, W, P, static_cast<char*>(workspace), &ws);
     if (ws_bytes < need) return fail(MPIV_ERR_ARG, "%s: workspace too small (%zu < %zu bytes)", nm, ws_bytes, need);
     const RenderGeom g = make_geom(H, W, P);
+    const ChunkGeom cg{(int)(st[1] / 4), (int)(st[2] / 4), (int)rec};
     const bool fast = H >= 2 && W >= 2;
-    const float4* pk = reinterpret_cast<const float4*>(packed);
-    const int64_t ps = (int64_t)(H + 2 * kPad) * (W + 2 * kPad);
-    const int HW = H * W;
-    const int K = (H + 1) * (W + 1);
-    const int64_t nk = (int64_t)P * K;
-    const int64_t nq = (int64_t)P * HW;
-    const unsigned nb = (unsigned)((nk + kScanTile - 1) / kScanTile);
-    const GradOut so{st[1], st[2], st[3], st[4]};
-    // dense [H,W,P,4] view gradients take the LDS-transposed gather
-    const bool dense = so.c == 1 && so.p == 4 && so.x == (int64_t)P * 4 && so.y == (int64_t)W * P * 4 &&
-                       (int64_t)H * W <= kMaxGridX && blocks(P, kGatherPl) <= kMaxGridYZ;
+    const int64_t HW = (int64_t)H * W;
+    const int64_t K = (int64_t)(H + 1) * (W + 1);
+    const unsigned chain_blocks = blocks(W, kTileX) * blocks(H, kTileY);
+    const int tiles_x = (int)blocks(W, kGTW);
+    const int64_t ntiles = (int64_t)tiles_x * blocks(H, kGTH);
+    const int64_t gather_blocks = ntiles * blocks(P, kGPl);
+    if (gather_blocks > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+    const int force = opt(kOptBwdFallback) != 0 || !fast;
+    const float margin = (float)opt(kOptBwdMargin) / 64.0f;
     hipStream_t q = S(stream);
-    if (hipMemsetAsync(ws.count, 0, (size_t)nk * 4, q) != hipSuccess)
+    if (hipMemsetAsync(ws.truth, 0, 2 * kCtrSlots * 8 + 256, q) != hipSuccess)  // truth, found (adjacent)
         return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
-    const unsigned tiles = blocks(W, kTileX) * blocks(H, kTileY);
     for (int v = 0; v < V; ++v) {
         const float* hv = homs + (int64_t)v * P * 9;
         const float* dv = dout + (int64_t)v * HW * 3;
+        const float* mv = mpi + (int64_t)v * st[0];
+        float4* gv = reinterpret_cast<float4*>(dmpi) + (int64_t)v * HW * P;
         if (fast)
-            render_bwd_chain_kernel<true><<<tiles, 256, 0, q>>>(pk, ps, g, hv, dv, ws);
+            bwd_chain_kernel<1><<<chain_blocks, 256, chain_lds, q>>>(mv, g, cg, hv, dv, ws);
         else
-            render_bwd_chain_kernel<false><<<tiles, 256, 0, q>>>(pk, ps, g, hv, dv, ws);
-        scan_tile_sums_kernel<<<nb, kScanBlock, 0, q>>>(ws.count, nk, ws.bsum);
-        scan_tile_offsets_kernel<<<1, kScanBlock, 0, q>>>(ws.bsum, (int)nb);
-        scan_apply_kernel<<<nb, kScanBlock, 0, q>>>(ws.count, nk, ws.bsum, ws.offs);
-        bucket_fill_kernel<<<blocks(nq, 256), 256, 0, q>>>(P, HW, K, ws);
-        if (hipMemsetAsync(ws.big, 0, 4, q) != hipSuccess) return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
-        bucket_sort_kernel<<<blocks(nk, 256), 256, 0, q>>>(nk, ws);
-        big_bucket_sort_kernel<<<256, 256, 0, q>>>(ws);
-        float* gv = dmpi + (int64_t)v * st[0];
-        if (dense && aligned16(gv))
-            render_bwd_gather_dense_kernel<<<dim3(blocks((int64_t)H * W, kWave), blocks(P, kGatherPl)),
-                                             kGatherPl * kWave, 0, q>>>(H, W, P, ws, reinterpret_cast<float4*>(gv));
-        else
-            render_bwd_gather_kernel<<<blocks(nq, 256), 256, 0, q>>>(H, W, P, ws, gv, so);
+            bwd_chain_kernel<0><<<chain_blocks, 256, chain_lds, q>>>(mv, g, cg, hv, dv, ws);
+        if (!force) {
+            bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
+            bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x, margin,
+                                                                           ws.box);
+            bwd_gather_kernel<<<(unsigned)gather_blocks, 256, 0, q>>>(g, hv, ws, gv, margin);
+        }
+        bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force);
+        for (int pc0 = 0; pc0 < P; pc0 += ws.pc) {  // fallback: returns at once unless flagged
+            const int pcn = std::min(ws.pc, P - pc0);
+            const int64_t nk = (int64_t)pcn * K, nq = (int64_t)pcn * HW;
+            const int nb = (int)((nk + kScanTile - 1) / kScanTile);
+            fb_zero_kernel<<<fb_grid(nk, 256), 256, 0, q>>>(ws, nk);
+            if (fast)
+                fb_key_kernel<true><<<fb_grid(nq, 256), 256, 0, q>>>(g, hv, pc0, pcn, ws);
+            else
+                fb_key_kernel<false><<<fb_grid(nq, 256), 256, 0, q>>>(g, hv, pc0, pcn, ws);
+            fb_scan_sums_kernel<<<fb_grid(nb, 1), kScanBlock, 0, q>>>(ws, nk, nb);
+            fb_scan_offsets_kernel<<<1, kScanBlock, 0, q>>>(ws, nb);
+            fb_scan_apply_kernel<<<fb_grid(nb, 1), kScanBlock, 0, q>>>(ws, nk, nb);
+            fb_fill_kernel<<<fb_grid(nq, 256), 256, 0, q>>>(HW, pcn, K, ws);
+            fb_big_reset_kernel<<<1, 1, 0, q>>>(ws);
+            fb_sort_kernel<<<fb_grid(nk, 256), 256, 0, q>>>(nk, ws);
+            fb_big_sort_kernel<<<256, 256, 0, q>>>(ws);
+            if (fast)
+                fb_gather_kernel<true><<<fb_grid(nq, 256), 256, 0, q>>>(g, hv, pc0, pcn, ws, gv);
+            else
+                fb_gather_kernel<false><<<fb_grid(nq, 256), 256, 0, q>>>(g, hv, pc0, pcn, ws, gv);
+        }
     }
     return launched(nm);
 }

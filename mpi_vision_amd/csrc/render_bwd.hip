@@ -6,136 +6,684 @@
 // The reference's gradient is a float sum per source texel whose ORDER is fixed by
 // ATen's grid_sampler_2d_backward CPU kernel: per (plane, view) slice the output
 // pixels are walked in flat chunks of 8; per chunk and channel the corners nw, ne,
-// sw, se are scattered over the chunk's lanes in order.  A GPU scatter with float
-// atomics would add in arrival order (nondeterministic, not bit-exact), so the
-// adjoint is computed as a deterministic GATHER instead:
+// sw, se are scattered over the chunk's lanes in order.  So texel t's sum runs over its
+// contributors sorted by the key (pixel/8, corner, pixel%8), from +0.  A scatter with
+// float atomics would add in arrival order; here every texel GATHERS its contributors in
+// that order instead.  Three steps per view, reading the reference's [B,H,W,P,4] tensor
+// in place (no pack):
 //
-//  1. chain  (one work-item per output pixel, planes back to front then front to
-//            back): recompute the forward (same recipe as render.hip), keep the
-//            prefix out_{p-1} and the sample s_p per plane in the workspace, then
-//            walk the over-chain backwards exactly like autograd's Mul/Rsub
-//            backward: d rgb = g*a, d a = sum(g*rgb) + -(sum(g*out_{p-1})),
-//            g *= (1 - a).  Each (plane, pixel) also records its bilinear fractions
-//            and the bucket of its north-west tap; bucket sizes are counted.
-//  2. scan   exclusive prefix sum of the bucket sizes (3 kernels).
-//  3. bucket pixel ids into their buckets (atomic slot claim), then sort each
-//            bucket by pixel id: buckets of <= kSmallBucket ids (~1 pixel for
-//            non-minifying warps) by one thread, larger ones (minification, degenerate
-//            homographies: up to every pixel of a plane in one bucket) by a block-wide
-//            merge sort, so no bucket size costs O(n^2) on one lane.
-//  4. gather (one work-item per source texel): the texel is the nw tap of bucket
-//            (x, y), the ne tap of bucket (x-1, y), sw of (x, y-1), se of (x-1, y-1);
-//            the four sorted lists are merged by the reference's order key
-//            (pixel/8, corner, pixel%8) and summed in that order, from +0.
-// Every product and sum is a single fp32 rounding written out explicitly (the
-// library builds with -ffp-contract=off).
+//  1. chain  (bwd_chain_kernel; render_chunk.hip's lane mapping: lanes = (pixel, plane
+//            of an 8-plane chunk), so a tap instruction reads whole 128-B pixel lines).
+//            Pass 1 composites planes 0..P-1 like the forward and checkpoints the colour
+//            before every chunk; pass 2 walks the chunks back to front, re-samples each
+//            one, rebuilds its prefixes out_{p-1} from the checkpoint in registers and runs
+//            autograd's Mul/Rsub backward over it: d rgb = g*a, d a = sum(g*rgb) +
+//            -(sum(g*out_{p-1})), g *= (1 - a).  Only d s_p (16 B per plane-pixel) is
+//            written.  It also counts every (sample, in-image tap) pair: the number of
+//            (texel, contributor) pairs step 2 must find.
+//  2. gather (bwd_gather_kernel): a block owns a 64x4 texel tile of 8 planes.  Per plane
+//            it maps the tile (one texel margin) back through the inverse homography to a
+//            box of output pixels, recomputes their sample positions with the forward's
+//            recipe (bit-identical) and stages (nw-tap bucket, fractions, d s) in LDS; each
+//            texel then scans the pixels of ITS window (the inverse image of the 2x2 texels
+//            whose samples can touch it) in pixel order, collects the hits of one 8-pixel
+//            chunk in a 32-bit mask indexed (corner, pixel%8) and adds them in mask-bit
+//            order -- exactly the reference's key order.  A texel's 8 planes leave as one
+//            128-B run.  Found pairs are counted.
+//  3. check  (bwd_check_kernel): the windows come from float inverse maps, so they are a
+//            guess that the count makes exact: every found pair is genuine and found at
+//            most once, so found == truth iff nothing was missed.  On a mismatch (or a
+//            geometry the gather refuses: plane behind the camera over a tile, boxes beyond
+//            LDS, a window whose 8-pixel chunks wrap rows) a device flag turns on the
+//            fallback: the general bucket pipeline below (counting sort of every sample by
+//            its nw tap, per-bucket pixel order, per-texel merge of the four buckets),
+//            launched always but returning at once while the flag is clear, over plane
+//            chunks so its workspace stays a fraction of d s.
+// Every product and sum is a single fp32 rounding written out explicitly (the library
+// builds with -ffp-contract=off).
 #include "mpiv_common.hpp"
 
 namespace mpiv {
 
-constexpr int kGridVec = 8;       // grid_sampler_2d_backward chunk width (oracle.GRID_VEC)
-constexpr int kScanItems = 16;    // items per thread in the bucket scan
+constexpr int kGridVec = 8;        // grid_sampler_2d_backward chunk width (oracle.GRID_VEC)
+constexpr int kBwdCH = 8;          // chain: planes per chunk
+constexpr int kGTW = 64;           // gather: texel tile width (a wave = one tile row)
+constexpr int kGTH = 4;            // gather: tile rows (4 waves)
+constexpr int kGPl = 8;            // gather: planes per block (one 128-B gradient run per texel)
+constexpr int kGCap = 1024;        // gather: output pixels staged per pass
+constexpr int kGMaxBox = 64 * kGCap;  // gather: larger boxes (extreme magnification) -> fallback
+constexpr int kCtrSlots = 64;      // the two pair counters are spread over 64 words each
+constexpr unsigned long long kUnsafe = 1ull << 40;  // > any truth count: forces the fallback
+
+constexpr int kScanItems = 16;     // fallback: items per thread in the bucket scan
 constexpr int kScanBlock = 256;
 constexpr int kScanTile = kScanItems * kScanBlock;
-
-constexpr int kSmallBucket = 32;  // larger buckets are sorted by a whole block
+constexpr int kSmallBucket = 32;   // fallback: larger buckets are sorted by a whole block
+constexpr int kFbGrid = 1024;      // fallback kernels: grid-stride grid (cheap when gated off)
 
 struct BwdWs {
-    float4* prev;  // [P][HW]  out_{p-1} (rgb, 0)
-    float4* ds;    // [P][HW]  sample s_p, then d s_p = (d rgb, d a)
-    float2* fw;    // [P][HW]  bilinear fractions (wx, wy)
-    int* key;      // [P][HW]  nw-tap bucket in the (H+1) x (W+1) grid, -1 = no tap in the image;
+    float4* ds;    // [P][HW]  d sample (d rgb, d a) per plane-pixel
+    float4* ckpt;  // [nchunk][HW] composited colour before chunk c (c >= 1)
+    float* inv;    // [P][12]  texel -> output pixel inverse map (9 floats), [9] = valid
+    int4* box;     // [P][tiles] gather pixel box (x0, x1, y0, y1); x0 = -2: the block cannot gather
+    unsigned long long* truth;  // [kCtrSlots] (sample, in-image tap) pairs
+    unsigned long long* found;  // [kCtrSlots] (texel, contributor) pairs gathered
+    int* flag;     // 1: the fallback recomputes every plane of the view
+    // fallback: bucket pipeline over chunks of pc planes
+    int pc;
+    int* key;      // [pc][HW] nw-tap bucket in the (H+1) x (W+1) grid, -1 = no tap in the image;
                    //          after the fill: merge-sort scratch (same offsets as ids)
-    int* count;    // [P*K]    bucket sizes; zero on entry and on exit of every view
-    int* offs;     // [P*K+1]  exclusive scan of count
-    int* ids;      // [P*HW]   pixel ids grouped by bucket
+    int* count;    // [pc*K]   bucket sizes; zero after every fill
+    int* offs;     // [pc*K+1] exclusive scan of count
+    int* ids;      // [pc*HW]  pixel ids grouped by bucket, sorted within a bucket
     int* bsum;     // scan block sums
-    int* big;      // [0] = number of large buckets, [1..] their indices (P*HW/(kSmallBucket+1) max)
+    int* big;      // [0] = number of large buckets, [1..] their indices
 };
 
-// ---- 1. forward recompute + over-chain adjoint, one work-item per output pixel ----
-template <bool FAST>
-__global__ __launch_bounds__(256) void render_bwd_chain_kernel(const float4* __restrict__ planes,
-                                                               int64_t plane_stride, RenderGeom g,
-                                                               const float* __restrict__ homs,
-                                                               const float* __restrict__ dout, BwdWs ws) {
-    const int tiles_x = (g.W + kTileX - 1) / kTileX;
-    const int x = (blockIdx.x % tiles_x) * kTileX + (threadIdx.x & (kWave - 1));
-    const int y = (blockIdx.x / tiles_x) * kTileY + (threadIdx.x >> 6);
-    if (x >= g.W || y >= g.H) return;
-    const int HW = g.H * g.W;
-    const int pix = y * g.W + x;
-    const int K1 = g.W + 1;
-    const int K = (g.H + 1) * K1;
-    const float fx = (float)x, fy = (float)y;
+// ---- 1. chain: forward recompute + over-chain adjoint, in place ----------------------
 
-    float cr = -0.0f, cg = -0.0f, cb = -0.0f;  // plane 0 replaces it exactly (render.hip)
-    // plane p's sample: position, then its four taps in flight (the last plane is
-    // re-issued past the end so every iteration issues; render.hip's ping-pong)
-    struct Sample {
-        TapSet ts;
+// sample position with the forward kernels' recipe: MODE 0 = the reference's plain
+// divisions (H or W < 2), 1 = fast recipe with the per-sample division guard, 2 = fast
+// recipe with the division proven for the whole tile (render.hip div2_rect_safe)
+template <int MODE>
+__device__ __forceinline__ void bwd_pos(const float* h, float fx, float fy, const RenderGeom& g, float& px,
+                                        float& py) {
+    if (MODE == 0)
+        hom_sample_pos(h, fx, fy, g.hm1, g.wm1, g.half_w, g.half_h, px, py);
+    else
+        chunk_pos<MODE == 1>(h, fx, fy, g, px, py);
+}
+
+template <int MODE>
+__device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, const RenderGeom& g,
+                                               const ChunkGeom& cg, const float* __restrict__ hs,
+                                               f32x4* __restrict__ slot, int tx0, int y, int lane,
+                                               const float* __restrict__ dout, const BwdWs& ws) {
+    constexpr int CH = kBwdCH, PPS = kWave / CH;
+    const int j = lane % CH, i = lane / CH;
+    const float fy = (float)y;
+    const int n = (g.P + CH - 1) / CH;
+    const int64_t HW = (int64_t)g.H * g.W;
+    const int x = tx0 + lane;  // this lane's pixel in the composite phases
+    const bool xin = x < g.W;
+    const int64_t pix = (int64_t)y * g.W + x;
+    float h[9];
+    auto load_h = [&](int c, float* d) {
+        const int p = min(c * CH + j, g.P - 1);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) d[k] = hs[p * 9 + k];
+    };
+    auto rsrc = [&](int c) { return make_rsrc(view + (int64_t)c * CH * 4, cg.rec_bytes); };
+    int ntap = 0;
+    // sub-step k of chunk c: pixel tx0 + k*PPS + i, plane c*CH + j (taps counted in pass 1)
+    auto issue = [&](int c, int k, const float* hh, ChunkTaps& ts, bool cnt) {
+        const int xs = tx0 + k * PPS + i;
         float px, py;
+        bwd_pos<MODE>(hh, (float)xs, fy, g, px, py);
+        const int nt = issue_taps_chunk(rsrc(c), g, cg, j, c * CH + j < g.P, px, py, ts);
+        if (cnt && xs < g.W) ntap += nt;
     };
-    auto issue = [&](int p, Sample& sm) {
-        const int pc = p < g.P ? p : g.P - 1;
-        render_pos<FAST>(homs + (int64_t)pc * 9, fx, fy, g, sm.px, sm.py);
-        issue_taps_padded(make_rsrc(planes + (int64_t)pc * plane_stride, g.plane_bytes), g.W, g.H, g.Wp, g.org,
-                          g.row, sm.px, sm.py, sm.ts);
+    auto put = [&](int k, const ChunkTaps& ts) { slot[(k * PPS + i) * (CH + 1) + j] = blend_chunk(ts); };
+    ChunkTaps A, B;
+    // chunk c's samples into the slot; A holds its sub-step 0 on entry and sub-step 0 of
+    // chunk cn (issued ahead, with cn's homography in h) on exit
+    auto sample_chunk = [&](int c, int cn, bool cnt, bool cnt_next) {
+#pragma unroll
+        for (int k = 0; k < CH; k += 2) {
+            issue(c, k + 1, h, B, cnt);
+            __builtin_amdgcn_sched_barrier(0);
+            put(k, A);
+            if (k + 2 < CH) {
+                issue(c, k + 2, h, A, cnt);
+            } else {
+                load_h(cn, h);
+                issue(cn, 0, h, A, cnt_next);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            put(k + 1, B);
+        }
     };
-    auto consume = [&](int p, const Sample& sm) {
-        const f32x4 s = blend_taps(sm.ts);
-        const float fx0 = floorf(sm.px), fy0 = floorf(sm.py);
-        const int64_t q = (int64_t)p * HW + pix;
-        ws.fw[q] = make_float2(sm.px - fx0, sm.py - fy0);
-        // some tap of this sample lies in the image iff the nw tap is in [-1, W-1] x [-1, H-1]
-        // (float compares: NaN positions have no taps, as in the reference's masks)
+    const f32x4* row = slot + lane * (CH + 1);
+    // ---- pass 1: planes 0 .. P-1 like the forward (plane 0 replaces the -0 start
+    // exactly, render.hip), the colour checkpointed before every chunk.  The last chunk
+    // stays in the slot for pass 2; chunk n-2 is issued ahead.
+    float cr = -0.0f, cgc = -0.0f, cb = -0.0f;
+    load_h(0, h);
+    issue(0, 0, h, A, true);
+    for (int c = 0; c < n; ++c) {
+        const bool last = c == n - 1;
+        sample_chunk(c, last ? max(n - 2, 0) : c + 1, true, !last);
+        if (last) break;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {  // a chunk before the last is full
+            const f32x4 s = row[k];
+            const float a = (c == 0 && k == 0) ? 1.0f : s[3];
+            const float om = 1.0f - a;
+            cr = over(s[0], a, om, cr);
+            cgc = over(s[1], a, om, cgc);
+            cb = over(s[2], a, om, cb);
+        }
+        if (xin) ws.ckpt[(int64_t)(c + 1) * HW + pix] = make_float4(cr, cgc, cb, 0.0f);
+    }
+    // ---- pass 2: chunks back to front; over_composite backward (utils.py:149-156 under
+    // autograd), planes P-1 .. 0
+    float g0 = 0.0f, g1 = 0.0f, g2 = 0.0f;
+    if (xin) {
+        const float* d = dout + pix * 3;
+        g0 = d[0];
+        g1 = d[1];
+        g2 = d[2];
+    }
+    for (int c = n - 1; c >= 0; --c) {
+        float4 pre = make_float4(cr, cgc, cb, 0.0f);  // c = n-1: pass 1's colour
+        if (c < n - 1) {
+            if (c == 0)
+                pre = make_float4(-0.0f, -0.0f, -0.0f, 0.0f);
+            else if (xin)
+                pre = ws.ckpt[(int64_t)c * HW + pix];
+            sample_chunk(c, c > 0 ? c - 1 : 0, false, false);
+        }
+        // prefixes out_{p-1} of the chunk's planes, recomputed in the forward's order
+        float pr[CH][3];
+        pr[0][0] = pre.x;
+        pr[0][1] = pre.y;
+        pr[0][2] = pre.z;
+#pragma unroll
+        for (int k = 0; k + 1 < CH; ++k) {
+            const int p = c * CH + k;
+            float r = pr[k][0], gr = pr[k][1], b = pr[k][2];
+            if (p < g.P) {
+                const f32x4 s = row[k];
+                const float a = p == 0 ? 1.0f : s[3];
+                const float om = 1.0f - a;
+                r = over(s[0], a, om, r);
+                gr = over(s[1], a, om, gr);
+                b = over(s[2], a, om, b);
+            }
+            pr[k + 1][0] = r;
+            pr[k + 1][1] = gr;
+            pr[k + 1][2] = b;
+        }
+#pragma unroll
+        for (int k = CH - 1; k >= 0; --k) {
+            const int p = c * CH + k;
+            if (p < g.P) {
+                const f32x4 s = row[k];
+                float4 d;
+                if (p >= 1) {
+                    const float a = s[3], om = 1.0f - a;
+                    float s1 = g0 * s[0];
+                    s1 = s1 + g1 * s[1];
+                    s1 = s1 + g2 * s[2];
+                    float s2 = g0 * pr[k][0];
+                    s2 = s2 + g1 * pr[k][1];
+                    s2 = s2 + g2 * pr[k][2];
+                    d = make_float4(g0 * a, g1 * a, g2 * a, s1 + (-s2));
+                    g0 = g0 * om;
+                    g1 = g1 * om;
+                    g2 = g2 * om;
+                } else {
+                    d = make_float4(g0, g1, g2, 0.0f);  // plane 0: output = rgb_0, alpha unused
+                }
+                if (xin) ws.ds[(int64_t)p * HW + pix] = d;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) ntap += __shfl_xor(ntap, off);
+    if (lane == 0 && ntap) atomicAdd(&ws.truth[blockIdx.x % kCtrSlots], (unsigned long long)ntap);
+}
+
+// One block = 4 waves = a 64x4 output tile of one view.  Dynamic LDS: 4 per-wave sample
+// slots (64 x (CH+1) float4) + the view's P homographies.  MODE 0: generic recipe
+// (H or W < 2); 1: fast recipe, the tile's division proof picks the unguarded path.
+template <int MODE>
+__global__ __launch_bounds__(256) void bwd_chain_kernel(const float* __restrict__ view, RenderGeom g, ChunkGeom cg,
+                                                        const float* __restrict__ homs,
+                                                        const float* __restrict__ dout, BwdWs ws) {
+    extern __shared__ float4 bwd_lds[];
+    f32x4* slots = reinterpret_cast<f32x4*>(bwd_lds);
+    float* hs = reinterpret_cast<float*>(bwd_lds) + 4 * kWave * (kBwdCH + 1) * 4;
+    const int tiles_x = (g.W + kTileX - 1) / kTileX;
+    const int tile = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * kTileY;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+    for (int k = threadIdx.x; k < g.P * 9; k += 256) hs[k] = homs[k];
+    bool ok = MODE != 0;
+    if (MODE != 0) {
+        const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
+        const float y0 = (float)ty0, y1 = (float)min(ty0 + kTileY - 1, g.H - 1);
+        for (int p = (int)threadIdx.x; p < g.P; p += 256) ok = ok && div2_rect_safe(homs + (int64_t)p * 9, x0, x1, y0, y1);
+    }
+    const bool proven = __syncthreads_and(ok);  // also publishes hs
+    const int y = ty0 + wave;
+    if (y >= g.H) return;  // whole wave; no barrier follows
+    f32x4* slot = slots + wave * kWave * (kBwdCH + 1);
+    if (MODE == 0)
+        bwd_chain_wave<0>(view, g, cg, hs, slot, tx0, y, lane, dout, ws);
+    else if (proven)
+        bwd_chain_wave<2>(view, g, cg, hs, slot, tx0, y, lane, dout, ws);
+    else
+        bwd_chain_wave<1>(view, g, cg, hs, slot, tx0, y, lane, dout, ws);
+}
+
+// ---- 2. gather: per-texel sums in the reference's order ------------------------------
+
+// Per plane, the inverse of F = T S H, the map from an output pixel (x, y, 1) to its
+// sample position: px = (W/(H-1)) * u/w - 0.5, py = (H/(W-1)) * v/w - 0.5 (the swapped
+// normalisation of utils.py:188 and grid_sample's unnormalise, in exact arithmetic).
+// F^-1 (x', y', z') of a texel point is (x, y, 1) / w, so z' > 0 exactly where the point is
+// the image of pixels in front of the camera.  Computed in double, stored as floats: the
+// windows built from it are guesses checked by the pair count.
+__global__ __launch_bounds__(64) void bwd_inverse_kernel(const float* __restrict__ homs, int P, double sx,
+                                                         double sy, float* __restrict__ inv) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const float* h = homs + (int64_t)p * 9;
+    double f[9];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        f[c] = sx * (double)h[c] - 0.5 * (double)h[6 + c];
+        f[3 + c] = sy * (double)h[3 + c] - 0.5 * (double)h[6 + c];
+        f[6 + c] = (double)h[6 + c];
+    }
+    double a[9];
+    a[0] = f[4] * f[8] - f[5] * f[7];
+    a[1] = f[2] * f[7] - f[1] * f[8];
+    a[2] = f[1] * f[5] - f[2] * f[4];
+    a[3] = f[5] * f[6] - f[3] * f[8];
+    a[4] = f[0] * f[8] - f[2] * f[6];
+    a[5] = f[2] * f[3] - f[0] * f[5];
+    a[6] = f[3] * f[7] - f[4] * f[6];
+    a[7] = f[1] * f[6] - f[0] * f[7];
+    a[8] = f[0] * f[4] - f[1] * f[3];
+    const double det = f[0] * a[0] + f[1] * a[3] + f[2] * a[6];
+    float* o = inv + (int64_t)p * 12;
+    bool ok = det != 0.0 && __builtin_isfinite(det);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const float v = ok ? (float)(a[k] / det) : 0.0f;
+        ok = ok && __builtin_isfinite(v);
+        o[k] = v;
+    }
+    o[9] = ok ? 1.0f : 0.0f;
+}
+
+// texel point (X, Y) -> output pixel point; false unless in front of the camera
+__device__ __forceinline__ bool inv_map(const float* m, float X, float Y, float& x, float& y) {
+    const float z = __builtin_fmaf(m[7], Y, m[6] * X) + m[8];
+    const float r = __builtin_amdgcn_rcpf(z);
+    x = (__builtin_fmaf(m[1], Y, m[0] * X) + m[2]) * r;
+    y = (__builtin_fmaf(m[4], Y, m[3] * X) + m[5]) * r;
+    return z > 0.0f && __builtin_isfinite(x) && __builtin_isfinite(y);
+}
+
+// Integer pixel range [lo, hi] covering [a - e, b + e], clamped to [cl, ch] (empty: lo > hi).
+__device__ __forceinline__ void pix_range(float a, float b, float e, int cl, int ch, int& lo, int& hi) {
+    lo = (int)ceilf(__builtin_fmaxf(a - e, (float)cl));
+    hi = (int)floorf(__builtin_fminf(b + e, (float)ch));
+}
+
+// Per (plane, gather tile): the box of output pixels whose samples can have a nw tap in
+// the tile's bucket region [tx0-1, tx0+kGTW] x [ty0-1, ty0+kGTH] (inverse image of its
+// corners, widened by `margin`), clamped to the frame; x0 = -2 when the block cannot gather
+// the plane (no inverse, a corner behind the camera, a box beyond the staging limits, or an
+// 8-pixel chunk wrapping rows across two passes): the check then sends the view to the
+// fallback.  x0 > x1 or y0 > y1: no pixel samples the tile.
+constexpr int kGTHc = kGTH;
+constexpr int kBoxProven = 1 << 30;
+__global__ __launch_bounds__(256) void bwd_box_kernel(RenderGeom g, const float* __restrict__ homs,
+                                                      const float* __restrict__ inv, int ntiles, int tiles_x,
+                                                      float margin, int4* __restrict__ box) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)g.P * ntiles) return;
+    const int p = (int)(i / ntiles), tile = (int)(i - (int64_t)p * ntiles);
+    const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTHc;
+    const float* iv = inv + (int64_t)p * 12;
+    float m[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) m[k] = iv[k];
+    bool bad = iv[9] == 0.0f;
+    float xmn = __builtin_inff(), xmx = -__builtin_inff(), ymn = __builtin_inff(), ymx = -__builtin_inff();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float xx, yy;
+        const bool okc =
+            inv_map(m, (float)((c & 1) ? tx0 + kGTW : tx0 - 1), (float)((c & 2) ? ty0 + kGTHc : ty0 - 1), xx, yy);
+        bad = bad || !okc;
+        xmn = __builtin_fminf(xmn, xx);
+        xmx = __builtin_fmaxf(xmx, xx);
+        ymn = __builtin_fminf(ymn, yy);
+        ymx = __builtin_fmaxf(ymx, yy);
+    }
+    int bx0 = 0, bx1 = -1, by0 = 0, by1 = -1;
+    if (!bad) {
+        pix_range(xmn, xmx, margin, 0, g.W - 1, bx0, bx1);
+        pix_range(ymn, ymx, margin, 0, g.H - 1, by0, by1);
+        const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
+        if (bw > 0 && bh > 0) {
+            const int rpp = bw <= kGCap ? kGCap / bw : 1;
+            bad = bw > kGCap || (int64_t)bw * bh > kGMaxBox ||
+                  (bh > rpp && (g.W & 7) && bx0 <= 6 && bx1 >= g.W - 7);
+        }
+    }
+    // bit 30 of y1: the fast division is proven for every pixel of the box (render.hip
+    // div2_rect_safe), so the gather's fill needs no per-sample guard
+    const bool proven = !bad && bx0 <= bx1 && by0 <= by1 &&
+                        div2_rect_safe(homs + (int64_t)p * 9, (float)bx0, (float)bx1, (float)by0, (float)by1);
+    box[i] = bad ? make_int4(-2, -3, 0, -1) : make_int4(bx0, bx1, by0, by1 | (proven ? kBoxProven : 0));
+}
+
+__device__ __forceinline__ void sort4(unsigned& a, unsigned& b, unsigned& c, unsigned& d) {
+    auto cx = [](unsigned& x, unsigned& y) {
+        const unsigned lo = min(x, y), hi = max(x, y);
+        x = lo;
+        y = hi;
+    };
+    cx(a, b); cx(c, d); cx(a, c); cx(b, d); cx(b, c);
+}
+
+// 8-input sorting network (19 comparators; checked exhaustively by the 0-1 principle)
+__device__ __forceinline__ void sort8(unsigned* k) {
+    auto cx = [&](int a, int b) {
+        const unsigned lo = min(k[a], k[b]), hi = max(k[a], k[b]);
+        k[a] = lo;
+        k[b] = hi;
+    };
+    cx(0, 1); cx(2, 3); cx(4, 5); cx(6, 7);
+    cx(0, 2); cx(1, 3); cx(4, 6); cx(5, 7);
+    cx(1, 2); cx(5, 6); cx(0, 4); cx(3, 7);
+    cx(1, 5); cx(2, 6);
+    cx(1, 4); cx(3, 6);
+    cx(2, 4); cx(3, 5);
+    cx(3, 4);
+}
+
+constexpr int kGTB = kGTW + 1;              // bucket row pitch: nw taps x in [tx0-1, tx0+kGTW-1]
+constexpr int kGNB = kGTB * (kGTH + 1);     // nw-tap buckets of a tile
+constexpr int kGBCap = 2;                   // entries per bucket list (more: the window scan)
+
+// Grid: (texel tiles) x (groups of kGPl planes), XCD-aware (neighbouring tiles of one
+// plane group, whose pixel boxes overlap, share an XCD's L2).  The d-sample contribution
+// of pixel q to texel t: weight(corner) * d s_q, added in key order from +0.
+//
+// Per plane and pass: the box's pixels are staged (sample position -> nw-tap bucket,
+// fractions, d s) and pushed onto their bucket's list (LDS atomic slot, <= 2 entries, each
+// the pixel's order key without the corner: ((pixel/8 - pass base) << 16 | pixel%8 << 11 |
+// staged index)).  A texel is the nw / ne / sw / se tap of the samples in buckets t, t-1,
+// t-row, t-row-1: their <= 8 keys, or-ed with the corner (bits 14-15), sort into exactly the
+// reference's order (pixel/8, corner, pixel%8), and the staged index rides in the low bits.
+// A bucket with more entries (magnification: several pixels per texel) makes the block
+// scan per-texel windows of the inverse map instead (one 8-pixel chunk at a time).
+__global__ __launch_bounds__(256) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
+                                                         float4* __restrict__ dmpi, float margin) {
+    __shared__ int s_code[kGCap];     // local nw-tap bucket of the staged pixel, -1 = none
+    __shared__ float2 s_fr[kGCap];    // its bilinear fractions (px - floor px, py - floor py)
+    __shared__ float4 s_ds[kGCap];    // its d sample
+    __shared__ uint2 s_bent[kGNB];    // bucket lists (kGBCap entries)
+    __shared__ int s_bcnt[2][kGNB];   // bucket sizes, by pass parity (one is zeroed while the other is in use)
+    __shared__ int s_ovf[2];          // a list overflowed in this pass
+    constexpr int TB = kGTB;
+    const int tiles_x = (g.W + kGTW - 1) / kGTW;
+    const int ntiles = tiles_x * ((g.H + kGTH - 1) / kGTH);
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int tile = lb % ntiles, p0 = (lb / ntiles) * kGPl;
+    const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTH;
+    const int tx = tx0 + (threadIdx.x & (kWave - 1)), ty = ty0 + (threadIdx.x >> 6);
+    const bool tin = tx < g.W && ty < g.H;
+    const int64_t HW = (int64_t)g.H * g.W;
+    const int bt = (ty - ty0 + 1) * TB + (tx - tx0 + 1);  // bucket of the texel as an nw tap
+    for (int b = threadIdx.x; b < 2 * kGNB; b += 256) (&s_bcnt[0][0])[b] = 0;
+    if (threadIdx.x < 2) s_ovf[threadIdx.x] = 0;
+    int par = 0;
+    unsigned hits = 0;    // (texel, contributor) pairs found by this thread
+    bool unsafe = false;  // a plane this block could not order (the view goes to the fallback)
+    f32x4 acc[kGPl];
+#pragma unroll
+    for (int jj = 0; jj < kGPl; ++jj) {
+        acc[jj] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const int p = p0 + jj;
+        if (p >= g.P) continue;  // block-uniform
+        const int4 bx = ws.box[(int64_t)p * ntiles + tile];  // bwd_box_kernel
+        const int bx0 = bx.x, bx1 = bx.y, by0 = bx.z, by1 = bx.w & ~kBoxProven;
+        const bool proven = (bx.w & kBoxProven) != 0;
+        if (bx0 == -2) {  // this block cannot gather the plane: the check sends the view to the fallback
+            unsafe = true;
+            continue;
+        }
+        const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
+        if (bw <= 0 || bh <= 0) continue;  // no pixel samples the tile: zero gradient (counted)
+        const int rpp = kGCap / bw;  // box rows per pass
+        const float* hp = homs + (int64_t)p * 9;
+        for (int ra = by0; ra <= by1; ra += rpp) {
+            const int rb = min(by1 + 1, ra + rpp);
+            const int np = (rb - ra) * bw;
+            const int gbase = (ra * g.W) >> 3;  // the pass's first 8-pixel chunk
+            __syncthreads();  // the previous pass's readers are done
+            {
+                int* cnt = s_bcnt[par];
+                // order keys hold (chunk - gbase) in 16 bits
+                if (threadIdx.x == 0 && (int64_t)(rb - ra + 1) * g.W >= ((int64_t)1 << 19)) s_ovf[par] = 1;
+                const float rbw = 1.0f / (float)bw;
+                for (int q = threadIdx.x; q < np; q += 256) {
+                    const int r = (int)(((float)q + 0.5f) * rbw);  // q / bw: q, bw <= 1024, error << 0.5/bw
+                    const int yy = ra + r, xx = bx0 + (q - r * bw);
+                    float px, py;
+                    if (proven)
+                        render_pos_fast<false>(hp, (float)xx, (float)yy, g, px, py);
+                    else
+                        render_pos<true>(hp, (float)xx, (float)yy, g, px, py);
+                    const float fx0 = floorf(px), fy0 = floorf(py);
+                    const float lx = fx0 - (float)(tx0 - 1), ly = fy0 - (float)(ty0 - 1);
+                    const bool in = lx >= 0.0f && lx <= (float)kGTW && ly >= 0.0f && ly <= (float)kGTH;
+                    const int code = in ? (int)ly * TB + (int)lx : -1;
+                    s_code[q] = code;
+                    if (in) {
+                        s_fr[q] = make_float2(px - fx0, py - fy0);
+                        s_ds[q] = ws.ds[(int64_t)p * HW + (int64_t)yy * g.W + xx];
+                        const int pix = yy * g.W + xx;
+                        const unsigned e = ((unsigned)((pix >> 3) - gbase) << 16) | ((unsigned)(pix & 7) << 11) |
+                                           (unsigned)q;
+                        const int slot = atomicAdd(&cnt[code], 1);
+                        if (slot < kGBCap)
+                            (slot == 0 ? s_bent[code].x : s_bent[code].y) = e;
+                        else
+                            s_ovf[par] = 1;
+                    }
+                }
+                for (int b = threadIdx.x; b < kGNB; b += 256) s_bcnt[par ^ 1][b] = 0;  // for the next pass
+                if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
+            }
+            __syncthreads();
+            const bool ovf = s_ovf[par] != 0;
+            if (tin && !ovf) {
+                // the texel's <= 8 contributors: buckets t (nw), t-1 (ne), t-row (sw), t-row-1 (se)
+                const int* cnt = s_bcnt[par];
+                unsigned key[8];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int b = bt - (c & 1) - (c >> 1) * TB;
+                    const int n = cnt[b];
+                    const uint2 e = s_bent[b];
+                    key[2 * c] = n > 0 ? (e.x | ((unsigned)c << 14)) : 0xFFFFFFFFu;
+                    key[2 * c + 1] = n > 1 ? (e.y | ((unsigned)c << 14)) : 0xFFFFFFFFu;
+                }
+                bool two = false;  // some bucket of this texel holds two pixels
+#pragma unroll
+                for (int c = 0; c < 4; ++c) two = two || key[2 * c + 1] != 0xFFFFFFFFu;
+                if (__any(two)) {
+                    sort8(key);
+                } else {  // one pixel per bucket in the whole wave (no magnification): 4 keys
+                    sort4(key[0], key[2], key[4], key[6]);
+                    key[1] = key[2];
+                    key[2] = key[4];
+                    key[3] = key[6];
+                    key[4] = key[5] = key[6] = key[7] = 0xFFFFFFFFu;
+                }
+                // valid keys sort first; a batch's reads are skipped when no lane of the wave
+                // has that many contributors
+#pragma unroll
+                for (int k0 = 0; k0 < 8; k0 += 4) {
+                    if (key[k0] == 0xFFFFFFFFu) break;  // this lane is done (others may go on)
+                    float2 f[4];
+                    float4 d[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (key[k0 + k] != 0xFFFFFFFFu) {
+                            const int q = (int)(key[k0 + k] & (kGCap * 2 - 1));
+                            f[k] = s_fr[q];
+                            d[k] = s_ds[q];
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (key[k0 + k] != 0xFFFFFFFFu) {
+                            const float wx = f[k].x, ex = 1.0f - wx;
+                            const float wy = f[k].y, sy = 1.0f - wy;
+                            const unsigned c = key[k0 + k] >> 14;  // corner bits 14-15 (+ chunk bits above)
+                            const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
+                            acc[jj][0] = acc[jj][0] + w * d[k].x;
+                            acc[jj][1] = acc[jj][1] + w * d[k].y;
+                            acc[jj][2] = acc[jj][2] + w * d[k].z;
+                            acc[jj][3] = acc[jj][3] + w * d[k].w;
+                            ++hits;
+                        }
+                    }
+                }
+            } else if (tin) {
+                // window scan: the inverse image of the texels [tx-1, tx+1] x [ty-1, ty+1]
+                // whose samples have this texel as a tap, candidates in pixel order, the hits
+                // of one 8-pixel chunk collected in a mask (bit corner*8 + pixel%8) and added
+                // in bit order
+                const float* iv = ws.inv + (int64_t)p * 12;
+                float m[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) m[k] = iv[k];
+                int wx0 = 0, wx1 = -1, wy0 = 0, wy1 = -1;
+                float a0 = __builtin_inff(), a1 = -__builtin_inff(), b0 = __builtin_inff(), b1 = -__builtin_inff();
+                bool lbad = false;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    float xx, yy;
+                    const bool okc =
+                        inv_map(m, (float)(tx + ((c & 1) ? 1 : -1)), (float)(ty + ((c & 2) ? 1 : -1)), xx, yy);
+                    lbad = lbad || !okc;
+                    a0 = __builtin_fminf(a0, xx);
+                    a1 = __builtin_fmaxf(a1, xx);
+                    b0 = __builtin_fminf(b0, yy);
+                    b1 = __builtin_fmaxf(b1, yy);
+                }
+                if (!lbad) {
+                    pix_range(a0, a1, margin, bx0, bx1, wx0, wx1);
+                    pix_range(b0, b1, margin, by0, by1, wy0, wy1);
+                    // a wrapping 8-pixel chunk must not have window pixels in two rows: the
+                    // per-row flush below would split its order
+                    if ((g.W & 7) && wy1 > wy0 && wx1 >= g.W - 7 && wx0 <= 6) lbad = true;
+                }
+                if (lbad) {
+                    unsafe = true;
+                    wy1 = wy0 - 1;
+                }
+                const int ya = max(wy0, ra), yb = min(wy1, rb - 1);
+                for (int yy = ya; yy <= yb; ++yy) {
+                    const int rowbase = (yy - ra) * bw - bx0;  // staged index of pixel (x, yy): rowbase + x
+                    const int pixrow = yy * g.W;
+                    int cur = -1;     // 8-pixel chunk (pixel / 8) of the hits in `msk`
+                    unsigned msk = 0;
+                    auto flush = [&]() {
+                        while (msk) {
+                            const int b = __builtin_ctz(msk);
+                            msk &= msk - 1;
+                            const int idx = rowbase + (cur * kGridVec + (b & 7) - pixrow);
+                            const float2 f = s_fr[idx];
+                            const float4 d = s_ds[idx];
+                            const float wx = f.x, ex = 1.0f - wx;
+                            const float wy = f.y, sy = 1.0f - wy;
+                            const int c = b >> 3;
+                            const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
+                            acc[jj][0] = acc[jj][0] + w * d.x;
+                            acc[jj][1] = acc[jj][1] + w * d.y;
+                            acc[jj][2] = acc[jj][2] + w * d.z;
+                            acc[jj][3] = acc[jj][3] + w * d.w;
+                            ++hits;
+                        }
+                    };
+                    for (int xx = wx0; xx <= wx1; ++xx) {
+                        const int code = s_code[rowbase + xx];
+                        const int dd = bt - code;  // 0: nw tap, 1: ne, TB: sw, TB+1: se
+                        const int c = code < 0 ? -1 : dd == 0 ? 0 : dd == 1 ? 1 : dd == TB ? 2 : dd == TB + 1 ? 3 : -1;
+                        if (c >= 0) {
+                            const int px = pixrow + xx;
+                            if ((px >> 3) != cur) {
+                                flush();
+                                cur = px >> 3;
+                            }
+                            msk |= 1u << (c * 8 + (px & 7));
+                        }
+                    }
+                    flush();
+                }
+            }
+            par ^= 1;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) hits += __shfl_xor(hits, off);
+    const unsigned long long tot = (unsigned long long)hits + (__any(unsafe) ? kUnsafe : 0ull);
+    if ((threadIdx.x & (kWave - 1)) == 0 && tot) atomicAdd(&ws.found[blockIdx.x % kCtrSlots], tot);
+    if (tin) {
+        float4* o = dmpi + ((int64_t)ty * g.W + tx) * g.P + p0;
+#pragma unroll
+        for (int jj = 0; jj < kGPl; ++jj)
+            if (p0 + jj < g.P) o[jj] = make_float4(acc[jj][0], acc[jj][1], acc[jj][2], acc[jj][3]);
+    }
+}
+
+// ---- 3. check: found == truth, else the fallback runs; counters reset for the next view
+__global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force) {
+    const int l = threadIdx.x;
+    unsigned long long t = ws.truth[l], f = ws.found[l];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        t += __shfl_xor(t, off);
+        f += __shfl_xor(f, off);
+    }
+    ws.truth[l] = 0;
+    ws.found[l] = 0;
+    if (l == 0) *ws.flag = (force || t != f) ? 1 : 0;
+}
+
+// ---- fallback: the general bucket pipeline (runs only when *flag is set) -------------
+
+__device__ __forceinline__ bool fb_off(const BwdWs& ws) { return *ws.flag == 0; }
+
+__global__ __launch_bounds__(256) void fb_zero_kernel(BwdWs ws, int64_t n) {
+    if (fb_off(ws)) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) ws.count[i] = 0;
+}
+
+// nw-tap bucket of every (plane of the chunk, pixel) sample; bucket sizes counted
+template <bool FAST>
+__global__ __launch_bounds__(256) void fb_key_kernel(RenderGeom g, const float* __restrict__ homs, int pc0, int pcn,
+                                                     BwdWs ws) {
+    if (fb_off(ws)) return;
+    const int64_t HW = (int64_t)g.H * g.W;
+    const int K1 = g.W + 1;
+    const int64_t K = (int64_t)(g.H + 1) * K1;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < pcn * HW; q += (int64_t)gridDim.x * 256) {
+        const int pl = (int)(q / HW);
+        const int pix = (int)(q - pl * HW);
+        const int y = pix / g.W, x = pix - y * g.W;
+        float px, py;
+        render_pos<FAST>(homs + (int64_t)(pc0 + pl) * 9, (float)x, (float)y, g, px, py);
+        const float fx0 = floorf(px), fy0 = floorf(py);
+        // some tap lies in the image iff the nw tap is in [-1, W-1] x [-1, H-1] (NaN: none)
         const bool in = fx0 >= -1.0f && fx0 <= (float)(g.W - 1) && fy0 >= -1.0f && fy0 <= (float)(g.H - 1);
         const int k = in ? ((int)fy0 + 1) * K1 + (int)fx0 + 1 : -1;
         ws.key[q] = k;
-        if (in) atomicAdd(&ws.count[(int64_t)p * K + k], 1);
-        ws.prev[q] = make_float4(cr, cg, cb, 0.0f);
-        ws.ds[q] = make_float4(s[0], s[1], s[2], s[3]);
-        const float a = p == 0 ? 1.0f : s[3];
-        const float om = 1.0f - a;
-        cr = over(s[0], a, om, cr);
-        cg = over(s[1], a, om, cg);
-        cb = over(s[2], a, om, cb);
-    };
-    Sample A, B;
-    issue(0, A);
-    int p = 0;
-    for (; p + 1 < g.P; p += 2) {
-        issue(p + 1, B);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(p, A);
-        issue(p + 2, A);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(p + 1, B);
+        if (in) atomicAdd(&ws.count[pl * K + k], 1);
     }
-    if (p < g.P) consume(p, A);
-    // over_composite backward (utils.py:149-156 under autograd), front to back
-    const float* d = dout + (int64_t)pix * 3;
-    float g0 = d[0], g1 = d[1], g2 = d[2];
-    for (int p = g.P - 1; p >= 1; --p) {
-        const int64_t q = (int64_t)p * HW + pix;
-        const float4 s = ws.ds[q];
-        const float4 o = ws.prev[q];
-        const float a = s.w, om = 1.0f - a;
-        float s1 = g0 * s.x;
-        s1 = s1 + g1 * s.y;
-        s1 = s1 + g2 * s.z;
-        float s2 = g0 * o.x;
-        s2 = s2 + g1 * o.y;
-        s2 = s2 + g2 * o.z;
-        ws.ds[q] = make_float4(g0 * a, g1 * a, g2 * a, s1 + (-s2));
-        g0 = g0 * om;
-        g1 = g1 * om;
-        g2 = g2 * om;
-    }
-    ws.ds[pix] = make_float4(g0, g1, g2, 0.0f);  // plane 0: output = rgb_0, alpha unused
 }
-
-// ---- 2. exclusive scan of the bucket sizes -------------------------------------------
 
 __device__ __forceinline__ int block_exclusive_scan(int v, int* s_tmp, int& total) {
     // 256 threads: inclusive Hillis-Steele scan through LDS
@@ -153,124 +701,99 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* s_tmp, int& tota
     return incl - v;
 }
 
-__global__ __launch_bounds__(kScanBlock) void scan_tile_sums_kernel(const int* __restrict__ in, int64_t n,
-                                                                    int* __restrict__ bsum) {
+__global__ __launch_bounds__(kScanBlock) void fb_scan_sums_kernel(BwdWs ws, int64_t n, int nb) {
     __shared__ int s_tmp[kScanBlock];
-    const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-    int sum = 0;
-    if (base + kScanItems <= n) {  // whole item run in range: 16-B loads (base is 64-B aligned)
-        const int4* v4 = reinterpret_cast<const int4*>(in + base);
-#pragma unroll
-        for (int i = 0; i < kScanItems / 4; ++i) {
-            const int4 v = v4[i];
-            sum += v.x + v.y + v.z + v.w;
-        }
-    } else {
-#pragma unroll
+    if (fb_off(ws)) return;
+    for (int tb = blockIdx.x; tb < nb; tb += gridDim.x) {
+        const int64_t base = (int64_t)tb * kScanTile + (int64_t)threadIdx.x * kScanItems;
+        int sum = 0;
         for (int i = 0; i < kScanItems; ++i)
-            if (base + i < n) sum += in[base + i];
+            if (base + i < n) sum += ws.count[base + i];
+        int total;
+        block_exclusive_scan(sum, s_tmp, total);
+        if (threadIdx.x == 0) ws.bsum[tb] = total;
     }
-    int total;
-    block_exclusive_scan(sum, s_tmp, total);
-    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
 // single block: exclusive scan of the nb tile sums in place
-__global__ __launch_bounds__(kScanBlock) void scan_tile_offsets_kernel(int* __restrict__ bsum, int nb) {
+__global__ __launch_bounds__(kScanBlock) void fb_scan_offsets_kernel(BwdWs ws, int nb) {
     __shared__ int s_tmp[kScanBlock];
+    if (fb_off(ws)) return;
     int carry = 0;
     for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
         const int i = c0 + threadIdx.x;
-        const int v = i < nb ? bsum[i] : 0;
+        const int v = i < nb ? ws.bsum[i] : 0;
         int total;
         const int ex = block_exclusive_scan(v, s_tmp, total);
-        if (i < nb) bsum[i] = carry + ex;
+        if (i < nb) ws.bsum[i] = carry + ex;
         carry += total;
     }
 }
 
-__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const int* __restrict__ in, int64_t n,
-                                                                const int* __restrict__ bsum,
-                                                                int* __restrict__ out) {
+__global__ __launch_bounds__(kScanBlock) void fb_scan_apply_kernel(BwdWs ws, int64_t n, int nb) {
     __shared__ int s_tmp[kScanBlock];
-    const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-    int v[kScanItems];
-    int sum = 0;
-    const bool full = base + kScanItems <= n;  // whole run in range: 16-B loads and stores
-    if (full) {
-        const int4* v4 = reinterpret_cast<const int4*>(in + base);
-#pragma unroll
-        for (int i = 0; i < kScanItems / 4; ++i) {
-            const int4 q = v4[i];
-            v[4 * i] = q.x; v[4 * i + 1] = q.y; v[4 * i + 2] = q.z; v[4 * i + 3] = q.w;
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < kScanItems; ++i) v[i] = base + i < n ? in[base + i] : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < kScanItems; ++i) sum += v[i];
-    int total;
-    int run = bsum[blockIdx.x] + block_exclusive_scan(sum, s_tmp, total);
-    if (full) {  // out = offs + 0: 16-B aligned like in
-        int4* o4 = reinterpret_cast<int4*>(out + base);
-#pragma unroll
-        for (int i = 0; i < kScanItems / 4; ++i) {
-            int4 q;
-            q.x = run; run += v[4 * i];
-            q.y = run; run += v[4 * i + 1];
-            q.z = run; run += v[4 * i + 2];
-            q.w = run; run += v[4 * i + 3];
-            o4[i] = q;
-        }
-    } else {
+    if (fb_off(ws)) return;
+    for (int tb = blockIdx.x; tb < nb; tb += gridDim.x) {
+        const int64_t base = (int64_t)tb * kScanTile + (int64_t)threadIdx.x * kScanItems;
+        int v[kScanItems];
+        int sum = 0;
 #pragma unroll
         for (int i = 0; i < kScanItems; ++i) {
-            if (base + i < n) out[base + i] = run;
+            v[i] = base + i < n ? ws.count[base + i] : 0;
+            sum += v[i];
+        }
+        int total;
+        int run = ws.bsum[tb] + block_exclusive_scan(sum, s_tmp, total);
+#pragma unroll
+        for (int i = 0; i < kScanItems; ++i) {
+            if (base + i < n) ws.offs[base + i] = run;
             run += v[i];
         }
+        if (tb == nb - 1 && threadIdx.x == kScanBlock - 1) ws.offs[n] = run;  // grand total
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanBlock - 1) out[n] = run;  // grand total
 }
 
-// ---- 3. pixel ids into buckets, then each bucket sorted by pixel id ------------------
-
-__global__ __launch_bounds__(256) void bucket_fill_kernel(int P, int HW, int K, BwdWs ws) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= (int64_t)P * HW) return;
-    const int k = ws.key[q];
-    if (k < 0) return;
-    const int p = (int)(q / HW), pix = (int)(q - (int64_t)p * HW);
-    const int64_t pk = (int64_t)p * K + k;
-    const int slot = atomicSub(&ws.count[pk], 1) - 1;  // count returns to 0 for the next view
-    ws.ids[ws.offs[pk] + slot] = pix;
+// pixel ids into their buckets (atomic slot claim; count returns to 0 for the next chunk)
+__global__ __launch_bounds__(256) void fb_fill_kernel(int64_t HW, int pcn, int64_t K, BwdWs ws) {
+    if (fb_off(ws)) return;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < pcn * HW; q += (int64_t)gridDim.x * 256) {
+        const int k = ws.key[q];
+        if (k < 0) continue;
+        const int64_t pl = q / HW;
+        const int64_t pk = pl * K + k;
+        const int slot = atomicSub(&ws.count[pk], 1) - 1;
+        ws.ids[ws.offs[pk] + slot] = (int)(q - pl * HW);
+    }
 }
 
-__global__ __launch_bounds__(256) void bucket_sort_kernel(int64_t nbuckets, BwdWs ws) {
-    const int64_t pk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (pk >= nbuckets) return;
-    const int b = ws.offs[pk], e = ws.offs[pk + 1];
-    if (e - b > kSmallBucket) {  // left to big_bucket_sort_kernel
-        ws.big[1 + atomicAdd(&ws.big[0], 1)] = (int)pk;
-        return;
-    }
-    for (int i = b + 1; i < e; ++i) {  // insertion sort (at most kSmallBucket ids)
-        const int v = ws.ids[i];
-        int j = i - 1;
-        while (j >= b && ws.ids[j] > v) {
-            ws.ids[j + 1] = ws.ids[j];
-            --j;
+// each bucket sorted by pixel id: <= kSmallBucket ids by one thread, larger ones
+// (minification, degenerate homographies) listed for fb_big_sort_kernel
+__global__ __launch_bounds__(256) void fb_sort_kernel(int64_t nbuckets, BwdWs ws) {
+    if (fb_off(ws)) return;
+    for (int64_t pk = (int64_t)blockIdx.x * 256 + threadIdx.x; pk < nbuckets; pk += (int64_t)gridDim.x * 256) {
+        const int b = ws.offs[pk], e = ws.offs[pk + 1];
+        if (e - b > kSmallBucket) {
+            ws.big[1 + atomicAdd(&ws.big[0], 1)] = (int)pk;
+            continue;
         }
-        ws.ids[j + 1] = v;
+        for (int i = b + 1; i < e; ++i) {  // insertion sort (at most kSmallBucket ids)
+            const int v = ws.ids[i];
+            int jx = i - 1;
+            while (jx >= b && ws.ids[jx] > v) {
+                ws.ids[jx + 1] = ws.ids[jx];
+                --jx;
+            }
+            ws.ids[jx + 1] = v;
+        }
     }
 }
 
-// Sorts the large buckets listed by bucket_sort_kernel: each block takes buckets
-// blockIdx.x, blockIdx.x + gridDim.x, ... and merge-sorts one at a time, all threads
-// together (runs of width w merged pairwise per pass; output element k of a pair found
-// by a merge-path binary search; ids within a bucket are distinct).  The scratch is the
-// bucket's range of `key` (dead after the fill).  O(n log^2 n / threads) per bucket.
-__global__ __launch_bounds__(256) void big_bucket_sort_kernel(BwdWs ws) {
+// The large buckets: each block merge-sorts one at a time with all threads (runs of width
+// w merged pairwise per pass, output element k of a pair found by a merge-path binary
+// search; ids within a bucket are distinct).  Scratch: the bucket's range of `key` (dead
+// after the fill).  O(n log^2 n / threads) per bucket.  Resets the list for the next chunk.
+__global__ __launch_bounds__(256) void fb_big_sort_kernel(BwdWs ws) {
+    if (fb_off(ws)) return;
     const int nbig = ws.big[0];
     for (int i = blockIdx.x; i < nbig; i += gridDim.x) {
         const int pk = ws.big[1 + i];
@@ -280,16 +803,18 @@ __global__ __launch_bounds__(256) void big_bucket_sort_kernel(BwdWs ws) {
         for (int w = 1; w < n; w <<= 1) {
             for (int k0 = threadIdx.x; k0 < n; k0 += blockDim.x) {
                 const int s0 = (k0 / (2 * w)) * (2 * w);
-                const int m = min(s0 + w, n), e = min(s0 + 2 * w, n);
+                const int mm = min(s0 + w, n), e = min(s0 + 2 * w, n);
                 const int k = k0 - s0;
                 const int* A = src + s0;
-                const int* Bv = src + m;
-                const int la = m - s0, lb = e - m;
+                const int* Bv = src + mm;
+                const int la = mm - s0, lb = e - mm;
                 int lo = max(0, k - lb), hi = min(k, la);
                 while (lo < hi) {  // number of A's elements among the pair's first k outputs
                     const int mid = (lo + hi) >> 1;
-                    if (A[mid] < Bv[k - 1 - mid]) lo = mid + 1;
-                    else hi = mid;
+                    if (A[mid] < Bv[k - 1 - mid])
+                        lo = mid + 1;
+                    else
+                        hi = mid;
                 }
                 const int ib = k - lo;
                 dst[k0] = (lo < la && (ib >= lb || A[lo] < Bv[ib])) ? A[lo] : Bv[ib];
@@ -305,100 +830,76 @@ __global__ __launch_bounds__(256) void big_bucket_sort_kernel(BwdWs ws) {
     }
 }
 
-// ---- 4. per-texel gather in the reference's scatter order ----------------------------
-
-struct GradOut {
-    int64_t y, x, p, c;  // element strides of one view of d rgba_layers [H, W, P, 4]
-};
+// big list cleared after the sort kernels of a chunk (one thread)
+__global__ void fb_big_reset_kernel(BwdWs ws) {
+    if (fb_off(ws)) return;
+    ws.big[0] = 0;
+}
 
 __device__ __forceinline__ unsigned order_key(int pix, int corner) {
     return ((unsigned)(pix / kGridVec) << 5) | ((unsigned)corner << 3) | (unsigned)(pix % kGridVec);
 }
 
-// Sum of the gradient contributions of texel t of plane p, in the reference's order.
-__device__ __forceinline__ float4 gather_texel(int H, int W, int p, int t, const BwdWs& ws) {
-    const int HW = H * W;
-    const int ty = t / W, tx = t - ty * W;
-    const int K1 = W + 1;
-    const int64_t base = (int64_t)p * (H + 1) * K1;
-    // the texel is the nw / ne / sw / se tap of the samples in these nw-tap buckets
-    const int64_t bk[4] = {base + (int64_t)(ty + 1) * K1 + tx + 1, base + (int64_t)(ty + 1) * K1 + tx,
-                           base + (int64_t)ty * K1 + tx + 1, base + (int64_t)ty * K1 + tx};
-    int pos[4], end[4];
-    unsigned head[4];
+// Texel t of plane pc0 + pl: its four nw-tap buckets (the samples having it as nw, ne, sw,
+// se tap) merged by the reference's order key; fractions recomputed from the position.
+template <bool FAST>
+__global__ __launch_bounds__(256) void fb_gather_kernel(RenderGeom g, const float* __restrict__ homs, int pc0,
+                                                        int pcn, BwdWs ws, float4* __restrict__ dmpi) {
+    if (fb_off(ws)) return;
+    const int64_t HW = (int64_t)g.H * g.W;
+    const int K1 = g.W + 1;
+    const int64_t K = (int64_t)(g.H + 1) * K1;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < pcn * HW; q += (int64_t)gridDim.x * 256) {
+        const int pl = (int)(q / HW);
+        const int t = (int)(q - pl * HW);
+        const int ty = t / g.W, tx = t - ty * g.W;
+        const float* h = homs + (int64_t)(pc0 + pl) * 9;
+        const int64_t base = pl * K;
+        const int64_t bk[4] = {base + (int64_t)(ty + 1) * K1 + tx + 1, base + (int64_t)(ty + 1) * K1 + tx,
+                               base + (int64_t)ty * K1 + tx + 1, base + (int64_t)ty * K1 + tx};
+        int pos[4], end[4];
+        unsigned head[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        pos[c] = ws.offs[bk[c]];
-        end[c] = ws.offs[bk[c] + 1];
-        head[c] = pos[c] < end[c] ? order_key(ws.ids[pos[c]], c) : 0xFFFFFFFFu;
-    }
-    const float4* dsp = ws.ds + (int64_t)p * HW;
-    const float2* fwp = ws.fw + (int64_t)p * HW;
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-    for (;;) {
-        int c = 0;
-        unsigned m = head[0];
-#pragma unroll
-        for (int k = 1; k < 4; ++k)
-            if (head[k] < m) {
-                m = head[k];
-                c = k;
-            }
-        if (m == 0xFFFFFFFFu) break;
-        int pix = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {  // static indexing keeps pos/head in registers
-            if (k == c) {
-                pix = ws.ids[pos[k]];
-                ++pos[k];
-                head[k] = pos[k] < end[k] ? order_key(ws.ids[pos[k]], k) : 0xFFFFFFFFu;
-            }
+        for (int c = 0; c < 4; ++c) {
+            pos[c] = ws.offs[bk[c]];
+            end[c] = ws.offs[bk[c] + 1];
+            head[c] = pos[c] < end[c] ? order_key(ws.ids[pos[c]], c) : 0xFFFFFFFFu;
         }
-        const float2 f = fwp[pix];
-        const float wx = f.x, ex = 1.0f - wx;
-        const float wy = f.y, sy = 1.0f - wy;
-        const float w = c == 0 ? sy * ex : c == 1 ? sy * wx : c == 2 ? wy * ex : wy * wx;
-        const float4 d = dsp[pix];
-        a0 = a0 + w * d.x;
-        a1 = a1 + w * d.y;
-        a2 = a2 + w * d.z;
-        a3 = a3 + w * d.w;
+        const float4* dsp = ws.ds + (int64_t)(pc0 + pl) * HW;
+        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+        for (;;) {
+            int c = 0;
+            unsigned m = head[0];
+#pragma unroll
+            for (int k = 1; k < 4; ++k)
+                if (head[k] < m) {
+                    m = head[k];
+                    c = k;
+                }
+            if (m == 0xFFFFFFFFu) break;
+            int pix = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {  // static indexing keeps pos/head in registers
+                if (k == c) {
+                    pix = ws.ids[pos[k]];
+                    ++pos[k];
+                    head[k] = pos[k] < end[k] ? order_key(ws.ids[pos[k]], k) : 0xFFFFFFFFu;
+                }
+            }
+            const int py_ = pix / g.W;
+            float px, py;
+            render_pos<FAST>(h, (float)(pix - py_ * g.W), (float)py_, g, px, py);
+            const float wx = px - floorf(px), ex = 1.0f - wx;
+            const float wy = py - floorf(py), sy = 1.0f - wy;
+            const float w = c == 0 ? sy * ex : c == 1 ? sy * wx : c == 2 ? wy * ex : wy * wx;
+            const float4 d = dsp[pix];
+            a0 = a0 + w * d.x;
+            a1 = a1 + w * d.y;
+            a2 = a2 + w * d.z;
+            a3 = a3 + w * d.w;
+        }
+        dmpi[(int64_t)t * g.P + pc0 + pl] = make_float4(a0, a1, a2, a3);
     }
-    return make_float4(a0, a1, a2, a3);
-}
-
-// Generic output strides: one work-item per (plane, texel), planes outermost.
-__global__ __launch_bounds__(256) void render_bwd_gather_kernel(int H, int W, int P, BwdWs ws,
-                                                                float* __restrict__ dmpi, GradOut so) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int HW = H * W;
-    if (q >= (int64_t)P * HW) return;
-    const int p = (int)(q / HW), t = (int)(q - (int64_t)p * HW);
-    const int ty = t / W, tx = t - ty * W;
-    const float4 a = gather_texel(H, W, p, t, ws);
-    float* o = dmpi + ty * so.y + tx * so.x + p * so.p;
-    o[0] = a.x;
-    o[so.c] = a.y;
-    o[2 * so.c] = a.z;
-    o[3 * so.c] = a.w;
-}
-
-// Dense output ([H,W,P,4] contiguous, 16-B aligned): a block gathers 64 texels x 8
-// planes (wave = plane: the workspace reads stay coalesced) and writes them through
-// LDS as one 128-B run per texel (8 planes x 16 B) -- the direct form writes 4-B pieces
-// at a P*16-B lane stride.
-constexpr int kGatherPl = 8;
-__global__ __launch_bounds__(kGatherPl * 64) void render_bwd_gather_dense_kernel(int H, int W, int P, BwdWs ws,
-                                                                              float4* __restrict__ dmpi) {
-    __shared__ float4 tile[kGatherPl][kWave + 1];
-    const int HW = H * W;
-    const int t0 = blockIdx.x * kWave, p0 = blockIdx.y * kGatherPl;
-    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
-    const int t = t0 + lane, p = p0 + w;
-    if (t < HW && p < P) tile[w][lane] = gather_texel(H, W, p, t, ws);
-    __syncthreads();
-    const int i = threadIdx.x / kGatherPl, j = threadIdx.x % kGatherPl;  // texel, plane (plane fastest)
-    if (t0 + i < HW && p0 + j < P) dmpi[(int64_t)(t0 + i) * P + p0 + j] = tile[j][i];
 }
 
 }  // namespace mpiv

@@ -74,8 +74,10 @@ __device__ __forceinline__ f32x4 blend_chunk(const ChunkTaps& t) {
 // clamped into [-2, W] x [-2, H] (defined int conversion; NaN maps to a bound and its NaN
 // weights still poison the sample, as in the reference); a tap outside the image, or any
 // tap of a lane past the last plane, gets kOOB: the buffer unit returns 0 without an access.
-__device__ __forceinline__ void issue_taps_chunk(__amdgpu_buffer_rsrc_t r, const RenderGeom& g, const ChunkGeom& cg,
-                                                 int jt, bool live, float px, float py, ChunkTaps& t) {
+// Returns the number of taps inside the image (0 for dead lanes; the backward counts the
+// texel contributions it must find, render_bwd.hip).
+__device__ __forceinline__ int issue_taps_chunk(__amdgpu_buffer_rsrc_t r, const RenderGeom& g, const ChunkGeom& cg,
+                                                int jt, bool live, float px, float py, ChunkTaps& t) {
     const float fx0 = floorf(px), fy0 = floorf(py);
     t.wx = px - fx0;
     t.wy = py - fy0;
@@ -90,6 +92,7 @@ __device__ __forceinline__ void issue_taps_chunk(__amdgpu_buffer_rsrc_t r, const
     t.b = llvm_raw_buffer_load_v4f32(r, (x1 && y0) ? off + pb : kOOB, 0, 0);
     t.c = llvm_raw_buffer_load_v4f32(r, (x0 && y1) ? off + rb : kOOB, 0, 0);
     t.d = llvm_raw_buffer_load_v4f32(r, (x1 && y1) ? off + rb + pb : kOOB, 0, 0);
+    return ((int)x0 + (int)x1) * ((int)y0 + (int)y1);
 }
 
 // LDS: [4 waves][64 / SPLIT pixels][CH + 1] float4 sample slots (one pad texel per pixel

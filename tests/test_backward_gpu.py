@@ -27,13 +27,36 @@ def grad():
     return np.load(os.path.join(GOLD, "grad.npz"))
 
 
+# "tile": the production path (tile gather, pair count checked); "fallback": the bucket
+# pipeline for every view (bwd_fallback=1); "miss": windows 1.5 px too small
+# (bwd_margin=-96), so the tile gather misses contributors and the count must send every
+# such view to the fallback -- all three bit-exact.
+BWD_MODES = {"tile": {}, "fallback": {"bwd_fallback": 1}, "miss": {"bwd_margin": -96}}
+
+
+@pytest.fixture(params=list(BWD_MODES))
+def bwd_mode(request, kopts):
+    kopts(**BWD_MODES[request.param])
+    return request.param
+
+
+def _backward_flag(mpi, homs, dout, dev):
+    """(gradient, fallback flag of the last view) through a caller-owned workspace."""
+    B, H, W, P, _ = mpi.shape
+    L = _lib.load()
+    ws = torch.zeros(L.mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    got = _lib.render_backward(mpi, homs, dout, workspace=ws)
+    off = _lib.bwd_flag_offset(H, W, P)
+    return got, int(ws[off:off + 4].view(torch.int32).item())
+
+
 def _inputs(grad, name, dev):
     t = {k: torch.tensor(grad[f"{name}_{k}"]).to(dev) for k in ("pose", "K", "depths", "dout")}
     return torch.tensor(grad[f"{name}_mpi"]), t
 
 
 @pytest.mark.parametrize("name", ["ga", "gbig", "gbin"])
-def test_backward_matches_reference_autograd(name, grad, dev):
+def test_backward_matches_reference_autograd(name, grad, dev, bwd_mode):
     mpi, t = _inputs(grad, name, dev)
     leaf = mpi.to(dev).requires_grad_(True)
     out = mv.mpi_render_view_torch(leaf, t["pose"], t["depths"], t["K"])
@@ -42,7 +65,7 @@ def test_backward_matches_reference_autograd(name, grad, dev):
     assert_bits(leaf.grad, grad[f"{name}_grad"], f"{name} d rgba_layers")
 
 
-def test_backward_collapsing_homography_vs_oracle(dev):
+def test_backward_collapsing_homography_vs_oracle(dev, bwd_mode):
     """Homographies that send many target pixels to one source texel: plane 0
     maps the whole frame to one point (one bucket holding every pixel), plane 1 minifies
     ~16x (buckets of ~70 pixels), plane 2 is a mild warp.  The large buckets take the
@@ -61,7 +84,7 @@ def test_backward_collapsing_homography_vs_oracle(dev):
     assert np.abs(want[0, :, :, 0]).max() > 1.0  # plane 0's one texel gathered the whole frame
 
 
-def test_backward_broadcast_mpi(grad, dev):
+def test_backward_broadcast_mpi(grad, dev, bwd_mode):
     """Broadcast MPI (stride-0 batch): per-view gradients are bit-exact to the oracle;
     their sum (torch's expand backward on the GPU) matches the reference within 1e-6."""
     mpi, t = _inputs(grad, "gbc", dev)
@@ -77,7 +100,7 @@ def test_backward_broadcast_mpi(grad, dev):
     assert_bits(per_view, want, "per-view grads")
 
 
-def test_backward_extreme_poses_vs_oracle(dev):
+def test_backward_extreme_poses_vs_oracle(dev, bwd_mode):
     """Large rotations / translations, planes behind the camera, strong magnification and
     minification (buckets with many / no pixels): bit-exact to the oracle."""
     g = torch.Generator().manual_seed(5)
@@ -97,8 +120,9 @@ def test_backward_extreme_poses_vs_oracle(dev):
     assert_bits(got, want, "extreme poses")
 
 
-def test_backward_medium_case_vs_oracle(dev):
-    """A 192x320x24 MPI over a camera-path pose: bit-exact to the oracle."""
+def test_backward_medium_case_vs_oracle(dev, bwd_mode):
+    """A 192x320x24 MPI over a camera-path pose: bit-exact to the oracle; the tile gather
+    handles it without the fallback, and a too-small window is caught by the count."""
     H, W, P = 192, 320, 24
     mpi = configs.synthetic_mpi(1, H, W, P, 9)
     c = configs.config4()
@@ -107,8 +131,9 @@ def test_backward_medium_case_vs_oracle(dev):
                                      K, 1)
     dout = torch.rand((1, H, W, 3), generator=torch.Generator().manual_seed(3)) * 2 - 1
     want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
-    got = _lib.render_backward(mpi.to(dev), homs, dout.to(dev))
+    got, flag = _backward_flag(mpi.to(dev), homs, dout.to(dev), dev)
     assert_bits(got, want, "medium case")
+    assert flag == (0 if bwd_mode == "tile" else 1)
 
 
 def test_backward_deterministic(grad, dev):
@@ -161,3 +186,41 @@ def test_training_loss_gradient_hip_assembly(grad, dev):
     loss.backward()
     np.testing.assert_allclose(loss.item(), float(grad["loss_value"]), rtol=1e-6)
     np.testing.assert_allclose(pred.grad.cpu().numpy(), grad["loss_grad"], rtol=0, atol=1e-6)
+
+
+def test_backward_strided_layout_vs_oracle(dev):
+    """An MPI whose planes are not contiguous per pixel (a permuted [B,P,H,W,4] tensor) is
+    made contiguous first; odd sizes (W % 8 != 0, partial plane chunk and gather group)."""
+    H, W, P = 37, 53, 11
+    base = configs.synthetic_mpi(1, H, W, P, 4)
+    mpi = base.permute(0, 3, 1, 2, 4).contiguous().permute(0, 2, 3, 1, 4)
+    assert mpi.stride(3) != 4
+    c = configs.config4()
+    K = configs.f32([configs.intrinsics_matrix(40.0, 40.0, 26.0, 18.0)])
+    homs = _host.render_homographies(configs.f32([c["poses"][300]]), configs.f32(configs.inv_depths(1, 50, P)), K, 1)
+    dout = torch.rand((1, H, W, 3), generator=torch.Generator().manual_seed(8)) * 2 - 1
+    want = oracle.render_backward(base.numpy(), homs.numpy(), dout.numpy())
+    got, flag = _backward_flag(mpi.to(dev), homs, dout.to(dev), dev)
+    assert_bits(got, want, "strided layout")
+    assert flag == 0
+
+
+@pytest.mark.parametrize("cfg", ["config2", "config4"])
+def test_backward_full_size_tile_equals_fallback(cfg, dev, kopts):
+    """BASELINE config 2 (1024x576x32, the stretched normalisation) and config 4
+    (1024x1024x128) at full size: the tile gather takes every plane (flag 0) and its
+    gradient is bit-identical to the bucket fallback's (the algorithm the small cases pin
+    to the reference and the oracle)."""
+    c = getattr(configs, cfg)()
+    H, W, P = c["H"], c["W"], c["P"]
+    g = torch.Generator(device=dev).manual_seed(11)
+    mpi = torch.rand((1, H, W, P, 4), generator=g, device=dev)
+    homs = _host.render_homographies(configs.f32(c["poses"][7:8]), configs.f32(c["depths"]),
+                                     configs.f32([c["K"]]), 1)
+    dout = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    fast, flag = _backward_flag(mpi, homs, dout, dev)
+    assert flag == 0
+    kopts(bwd_fallback=1)
+    slow, flag = _backward_flag(mpi, homs, dout, dev)
+    assert flag == 1
+    assert torch.equal(fast.view(torch.int32), slow.view(torch.int32))

@@ -1,4 +1,10 @@
 set -u
 mkdir -p gpurun_out
-TAG=r02b timeout -k 10 900 bash tools/profile.sh > gpurun_out/profile.log 2>&1; rc=$?; tail -3 gpurun_out/profile.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python -u bench.py > gpurun_out/bench_r02d.json 2> gpurun_out/bench_r02d.err; rc=$?; tail -c 1500 gpurun_out/bench_r02d.json; exit $rc
+ROOT=$(pwd)
+timeout -k 10 400 python -u -m pytest tests/test_backward_gpu.py -x -v --timeout 180 --timeout-method thread > gpurun_out/bwd_tests.log 2>&1; rc=$?
+echo "tests rc=$rc"; tail -15 gpurun_out/bwd_tests.log
+[ $rc -eq 0 ] || exit $rc
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof_bwd2 -o run -- python -u $ROOT/tools/bench_configs.py --only bwd --iters 8 > $ROOT/gpurun_out/prof_bwd2.log 2>&1; rc=$?
+grep config $ROOT/gpurun_out/prof_bwd2.log
+exit $rc
