@@ -65,6 +65,15 @@ int mpiv_debug_set(const char *name, int value);
 int mpiv_render(const float *mpi, const int64_t mpi_strides[5], int B, int H, int W, int P,
                 const float *homs, float *out, void *stream);
 
+/* mpiv_render for training (the forward of RenderFunction when rgba_layers needs a
+ * gradient): the same frames, bit for bit, from the in-place chunked kernel, plus the
+ * composited colour before every 8-plane chunk, ckpt [B][ceil(P/8)][H][W] float4 (16-B
+ * aligned; chunk 0's slot is unused), which mpiv_render_backward takes instead of
+ * recomputing the forward composite.  Needs the in-place layout (16-B texels, planes
+ * contiguous per pixel, strides[3] == 4, strides[4] == 1), H, W >= 2 and P <= 796. */
+int mpiv_render_train(const float *mpi, const int64_t mpi_strides[5], int B, int H, int W, int P,
+                      const float *homs, float *out, float *ckpt, void *stream);
+
 /* Layout pack for repeated rendering of one MPI: one view [H,W,P,4] (element
  * strides strides[4] = H,W,P,C) -> plane-major packed [P][H+4][W+4][4] (16-B
  * aligned, contiguous) with a 2-texel zero border around every plane; image texel
@@ -125,13 +134,15 @@ size_t mpiv_render_backward_workspace_size(int H, int W, int P);
  *          with 16-byte aligned texels and planes contiguous per pixel (strides[3] == 4,
  *          strides[4] == 1; a stride-0 broadcast batch is fine); P <= 796;
  * homs:    [V][P][9] (the forward's); dout: [V,H,W,3] contiguous incoming gradient;
+ * ckpt:    NULL, or the checkpoints mpiv_render_train wrote in the forward of these views
+ *          (then the adjoint skips recomputing the forward composite);
  * dmpi:    [V,H,W,P,4] contiguous, 16-byte aligned: view v's gradient is written (not
  *          accumulated);
  * workspace: >= mpiv_render_backward_workspace_size(H, W, P) bytes, 256-B aligned.
  * Deterministic (no float atomics); H*W < 2^26, P*H*W < 2^31. */
 int mpiv_render_backward(const float *mpi, const int64_t mpi_strides[5], int V, int H, int W, int P,
-                         const float *homs, const float *dout, float *dmpi, void *workspace,
-                         size_t workspace_bytes, void *stream);
+                         const float *homs, const float *dout, const float *ckpt, float *dmpi,
+                         void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---- MPI assembly from the network output ------------------------------- */
 

@@ -48,7 +48,8 @@ _SIGS = {
     "mpiv_plane_sweep_padded": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
     "mpiv_preprocess": [_vp, _i64, _vp, _vp],
     "mpiv_deprocess_u8": [_vp, _i64, _vp, _vp],
-    "mpiv_render_backward": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp],
+    "mpiv_render_backward": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp],
+    "mpiv_render_train": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp],
     "mpiv_plane_sweep_padded_into": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,
                                      _vp],
     "mpiv_assemble_mpi": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
@@ -451,14 +452,33 @@ def bwd_flag_offset(H: int, W: int, P: int) -> int:
     return a(P * H * W * 16) + a((P + 7) // 8 * H * W * 16) + a(P * 48) + 2 * a(64 * 8)
 
 
+def render_train(rgba_layers: torch.Tensor, homs: torch.Tensor):
+    """The forward for training: (frames [B,H,W,3], checkpoints [B,ceil(P/8),H,W,4]) from
+    mpiv_render_train -- frames bit-identical to render() -- or (render(), None) when the
+    layout is not read in place (a broadcast batch renders from one packed copy instead)."""
+    dev = _dev(rgba_layers)
+    B, H, W, P, _ = rgba_layers.shape
+    if homs.shape[0] != B or homs.shape[1] != P:
+        raise RuntimeError(f"shape mismatch: MPI batch/planes {B}/{P} vs poses/planes {homs.shape[0]}/{homs.shape[1]}")
+    if (B > 1 and rgba_layers.stride(0) == 0) or not chunk_layout_ok(rgba_layers) or \
+            4 * 64 * 9 * 16 + P * 36 > _CHUNK_LDS:
+        return render(rgba_layers, homs), None
+    h = _up(homs, dev)
+    out = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32)
+    ckpt = torch.empty((B, (P + 7) // 8, H, W, 4), device=dev, dtype=torch.float32)
+    _call("mpiv_render_train", rgba_layers, _strides(rgba_layers), B, H, W, P, h, out, ckpt, _stream(dev))
+    return out, ckpt
+
+
 def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.Tensor,
-                    workspace: torch.Tensor | None = None) -> torch.Tensor:
+                    workspace: torch.Tensor | None = None, ckpt: torch.Tensor | None = None) -> torch.Tensor:
     """d(mpi_render_view_torch)/d(rgba_layers): rgba_layers [B,H,W,P,4] (read in place when
     its planes are contiguous per pixel, incl. a stride-0 broadcast batch; other layouts
     are made contiguous first), homs [B,P,9] (the forward's), dout [B,H,W,3] ->
     [B,H,W,P,4] contiguous, one gradient per view (a broadcast input's views are summed
     by autograd's expand backward, as in the reference).  Bit-exact to the reference's
-    CPU autograd (render_bwd.hip)."""
+    CPU autograd (render_bwd.hip).  ckpt: render_train()'s checkpoints of the same views
+    (skips recomputing the forward composite)."""
     dev = _dev(rgba_layers, dout)
     B, H, W, P, _ = rgba_layers.shape
     if tuple(dout.shape) != (B, H, W, 3):
@@ -472,7 +492,10 @@ def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.T
     grad = torch.empty((B, H, W, P, 4), device=dev, dtype=torch.float32)
     h = _up(homs.reshape(B, P, 9), dev)
     dout = dout.contiguous()
-    _call("mpiv_render_backward", src, _strides(src), B, H, W, P, h, dout, grad, ws, ws.numel(), _stream(dev))
+    if ckpt is not None and (tuple(ckpt.shape) != (B, (P + 7) // 8, H, W, 4) or not ckpt.is_contiguous()
+                             or ckpt.device != dev or ckpt.dtype != torch.float32):
+        raise RuntimeError(f"ckpt must be render_train()'s contiguous [{B},{(P + 7) // 8},{H},{W},4] tensor")
+    _call("mpiv_render_backward", src, _strides(src), B, H, W, P, h, dout, ckpt, grad, ws, ws.numel(), _stream(dev))
     return grad
 
 
@@ -483,15 +506,19 @@ class RenderFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, rgba_layers, homs):
-        ctx.save_for_backward(rgba_layers)
         ctx.homs = homs
+        if ctx.needs_input_grad[0]:  # keep the composite checkpoints for the backward
+            out, ckpt = render_train(rgba_layers, homs)
+            ctx.save_for_backward(rgba_layers, ckpt)
+            return out
+        ctx.save_for_backward(rgba_layers, None)
         return render(rgba_layers, homs)
 
     @staticmethod
     @once_differentiable
     def backward(ctx, dout):
-        (rgba_layers,) = ctx.saved_tensors
-        grad = render_backward(rgba_layers, ctx.homs, dout) if ctx.needs_input_grad[0] else None
+        rgba_layers, ckpt = ctx.saved_tensors
+        grad = render_backward(rgba_layers, ctx.homs, dout, ckpt=ckpt) if ctx.needs_input_grad[0] else None
         return grad, None
 
 

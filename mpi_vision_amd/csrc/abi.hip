@@ -139,13 +139,13 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_render: too many blocks");
         const ChunkGeom cg{(int)(s.y / 4), (int)(s.x / 4), (int)rec};
         if (CH == 8 && SPLIT == 2)
-            render_chunk_kernel<8, 2><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
+            render_chunk_kernel<8, 2><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out, nullptr);
         else if (CH == 8)
-            render_chunk_kernel<8, 1><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
+            render_chunk_kernel<8, 1><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out, nullptr);
         else if (SPLIT == 2)
-            render_chunk_kernel<4, 2><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
+            render_chunk_kernel<4, 2><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out, nullptr);
         else
-            render_chunk_kernel<4, 1><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out);
+            render_chunk_kernel<4, 1><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out, nullptr);
         return launched("mpiv_render");
     }
     // footprints staged through LDS, read in place (render_lds.hip render_lds_native_kernel):
@@ -162,6 +162,26 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
     else if (fast) render_native_kernel<false, true><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
     else render_native_kernel<false, false><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
     return launched("mpiv_render");
+}
+
+int mpiv_render_train(const float* mpi, const int64_t st[5], int B, int H, int W, int P, const float* homs,
+                      float* out, float* ckpt, void* stream) {
+    const char* nm = "mpiv_render_train";
+    if (!mpi || !st || !homs || !out || !ckpt) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (B <= 0 || H < 2 || W < 2 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape (H, W >= 2)", nm);
+    const int64_t rec = ((int64_t)(H - 1) * st[1] + (int64_t)(W - 1) * st[2]) * 4 + 8 * 16;
+    const size_t ch_lds = (size_t)4 * kWave * 9 * 16 + (size_t)P * 36;
+    if (st[4] != 1 || st[3] != 4 || st[0] % 4 || st[1] % 4 || st[2] % 4 || st[1] < 0 || st[2] < 0 ||
+        !aligned16(mpi) || !aligned16(ckpt) || rec >= (int64_t)kOOB || st[1] / 4 >= (1 << 22) ||
+        st[2] / 4 >= (1 << 22) || ch_lds > (size_t)kChunkMaxLds)
+        return fail(MPIV_ERR_ARG, "%s: rgba_layers must be read in place (16-byte texels, planes contiguous per "
+                    "pixel, one view below 2 GiB, P <= 796)", nm);
+    const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * B;
+    if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+    const ChunkGeom cg{(int)(st[1] / 4), (int)(st[2] / 4), (int)rec};
+    render_chunk_kernel<8, 1><<<(unsigned)nb, 256, ch_lds, S(stream)>>>(mpi, st[0], make_geom(H, W, P), cg, B, homs,
+                                                                        out, reinterpret_cast<float4*>(ckpt));
+    return launched(nm);
 }
 
 int mpiv_pack_planes(const float* mpi, const int64_t st[4], int H, int W, int P, float* packed, void* stream) {
@@ -407,7 +427,8 @@ size_t mpiv_render_backward_workspace_size(int H, int W, int P) {
 }
 
 int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, int W, int P, const float* homs,
-                         const float* dout, float* dmpi, void* workspace, size_t ws_bytes, void* stream) {
+                         const float* dout, const float* ckpt, float* dmpi, void* workspace, size_t ws_bytes,
+                         void* stream) {
     const char* nm = "mpiv_render_backward";
     if (!mpi || !st || !homs || !dout || !dmpi || !workspace) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
     if (V <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
@@ -421,6 +442,8 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const size_t chain_lds = (size_t)4 * kWave * (kBwdCH + 1) * 16 + (size_t)P * 36;
     if (chain_lds > (size_t)kChunkMaxLds) return fail(MPIV_ERR_ARG, "%s: more than %d planes", nm,
                                                       (int)((kChunkMaxLds - 4 * kWave * (kBwdCH + 1) * 16) / 36));
+    if (ckpt && (!aligned16(ckpt) || H < 2 || W < 2))
+        return fail(MPIV_ERR_ARG, "%s: checkpoints must be 16-byte aligned (and come from mpiv_render_train)", nm);
     if (!aligned16(dmpi) || (reinterpret_cast<uintptr_t>(workspace) & 255))
         return fail(MPIV_ERR_ARG, "%s: d rgba_layers must be 16-byte and workspace 256-byte aligned", nm);
     // pixel ids, bucket ids and order keys are 32-bit
@@ -449,10 +472,14 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         const float* dv = dout + (int64_t)v * HW * 3;
         const float* mv = mpi + (int64_t)v * st[0];
         float4* gv = reinterpret_cast<float4*>(dmpi) + (int64_t)v * HW * P;
-        if (fast)
-            bwd_chain_kernel<1><<<chain_blocks, 256, chain_lds, q>>>(mv, g, cg, hv, dv, ws);
+        const float4* ck = ckpt ? reinterpret_cast<const float4*>(ckpt) + (int64_t)v * ((P + kBwdCH - 1) / kBwdCH) * HW
+                                : nullptr;
+        if (fast && ck)
+            bwd_chain_kernel<1, true><<<chain_blocks, 256, chain_lds, q>>>(mv, g, cg, hv, dv, ck, ws);
+        else if (fast)
+            bwd_chain_kernel<1, false><<<chain_blocks, 256, chain_lds, q>>>(mv, g, cg, hv, dv, nullptr, ws);
         else
-            bwd_chain_kernel<0><<<chain_blocks, 256, chain_lds, q>>>(mv, g, cg, hv, dv, ws);
+            bwd_chain_kernel<0, false><<<chain_blocks, 256, chain_lds, q>>>(mv, g, cg, hv, dv, nullptr, ws);
         if (!force) {
             bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
             bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x, margin,

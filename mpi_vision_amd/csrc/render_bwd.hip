@@ -94,11 +94,14 @@ __device__ __forceinline__ void bwd_pos(const float* h, float fx, float fy, cons
         chunk_pos<MODE == 1>(h, fx, fy, g, px, py);
 }
 
-template <int MODE>
+// CK: the forward's checkpoints (mpiv_render_train, [nchunk][HW] of this view) replace
+// pass 1; every sample is then issued (and its taps counted) in pass 2 only.
+template <int MODE, bool CK>
 __device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, const RenderGeom& g,
                                                const ChunkGeom& cg, const float* __restrict__ hs,
                                                f32x4* __restrict__ slot, int tx0, int y, int lane,
-                                               const float* __restrict__ dout, const BwdWs& ws) {
+                                               const float* __restrict__ dout, const float4* __restrict__ ck,
+                                               const BwdWs& ws) {
     constexpr int CH = kBwdCH, PPS = kWave / CH;
     const int j = lane % CH, i = lane / CH;
     const float fy = (float)y;
@@ -148,22 +151,27 @@ __device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, c
     // exactly, render.hip), the colour checkpointed before every chunk.  The last chunk
     // stays in the slot for pass 2; chunk n-2 is issued ahead.
     float cr = -0.0f, cgc = -0.0f, cb = -0.0f;
-    load_h(0, h);
-    issue(0, 0, h, A, true);
-    for (int c = 0; c < n; ++c) {
-        const bool last = c == n - 1;
-        sample_chunk(c, last ? max(n - 2, 0) : c + 1, true, !last);
-        if (last) break;
+    if (CK) {
+        load_h(n - 1, h);
+        issue(n - 1, 0, h, A, true);
+    } else {
+        load_h(0, h);
+        issue(0, 0, h, A, true);
+        for (int c = 0; c < n; ++c) {
+            const bool last = c == n - 1;
+            sample_chunk(c, last ? max(n - 2, 0) : c + 1, true, !last);
+            if (last) break;
 #pragma unroll
-        for (int k = 0; k < CH; ++k) {  // a chunk before the last is full
-            const f32x4 s = row[k];
-            const float a = (c == 0 && k == 0) ? 1.0f : s[3];
-            const float om = 1.0f - a;
-            cr = over(s[0], a, om, cr);
-            cgc = over(s[1], a, om, cgc);
-            cb = over(s[2], a, om, cb);
+            for (int k = 0; k < CH; ++k) {  // a chunk before the last is full
+                const f32x4 s = row[k];
+                const float a = (c == 0 && k == 0) ? 1.0f : s[3];
+                const float om = 1.0f - a;
+                cr = over(s[0], a, om, cr);
+                cgc = over(s[1], a, om, cgc);
+                cb = over(s[2], a, om, cb);
+            }
+            if (xin) ws.ckpt[(int64_t)(c + 1) * HW + pix] = make_float4(cr, cgc, cb, 0.0f);
         }
-        if (xin) ws.ckpt[(int64_t)(c + 1) * HW + pix] = make_float4(cr, cgc, cb, 0.0f);
     }
     // ---- pass 2: chunks back to front; over_composite backward (utils.py:149-156 under
     // autograd), planes P-1 .. 0
@@ -176,12 +184,12 @@ __device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, c
     }
     for (int c = n - 1; c >= 0; --c) {
         float4 pre = make_float4(cr, cgc, cb, 0.0f);  // c = n-1: pass 1's colour
-        if (c < n - 1) {
+        if (CK || c < n - 1) {
             if (c == 0)
                 pre = make_float4(-0.0f, -0.0f, -0.0f, 0.0f);
             else if (xin)
-                pre = ws.ckpt[(int64_t)c * HW + pix];
-            sample_chunk(c, c > 0 ? c - 1 : 0, false, false);
+                pre = CK ? ck[(int64_t)c * HW + pix] : ws.ckpt[(int64_t)c * HW + pix];
+            sample_chunk(c, c > 0 ? c - 1 : 0, CK, CK && c > 0);
         }
         // prefixes out_{p-1} of the chunk's planes, recomputed in the forward's order
         float pr[CH][3];
@@ -237,10 +245,11 @@ __device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, c
 // One block = 4 waves = a 64x4 output tile of one view.  Dynamic LDS: 4 per-wave sample
 // slots (64 x (CH+1) float4) + the view's P homographies.  MODE 0: generic recipe
 // (H or W < 2); 1: fast recipe, the tile's division proof picks the unguarded path.
-template <int MODE>
+template <int MODE, bool CK>
 __global__ __launch_bounds__(256) void bwd_chain_kernel(const float* __restrict__ view, RenderGeom g, ChunkGeom cg,
                                                         const float* __restrict__ homs,
-                                                        const float* __restrict__ dout, BwdWs ws) {
+                                                        const float* __restrict__ dout,
+                                                        const float4* __restrict__ ck, BwdWs ws) {
     extern __shared__ float4 bwd_lds[];
     f32x4* slots = reinterpret_cast<f32x4*>(bwd_lds);
     float* hs = reinterpret_cast<float*>(bwd_lds) + 4 * kWave * (kBwdCH + 1) * 4;
@@ -260,11 +269,11 @@ __global__ __launch_bounds__(256) void bwd_chain_kernel(const float* __restrict_
     if (y >= g.H) return;  // whole wave; no barrier follows
     f32x4* slot = slots + wave * kWave * (kBwdCH + 1);
     if (MODE == 0)
-        bwd_chain_wave<0>(view, g, cg, hs, slot, tx0, y, lane, dout, ws);
+        bwd_chain_wave<0, CK>(view, g, cg, hs, slot, tx0, y, lane, dout, ck, ws);
     else if (proven)
-        bwd_chain_wave<2>(view, g, cg, hs, slot, tx0, y, lane, dout, ws);
+        bwd_chain_wave<2, CK>(view, g, cg, hs, slot, tx0, y, lane, dout, ck, ws);
     else
-        bwd_chain_wave<1>(view, g, cg, hs, slot, tx0, y, lane, dout, ws);
+        bwd_chain_wave<1, CK>(view, g, cg, hs, slot, tx0, y, lane, dout, ck, ws);
 }
 
 // ---- 2. gather: per-texel sums in the reference's order ------------------------------
@@ -631,7 +640,7 @@ __global__ __launch_bounds__(256) void bwd_gather_kernel(RenderGeom g, const flo
     for (int off = 32; off >= 1; off >>= 1) hits += __shfl_xor(hits, off);
     const unsigned long long tot = (unsigned long long)hits + (__any(unsafe) ? kUnsafe : 0ull);
     if ((threadIdx.x & (kWave - 1)) == 0 && tot) atomicAdd(&ws.found[blockIdx.x % kCtrSlots], tot);
-    if (tin) {
+    if (tin) {  // the texel's kGPl planes: one 128-B run
         float4* o = dmpi + ((int64_t)ty * g.W + tx) * g.P + p0;
 #pragma unroll
         for (int jj = 0; jj < kGPl; ++jj)

@@ -110,7 +110,8 @@ template <int CH, int SPLIT, bool GUARD>
 __device__ __forceinline__ void render_chunk_wave(const float* __restrict__ view, const RenderGeom& g,
                                                   const ChunkGeom& cg, const float* __restrict__ hs,
                                                   f32x4* __restrict__ slot, int tx0, int y, int lane,
-                                                  float& cr, float& cg_, float& cb) {
+                                                  float& cr, float& cg_, float& cb, float4* __restrict__ ck,
+                                                  int64_t ck_stride) {
     constexpr int PPS = kWave / CH;  // pixels per sub-step
     const int j = lane % CH, i = lane / CH;
     const float fy = (float)y;
@@ -164,6 +165,8 @@ __device__ __forceinline__ void render_chunk_wave(const float* __restrict__ view
     issue(0, 0, h, A);
     for (int c = 0; c < nchunk; ++c) {
         const int cn = c + 1 < nchunk ? c + 1 : c;  // past the end: re-issue (cached, unused)
+        // training: the colour before chunk c, the render backward's checkpoint (render_bwd.hip)
+        if (ck && c > 0) ck[c * ck_stride] = make_float4(cr, cg_, cb, 0.0f);
 #pragma unroll
         for (int k = 0; k < CH; k += 2) {  // A holds sub-step k
             issue(c, k + 1, h, B);
@@ -188,7 +191,8 @@ template <int CH, int SPLIT>
 __global__ __launch_bounds__(256, SPLIT == 2 ? 6 : 1) void render_chunk_kernel(const float* __restrict__ mpi, int64_t view_stride,
                                                            RenderGeom g, ChunkGeom cg, int V,
                                                            const float* __restrict__ homs,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ out,
+                                                           float4* __restrict__ ckpt) {
     extern __shared__ float4 chunk_lds[];
     f32x4* slots = reinterpret_cast<f32x4*>(chunk_lds);
     float* hs = reinterpret_cast<float*>(chunk_lds) + chunk_slot_floats<CH, SPLIT>();
@@ -211,11 +215,14 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 6 : 1) void render_chunk_kernel(c
     const float* view = mpi + (int64_t)v * view_stride;
     f32x4* slot = slots + wave * (kWave / SPLIT) * (CH + 1);
     float cr = -0.0f, cgr = -0.0f, cb = -0.0f;
-    if (proven)
-        render_chunk_wave<CH, SPLIT, false>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb);
-    else
-        render_chunk_wave<CH, SPLIT, true>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb);
     const int x = tx0 + lane;
+    // checkpoints [V][nchunk][H][W] (nullptr: inference; SPLIT = 1 only: lane = pixel)
+    const int64_t HW = (int64_t)g.H * g.W;
+    float4* ck = (ckpt && x < g.W) ? ckpt + ((int64_t)v * ((g.P + CH - 1) / CH)) * HW + (int64_t)y * g.W + x : nullptr;
+    if (proven)
+        render_chunk_wave<CH, SPLIT, false>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb, ck, HW);
+    else
+        render_chunk_wave<CH, SPLIT, true>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb, ck, HW);
     if (x < g.W) {
         float* o = out + (((int64_t)v * g.H + y) * g.W + x) * 3;
         o[0] = cr;

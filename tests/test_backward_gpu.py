@@ -224,3 +224,26 @@ def test_backward_full_size_tile_equals_fallback(cfg, dev, kopts):
     slow, flag = _backward_flag(mpi, homs, dout, dev)
     assert flag == 1
     assert torch.equal(fast.view(torch.int32), slow.view(torch.int32))
+
+
+@pytest.mark.parametrize("cfg", ["config2", "config4"])
+def test_training_forward_checkpoints(cfg, dev):
+    """mpiv_render_train: frames bit-identical to the inference render; the backward fed its
+    checkpoints (one pass) is bit-identical to the backward that recomputes them (two
+    passes); two views in one launch (non-broadcast [2,H,W,P,4])."""
+    c = getattr(configs, cfg)()
+    H, W, P = c["H"], c["W"], c["P"]
+    if cfg == "config4":
+        H = W = 256  # full width of the pose set, fewer rows: two views stay small
+    g = torch.Generator(device=dev).manual_seed(5)
+    mpi = torch.rand((2, H, W, P, 4), generator=g, device=dev)
+    K = configs.intrinsics_matrix(W * 0.9, W * 0.9, W / 2, H / 2)
+    homs = _host.render_homographies(configs.f32(c["poses"][3:5]), configs.f32(c["depths"]), configs.f32([K, K]),
+                                     2).to(dev)
+    out, ck = _lib.render_train(mpi, homs)
+    assert ck is not None and ck.shape == (2, (P + 7) // 8, H, W, 4)
+    assert torch.equal(out.view(torch.int32), _lib.render(mpi, homs).view(torch.int32))
+    dout = torch.rand((2, H, W, 3), generator=g, device=dev) * 2 - 1
+    a = _lib.render_backward(mpi, homs, dout)
+    b = _lib.render_backward(mpi, homs, dout, ckpt=ck)
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))

@@ -34,11 +34,13 @@ int main() {
     EXPECT(mpiv_render_packed_ct(f, 4, 4, 8, 5, 3, 0, f, 1, f, nullptr) == MPIV_ERR_ARG);
     EXPECT(mpiv_combine_ct(f, 0, 4, f, nullptr) == MPIV_ERR_ARG);
     const int64_t stb[5] = {4 * 4 * 2 * 4, 4 * 2 * 4, 2 * 4, 4, 1};  // [1,4,4,2,4] contiguous
-    EXPECT(mpiv_render_backward(f, stb, 1, 4, 4, 2, f, f, f, nullptr, 0, nullptr) == MPIV_ERR_ARG);
-    EXPECT(mpiv_render_backward(f, stb, 1, 4, 4, 2, f, f, f, reinterpret_cast<void*>(256), 0, nullptr) == MPIV_ERR_ARG);
+    EXPECT(mpiv_render_backward(f, stb, 1, 4, 4, 2, f, f, nullptr, f, nullptr, 0, nullptr) == MPIV_ERR_ARG);
+    EXPECT(mpiv_render_backward(f, stb, 1, 4, 4, 2, f, f, nullptr, f, reinterpret_cast<void*>(256), 0, nullptr) == MPIV_ERR_ARG);
     EXPECT(std::strstr(mpiv_last_error(), "workspace too small") != nullptr);
-    EXPECT(mpiv_render_backward(f, st5, 1, 4, 4, 2, f, f, f, reinterpret_cast<void*>(256), 0, nullptr) == MPIV_ERR_ARG);
+    EXPECT(mpiv_render_backward(f, st5, 1, 4, 4, 2, f, f, nullptr, f, reinterpret_cast<void*>(256), 0, nullptr) == MPIV_ERR_ARG);
     EXPECT(std::strstr(mpiv_last_error(), "planes contiguous per pixel") != nullptr);
+    EXPECT(mpiv_render_train(f, st5, 1, 4, 4, 2, f, f, f, nullptr) == MPIV_ERR_ARG);
+    EXPECT(mpiv_render_train(f, stb, 1, 4, 4, 2, f, f, nullptr, nullptr) == MPIV_ERR_ARG);
     EXPECT(mpiv_render_backward_workspace_size(0, 4, 4) == 0);
     EXPECT(mpiv_render_backward_workspace_size(64, 64, 8) > (size_t)64 * 64 * 8 * 16);
     EXPECT(mpiv_plane_sweep(f, st4, 1, 4, 4, 0, f, f, f, 2, 4, 4, f, nullptr) == MPIV_ERR_ARG);

@@ -267,7 +267,15 @@ def bwd(dev, it, wu):
         dout = torch.rand((1, H, W, 3), device=dev) * 2 - 1
         ms, mn = timed(lambda: _lib.render_backward(mpi, homs, dout), max(3, it // 4), 1)
         ws = _lib.load().mpiv_render_backward_workspace_size(H, W, P)
-        report(f"{name} render backward {W}x{H}x{P}, 1 view (pack + chain + scan + bucket + gather)", ms, mn,
+        report(f"{name} render backward {W}x{H}x{P}, 1 view, no forward checkpoints (chain 2 passes + gather)", ms,
+               mn, P * H * W * 32, H * W / 1e6, extra={"workspace_GB": round(ws / 1e9, 3)})
+        hd = homs.to(dev)
+        ms, mn = timed(lambda: _lib.render_train(mpi, hd), max(3, it // 4), 1)
+        report(f"{name} training forward {W}x{H}x{P}, 1 view (frame + composite checkpoints)", ms, mn,
+               P * H * W * 16 + H * W * 12 + (P + 7) // 8 * H * W * 16, H * W / 1e6)
+        _, ck = _lib.render_train(mpi, hd)
+        ms, mn = timed(lambda: _lib.render_backward(mpi, hd, dout, ckpt=ck), max(3, it // 4), 1)
+        report(f"{name} render backward {W}x{H}x{P}, 1 view, forward checkpoints (chain 1 pass + gather)", ms, mn,
                P * H * W * 32, H * W / 1e6, extra={"workspace_GB": round(ws / 1e9, 3)})
 
 
