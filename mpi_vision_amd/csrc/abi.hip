@@ -417,7 +417,6 @@ size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
     return off;
 }
 
-inline unsigned fb_grid(int64_t n, int per) { return (unsigned)std::min<int64_t>(kFbGrid, std::max<int64_t>(1, (n + per - 1) / per)); }
 
 }  // namespace
 
@@ -456,7 +455,6 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const ChunkGeom cg{(int)(st[1] / 4), (int)(st[2] / 4), (int)rec};
     const bool fast = H >= 2 && W >= 2;
     const int64_t HW = (int64_t)H * W;
-    const int64_t K = (int64_t)(H + 1) * (W + 1);
     const unsigned chain_blocks = blocks(W, kTileX) * blocks(H, kTileY);
     const int tiles_x = (int)blocks(W, kGTW);
     const int64_t ntiles = (int64_t)tiles_x * blocks(H, kGTH);
@@ -465,6 +463,25 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const int force = opt(kOptBwdFallback) != 0 || !fast;
     const float margin = (float)opt(kOptBwdMargin) / 64.0f;
     hipStream_t q = S(stream);
+    // fallback grid: every block resident (cooperative launch), at most 4 per CU; queried
+    // once per device (relaxed atomics: racing first calls store the same value)
+    static int s_fb_blocks[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(MPIV_ERR_HIP, "%s: hipGetDevice failed", nm);
+    int fbb = __atomic_load_n(&s_fb_blocks[dev], __ATOMIC_RELAXED);
+    if (fbb == 0) {
+        int ncu = 0, pc_t = 0, pc_f = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_t, (const void*)bwd_fallback_kernel<true>, 256, 0) !=
+                hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_f, (const void*)bwd_fallback_kernel<false>, 256, 0) !=
+                hipSuccess ||
+            ncu <= 0 || pc_t <= 0 || pc_f <= 0)
+            return fail(MPIV_ERR_HIP, "%s: device query failed", nm);
+        fbb = ncu * std::min(std::min(pc_t, pc_f), 4);
+        __atomic_store_n(&s_fb_blocks[dev], fbb, __ATOMIC_RELAXED);
+    }
+    const unsigned fb_blocks = (unsigned)fbb;
     if (hipMemsetAsync(ws.truth, 0, 2 * kCtrSlots * 8 + 256, q) != hipSuccess)  // truth, found (adjacent)
         return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
     for (int v = 0; v < V; ++v) {
@@ -487,27 +504,14 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
             bwd_gather_kernel<<<(unsigned)gather_blocks, 256, 0, q>>>(g, hv, ws, gv, margin);
         }
         bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force);
-        for (int pc0 = 0; pc0 < P; pc0 += ws.pc) {  // fallback: returns at once unless flagged
-            const int pcn = std::min(ws.pc, P - pc0);
-            const int64_t nk = (int64_t)pcn * K, nq = (int64_t)pcn * HW;
-            const int nb = (int)((nk + kScanTile - 1) / kScanTile);
-            fb_zero_kernel<<<fb_grid(nk, 256), 256, 0, q>>>(ws, nk);
-            if (fast)
-                fb_key_kernel<true><<<fb_grid(nq, 256), 256, 0, q>>>(g, hv, pc0, pcn, ws);
-            else
-                fb_key_kernel<false><<<fb_grid(nq, 256), 256, 0, q>>>(g, hv, pc0, pcn, ws);
-            fb_scan_sums_kernel<<<fb_grid(nb, 1), kScanBlock, 0, q>>>(ws, nk, nb);
-            fb_scan_offsets_kernel<<<1, kScanBlock, 0, q>>>(ws, nb);
-            fb_scan_apply_kernel<<<fb_grid(nb, 1), kScanBlock, 0, q>>>(ws, nk, nb);
-            fb_fill_kernel<<<fb_grid(nq, 256), 256, 0, q>>>(HW, pcn, K, ws);
-            fb_big_reset_kernel<<<1, 1, 0, q>>>(ws);
-            fb_sort_kernel<<<fb_grid(nk, 256), 256, 0, q>>>(nk, ws);
-            fb_big_sort_kernel<<<256, 256, 0, q>>>(ws);
-            if (fast)
-                fb_gather_kernel<true><<<fb_grid(nq, 256), 256, 0, q>>>(g, hv, pc0, pcn, ws, gv);
-            else
-                fb_gather_kernel<false><<<fb_grid(nq, 256), 256, 0, q>>>(g, hv, pc0, pcn, ws, gv);
-        }
+        // fallback: one cooperative launch, returns at once unless flagged
+        const float* hvc = hv;
+        void* args[] = {(void*)&g, (void*)&hvc, (void*)&ws, (void*)&gv};
+        const hipError_t e = fast ? hipLaunchCooperativeKernel(bwd_fallback_kernel<true>, dim3(fb_blocks), dim3(256),
+                                                               args, 0, q)
+                                  : hipLaunchCooperativeKernel(bwd_fallback_kernel<false>, dim3(fb_blocks), dim3(256),
+                                                               args, 0, q);
+        if (e != hipSuccess) return fail(MPIV_ERR_HIP, "%s: cooperative fallback launch failed: %s", nm, hipGetErrorString(e));
     }
     return launched(nm);
 }

@@ -41,6 +41,8 @@
 //            chunks so its workspace stays a fraction of d s.
 // Every product and sum is a single fp32 rounding written out explicitly (the library
 // builds with -ffp-contract=off).
+#include <hip/hip_cooperative_groups.h>
+
 #include "mpiv_common.hpp"
 
 namespace mpiv {
@@ -49,8 +51,20 @@ constexpr int kGridVec = 8;        // grid_sampler_2d_backward chunk width (orac
 constexpr int kBwdCH = 8;          // chain: planes per chunk
 constexpr int kGTW = 64;           // gather: texel tile width (a wave = one tile row)
 constexpr int kGTH = 4;            // gather: tile rows (4 waves)
-constexpr int kGPl = 8;            // gather: planes per block (one 128-B gradient run per texel)
-constexpr int kGCap = 1024;        // gather: output pixels staged per pass
+// gather tile constants (overridable for A/B builds, tools/gpu_ab_lib.sh); measured on
+// config 4 (profiles/r02_bwd_gather_ab.txt): 4 planes x 736 staged pixels at 6 waves/SIMD
+// 2.97 ms per backward, 8 planes x 1024 at 4 waves 3.40, 8 waves (any shape) spills
+#ifndef MPIV_GPL
+#define MPIV_GPL 4
+#endif
+#ifndef MPIV_GCAP
+#define MPIV_GCAP 736
+#endif
+#ifndef MPIV_GLB
+#define MPIV_GLB 6
+#endif
+constexpr int kGPl = MPIV_GPL;     // gather: planes per block (a texel's kGPl planes are one 16*kGPl-B run)
+constexpr int kGCap = MPIV_GCAP;   // gather: output pixels staged per pass
 constexpr int kGMaxBox = 64 * kGCap;  // gather: larger boxes (extreme magnification) -> fallback
 constexpr int kCtrSlots = 64;      // the two pair counters are spread over 64 words each
 constexpr unsigned long long kUnsafe = 1ull << 40;  // > any truth count: forces the fallback
@@ -59,7 +73,6 @@ constexpr int kScanItems = 16;     // fallback: items per thread in the bucket s
 constexpr int kScanBlock = 256;
 constexpr int kScanTile = kScanItems * kScanBlock;
 constexpr int kSmallBucket = 32;   // fallback: larger buckets are sorted by a whole block
-constexpr int kFbGrid = 1024;      // fallback kernels: grid-stride grid (cheap when gated off)
 
 struct BwdWs {
     float4* ds;    // [P][HW]  d sample (d rgb, d a) per plane-pixel
@@ -424,7 +437,7 @@ constexpr int kGBCap = 2;                   // entries per bucket list (more: th
 // reference's order (pixel/8, corner, pixel%8), and the staged index rides in the low bits.
 // A bucket with more entries (magnification: several pixels per texel) makes the block
 // scan per-texel windows of the inverse map instead (one 8-pixel chunk at a time).
-__global__ __launch_bounds__(256) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
+__global__ __launch_bounds__(256, MPIV_GLB) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
                                                          float4* __restrict__ dmpi, float margin) {
     __shared__ int s_code[kGCap];     // local nw-tap bucket of the staged pixel, -1 = none
     __shared__ float2 s_fr[kGCap];    // its bilinear fractions (px - floor px, py - floor py)
@@ -436,7 +449,8 @@ __global__ __launch_bounds__(256) void bwd_gather_kernel(RenderGeom g, const flo
     const int tiles_x = (g.W + kGTW - 1) / kGTW;
     const int ntiles = tiles_x * ((g.H + kGTH - 1) / kGTH);
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
-    const int tile = lb % ntiles, p0 = (lb / ntiles) * kGPl;
+    const int ngroups = (g.P + kGPl - 1) / kGPl;  // plane groups fastest: the blocks writing one texel's
+    const int tile = lb / ngroups, p0 = (lb % ngroups) * kGPl;  // gradient line run together
     const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTH;
     const int tx = tx0 + (threadIdx.x & (kWave - 1)), ty = ty0 + (threadIdx.x >> 6);
     const bool tin = tx < g.W && ty < g.H;
@@ -539,7 +553,7 @@ __global__ __launch_bounds__(256) void bwd_gather_kernel(RenderGeom g, const flo
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
                         if (key[k0 + k] != 0xFFFFFFFFu) {
-                            const int q = (int)(key[k0 + k] & (kGCap * 2 - 1));
+                            const int q = (int)(key[k0 + k] & 0x7FF);  // staged index: bits 0-10 (kGCap <= 2048)
                             f[k] = s_fr[q];
                             d[k] = s_ds[q];
                         }
@@ -663,36 +677,12 @@ __global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force) {
 }
 
 // ---- fallback: the general bucket pipeline (runs only when *flag is set) -------------
-
-__device__ __forceinline__ bool fb_off(const BwdWs& ws) { return *ws.flag == 0; }
-
-__global__ __launch_bounds__(256) void fb_zero_kernel(BwdWs ws, int64_t n) {
-    if (fb_off(ws)) return;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) ws.count[i] = 0;
-}
-
-// nw-tap bucket of every (plane of the chunk, pixel) sample; bucket sizes counted
-template <bool FAST>
-__global__ __launch_bounds__(256) void fb_key_kernel(RenderGeom g, const float* __restrict__ homs, int pc0, int pcn,
-                                                     BwdWs ws) {
-    if (fb_off(ws)) return;
-    const int64_t HW = (int64_t)g.H * g.W;
-    const int K1 = g.W + 1;
-    const int64_t K = (int64_t)(g.H + 1) * K1;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < pcn * HW; q += (int64_t)gridDim.x * 256) {
-        const int pl = (int)(q / HW);
-        const int pix = (int)(q - pl * HW);
-        const int y = pix / g.W, x = pix - y * g.W;
-        float px, py;
-        render_pos<FAST>(homs + (int64_t)(pc0 + pl) * 9, (float)x, (float)y, g, px, py);
-        const float fx0 = floorf(px), fy0 = floorf(py);
-        // some tap lies in the image iff the nw tap is in [-1, W-1] x [-1, H-1] (NaN: none)
-        const bool in = fx0 >= -1.0f && fx0 <= (float)(g.W - 1) && fy0 >= -1.0f && fy0 <= (float)(g.H - 1);
-        const int k = in ? ((int)fy0 + 1) * K1 + (int)fx0 + 1 : -1;
-        ws.key[q] = k;
-        if (in) atomicAdd(&ws.count[pl * K + k], 1);
-    }
-}
+// One cooperative launch per view (bwd_fallback_kernel, hipLaunchCooperativeKernel: every
+// block resident, so grid.sync() separates the phases); it returns at once while the flag
+// is clear.  Per chunk of ws.pc planes: nw-tap bucket of every sample and bucket sizes,
+// exclusive scan of the sizes, pixel ids into their buckets, each bucket sorted by pixel
+// id, then per texel the four buckets merged in the reference's order.  Each phase is a
+// grid-stride loop over blocks `bid` of `nblk`.
 
 __device__ __forceinline__ int block_exclusive_scan(int v, int* s_tmp, int& total) {
     // 256 threads: inclusive Hillis-Steele scan through LDS
@@ -710,204 +700,209 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* s_tmp, int& tota
     return incl - v;
 }
 
-__global__ __launch_bounds__(kScanBlock) void fb_scan_sums_kernel(BwdWs ws, int64_t n, int nb) {
-    __shared__ int s_tmp[kScanBlock];
-    if (fb_off(ws)) return;
-    for (int tb = blockIdx.x; tb < nb; tb += gridDim.x) {
-        const int64_t base = (int64_t)tb * kScanTile + (int64_t)threadIdx.x * kScanItems;
-        int sum = 0;
-        for (int i = 0; i < kScanItems; ++i)
-            if (base + i < n) sum += ws.count[base + i];
-        int total;
-        block_exclusive_scan(sum, s_tmp, total);
-        if (threadIdx.x == 0) ws.bsum[tb] = total;
-    }
-}
-
-// single block: exclusive scan of the nb tile sums in place
-__global__ __launch_bounds__(kScanBlock) void fb_scan_offsets_kernel(BwdWs ws, int nb) {
-    __shared__ int s_tmp[kScanBlock];
-    if (fb_off(ws)) return;
-    int carry = 0;
-    for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
-        const int i = c0 + threadIdx.x;
-        const int v = i < nb ? ws.bsum[i] : 0;
-        int total;
-        const int ex = block_exclusive_scan(v, s_tmp, total);
-        if (i < nb) ws.bsum[i] = carry + ex;
-        carry += total;
-    }
-}
-
-__global__ __launch_bounds__(kScanBlock) void fb_scan_apply_kernel(BwdWs ws, int64_t n, int nb) {
-    __shared__ int s_tmp[kScanBlock];
-    if (fb_off(ws)) return;
-    for (int tb = blockIdx.x; tb < nb; tb += gridDim.x) {
-        const int64_t base = (int64_t)tb * kScanTile + (int64_t)threadIdx.x * kScanItems;
-        int v[kScanItems];
-        int sum = 0;
-#pragma unroll
-        for (int i = 0; i < kScanItems; ++i) {
-            v[i] = base + i < n ? ws.count[base + i] : 0;
-            sum += v[i];
-        }
-        int total;
-        int run = ws.bsum[tb] + block_exclusive_scan(sum, s_tmp, total);
-#pragma unroll
-        for (int i = 0; i < kScanItems; ++i) {
-            if (base + i < n) ws.offs[base + i] = run;
-            run += v[i];
-        }
-        if (tb == nb - 1 && threadIdx.x == kScanBlock - 1) ws.offs[n] = run;  // grand total
-    }
-}
-
-// pixel ids into their buckets (atomic slot claim; count returns to 0 for the next chunk)
-__global__ __launch_bounds__(256) void fb_fill_kernel(int64_t HW, int pcn, int64_t K, BwdWs ws) {
-    if (fb_off(ws)) return;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < pcn * HW; q += (int64_t)gridDim.x * 256) {
-        const int k = ws.key[q];
-        if (k < 0) continue;
-        const int64_t pl = q / HW;
-        const int64_t pk = pl * K + k;
-        const int slot = atomicSub(&ws.count[pk], 1) - 1;
-        ws.ids[ws.offs[pk] + slot] = (int)(q - pl * HW);
-    }
-}
-
-// each bucket sorted by pixel id: <= kSmallBucket ids by one thread, larger ones
-// (minification, degenerate homographies) listed for fb_big_sort_kernel
-__global__ __launch_bounds__(256) void fb_sort_kernel(int64_t nbuckets, BwdWs ws) {
-    if (fb_off(ws)) return;
-    for (int64_t pk = (int64_t)blockIdx.x * 256 + threadIdx.x; pk < nbuckets; pk += (int64_t)gridDim.x * 256) {
-        const int b = ws.offs[pk], e = ws.offs[pk + 1];
-        if (e - b > kSmallBucket) {
-            ws.big[1 + atomicAdd(&ws.big[0], 1)] = (int)pk;
-            continue;
-        }
-        for (int i = b + 1; i < e; ++i) {  // insertion sort (at most kSmallBucket ids)
-            const int v = ws.ids[i];
-            int jx = i - 1;
-            while (jx >= b && ws.ids[jx] > v) {
-                ws.ids[jx + 1] = ws.ids[jx];
-                --jx;
-            }
-            ws.ids[jx + 1] = v;
-        }
-    }
-}
-
-// The large buckets: each block merge-sorts one at a time with all threads (runs of width
-// w merged pairwise per pass, output element k of a pair found by a merge-path binary
-// search; ids within a bucket are distinct).  Scratch: the bucket's range of `key` (dead
-// after the fill).  O(n log^2 n / threads) per bucket.  Resets the list for the next chunk.
-__global__ __launch_bounds__(256) void fb_big_sort_kernel(BwdWs ws) {
-    if (fb_off(ws)) return;
-    const int nbig = ws.big[0];
-    for (int i = blockIdx.x; i < nbig; i += gridDim.x) {
-        const int pk = ws.big[1 + i];
-        const int b = ws.offs[pk], n = ws.offs[pk + 1] - b;
-        int* src = ws.ids + b;
-        int* dst = ws.key + b;
-        for (int w = 1; w < n; w <<= 1) {
-            for (int k0 = threadIdx.x; k0 < n; k0 += blockDim.x) {
-                const int s0 = (k0 / (2 * w)) * (2 * w);
-                const int mm = min(s0 + w, n), e = min(s0 + 2 * w, n);
-                const int k = k0 - s0;
-                const int* A = src + s0;
-                const int* Bv = src + mm;
-                const int la = mm - s0, lb = e - mm;
-                int lo = max(0, k - lb), hi = min(k, la);
-                while (lo < hi) {  // number of A's elements among the pair's first k outputs
-                    const int mid = (lo + hi) >> 1;
-                    if (A[mid] < Bv[k - 1 - mid])
-                        lo = mid + 1;
-                    else
-                        hi = mid;
-                }
-                const int ib = k - lo;
-                dst[k0] = (lo < la && (ib >= lb || A[lo] < Bv[ib])) ? A[lo] : Bv[ib];
-            }
-            __syncthreads();
-            int* t = src;
-            src = dst;
-            dst = t;
-        }
-        if (src != ws.ids + b)
-            for (int k0 = threadIdx.x; k0 < n; k0 += blockDim.x) ws.ids[b + k0] = src[k0];
-        __syncthreads();
-    }
-}
-
-// big list cleared after the sort kernels of a chunk (one thread)
-__global__ void fb_big_reset_kernel(BwdWs ws) {
-    if (fb_off(ws)) return;
-    ws.big[0] = 0;
-}
-
 __device__ __forceinline__ unsigned order_key(int pix, int corner) {
     return ((unsigned)(pix / kGridVec) << 5) | ((unsigned)corner << 3) | (unsigned)(pix % kGridVec);
 }
 
-// Texel t of plane pc0 + pl: its four nw-tap buckets (the samples having it as nw, ne, sw,
-// se tap) merged by the reference's order key; fractions recomputed from the position.
 template <bool FAST>
-__global__ __launch_bounds__(256) void fb_gather_kernel(RenderGeom g, const float* __restrict__ homs, int pc0,
-                                                        int pcn, BwdWs ws, float4* __restrict__ dmpi) {
-    if (fb_off(ws)) return;
+__global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
+                                                           float4* __restrict__ dmpi) {
+    __shared__ int s_tmp[kScanBlock];
+    if (*ws.flag == 0) return;  // uniform over the grid: the tile gather was complete
+    namespace cgr = cooperative_groups;
+    cgr::grid_group grid = cgr::this_grid();
+    const int bid = blockIdx.x, nblk = gridDim.x, tid = threadIdx.x;
+    const int64_t gtid = (int64_t)bid * 256 + tid, gstride = (int64_t)nblk * 256;
     const int64_t HW = (int64_t)g.H * g.W;
     const int K1 = g.W + 1;
     const int64_t K = (int64_t)(g.H + 1) * K1;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < pcn * HW; q += (int64_t)gridDim.x * 256) {
-        const int pl = (int)(q / HW);
-        const int t = (int)(q - pl * HW);
-        const int ty = t / g.W, tx = t - ty * g.W;
-        const float* h = homs + (int64_t)(pc0 + pl) * 9;
-        const int64_t base = pl * K;
-        const int64_t bk[4] = {base + (int64_t)(ty + 1) * K1 + tx + 1, base + (int64_t)(ty + 1) * K1 + tx,
-                               base + (int64_t)ty * K1 + tx + 1, base + (int64_t)ty * K1 + tx};
-        int pos[4], end[4];
-        unsigned head[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            pos[c] = ws.offs[bk[c]];
-            end[c] = ws.offs[bk[c] + 1];
-            head[c] = pos[c] < end[c] ? order_key(ws.ids[pos[c]], c) : 0xFFFFFFFFu;
-        }
-        const float4* dsp = ws.ds + (int64_t)(pc0 + pl) * HW;
-        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-        for (;;) {
-            int c = 0;
-            unsigned m = head[0];
-#pragma unroll
-            for (int k = 1; k < 4; ++k)
-                if (head[k] < m) {
-                    m = head[k];
-                    c = k;
-                }
-            if (m == 0xFFFFFFFFu) break;
-            int pix = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {  // static indexing keeps pos/head in registers
-                if (k == c) {
-                    pix = ws.ids[pos[k]];
-                    ++pos[k];
-                    head[k] = pos[k] < end[k] ? order_key(ws.ids[pos[k]], k) : 0xFFFFFFFFu;
-                }
-            }
-            const int py_ = pix / g.W;
+    // bucket sizes start at zero (the fill returns them to zero for the next chunk)
+    for (int64_t i = gtid; i < (int64_t)ws.pc * K; i += gstride) ws.count[i] = 0;
+    grid.sync();
+    for (int pc0 = 0; pc0 < g.P; pc0 += ws.pc) {
+        const int pcn = min(ws.pc, g.P - pc0);
+        const int64_t nq = pcn * HW, nk = pcn * K;
+        const int nb = (int)((nk + kScanTile - 1) / kScanTile);
+        // nw-tap bucket of every (plane of the chunk, pixel) sample; sizes counted
+        for (int64_t q = gtid; q < nq; q += gstride) {
+            const int pl = (int)(q / HW);
+            const int pix = (int)(q - pl * HW);
+            const int y = pix / g.W, x = pix - y * g.W;
             float px, py;
-            render_pos<FAST>(h, (float)(pix - py_ * g.W), (float)py_, g, px, py);
-            const float wx = px - floorf(px), ex = 1.0f - wx;
-            const float wy = py - floorf(py), sy = 1.0f - wy;
-            const float w = c == 0 ? sy * ex : c == 1 ? sy * wx : c == 2 ? wy * ex : wy * wx;
-            const float4 d = dsp[pix];
-            a0 = a0 + w * d.x;
-            a1 = a1 + w * d.y;
-            a2 = a2 + w * d.z;
-            a3 = a3 + w * d.w;
+            render_pos<FAST>(homs + (int64_t)(pc0 + pl) * 9, (float)x, (float)y, g, px, py);
+            const float fx0 = floorf(px), fy0 = floorf(py);
+            // some tap lies in the image iff the nw tap is in [-1, W-1] x [-1, H-1] (NaN: none)
+            const bool in = fx0 >= -1.0f && fx0 <= (float)(g.W - 1) && fy0 >= -1.0f && fy0 <= (float)(g.H - 1);
+            const int k = in ? ((int)fy0 + 1) * K1 + (int)fx0 + 1 : -1;
+            ws.key[q] = k;
+            if (in) atomicAdd(&ws.count[pl * K + k], 1);
         }
-        dmpi[(int64_t)t * g.P + pc0 + pl] = make_float4(a0, a1, a2, a3);
+        grid.sync();
+        // exclusive scan of the sizes: tile sums, their scan (block 0), per-tile apply
+        for (int tb = bid; tb < nb; tb += nblk) {
+            const int64_t base = (int64_t)tb * kScanTile + (int64_t)tid * kScanItems;
+            int sum = 0;
+            for (int i = 0; i < kScanItems; ++i)
+                if (base + i < nk) sum += ws.count[base + i];
+            int total;
+            block_exclusive_scan(sum, s_tmp, total);
+            if (tid == 0) ws.bsum[tb] = total;
+        }
+        grid.sync();
+        if (bid == 0) {
+            int carry = 0;
+            for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
+                const int i = c0 + tid;
+                const int v = i < nb ? ws.bsum[i] : 0;
+                int total;
+                const int ex = block_exclusive_scan(v, s_tmp, total);
+                if (i < nb) ws.bsum[i] = carry + ex;
+                carry += total;
+            }
+            if (tid == 0) ws.big[0] = 0;
+        }
+        grid.sync();
+        for (int tb = bid; tb < nb; tb += nblk) {
+            const int64_t base = (int64_t)tb * kScanTile + (int64_t)tid * kScanItems;
+            int v[kScanItems];
+            int sum = 0;
+#pragma unroll
+            for (int i = 0; i < kScanItems; ++i) {
+                v[i] = base + i < nk ? ws.count[base + i] : 0;
+                sum += v[i];
+            }
+            int total;
+            int run = ws.bsum[tb] + block_exclusive_scan(sum, s_tmp, total);
+#pragma unroll
+            for (int i = 0; i < kScanItems; ++i) {
+                if (base + i < nk) ws.offs[base + i] = run;
+                run += v[i];
+            }
+            if (tb == nb - 1 && tid == kScanBlock - 1) ws.offs[nk] = run;  // grand total
+        }
+        grid.sync();
+        // pixel ids into their buckets (atomic slot claim; sizes return to zero)
+        for (int64_t q = gtid; q < nq; q += gstride) {
+            const int k = ws.key[q];
+            if (k < 0) continue;
+            const int64_t pl = q / HW;
+            const int64_t pk = pl * K + k;
+            const int slot = atomicSub(&ws.count[pk], 1) - 1;
+            ws.ids[ws.offs[pk] + slot] = (int)(q - pl * HW);
+        }
+        grid.sync();
+        // each bucket sorted by pixel id: <= kSmallBucket ids by one thread (insertion
+        // sort), larger ones (minification, degenerate homographies) listed for a block
+        for (int64_t pk = gtid; pk < nk; pk += gstride) {
+            const int b = ws.offs[pk], e = ws.offs[pk + 1];
+            if (e - b > kSmallBucket) {
+                ws.big[1 + atomicAdd(&ws.big[0], 1)] = (int)pk;
+                continue;
+            }
+            for (int i = b + 1; i < e; ++i) {
+                const int v = ws.ids[i];
+                int jx = i - 1;
+                while (jx >= b && ws.ids[jx] > v) {
+                    ws.ids[jx + 1] = ws.ids[jx];
+                    --jx;
+                }
+                ws.ids[jx + 1] = v;
+            }
+        }
+        grid.sync();
+        // the large buckets: one block each, merge sort with all threads (runs of width w
+        // merged pairwise per pass, output element k of a pair found by a merge-path binary
+        // search; ids within a bucket are distinct).  Scratch: the bucket's range of `key`
+        // (dead after the fill).  O(n log^2 n / threads) per bucket.
+        const int nbig = ws.big[0];
+        for (int i = bid; i < nbig; i += nblk) {
+            const int pk = ws.big[1 + i];
+            const int b = ws.offs[pk], n = ws.offs[pk + 1] - b;
+            int* src = ws.ids + b;
+            int* dst = ws.key + b;
+            for (int w = 1; w < n; w <<= 1) {
+                for (int k0 = tid; k0 < n; k0 += 256) {
+                    const int s0 = (k0 / (2 * w)) * (2 * w);
+                    const int mm = min(s0 + w, n), e = min(s0 + 2 * w, n);
+                    const int k = k0 - s0;
+                    const int* A = src + s0;
+                    const int* Bv = src + mm;
+                    const int la = mm - s0, lb = e - mm;
+                    int lo = max(0, k - lb), hi = min(k, la);
+                    while (lo < hi) {  // number of A's elements among the pair's first k outputs
+                        const int mid = (lo + hi) >> 1;
+                        if (A[mid] < Bv[k - 1 - mid])
+                            lo = mid + 1;
+                        else
+                            hi = mid;
+                    }
+                    const int ib = k - lo;
+                    dst[k0] = (lo < la && (ib >= lb || A[lo] < Bv[ib])) ? A[lo] : Bv[ib];
+                }
+                __syncthreads();
+                int* t = src;
+                src = dst;
+                dst = t;
+            }
+            if (src != ws.ids + b)
+                for (int k0 = tid; k0 < n; k0 += 256) ws.ids[b + k0] = src[k0];
+            __syncthreads();
+        }
+        grid.sync();
+        // texel t of plane pc0 + pl: its four nw-tap buckets (the samples having it as nw,
+        // ne, sw, se tap) merged by the reference's order key; fractions from the position
+        for (int64_t q = gtid; q < nq; q += gstride) {
+            const int pl = (int)(q / HW);
+            const int t = (int)(q - pl * HW);
+            const int ty = t / g.W, tx = t - ty * g.W;
+            const float* h = homs + (int64_t)(pc0 + pl) * 9;
+            const int64_t base = pl * K;
+            const int64_t bk[4] = {base + (int64_t)(ty + 1) * K1 + tx + 1, base + (int64_t)(ty + 1) * K1 + tx,
+                                   base + (int64_t)ty * K1 + tx + 1, base + (int64_t)ty * K1 + tx};
+            int pos[4], end[4];
+            unsigned head[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                pos[c] = ws.offs[bk[c]];
+                end[c] = ws.offs[bk[c] + 1];
+                head[c] = pos[c] < end[c] ? order_key(ws.ids[pos[c]], c) : 0xFFFFFFFFu;
+            }
+            const float4* dsp = ws.ds + (int64_t)(pc0 + pl) * HW;
+            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+            for (;;) {
+                int c = 0;
+                unsigned m = head[0];
+#pragma unroll
+                for (int k = 1; k < 4; ++k)
+                    if (head[k] < m) {
+                        m = head[k];
+                        c = k;
+                    }
+                if (m == 0xFFFFFFFFu) break;
+                int pix = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {  // static indexing keeps pos/head in registers
+                    if (k == c) {
+                        pix = ws.ids[pos[k]];
+                        ++pos[k];
+                        head[k] = pos[k] < end[k] ? order_key(ws.ids[pos[k]], k) : 0xFFFFFFFFu;
+                    }
+                }
+                const int py_ = pix / g.W;
+                float px, py;
+                render_pos<FAST>(h, (float)(pix - py_ * g.W), (float)py_, g, px, py);
+                const float wx = px - floorf(px), ex = 1.0f - wx;
+                const float wy = py - floorf(py), sy = 1.0f - wy;
+                const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
+                const float4 d = dsp[pix];
+                a0 = a0 + w * d.x;
+                a1 = a1 + w * d.y;
+                a2 = a2 + w * d.z;
+                a3 = a3 + w * d.w;
+            }
+            dmpi[(int64_t)t * g.P + pc0 + pl] = make_float4(a0, a1, a2, a3);
+        }
+        grid.sync();  // the chunk's arrays are reused by the next one
     }
 }
 
