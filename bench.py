@@ -167,6 +167,42 @@ def sha16(t: torch.Tensor) -> str:
     return hashlib.sha256(t.detach().cpu().contiguous().numpy().tobytes()).hexdigest()[:16]
 
 
+def training_leg(dev, stream, n=10):
+    """The training caller's path at config-4 size (notebook loss, ipynb cell 12 L42: a
+    non-broadcast [1,H,W,P,4] MPI rendered and differentiated): the training forward
+    (frame + composite checkpoints, mpiv_render_train) and the bit-exact backward
+    (mpiv_render_backward) fed those checkpoints, plus the backward without them; HIP
+    events on the launch stream, one view, synthetic data generated on the device."""
+    c4 = configs.config4()
+    H, W, P = c4["H"], c4["W"], c4["P"]
+    g = torch.Generator(device=dev).manual_seed(7)
+    mpi = torch.rand((1, H, W, P, 4), generator=g, device=dev)
+    homs = _host.render_homographies(configs.f32(c4["poses"][100:101]), configs.f32(c4["depths"]),
+                                     configs.f32([c4["K"]]), 1).to(dev)
+    dout = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    ws = torch.empty(_lib.load().mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    _, ck = _lib.render_train(mpi, homs)
+    fwd_ms = event_ms(lambda: _lib.render_train(mpi, homs), n, stream)
+    g1 = _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)
+    bwd_ms = event_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck), n, stream)
+    g2 = _lib.render_backward(mpi, homs, dout, workspace=ws)
+    bwd2_ms = event_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws), n, stream)
+    flag = int(ws[_lib.bwd_flag_offset(H, W, P):][:4].view(torch.int32).item())
+    same = bool(torch.equal(g1.view(torch.int32), g2.view(torch.int32)))
+    mpi_bytes = P * H * W * 16
+    res = {"workload": "BASELINE config 4 MPI (1024x1024x128), one non-broadcast view: training forward + backward",
+           "forward_ms": round(fwd_ms, 4), "backward_ms": round(bwd_ms, 4),
+           "backward_no_ckpt_ms": round(bwd2_ms, 4), "step_ms": round(fwd_ms + bwd_ms, 4),
+           "backward_alg_bytes": 2 * mpi_bytes + H * W * 12,
+           "backward_alg_def": "MPI read + d MPI written + d frame read (workspace traffic not counted)",
+           "backward_hbm_frac": round((2 * mpi_bytes + H * W * 12) / (bwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "workspace_GB": round(ws.numel() / 1e9, 3), "fallback_flag": flag,
+           "ckpt_grad_bit_identical": same}
+    del mpi, ws, g1, g2, ck
+    torch.cuda.empty_cache()
+    return res
+
+
 def config5_leg(world, rank, dev, steps, warmup):
     """BASELINE config 5: the 256-plane 4096x2160 MPI (36.2 GB), one pose, planes sharded
     over the ranks.  Each rank generates its plane range on the device (counter-based
@@ -355,6 +391,7 @@ def main():
     if packed is not None:
         del view
     torch.cuda.empty_cache()
+    train = training_leg(dev, stream) if (world == 1 and not args.no_extras) else None
     c5 = None if (args.no_config5 or args.no_extras) else config5_leg(world, rank, dev, max(3, args.steps // 2), 1)
 
     if rank == 0:
@@ -391,6 +428,7 @@ def main():
                                   "sha16": timed_frame_sha, "bit_exact": timed_frame_sha == one_sha},
             "cpu_baseline": None,
             "config5_plane_sharded": c5,
+            "training_render_backward": train,
         }
         if world == 1 and args.cpu_seconds > 0 and not args.no_extras:
             # the GPU frame of the first view of step 0, to cross-check the CPU sample bit-exactly

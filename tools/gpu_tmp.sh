@@ -1,13 +1,9 @@
 set -u
 mkdir -p gpurun_out
 ROOT=$(pwd)
-timeout -k 10 300 python -u -m pytest tests/test_backward_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/bwd_tests.log 2>&1; rc=$?
-echo "bwd tests rc=$rc"; tail -3 gpurun_out/bwd_tests.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
+echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
-echo "tests rc=$rc"; tail -3 gpurun_out/gpu_tests.log
-[ $rc -eq 0 ] || exit $rc
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof_bwd2 -o run -- python -u $ROOT/tools/bench_configs.py --only bwd --iters 8 > $ROOT/gpurun_out/prof_bwd2.log 2>&1; rc=$?
-grep config $ROOT/gpurun_out/prof_bwd2.log
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_r02e.json 2> gpurun_out/bench_r02e.err; rc=$?
+echo "bench rc=$rc"; tail -c 2500 gpurun_out/bench_r02e.json
 exit $rc
