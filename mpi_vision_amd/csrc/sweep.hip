@@ -518,6 +518,15 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
         so_w[k] = swz((lane & 15) * 4 * C + (lane >> 4) * C + k);
         so_r[k] = swz(k * kWave + lane);
     }
+#ifndef MPIV_SWEEP_HOIST
+#define MPIV_SWEEP_HOIST 1
+#endif
+    // When the thread stride is a multiple of the 16-pixel block's groups (D = 64: 256
+    // groups), a thread's depth group is the same in every iteration: its 4 depths are read
+    // from LDS once, not once per iteration (one LDS round trip fewer per iteration).
+    const bool hoist = MPIV_SWEEP_HOIST && pix16 && d4 && kSLThreads % nb16 == 0;
+    f32x4 dqh = {0.f, 0.f, 0.f, 0.f};
+    if (hoist) dqh = *reinterpret_cast<const f32x4*>(&s_dep[((threadIdx.x % nb16) >> 4) * kSweepDG]);
     for (int gi = threadIdx.x; gi < ngr; gi += kSLThreads) {
         int tr = 0;  // tile row of group gi
 #pragma unroll
@@ -539,7 +548,10 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
         // blends) with the rare fix-ups behind wave-uniform tests, so their LDS reads are
         // in flight together instead of one round trip per sample.
         float su[kSweepDG], sv[kSweepDG], dq[kSweepDG];
-        if (d4) {
+        if (hoist) {
+#pragma unroll
+            for (int j = 0; j < kSweepDG; ++j) dq[j] = dqh[j];
+        } else if (d4) {
             const f32x4 q = *reinterpret_cast<const f32x4*>(&s_dep[dg * kSweepDG]);
 #pragma unroll
             for (int j = 0; j < kSweepDG; ++j) dq[j] = q[j];
@@ -582,7 +594,30 @@ __global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
         }
         f32x4 s[kSweepDG];
         bool staged = pitch > 0;
-        if (staged && C == 3) {  // RGB: 12-B tap reads, 3-channel blends
+#ifndef MPIV_SWEEP_B128
+#define MPIV_SWEEP_B128 1
+#endif
+        if (MPIV_SWEEP_B128 && staged && C == 3) {
+            // RGB through 16-B tap reads (ds_read_b128: 4 LDS cycles per wave read,
+            // ds_read_b96: 8), at most 12 in flight: depth 3's taps are issued into the
+            // registers depth 0's blend frees
+            TapSet ts[kSweepDG];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) staged = lds_issue(s_src, lbx, px[j], py[j], ts[j]) && staged;
+            s[0] = blend_taps3(TapSet3{ts[0].a.xyz, ts[0].b.xyz, ts[0].c.xyz, ts[0].d.xyz, ts[0].nw, ts[0].ne,
+                                       ts[0].sw, ts[0].se});
+            asm volatile("" ::"v"(ts[0].a), "v"(ts[0].b), "v"(ts[0].c), "v"(ts[0].d));
+            staged = lds_issue(s_src, lbx, px[3], py[3], ts[3]) && staged;
+#pragma unroll
+            for (int j = 1; j < kSweepDG; ++j)
+                s[j] = blend_taps3(TapSet3{ts[j].a.xyz, ts[j].b.xyz, ts[j].c.xyz, ts[j].d.xyz, ts[j].nw, ts[j].ne,
+                                           ts[j].sw, ts[j].se});
+            // the dead 4th channels keep their registers until the reads are consumed (else a
+            // WAW wait serialises the reads, as in the C < 4 path below)
+#pragma unroll
+            for (int j = 1; j < kSweepDG; ++j)
+                asm volatile("" ::"v"(ts[j].a), "v"(ts[j].b), "v"(ts[j].c), "v"(ts[j].d));
+        } else if (staged && C == 3) {  // RGB: 12-B tap reads, 3-channel blends
             TapSet3 ts[kSweepDG];
 #pragma unroll
             for (int j = 0; j < kSweepDG; ++j) staged = lds_issue3(s_src, lbx, px[j], py[j], ts[j]) && staged;
