@@ -339,8 +339,10 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// C <= 3 must keep 4 waves per SIMD (two 512-thread blocks per CU, which the LDS allows):
+// the register allocator otherwise lands a few VGPRs above 128 and halves the occupancy.
 template <int C>
-__global__ __launch_bounds__(kSLThreads) void plane_sweep_lds_kernel(
+__global__ __launch_bounds__(kSLThreads) __attribute__((amdgpu_waves_per_eu(C <= 3 ? 4 : 1))) void plane_sweep_lds_kernel(
     const float4* __restrict__ img4, SweepParams sp, PadGeom pg, float rc_hs, float rc_ws, FastDiv fd_g,
     FastDiv fd_b, const float* __restrict__ ki, const float* __restrict__ proj, const float* __restrict__ depths,
     float* __restrict__ out, int64_t out_bstride, int64_t out_pstride, int vec, int shrink) {

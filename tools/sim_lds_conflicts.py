@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""LDS bank-conflict model of the LDS-staged sweep's tap reads (config 3), per lane mapping.
+
+ds_read_b128 serves a wave in 4 lane groups of 16 (MI355X_MICROARCH.md LDS table); a 16-B
+texel at LDS texel index t occupies bank slot t % 16; a group costs max over slots of the
+number of distinct texels read there (identical texels broadcast).  Tap positions come
+from the config-3 geometry in float64 (close enough to the kernel's fp32 for a model).
+
+    python tools/sim_lds_conflicts.py [--tiles 300]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from mpi_vision_amd import configs  # noqa: E402
+
+G128 = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+        list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+G128 += [[l + 32 for l in g] for g in G128[:1]] + [[l + 32 for l in G128[1]]]
+G128 = [G128[0], G128[1], [l + 32 for l in G128[0]], [l + 32 for l in G128[1]]]
+
+
+def mappings():
+    m = {}
+    m["M0 pixel-fastest (production)"] = [(l & 15, l >> 4) for l in range(64)]
+    gm = [None] * 64  # b128 group g <- depth group g, pixels in order
+    for g, lanes in enumerate(G128):
+        for i, l in enumerate(lanes):
+            gm[l] = (i, g)
+    m["one depth group per b128 lane group"] = gm
+    g8 = [None] * 64  # group g <- pixels 8*(g%2).. x depth groups 2*(g//2) + {0,1}
+    for g, lanes in enumerate(G128):
+        for i, l in enumerate(lanes):
+            g8[l] = (8 * (g % 2) + (i % 8), 2 * (g // 2) + i // 8)
+    m["8 pixels x 2 depth groups per lane group"] = g8
+    g4 = [None] * 64  # group g <- pixels 4g..4g+3 x all 4 depth groups
+    for g, lanes in enumerate(G128):
+        for i, l in enumerate(lanes):
+            g4[l] = (4 * g + (i % 4), i // 4)
+    m["4 pixels x 4 depth groups per lane group"] = g4
+    g2 = [None] * 64  # group g <- pixels 2g+{0,1}+8k x 4 dq? : 8 px strided by 2 (even / odd) x 2 dq
+    for g, lanes in enumerate(G128):
+        for i, l in enumerate(lanes):
+            g2[l] = (2 * (i % 8) + (g % 2), 2 * (g // 2) + i // 8)
+    m["8 even|odd pixels x 2 depth groups"] = g2
+    return m
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", type=int, default=300)
+    ap.add_argument("--pad", type=int, default=-1, help="pad the box pitch to = PAD mod 16")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    c = configs.config3()
+    S, H, W, D = c["S"], c["H"], c["W"], c["D"]
+    K = np.array(c["K"], np.float64)
+    Ki = np.linalg.inv(K)
+    dep = np.array(c["depths"], np.float64)
+    rng = np.random.default_rng(0)
+    maps = {k: v for k, v in mappings().items() if a.only in k}
+    tot = {k: 0 for k in maps}
+    ninst = 0
+    for s in range(S):
+        pose = np.array(c["poses"][s], np.float64)
+        proj = np.eye(4)
+        proj[:3, :3] = K
+        proj = proj @ pose
+        for _ in range(a.tiles // S):
+            ty, tx = rng.integers(0, H // 4), rng.integers(0, W // 64)
+            ys, xs = ty * 4 + np.arange(4), tx * 64 + np.arange(64)
+            X, Y = np.meshgrid(xs, ys)
+            ray = np.einsum("ij,jhw->ihw", Ki, np.stack([X, Y, np.ones_like(X)]).astype(np.float64))
+            pts = ray[:, None] * dep[None, :, None, None]  # 3, D, 4, 64
+            hp = np.einsum("ij,jdhw->idhw", proj[:3, :3], pts) + proj[:3, 3][:, None, None, None]
+            u, v = hp[0] / (hp[2] + 1e-10), hp[1] / (hp[2] + 1e-10)
+            px = (2 * ((u + 0.5) / H) - 1 + 1) * W / 2 - 0.5  # swapped x / H (utils.py:444)
+            py = (2 * ((v + 0.5) / W) - 1 + 1) * H / 2 - 0.5
+            fx, fy = np.floor(px), np.floor(py)
+            if not (np.isfinite(fx).all() and np.isfinite(fy).all()):
+                continue
+            xl, yl = max(fx.min() - 1, -2), max(fy.min() - 1, -2)
+            xh, yh = min(fx.max() + 2, W + 1), min(fy.max() + 2, H + 1)
+            if xl > xh or yl > yh:
+                continue
+            pitch = int(xh - xl + 1)
+            if pitch * (yh - yl + 1) > 3072:
+                continue
+            if a.pad >= 0:
+                pitch += (a.pad - pitch) % 16
+            cx, cy = np.clip(fx - xl, 0, None), np.clip(fy - yl, 0, None)
+            t = (cy * pitch + cx).astype(np.int64)  # NW tap texel, [D, 4, 64]
+            for r in range(4):
+                for blk in range(4):
+                    for dg0 in range(0, D // 4, 4):
+                        for j in range(4):
+                            for tap in (0, 1, pitch, pitch + 1):
+                                ninst += 1
+                                for name, mp in maps.items():
+                                    cyc = 0
+                                    for lanes in G128:
+                                        slots = {}
+                                        for l in lanes:
+                                            pq, dq = mp[l]
+                                            tt = int(t[(dg0 + dq) * 4 + j, r, blk * 16 + pq]) + tap
+                                            slots.setdefault(tt % 16, set()).add(tt)
+                                        cyc += max(len(v) for v in slots.values())
+                                    tot[name] += cyc
+    for name, cyc in tot.items():
+        print(f"{name:45s} {cyc / ninst:6.3f} LDS cycles per b128 tap read (4 = conflict-free)")
+
+
+if __name__ == "__main__":
+    main()
