@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--views", type=int, default=125, help="views rendered per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 plane-sharded leg")
+    ap.add_argument("--no-training", action="store_true",
+                    help="skip the training (render backward) leg: its gated cooperative fallback launch makes "
+                         "rocprofv3 --kernel-trace crash in its own teardown (DESIGN.md section 7)")
     ap.add_argument("--no-extras", action="store_true",
                     help="only the timed config-4 launches (rocprofv3 runs: tools/profile.sh), no frame check, "
                          "single-view leg, gather probe or config-5 leg")
@@ -391,7 +394,7 @@ def main():
     if packed is not None:
         del view
     torch.cuda.empty_cache()
-    train = training_leg(dev, stream) if (world == 1 and not args.no_extras) else None
+    train = training_leg(dev, stream) if (world == 1 and not args.no_extras and not args.no_training) else None
     c5 = None if (args.no_config5 or args.no_extras) else config5_leg(world, rank, dev, max(3, args.steps // 2), 1)
 
     if rank == 0:

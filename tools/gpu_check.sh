@@ -20,7 +20,7 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 [ "${SKIP_PROF:-0}" = 1 ] && exit 0
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 ${PROF_LIMIT:-300} rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
-    -- python -u "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 > "$OUT/prof.log" 2>&1
+    -- python -u "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-training > "$OUT/prof.log" 2>&1
 rc=$?
 echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"
 find "$OUT/prof" -name "*stats*" | head
