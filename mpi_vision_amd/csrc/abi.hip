@@ -60,6 +60,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (render_rows_kernel; 100+R: state in LDS, render_rows_lds_kernel);
 //                      -1: off (one row per work-item), 0: automatic (R = 8 where it pays)
 //   sweep_tile=1       the sweep uses the tile kernel; sweep_store=k (k >= 0) the grouped one
+//   sweep_dlane=0      sweeps with D % 64 == 0 use the pixel-per-lane LDS kernel instead of the
+//                      depth-per-lane one (plane_sweep_dlane_kernel)
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
 //                      forces their per-sample global fallback (tests)
 //   bwd_fallback=1     mpiv_render_backward skips the tile gather and runs its bucket
@@ -70,12 +72,13 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 // Relaxed atomics: a launch reads each option once; setting options while another thread
 // launches is a test-harness race on which kernel runs, never on memory.
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
-                kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kNumOpts };
+                kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
+                kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
-                                         "render_tile", "bwd_fallback", "bwd_margin"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16};
+                                         "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -605,6 +608,19 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
         const dim3 lgrid((unsigned)tiles, B, 1);
         const int shrink = opt(kOptBoxShrink);
         const FastDiv fd_b = make_fastdiv((unsigned)(16 * NG));
+        if (D % kWave == 0 && opt(kOptSweepDlane) != 0) {
+#define MPIV_DLANE(CC)                                                                                           \
+    plane_sweep_dlane_kernel<CC><<<lgrid, kDLThreads, 0, q>>>(im, sp, pg, rc_hs, rc_ws, ki, proj, depths, out,   \
+                                                              out_bstride, out_pstride, (int)vec, shrink)
+            switch (C) {
+                case 1: MPIV_DLANE(1); break;
+                case 2: MPIV_DLANE(2); break;
+                case 3: MPIV_DLANE(3); break;
+                default: MPIV_DLANE(4); break;
+            }
+#undef MPIV_DLANE
+            return launched("mpiv_plane_sweep_padded");
+        }
 #define MPIV_LDS(CC)                                                                                          \
     plane_sweep_lds_kernel<CC><<<lgrid, kSLThreads, 0, q>>>(im, sp, pg, rc_hs, rc_ws, fd_g, fd_b, ki, proj, depths, \
                                                      out, out_bstride, out_pstride, (int)vec, shrink)

@@ -704,6 +704,306 @@ __global__ __launch_bounds__(kSLThreads) __attribute__((amdgpu_waves_per_eu(C <=
     }
 }
 
+// Depth range of the sweep, reduced by one wave: min, max, and whether any depth is not
+// finite (every lane gets the result).
+__device__ __forceinline__ void sweep_depth_range(const float* __restrict__ depths, int D, int lane, float& dmin,
+                                                  float& dmax, float& dbad) {
+    dmin = __builtin_inff();
+    dmax = -__builtin_inff();
+    dbad = 0.0f;
+    for (int i = lane; i < D; i += kWave) {
+        const float d = depths[i];
+        dmin = fminf(dmin, d);
+        dmax = fmaxf(dmax, d);
+        dbad = __builtin_isfinite(d) ? dbad : 1.0f;
+    }
+#pragma unroll
+    for (int k = 1; k < kWave; k <<= 1) {
+        dmin = fminf(dmin, __shfl_xor(dmin, k));
+        dmax = fmaxf(dmax, __shfl_xor(dmax, k));
+        dbad = fmaxf(dbad, __shfl_xor(dbad, k));
+    }
+}
+
+// A tile's staged source box and its two flags, computed by one wave (lanes 0..7 are the
+// 8 vertices; lane 0 holds the result).
+struct SweepBox {
+    int xl, yl, rows, pitch;  // pitch 0: gather every sample from global memory
+    int fast;                 // every sample of the tile is in div2_rn's fast range
+    int zero;                 // every tap of the tile lies outside the source image
+};
+
+__device__ __forceinline__ SweepBox sweep_tile_box(const float* __restrict__ k9, const float* __restrict__ m,
+                                                   const SweepParams& sp, float rc_hs, float rc_ws, int x0, int y0,
+                                                   int np, int nr, float dmin, float dmax, float dbad, int shrink,
+                                                   int lane) {
+    // vertex = lane % 8: (first | last pixel) x (first | last row) x (min | max depth)
+    const int vtx = lane & 7;
+    float rx, ry, rz;
+    ray(k9, (float)((vtx & 1) ? x0 + np - 1 : x0), (float)((vtx & 2) ? y0 + nr - 1 : y0), rx, ry, rz);
+    float px, py, den;
+    sweep_pos_fast(m, rx, ry, rz, (vtx & 4) ? dmax : dmin, sp, rc_hs, rc_ws, px, py, den);
+    // pu, pv and den are multi-affine in (x, y, depth): over the tile their extremes are
+    // at the 8 vertices, so vertex values a factor 2 inside div2_safe's range (room for
+    // rounding) prove the fast division exact for every sample of the tile
+    const float dep = (vtx & 4) ? dmax : dmin;
+    const float X = rx * dep, Y = ry * dep, Z = rz * dep;
+    const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+    const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+    const float ad = __builtin_fabsf(den);
+    int fastv = ad >= 0x1p-59f && ad <= 0x1p59f && __builtin_fmaxf(__builtin_fabsf(pu), __builtin_fabsf(pv)) <= 0x1p59f;
+    const bool fin = dbad == 0.0f && __builtin_isfinite(px) && __builtin_isfinite(py) && __builtin_fabsf(px) < 1e7f &&
+                     __builtin_fabsf(py) < 1e7f;
+    float xmin = floorf(px), xmax = xmin, ymin = floorf(py), ymax = ymin;
+    int pos = fin && den > 0.0f, neg = fin && den < 0.0f;
+#pragma unroll
+    for (int k = 1; k < 8; k <<= 1) {
+        xmin = fminf(xmin, __shfl_xor(xmin, k));
+        xmax = fmaxf(xmax, __shfl_xor(xmax, k));
+        ymin = fminf(ymin, __shfl_xor(ymin, k));
+        ymax = fmaxf(ymax, __shfl_xor(ymax, k));
+        pos &= __shfl_xor(pos, k);
+        neg &= __shfl_xor(neg, k);
+        fastv &= __shfl_xor(fastv, k);
+    }
+    SweepBox bx;
+    const bool ok = pos || neg;
+    bx.fast = ok && fin && fastv;
+    int xl = ok ? max((int)xmin - 1 + shrink, -2) : 0;
+    int xh = ok ? min((int)xmax + 2 - shrink, sp.Ws + 1) : 0;
+    int yl = ok ? max((int)ymin - 1 + shrink, -2) : 0;
+    int yh = ok ? min((int)ymax + 2 - shrink, sp.Hs + 1) : 0;
+    // A footprint wholly beyond one side of the image (the reference's swapped x / H
+    // normalisation sends every sample past x = 3W/4 out of a landscape source) stages the
+    // 3 columns (rows) at that edge: origins past the edge are then read exactly as the
+    // border's zeros (LdsBox's open border edges), so these tiles stay on the LDS path
+    // instead of gathering zeros from memory.
+    if (ok && xl > xh) {
+        xl = xh == sp.Ws + 1 ? sp.Ws - 1 : -2;
+        xh = xl + 2;
+    }
+    if (ok && yl > yh) {
+        yl = yh == sp.Hs + 1 ? sp.Hs - 1 : -2;
+        yh = yl + 2;
+    }
+    const int width = xh - xl + 1, rows = yh - yl + 1;
+    const bool fits = ok && width >= 2 && rows >= 2 && width <= kSLCap && rows <= kSLCap && width * rows <= kSLCap;
+    bx.xl = xl;
+    bx.yl = yl;
+    bx.rows = rows;
+    bx.pitch = fits ? width : 0;
+    // Every tap of every sample outside the image: each sample is a blend of four zero
+    // texels with finite non-negative weights, i.e. exactly +0.  Interior samples lie in
+    // the hull of the 8 vertex positions (the box argument above) up to rounding far below
+    // the one-texel margin while |coordinates| < 2^16.
+    const bool small = xmin > -65536.0f && xmax < 65536.0f && ymin > -65536.0f && ymax < 65536.0f;
+    bx.zero = ok && small && shrink == 0 &&
+              ((int)xmin - 1 >= sp.Ws || (int)xmax + 2 <= -1 || (int)ymin - 1 >= sp.Hs || (int)ymax + 2 <= -1);
+    return bx;
+}
+
+// The all-+0 output of a zero tile (NT threads of the block).
+template <int C, int NT>
+__device__ __forceinline__ void sweep_zero_tile(float* __restrict__ out, int64_t out_bstride, int64_t out_pstride,
+                                                const SweepParams& sp, int vec, int b, int x0, int y0, int np,
+                                                int nr) {
+    const int64_t run = (int64_t)np * sp.D * C;
+    for (int tr = 0; tr < nr; ++tr) {
+        float* ob = out + (int64_t)b * out_bstride + ((int64_t)(y0 + tr) * sp.Wt + x0) * out_pstride;
+        if (vec && out_pstride == (int64_t)sp.D * C && run % 4 == 0) {  // one dense 16-B-aligned run
+            f32x4* o4 = reinterpret_cast<f32x4*>(ob);
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            for (int64_t i = threadIdx.x; i < run / 4; i += NT) __builtin_nontemporal_store(z, o4 + i);
+        } else {
+            for (int64_t i = threadIdx.x; i < run; i += NT) {
+                const int pxl = (int)(i / (sp.D * C)), e = (int)(i - (int64_t)pxl * sp.D * C);
+                ob[(int64_t)pxl * out_pstride + e] = 0.0f;
+            }
+        }
+    }
+}
+
+// Register-staged box fill (the non-persistent kernel): box texel idx = row * pitch + col
+// <- padded-plane texel.
+template <int NT>
+__device__ __forceinline__ void sweep_fill_box(float4* __restrict__ s_src, __amdgpu_buffer_rsrc_t r,
+                                               const PadGeom& pg, const SweepBox& bx) {
+    constexpr int kFill = kSLCap / NT;  // staged texels per thread
+    const int nfp = bx.rows * bx.pitch;
+    const float rp = 1.0f / (float)bx.pitch;
+    const int org = (bx.yl + kPad) * pg.Wp + bx.xl + kPad;  // >= 0: boxes start at -2
+    // every slot of the staging array is written (texels past the box as zeros: the
+    // out-of-range buffer offset), so the loads and stores need no guards
+    f32x4 stg[kFill];
+#pragma unroll
+    for (int k = 0; k < kFill; ++k) {
+        const int idx = threadIdx.x + NT * k;
+        int row = (int)((float)idx * rp);  // idx < 2^12: off by at most one, corrected
+        row -= row * bx.pitch > idx ? 1 : 0;
+        row += (row + 1) * bx.pitch <= idx ? 1 : 0;
+        stg[k] = llvm_raw_buffer_load_v4f32(r, idx < nfp ? (org + row * pg.Wp + idx - row * bx.pitch) * 16 : kOOB,
+                                            0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < kFill; ++k) *reinterpret_cast<f32x4*>(&s_src[threadIdx.x + NT * k]) = stg[k];
+}
+
+
+// Depth-per-lane LDS sweep (the default when D is a multiple of 64, C <= 4).  The box
+// staging is plane_sweep_lds_kernel's, but a wave's 64 lanes are the 64 depths of ONE target
+// pixel (depth chunk), and it takes two pixels per iteration:
+//  * a lane's depth is a register (no depth table in LDS), and the pixel's D*C-float run of
+//    the volume leaves as one lane-contiguous store per 64 depths (64 x C floats): whole
+//    lines, no per-wave store slot, no LDS round trip between the blend and the store;
+//  * without the 24 KiB store slot and the depth table a block needs 48 KiB of LDS, so three
+//    blocks fit a CU, and two samples in flight per lane keep the VGPRs under 80: 6 waves per
+//    SIMD instead of 4.
+// The ray of the pixel is the same in every lane (a wave-uniform VALU value).  Per sample the
+// arithmetic is the same sequence as plane_sweep_lds_kernel's (bit-identical output).
+constexpr int kDLThreads = 512;
+constexpr int kDLWaves = kDLThreads / kWave;
+#ifndef MPIV_DLPIX
+#define MPIV_DLPIX 2
+#endif
+constexpr int kDLPix = MPIV_DLPIX;  // pixels (samples per lane) per iteration
+static_assert(kSLCap % kDLThreads == 0, "sweep_fill_box writes every staging slot");
+
+template <int C>
+__global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
+    const float4* __restrict__ img4, SweepParams sp, PadGeom pg, float rc_hs, float rc_ws,
+    const float* __restrict__ ki, const float* __restrict__ proj, const float* __restrict__ depths,
+    float* __restrict__ out, int64_t out_bstride, int64_t out_pstride, int vec, int shrink) {
+    __shared__ __attribute__((aligned(16))) float4 s_src[kSLCap];
+    __shared__ SweepBox s_box;
+
+    const int segs = (sp.Wt + kSLP - 1) / kSLP;
+    const int b = blockIdx.y;
+    const int ty = blockIdx.x / segs;
+    const int y0 = ty * kSLR, x0 = (blockIdx.x - ty * segs) * kSLP;
+    const int np = min(kSLP, sp.Wt - x0), nr = min(kSLR, sp.Ht - y0);
+    const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const float* k9 = ki + (int64_t)b * 9;
+    const float* m = proj + (int64_t)b * 16;
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(img4 + (int64_t)b * (pg.plane_bytes / 16), pg.plane_bytes);
+
+    if (wave == 0) {
+        float dmin, dmax, dbad;
+        sweep_depth_range(depths, sp.D, lane, dmin, dmax, dbad);
+        const SweepBox bx = sweep_tile_box(k9, m, sp, rc_hs, rc_ws, x0, y0, np, nr, dmin, dmax, dbad, shrink, lane);
+        if (lane == 0) s_box = bx;
+    }
+    __syncthreads();
+    SweepBox bx;
+    bx.xl = __builtin_amdgcn_readfirstlane(s_box.xl);
+    bx.yl = __builtin_amdgcn_readfirstlane(s_box.yl);
+    bx.rows = __builtin_amdgcn_readfirstlane(s_box.rows);
+    bx.pitch = __builtin_amdgcn_readfirstlane(s_box.pitch);
+    bx.fast = __builtin_amdgcn_readfirstlane(s_box.fast);
+    bx.zero = __builtin_amdgcn_readfirstlane(s_box.zero);
+    if (bx.zero) {  // the tile's output is all +0: store it
+        sweep_zero_tile<C, kDLThreads>(out, out_bstride, out_pstride, sp, vec, b, x0, y0, np, nr);
+        return;
+    }
+    if (bx.pitch > 0) sweep_fill_box<kDLThreads>(s_src, r, pg, bx);
+    __syncthreads();
+
+    const int pitch = bx.pitch;
+    const bool all_fast = bx.fast != 0;
+    const LdsBox lbx = make_lds_box(bx.xl, bx.yl, bx.rows, pitch, sp.Ws, sp.Hs);
+    const int nchunk = sp.D / kWave;  // D % 64 == 0 (host)
+    typedef float f32xC __attribute__((ext_vector_type(C), aligned(4)));
+    // (tile row, 64-depth chunk, pixel pair) loops, all wave-uniform and division-free (the
+    // scalar unit is shared by the CU's waves: integer divisions per item measured 3x the SALU)
+    for (int tr = 0; tr < nr; ++tr)
+    for (int ch = 0; ch < nchunk; ++ch) {
+    const float dq = depths[ch * kWave + lane];
+    float* orow = out + (int64_t)b * out_bstride + ((int64_t)(y0 + tr) * sp.Wt + x0) * out_pstride +
+                  (int64_t)(ch * kWave + lane) * C;
+    for (int p0 = wave * kDLPix; p0 < np; p0 += kDLWaves * kDLPix) {
+        float px[kDLPix], py[kDLPix], rxs[kDLPix], rys[kDLPix], rzs[kDLPix], dep[kDLPix];
+        float* o[kDLPix];
+        bool live[kDLPix];
+#pragma unroll
+        for (int j = 0; j < kDLPix; ++j) {
+            live[j] = p0 + j < np;
+            const int pl = min(p0 + j, np - 1);  // a missing last pixel repeats the previous one (not stored)
+            ray(k9, (float)(x0 + pl), (float)(y0 + tr), rxs[j], rys[j], rzs[j]);  // pixel2cam_torch, utils.py:370
+            dep[j] = dq;
+            o[j] = orow + (int64_t)pl * out_pstride;
+        }
+        float su[kDLPix], sv[kDLPix];
+        bool fast = true;
+#pragma unroll
+        for (int j = 0; j < kDLPix; ++j) {
+            const float X = rxs[j] * dep[j], Y = rys[j] * dep[j], Z = rzs[j] * dep[j];
+            const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+            const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+            const float den = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11] + 1e-10f;
+            if (!all_fast) fast = fast && div2_safe(pu, pv, den);
+            div2_fast(pu, pv, den, su[j], sv[j]);  // cam2pixel_torch, utils.py:388-391
+        }
+        if (__builtin_amdgcn_ballot_w64(!fast)) {  // rare: a quotient outside the fast path's range
+#pragma unroll
+            for (int j = 0; j < kDLPix; ++j) {
+                const float X = rxs[j] * dep[j], Y = rys[j] * dep[j], Z = rzs[j] * dep[j];
+                const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+                const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+                const float den = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11] + 1e-10f;
+                if (!div2_safe(pu, pv, den)) {
+                    su[j] = div_rn(pu, den);
+                    sv[j] = div_rn(pv, den);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kDLPix; ++j) {
+            const float cx = div_const(su[j] + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
+            const float cy = div_const(sv[j] + 0.5f, sp.fws, rc_ws);  //          y / W
+            px[j] = unnormalize(to_grid(cx), sp.half_ws);
+            py[j] = unnormalize(to_grid(cy), sp.half_hs);
+        }
+        f32x4 s[kDLPix];
+        bool staged = pitch > 0;
+        if (staged) {  // 16-B tap reads (ds_read_b128: 4 LDS cycles, ds_read_b96 8)
+            TapSet ts[kDLPix];
+#pragma unroll
+            for (int j = 0; j < kDLPix; ++j) staged = lds_issue(s_src, lbx, px[j], py[j], ts[j]) && staged;
+#pragma unroll
+            for (int j = 0; j < kDLPix; ++j) s[j] = blend_taps(ts[j]);
+            // the unused channels' registers stay allocated until the reads are consumed
+            // (else a WAW wait serialises the reads)
+#pragma unroll
+            for (int j = 0; j < kDLPix; ++j)
+                asm volatile("" ::"v"(ts[j].a), "v"(ts[j].b), "v"(ts[j].c), "v"(ts[j].d));
+        }
+        if (__builtin_amdgcn_ballot_w64(!staged)) {  // wave-uniform test, then per lane
+            if (!staged) {                            // a tap origin not staged: gather from global memory
+#pragma unroll
+                for (int j = 0; j < kDLPix; ++j) {
+                    TapSet ts;
+                    issue_taps_padded(r, sp.Ws, sp.Hs, pg.Wp, pg.org, pg.row, px[j], py[j], ts);
+                    s[j] = blend_taps(ts);
+                    asm volatile("" ::: "memory");
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kDLPix; ++j) {
+            if (live[j]) {  // wave-uniform
+                f32xC v;
+#pragma unroll
+                for (int c = 0; c < C; ++c) v[c] = s[j][c];
+                if (vec) __builtin_nontemporal_store(v, reinterpret_cast<f32xC*>(o[j]));
+                else {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) o[j][c] = v[c];
+                }
+            }
+        }
+    }
+    }
+}
+
 // projective_inverse_warp_torch[2] with a per-pixel depth map [B, Ht, Wt] (any
 // strides) -> [B, Ht, Wt, C]
 __global__ __launch_bounds__(256) void inverse_warp_kernel(const float* __restrict__ img, ImgStrides s,

@@ -58,8 +58,11 @@ def test_inverse_warp_single_depth(small, meta, dev):
     assert_bits(out.cpu().numpy(), small["psv_a_out"][..., 6:9])
 
 
-def test_plane_sweep_c3(large, meta, dev):
-    """Config 3: 5 x 1024x768 sources -> 64 planes (the full [5,768,1024,192] volume)."""
+@pytest.mark.parametrize("dlane", ["1", "0"])
+def test_plane_sweep_c3(dlane, large, meta, dev, kopts):
+    """Config 3: 5 x 1024x768 sources -> 64 planes (the full [5,768,1024,192] volume), through
+    the depth-per-lane LDS kernel (default for D % 64 == 0) and the pixel-per-lane one."""
+    kopts(sweep_dlane=dlane)
     c3 = configs.config3()
     g = torch.Generator().manual_seed(c3["seed"])
     img = torch.rand((c3["S"], c3["H"], c3["W"], 3), generator=g, dtype=torch.float32)
@@ -274,3 +277,65 @@ def test_inverse_warp2_depth_map_vs_reference(warp, dev):
     Ht, Wt = (int(v) for v in warp["piw2_tgt"])
     out = mv.projective_inverse_warp_torch2(t["img"], t["depth"], t["pose"], t["Ks"], t["Kt"], Ht, Wt)
     assert_bits(out, warp["piw2_out"], "piw2")
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 4])
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("shrink", ["0", "3"])
+def test_plane_sweep_depth_lanes_vs_oracle(C, D, shrink, dev, kopts):
+    """The depth-per-lane LDS kernel (D a multiple of 64: one or two 64-depth chunks per
+    pixel), odd target sizes (a partial last 64-pixel segment and 4-row tile, an odd number
+    of (pixel, chunk) items per block), separate source / target intrinsics; also with
+    shrunk boxes (most samples through its global fallback): bit-exact to the oracle."""
+    from mpi_vision_amd import _host, _lib
+    from oracle import oracle
+    kopts(box_shrink=shrink)
+    g = torch.Generator().manual_seed(140 + C + D)
+    B, Hs, Ws, Ht, Wt = 2, 41, 89, 23, 75
+    img = torch.rand((B, Hs, Ws, C), generator=g)
+    Ks = configs.f32([configs.intrinsics_matrix(55.0, 57.0, 44.0, 20.0)] * B)
+    Kt = configs.f32([configs.intrinsics_matrix(50.0, 49.0, 37.0, 11.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(2.5 * k - 1.0), (0.15 * k - 0.08, 0.02, -0.01))
+                         for k in range(B)])
+    depths = configs.inv_depths(0.9, 50, D)
+    ki, proj = _host.psv_matrices(Ks, Kt, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Ht, Wt)
+    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Ht, Wt)
+    assert_bits(out.cpu().numpy(), want, f"C={C} D={D} shrink={shrink}")
+
+
+@pytest.mark.parametrize("C", [3, 4])
+def test_plane_sweep_depth_lanes_off_image(C, dev):
+    """Depth-per-lane kernel on landscape sources with footprints wholly off the image (zero
+    tiles and border-collapsed boxes), D = 64: bit-exact to the oracle, zeros included."""
+    from mpi_vision_amd import _host, _lib
+    from oracle import oracle
+    g = torch.Generator().manual_seed(177 + C)
+    B, Hs, Ws, D = 3, 60, 160, 64
+    img = torch.rand((B, Hs, Ws, C), generator=g) + 0.5
+    K = configs.f32([configs.intrinsics_matrix(150.0, 150.0, 80.0, 30.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(0.5), (0.1, 0.01, 0.0)),
+                         configs.pose_from(configs.rot_y(-20.0), (1.5, 0.2, 0.1)),
+                         configs.pose_from(configs.rot_y(40.0), (-2.0, -0.5, 0.3))])
+    depths = configs.inv_depths(1, 50, D)
+    ki, proj = _host.psv_matrices(K, K, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Hs, Ws)
+    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Hs, Ws)
+    assert_bits(out.cpu().numpy(), want, f"C={C}")
+    assert (want == 0).mean() > 0.2
+
+
+def test_format_network_input_depth_lanes_strided(small, dev, kopts):
+    """format_network_input_torch with 64 planes: every source swept by the depth-per-lane
+    kernel straight into its channel slice of the network input (strided output rows),
+    bit-identical to the pixel-per-lane kernel (itself pinned by the reference golden of
+    test_format_network_input)."""
+    t = {k: torch.tensor(small[f"fni_{k}"]).to(dev) for k in ("ref", "src", "ref_pose", "src_poses", "K")}
+    planes = configs.inv_depths(1.0, 100.0, 64)
+    outs = []
+    for dl in ("1", "0"):
+        kopts(sweep_dlane=dl)
+        outs.append(mv.format_network_input_torch(None, t["ref"], t["src"], t["ref_pose"], t["src_poses"], planes,
+                                                  t["K"]).cpu().numpy())
+    assert outs[0].shape == outs[1].shape
+    assert_bits(outs[0], outs[1])

@@ -123,7 +123,10 @@ def c3(dev, it, wu):
     ms, mn = timed(lambda: out.fill_(1.0), it, wu)
     report(f"c3 write-bandwidth reference: torch fill_ of the {S}x{H}x{W}x{D * 3} volume", ms, mn,
            S * D * H * W * 12)
-    for label, opts in (("LDS-staged kernel (default)", {}), ("tile kernel", {"sweep_tile": 1}),
+    for label, opts in (("pixel-per-lane LDS kernel (warm-up)", {"sweep_dlane": 0}),
+                        ("depth-per-lane LDS kernel (default)", {}), ("pixel-per-lane LDS kernel", {"sweep_dlane": 0}),
+                        ("depth-per-lane LDS kernel (default), again", {}),
+                        ("pixel-per-lane LDS kernel, again", {"sweep_dlane": 0}), ("tile kernel", {"sweep_tile": 1}),
                         ("grouped kernel, store mode 1", {"sweep_store": 1}),
                         ("grouped kernel, store mode 2", {"sweep_store": 2})):
         with _lib.debug(**opts):

@@ -3,7 +3,7 @@
 
     python tools/pmc_sweep.py [--store lds|tile|0|1|2] [--iters 3]
 
-lds = the default LDS-staged kernel, tile = the tile kernel, 0/1/2 = the grouped
+lds = the default LDS-staged kernel, pixlane = the pixel-per-lane LDS kernel, tile = the tile kernel, 0/1/2 = the grouped
 kernel's store modes.
 """
 import argparse
@@ -20,7 +20,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--store", default="lds")
 ap.add_argument("--iters", type=int, default=3)
 a = ap.parse_args()
-if a.store == "tile":
+if a.store == "pixlane":
+    _lib.load().mpiv_debug_set(b"sweep_dlane", 0)
+elif a.store == "tile":
     _lib.load().mpiv_debug_set(b"sweep_tile", 1)
 elif a.store != "lds":
     _lib.load().mpiv_debug_set(b"sweep_store", int(a.store))

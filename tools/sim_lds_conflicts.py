@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--tiles", type=int, default=300)
     ap.add_argument("--pad", type=int, default=-1, help="pad the box pitch to = PAD mod 16")
     ap.add_argument("--only", default="")
+    ap.add_argument("--depth-lanes", action="store_true", help="also model lanes = the 64 depths of one pixel")
     a = ap.parse_args()
     c = configs.config3()
     S, H, W, D = c["S"], c["H"], c["W"], c["D"]
@@ -64,6 +65,7 @@ def main():
     rng = np.random.default_rng(0)
     maps = {k: v for k, v in mappings().items() if a.only in k}
     tot = {k: 0 for k in maps}
+    dninst, dcyc = [0], [0]
     ninst = 0
     for s in range(S):
         pose = np.array(c["poses"][s], np.float64)
@@ -94,6 +96,19 @@ def main():
                 pitch += (a.pad - pitch) % 16
             cx, cy = np.clip(fx - xl, 0, None), np.clip(fy - yl, 0, None)
             t = (cy * pitch + cx).astype(np.int64)  # NW tap texel, [D, 4, 64]
+            if a.depth_lanes:
+                for r in range(4):
+                    for x in range(64):
+                        for tap in (0, 1, pitch, pitch + 1):
+                            dninst[0] += 1
+                            cyc = 0
+                            for lanes in G128:
+                                slots = {}
+                                for l in lanes:
+                                    tt = int(t[l, r, x]) + tap
+                                    slots.setdefault(tt % 16, set()).add(tt)
+                                cyc += max(len(v) for v in slots.values())
+                            dcyc[0] += cyc
             for r in range(4):
                 for blk in range(4):
                     for dg0 in range(0, D // 4, 4):
@@ -112,6 +127,8 @@ def main():
                                     tot[name] += cyc
     for name, cyc in tot.items():
         print(f"{name:45s} {cyc / ninst:6.3f} LDS cycles per b128 tap read (4 = conflict-free)")
+    if a.depth_lanes:
+        print(f"{'lanes = 64 depths of one pixel':45s} {dcyc[0] / dninst[0]:6.3f} LDS cycles per b128 tap read")
 
 
 if __name__ == "__main__":
