@@ -60,8 +60,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (render_rows_kernel; 100+R: state in LDS, render_rows_lds_kernel);
 //                      -1: off (one row per work-item), 0: automatic (R = 8 where it pays)
 //   sweep_tile=1       the sweep uses the tile kernel; sweep_store=k (k >= 0) the grouped one
-//   sweep_dlane=0      sweeps with D % 64 == 0 use the pixel-per-lane LDS kernel instead of the
-//                      depth-per-lane one (plane_sweep_dlane_kernel)
+//   sweep_dlane=0      the LDS sweep runs pixel-per-lane (plane_sweep_lds_kernel) instead of
+//                      depth-per-lane (plane_sweep_dlane_kernel)
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
 //                      forces their per-sample global fallback (tests)
 //   bwd_fallback=1     mpiv_render_backward skips the tile gather and runs its bucket
@@ -598,7 +598,9 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
     int store = dense ? 2 : vec ? 1 : 0;
     const int o_store = opt(kOptSweepStore);  // A/B only: the grouped kernel's store modes
     const bool grouped = o_store >= 0;
-    const bool tile = !grouped && (opt(kOptSweepTile) || D > kSweepMaxLdsD);
+    // the depth-per-lane kernel reads the depths from global memory (any D); the pixel-per-lane
+    // one stages them in LDS (D <= kSweepMaxLdsD, else the tile kernel)
+    const bool tile = !grouped && (opt(kOptSweepTile) || (D > kSweepMaxLdsD && opt(kOptSweepDlane) == 0));
     if (grouped) store = min(store, o_store);
     hipStream_t q = S(stream);
     if (!grouped && !tile) {
@@ -608,7 +610,7 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
         const dim3 lgrid((unsigned)tiles, B, 1);
         const int shrink = opt(kOptBoxShrink);
         const FastDiv fd_b = make_fastdiv((unsigned)(16 * NG));
-        if (D % kWave == 0 && opt(kOptSweepDlane) != 0) {
+        if (opt(kOptSweepDlane) != 0) {
 #define MPIV_DLANE(CC)                                                                                           \
     plane_sweep_dlane_kernel<CC><<<lgrid, kDLThreads, 0, q>>>(im, sp, pg, rc_hs, rc_ws, ki, proj, depths, out,   \
                                                               out_bstride, out_pstride, (int)vec, shrink)

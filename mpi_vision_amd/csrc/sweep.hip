@@ -910,23 +910,35 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     const int pitch = bx.pitch;
     const bool all_fast = bx.fast != 0;
     const LdsBox lbx = make_lds_box(bx.xl, bx.yl, bx.rows, pitch, sp.Ws, sp.Hs);
-    const int nchunk = sp.D / kWave;  // D % 64 == 0 (host)
+    // Lane -> (pixel of the wave's group, depth).  D <= 64: a group is ppw = 64 / D consecutive
+    // pixels and lane l takes pixel l / D, depth l % D (lanes past ppw * D idle), so the group's
+    // ppw * D * C floats are one contiguous run of the dense volume.  D > 64: a group is one
+    // pixel and the depths go in chunks of 64 (the last one partial).
+    const int D = sp.D;
+    const int ppw = D <= kWave ? kWave / D : 1;
+    const int lp = D <= kWave ? lane / D : 0;             // the lane's pixel within its group
+    const int ld = D <= kWave ? lane - lp * D : lane;     // the lane's depth within its chunk
+    const int nchunk = (D + kWave - 1) / kWave;
+    const int ngroup = (np + ppw - 1) / ppw;              // pixel groups per tile row
     typedef float f32xC __attribute__((ext_vector_type(C), aligned(4)));
-    // (tile row, 64-depth chunk, pixel pair) loops, all wave-uniform and division-free (the
-    // scalar unit is shared by the CU's waves: integer divisions per item measured 3x the SALU)
+    // (tile row, depth chunk, pair of pixel groups) loops, wave-uniform and free of integer
+    // divisions (the scalar unit is shared by the CU's waves: per-item divisions measured 3x
+    // the SALU instructions)
     for (int tr = 0; tr < nr; ++tr)
     for (int ch = 0; ch < nchunk; ++ch) {
-    const float dq = depths[ch * kWave + lane];
-    float* orow = out + (int64_t)b * out_bstride + ((int64_t)(y0 + tr) * sp.Wt + x0) * out_pstride +
-                  (int64_t)(ch * kWave + lane) * C;
-    for (int p0 = wave * kDLPix; p0 < np; p0 += kDLWaves * kDLPix) {
+    const int dl = ch * kWave + ld;
+    const bool dlive = (D <= kWave ? lane < ppw * D : dl < D);
+    const float dq = depths[min(dl, D - 1)];
+    float* orow = out + (int64_t)b * out_bstride + ((int64_t)(y0 + tr) * sp.Wt + x0) * out_pstride + (int64_t)dl * C;
+    for (int g0 = wave * kDLPix; g0 < ngroup; g0 += kDLWaves * kDLPix) {
         float px[kDLPix], py[kDLPix], rxs[kDLPix], rys[kDLPix], rzs[kDLPix], dep[kDLPix];
         float* o[kDLPix];
         bool live[kDLPix];
 #pragma unroll
         for (int j = 0; j < kDLPix; ++j) {
-            live[j] = p0 + j < np;
-            const int pl = min(p0 + j, np - 1);  // a missing last pixel repeats the previous one (not stored)
+            const int pix = (g0 + j) * ppw + lp;
+            live[j] = dlive && g0 + j < ngroup && pix < np;
+            const int pl = min(pix, np - 1);  // idle lanes recompute the last pixel (not stored)
             ray(k9, (float)(x0 + pl), (float)(y0 + tr), rxs[j], rys[j], rzs[j]);  // pixel2cam_torch, utils.py:370
             dep[j] = dq;
             o[j] = orow + (int64_t)pl * out_pstride;
@@ -989,7 +1001,7 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
         }
 #pragma unroll
         for (int j = 0; j < kDLPix; ++j) {
-            if (live[j]) {  // wave-uniform
+            if (live[j]) {
                 f32xC v;
 #pragma unroll
                 for (int c = 0; c < C; ++c) v[c] = s[j][c];

@@ -130,14 +130,15 @@ def test_plane_sweep_many_depths_vs_oracle(dev):
 
 @pytest.mark.parametrize("C", [1, 2, 3, 4])
 @pytest.mark.parametrize("shrink", ["0", "3"])
-def test_plane_sweep_lds_vs_oracle(C, shrink, dev, kopts):
+@pytest.mark.parametrize("dlane", ["1", "0"])
+def test_plane_sweep_lds_vs_oracle(C, shrink, dlane, dev, kopts):
     """The LDS-staged sweep with C = 1 and 4, a target size whose rows end in a partial
     64-pixel segment, separate source / target intrinsics and sizes (the _one2 geometry):
     bit-exact to the oracle, also with every staged box shrunk (box_shrink: most
     samples take the per-sample global fallback)."""
     from mpi_vision_amd import _host, _lib
     from oracle import oracle
-    kopts(box_shrink=shrink)
+    kopts(box_shrink=shrink, sweep_dlane=dlane)
     g = torch.Generator().manual_seed(31 + C)
     B, Hs, Ws, D, Ht, Wt = 2, 45, 97, 11, 38, 131
     img = torch.rand((B, Hs, Ws, C), generator=g)
@@ -152,10 +153,13 @@ def test_plane_sweep_lds_vs_oracle(C, shrink, dev, kopts):
     assert_bits(out.cpu().numpy(), want, f"C={C} shrink={shrink}")
 
 
-def test_plane_sweep_more_depths_than_lds_table(dev):
-    """D = 1030 > the LDS depth table: the tile kernel takes over, still bit-exact."""
+@pytest.mark.parametrize("dlane", ["1", "0"])
+def test_plane_sweep_more_depths_than_lds_table(dlane, dev, kopts):
+    """D = 1030 > the pixel-per-lane kernel's LDS depth table: the depth-per-lane kernel
+    (17 chunks, default) or the tile kernel takes over, still bit-exact."""
     from mpi_vision_amd import _host, _lib
     from oracle import oracle
+    kopts(sweep_dlane=dlane)
     g = torch.Generator().manual_seed(5)
     img = torch.rand((1, 9, 13, 3), generator=g)
     K = configs.f32([configs.intrinsics_matrix(12.0, 12.5, 6.0, 4.0)])
@@ -226,12 +230,14 @@ def test_plane_sweep_empty_inputs_raise_like_reference(dev):
 
 
 @pytest.mark.parametrize("C", [1, 2, 3, 4])
-def test_plane_sweep_pixel_interleaved_store_all_channels(C, dev):
+@pytest.mark.parametrize("dlane", ["0", "1"])
+def test_plane_sweep_pixel_interleaved_store_all_channels(C, dlane, dev, kopts):
     """Whole 16-pixel blocks and whole sets of 4 depth groups (Wt % 64 == 0, D % 16 == 0):
     the LDS kernel's pixel-interleaved order and its swizzled per-wave store slot (a
     different row rotation for C = 3 than for C = 1, 2, 4), bit-exact to the oracle."""
     from mpi_vision_amd import _host, _lib
     from oracle import oracle
+    kopts(sweep_dlane=dlane)  # 0: the pixel-per-lane kernel's pixel-interleaved store path
     g = torch.Generator().manual_seed(90 + C)
     B, Hs, Ws, D, Ht, Wt = 2, 40, 96, 32, 12, 128
     img = torch.rand((B, Hs, Ws, C), generator=g)
@@ -280,13 +286,13 @@ def test_inverse_warp2_depth_map_vs_reference(warp, dev):
 
 
 @pytest.mark.parametrize("C", [1, 2, 3, 4])
-@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("D", [6, 10, 16, 64, 100, 128])
 @pytest.mark.parametrize("shrink", ["0", "3"])
 def test_plane_sweep_depth_lanes_vs_oracle(C, D, shrink, dev, kopts):
-    """The depth-per-lane LDS kernel (D a multiple of 64: one or two 64-depth chunks per
-    pixel), odd target sizes (a partial last 64-pixel segment and 4-row tile, an odd number
-    of (pixel, chunk) items per block), separate source / target intrinsics; also with
-    shrunk boxes (most samples through its global fallback): bit-exact to the oracle."""
+    """The depth-per-lane LDS kernel: D <= 64 (64 // D pixels per wave slot, idle lanes when
+    D does not divide 64), D > 64 (64-depth chunks, a partial last one); odd target sizes (a
+    partial last 64-pixel segment and 4-row tile), separate source / target intrinsics; also
+    with shrunk boxes (most samples through its global fallback): bit-exact to the oracle."""
     from mpi_vision_amd import _host, _lib
     from oracle import oracle
     kopts(box_shrink=shrink)

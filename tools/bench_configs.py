@@ -133,6 +133,16 @@ def c3(dev, it, wu):
             ms, mn = timed(sweep, it, wu)
         report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, {label}", ms, mn, alg,
                extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
+    # the notebook's dataset PSV: 10 planes (inv_depths(1, 100, 10), ipynb cell 8 L73)
+    d10 = configs.f32(configs.inv_depths(1, 100, 10)).to(dev)
+    out10 = torch.empty((S, H, W, 10 * 3), device=dev)
+    sweep10 = lambda: _lib._call("mpiv_plane_sweep_padded", img4, S, H, W, 3, ki, proj, d10, 10, H, W, out10,  # noqa: E731
+                                 _lib._stream(dev))
+    alg10 = S * H * W * 12 + S * 10 * H * W * 12
+    for label, opts in (("depth-per-lane (default)", {}), ("pixel-per-lane", {"sweep_dlane": 0})):
+        with _lib.debug(**opts):
+            ms, mn = timed(sweep10, it, wu)
+        report(f"c3 sources, 10 planes (notebook dataset PSV), {label}", ms, mn, alg10)
     ms, mn = timed(lambda: (pad(), sweep()), it, wu)
     report("c3 PSV plane_sweep_torch path (pad + padded kernel)", ms, mn, alg,
            extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
