@@ -60,6 +60,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (render_rows_kernel; 100+R: state in LDS, render_rows_lds_kernel);
 //                      -1: off (one row per work-item), 0: automatic (R = 8 where it pays)
 //   sweep_tile=1       the sweep uses the tile kernel; sweep_store=k (k >= 0) the grouped one
+//   render_vshare=-1|0|1  render_rows_kernel (R = 8) without / automatic (>= 3 views) / with
+//                      vertical tap reuse
 //   sweep_dlane=0      the LDS sweep runs pixel-per-lane (plane_sweep_lds_kernel) instead of
 //                      depth-per-lane (plane_sweep_dlane_kernel)
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
@@ -73,12 +75,13 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 // launches is a test-harness race on which kernel runs, never on memory.
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
-                kNumOpts };
+                kOptRenderVshare, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
-                                         "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1};
+                                         "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
+                                         "render_vshare"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -297,7 +300,12 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     const float sxr = (float)W / (float)(H > 1 ? H - 1 : 1), syr = (float)H / (float)(W > 1 ? W - 1 : 1);
     const bool square = sxr >= 0.8f && sxr <= 1.25f && syr >= 0.8f && syr <= 1.25f;
     const int rows_opt = opt(kOptRenderTile);
-    const int rows_auto = (square && (V <= 2 || V >= 32) && !opt(kOptRenderMv) && !opt(kOptRenderPair)) ? 8 : 0;
+    // R = 8 with vertical tap reuse from three views per launch up (the texture path, not HBM,
+    // binds there: 125 views 28.0 vs 30.7 ms, 8 views 1.98 vs 2.33 for the one-row kernel); at one
+    // or two views (HBM-bound) the reuse's extra dependency costs (0.51 vs 0.46 ms)
+    const int rows_auto = (square && !opt(kOptRenderMv) && !opt(kOptRenderPair)) ? 8 : 0;
+    const int vs_opt = opt(kOptRenderVshare);
+    const bool vs_auto = V >= 3;
     const int rows_sel = fast ? (rows_opt ? rows_opt : rows_auto) : 0;
     if (const int rows = rows_sel; rows == 108 || rows == 116 || rows == 132) {
         // R rows with the compositing state in LDS (render_rows_lds_kernel)
@@ -323,9 +331,17 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
         render_rows_kernel<true, R><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out); \
     else                                                                                                          \
         render_rows_kernel<false, R><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out)
+        const bool vs = vs_opt > 0 || (vs_opt == 0 && vs_auto && !rows_opt);
         if (rows == 2) MPIV_ROWS(2);
         else if (rows == 4) MPIV_ROWS(4);
-        else if (rows == 8) MPIV_ROWS(8);
+        else if (rows == 8 && vs) {
+            if (ct)
+                render_rows_kernel<true, 8, true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs,
+                                                                                 out);
+            else
+                render_rows_kernel<false, 8, true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs,
+                                                                                  out);
+        } else if (rows == 8) MPIV_ROWS(8);
         else MPIV_ROWS(16);
 #undef MPIV_ROWS
         return launched(nm);

@@ -314,6 +314,120 @@ __device__ __forceinline__ void render_rows_pixels(const float4* __restrict__ pl
     }
 }
 
+// The same with VERTICAL TAP SHARING (VS).  Along a lane's R rows the sample usually moves
+// down exactly one texel row in the same column (near-identity homographies): then row k's
+// north taps ARE row k-1's south taps, the same memory words (the clamped tap offsets are
+// compared), already in registers.  Row k always gathers its two south taps and gathers the
+// north pair only when some lane of the wave does not continue (a wave-uniform branch; lanes
+// that continue get the buffer's zero range there and take the previous row's south taps).
+// The texture path charges per wave instruction, so its work drops from 4 to ~2.5 gathers per
+// sample on a camera path; the result is bit-identical.
+template <bool CT, bool GUARD, int R>
+__device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__ planes, int64_t plane_stride,
+                                                      const RenderGeom& g, int p_begin, int p_end, int back,
+                                                      const float* __restrict__ hv, int x, int y0,
+                                                      float* cr, float* cg, float* cb, float* tt) {
+    static_assert(R % 2 == 0, "R must be even");
+    struct RowTaps {
+        f32x4 a, b, c, d;  // NW, NE (own, when not shared), SW, SE
+        float nw, ne, sw, se;
+        int off;           // byte offset of the NW tap in the padded plane
+        bool sh;           // NW, NE = the previous row's SW, SE
+        bool own;          // wave-uniform: some lane gathered its own north taps
+    };
+    const float fx = (float)x;
+    const bool replace_first = !CT || back;
+    const int last = p_end - 1;
+    auto hom = [&](int p) { return load_hom(hv + (int64_t)(p < last ? p : last) * 9); };
+    auto issue = [&](int p, int k, const Hom9& h, int prev_off, bool can_share, RowTaps& t) {
+        const int q = p < last ? p : last;
+        float px, py;
+        render_pos_fast<GUARD>(h.h, fx, (float)(y0 + k), g, px, py);
+        // issue_taps_padded's weights and clamped offset
+        const float fx0 = floorf(px), fy0 = floorf(py);
+        const float wx = px - fx0, ex = 1.0f - wx;
+        const float wy = py - fy0, sy = 1.0f - wy;
+        t.nw = sy * ex;
+        t.ne = sy * wx;
+        t.sw = wy * ex;
+        t.se = wy * wx;
+        const int cx = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)g.W);
+        const int cy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)g.H);
+        const int off = (__mul24(cy, g.Wp) + cx) * 16 + g.org;
+        t.off = off;
+        t.sh = can_share && off == prev_off + g.row;
+        const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes);
+        t.c = llvm_raw_buffer_load_v4f32(r, off, g.row, 0);
+        t.d = llvm_raw_buffer_load_v4f32(r, off + 16, g.row, 0);
+        t.a = f32x4{0.f, 0.f, 0.f, 0.f};  // defined on both paths (lets the allocator keep one register set)
+        t.b = t.a;
+        t.own = __builtin_amdgcn_ballot_w64(!t.sh) != 0;
+        if (t.own) {  // wave-uniform: some lane needs its own north taps
+            t.a = llvm_raw_buffer_load_v4f32(r, t.sh ? kOOB : off, 0, 0);
+            t.b = llvm_raw_buffer_load_v4f32(r, (t.sh ? kOOB - 16 : off) + 16, 0, 0);
+        }
+    };
+    auto consume = [&](const RowTaps& t, const f32x4& pc, const f32x4& pd, int k, bool first) {
+        f32x4 s;
+        f32x4 na = pc, nb = pd;  // every lane continues (the common case): no per-lane select
+#ifndef MPIV_VS_BRANCH
+#define MPIV_VS_BRANCH 1
+#endif
+        if (!MPIV_VS_BRANCH || t.own) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                na[c] = t.sh ? pc[c] : t.a[c];
+                nb[c] = t.sh ? pd[c] : t.b[c];
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {  // blend_taps' fma chain
+            float acc = na[c] * t.nw;
+            acc = __builtin_fmaf(nb[c], t.ne, acc);
+            acc = __builtin_fmaf(t.c[c], t.sw, acc);
+            acc = __builtin_fmaf(t.d[c], t.se, acc);
+            s[c] = acc;
+        }
+        const float a = first ? 1.0f : s[3];
+        const float om = 1.0f - a;
+        cr[k] = over(s[0], a, om, cr[k]);
+        cg[k] = over(s[1], a, om, cg[k]);
+        cb[k] = over(s[2], a, om, cb[k]);
+        if (CT) tt[k] = tt[k] * om;
+        // pin the blend here: IR passes otherwise sink it past the following rows' north-load
+        // branches, and every row's taps stay live at once (222 VGPRs)
+        asm volatile("" : "+v"(cr[k]), "+v"(cg[k]), "+v"(cb[k]));
+        if (CT) asm volatile("" : "+v"(tt[k]));
+    };
+    RowTaps A, B;
+    f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sd = sc;  // the previous row's south taps
+    Hom9 h = hom(p_begin), hn = hom(p_begin + 1);
+    issue(p_begin, 0, h, 0, false, A);
+    for (int p = p_begin; p < p_end; ++p) {
+        const bool first = replace_first && p == p_begin;
+#pragma unroll
+        for (int k = 0; k < R; k += 2) {  // A holds (p, k)
+            issue(p, k + 1, h, A.off, true, B);
+            asm volatile("" ::: "memory");  // no later row's loads above this point (IR passes hoist them
+            __builtin_amdgcn_sched_barrier(0);  // across the north-load branch otherwise: 222 VGPRs)
+            consume(A, sc, sd, k, first);
+            sc = A.c;
+            sd = A.d;
+            if (k + 2 < R)
+                issue(p, k + 2, h, B.off, true, A);
+            else
+                issue(p + 1, 0, hn, 0, false, A);  // past the end: the last plane again (cached, unused)
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            consume(B, sc, sd, k + 1, first);
+            sc = B.c;
+            sd = B.d;
+        }
+        h = hn;
+        hn = hom(p + 2);
+    }
+}
+
 // The same with the R rows' compositing state kept in LDS (rows loop not unrolled: the
 // register footprint of one sample in flight, so occupancy stays high for large R).
 // state: [R][256] float4 per block (cr, cg, cb, t).
@@ -414,7 +528,7 @@ __global__ __launch_bounds__(256) void render_rows_lds_kernel(const float4* __re
 // render_packed_kernel's contract (FAST recipe: H, W >= 2); a 256-thread block = 64 x 4R
 // tile, wave w owns rows w*R .. w*R+R-1; XCD-aware (tile, view) order, tile-level
 // division proof.
-template <bool CT, int R>
+template <bool CT, int R, bool VS = false>
 __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restrict__ planes, int64_t plane_stride,
                                                           RenderGeom g, int V, int p_begin, int p_end, int back,
                                                           const float* __restrict__ homs, float* __restrict__ out) {
@@ -449,7 +563,10 @@ __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restri
         }
         return;
     }
-    render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
+    if (VS)
+        render_rows_vs_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
+    else
+        render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const int y = y0 + k;

@@ -250,13 +250,16 @@ def test_multiview_kernel_bit_exact(shrink, dev, kopts):
 def _variant_env(kopts, mv):
     """mv "0" / "1": direct / multi-view LDS kernel; "pair" / "pair1": the pixel-pair
     tap-sharing kernel with two / one planes in flight (A/B); "ring<k>": the LDS-DMA ring
-    kernel with tile geometry k (render_ring.hip)."""
+    kernel with tile geometry k (render_ring.hip); "tile<R>": R rows per work-item
+    (render_rows_kernel), "tile8vs": with vertical tap sharing."""
     kopts(render_mv=1 if mv == "1" else 0, render_pair={"pair": 1, "pair1": 2}.get(mv, 0),
           render_ring=int(mv[4:]) if mv.startswith("ring") else -1,
-          render_tile=int(mv[4:]) if mv.startswith("tile") else -1)
+          render_tile=int(mv[4:].replace("vs", "")) if mv.startswith("tile") else -1,
+          render_vshare=1 if mv.endswith("vs") else 0)
 
 
-RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile16", "tile108", "tile116", "tile132"]
+RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile8vs", "tile16",
+        "tile108", "tile116", "tile132"]
 
 
 @pytest.mark.parametrize("variant", ["pair", "pair1"] + RING)
@@ -379,3 +382,20 @@ def test_ring_kernel_golden_cases(ring, name, small, meta, dev, kopts):
     H, W = mpi.shape[1], mpi.shape[2]
     want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.numpy())
     assert_bits(_lib.render_packed(_lib.pack_planes(mpi[0].to(dev)), homs).cpu().numpy(), want, "extreme views")
+
+
+@pytest.mark.parametrize("V", [1, 3, 40])
+def test_default_routing_square_camera_path(V, dev):
+    """Default routing on a square MPI (render_rows_kernel, R = 8; with vertical tap reuse
+    from 3 views per launch up) along the sway path, a frame height that is not a multiple
+    of the 32-row block tile: bit-exact to the oracle."""
+    from mpi_vision_amd import _host
+    H, W, P = 100, 100, 16
+    mpi = configs.synthetic_mpi(1, H, W, P, 21)
+    f = configs.focal_from_fov(W)
+    poses = configs.f32(configs.sway_path(1000)[300:300 + V])
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * V)
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(1, 100, P)), K, V)
+    want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.numpy())
+    got = _lib.render_packed(_lib.pack_planes(mpi[0].to(dev)), homs)
+    assert_bits(got.cpu().numpy(), want)

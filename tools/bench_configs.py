@@ -161,7 +161,9 @@ def c4(dev, it, wu):
         n_it = it if V < 125 else max(3, it // 4)
         for label, opts in (("default routing", {}), ("direct gathers", {"render_tile": -1}),
                             ("multi-view LDS kernel", {"render_mv": 1}),
-                            ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("rows x8 per lane", {"render_tile": 8}), ("rows x16 per lane", {"render_tile": 16})):
+                            ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("rows x8 per lane", {"render_tile": 8}),
+                            ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1}),
+                            ("rows x16 per lane", {"render_tile": 16})):
             if V == 125 and ("ring" in label or "LDS kernel" in label):
                 continue
             with _lib.debug(**opts):
@@ -257,7 +259,9 @@ def c5(dev, it, wu):
     homs_local = homs[:, :PL].contiguous().to(dev)
     ct = torch.empty((1, H, W, 4), device=dev)
     for label, opts in (("default routing", {}), ("direct gathers", {"render_tile": -1}),
-                        ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("rows x8 per lane", {"render_tile": 8}), ("rows x16 per lane", {"render_tile": 16})):
+                        ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("rows x8 per lane", {"render_tile": 8}),
+                            ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1}),
+                            ("rows x16 per lane", {"render_tile": 16})):
         with _lib.debug(**opts):
             ms, mn = timed(lambda: _lib.render_packed_ct(packed, homs_local, back=True, out=ct), it, wu)
         report(f"c5 plane shard: {PL} of {P} planes, 4096x2160 partial (C,T), {label}", ms, mn,
