@@ -194,6 +194,14 @@ int mpiv_plane_sweep(const float *img, const int64_t img_strides[4], int B, int 
                      const float *ki, const float *proj, const float *depths, int D, int Ht, int Wt,
                      float *out, void *stream);
 
+/* The same writing into a wider tensor (C <= 4): element (b, pixel, d, c) goes to
+ * out[b*out_bstride + pixel*out_pstride + d*C + c] (format_network_input_torch, utils.py:473-498,
+ * writes each source's volume at its channel offset of the concatenated network input);
+ * out_pstride >= D*C.  mpiv_plane_sweep with C <= 4 is this call with the dense strides. */
+int mpiv_plane_sweep_into(const float *img, const int64_t img_strides[4], int B, int Hs, int Ws, int C,
+                          const float *ki, const float *proj, const float *depths, int D, int Ht, int Wt,
+                          float *out, int64_t out_bstride, int64_t out_pstride, void *stream);
+
 /* Source images for the fast sweep: [B,Hs,Ws,C] (C <= 4, element strides) ->
  * img4 [B][Hs+4][Ws+4] 16-B texels (channels >= C zero) with a 2-texel zero border
  * (the packed-plane convention of mpiv_pack_planes), 16-B aligned. */

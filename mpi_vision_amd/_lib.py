@@ -50,6 +50,8 @@ _SIGS = {
     "mpiv_deprocess_u8": [_vp, _i64, _vp, _vp],
     "mpiv_render_backward": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp],
     "mpiv_render_train": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp],
+    "mpiv_plane_sweep_into": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,
+                              _vp],
     "mpiv_plane_sweep_padded_into": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,
                                      _vp],
     "mpiv_assemble_mpi": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
@@ -617,9 +619,9 @@ def _require_depths(depth_planes) -> None:
 
 def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.Tensor, tgt_h: int,
                 tgt_w: int) -> torch.Tensor:
-    """[B,Hs,Ws,C] -> PSV [B,tgt_h,tgt_w,D*C].  C <= 4: the source is padded once to
-    16-B texels with a zero border (B*(Hs+4)*(Ws+4)*16 bytes) and swept by the
-    buffer-load kernel; otherwise the generic strided kernel."""
+    """[B,Hs,Ws,C] -> PSV [B,tgt_h,tgt_w,D*C] in one launch (mpiv_plane_sweep): C <= 4 through
+    the depth-per-lane LDS kernel reading the source in place (any strides, no padded
+    copy), C > 4 through the generic strided kernel."""
     _require_depths(depth_planes)
     dev = _dev(img)
     B, Hs, Ws, C = img.shape
@@ -627,12 +629,24 @@ def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.T
     D = d.shape[0]
     out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
     kid, projd, dd = _up(ki, dev), _up(proj, dev), _up(d, dev)
-    if C <= 4 and (Hs + 4) * (Ws + 4) * 16 < 0x7FFFFF00:
-        img4 = pad_texels(img)
-        _call("mpiv_plane_sweep_padded", img4, B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out, _stream(dev))
-    else:
-        _call("mpiv_plane_sweep", img, _strides(img), B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out,
-              _stream(dev))
+    _call("mpiv_plane_sweep", img, _strides(img), B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out, _stream(dev))
+    return out
+
+
+def plane_sweep_padded(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.Tensor, tgt_h: int,
+                       tgt_w: int) -> torch.Tensor:
+    """plane_sweep through a padded 16-B texel copy of the source (mpiv_pad_texels +
+    mpiv_plane_sweep_padded; C <= 4): the pixel-per-lane / tile / grouped kernels' input
+    (A/B and tests)."""
+    _require_depths(depth_planes)
+    dev = _dev(img)
+    B, Hs, Ws, C = img.shape
+    d = torch.tensor([float(x) for x in depth_planes], dtype=torch.float32)
+    D = d.shape[0]
+    out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
+    img4 = pad_texels(img)
+    _call("mpiv_plane_sweep_padded", img4, B, Hs, Ws, C, _up(ki, dev), _up(proj, dev), _up(d, dev), D, tgt_h,
+          tgt_w, out, _stream(dev))
     return out
 
 
@@ -681,12 +695,10 @@ def network_input(ref_image, psv_src_images, rel_poses, depth_planes, intrinsics
     out = torch.empty((B, H, W, Ctot), device=dev, dtype=torch.float32)
     out[..., :3].copy_(ref_image)  # the concat's first slice is a plain copy (utils.py:491)
     dd = _up(d, dev)
-    img4 = torch.empty((B, H + 4, W + 4, 4), device=dev, dtype=torch.float32)
     for i, pose in enumerate(rel_poses):
-        src = psv_src_images[:, :, :, i * 3:(i + 1) * 3]
+        src = psv_src_images[:, :, :, i * 3:(i + 1) * 3]  # a strided channel slice, read in place
         ki, proj = psv_matrices(intrinsics, intrinsics, pose)
-        pad_texels(src, out=img4)
-        _call("mpiv_plane_sweep_padded_into", img4, B, H, W, 3, _up(ki, dev), _up(proj, dev), dd, D, H, W,
+        _call("mpiv_plane_sweep_into", src, _strides(src), B, H, W, 3, _up(ki, dev), _up(proj, dev), dd, D, H, W,
               out[..., 3 + i * D * 3:], H * W * Ctot, Ctot, _stream(dev))
     return out
 

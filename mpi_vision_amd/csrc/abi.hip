@@ -553,11 +553,58 @@ static SweepParams sweep_params(int B, int Hs, int Ws, int C, int D, int Ht, int
     return sp;
 }
 
+// plane_sweep_dlane_kernel on the caller's strided source (C <= 4): no padded copy
+static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4], int B, int Hs, int Ws, int C,
+                          const float* ki, const float* proj, const float* depths, int D, int Ht, int Wt, float* out,
+                          int64_t out_bstride, int64_t out_pstride, void* stream) {
+    if (out_pstride < (int64_t)D * C || out_pstride > (1 << 30) || out_bstride < (int64_t)Ht * Wt * out_pstride ||
+        (int64_t)Ht * Wt >= (1ll << 31))
+        return fail(MPIV_ERR_ARG, "%s: bad output strides", nm);
+    if (Hs >= (1 << 22) || Ws >= (1 << 22)) return fail(MPIV_ERR_ARG, "%s: a source side >= 2^22", nm);
+    const int64_t tiles = (int64_t)((Wt + kSLP - 1) / kSLP) * ((Ht + kSLR - 1) / kSLR);
+    if (B > kMaxGridYZ || tiles > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too large", nm);
+    const SweepParams sp = sweep_params(B, Hs, Ws, C, D, Ht, Wt);
+    const float rc_hs = 1.0f / sp.fhs, rc_ws = 1.0f / sp.fws;
+    const ImgStrides is{st[0], st[1], st[2], st[3]};
+    const bool vec = aligned16(out) && out_pstride % 4 == 0 && out_bstride % 4 == 0;
+    const dim3 lgrid((unsigned)tiles, B, 1);
+    const int shrink = opt(kOptBoxShrink);
+    hipStream_t q = S(stream);
+#define MPIV_DLRAW(CC)                                                                                         \
+    plane_sweep_dlane_kernel<CC, true><<<lgrid, kDLThreads, 0, q>>>(nullptr, PadGeom{0, 0, 0, 0}, img, is, sp, \
+                                                                    rc_hs, rc_ws, ki, proj, depths, out,       \
+                                                                    out_bstride, out_pstride, (int)vec, shrink)
+    switch (C) {
+        case 1: MPIV_DLRAW(1); break;
+        case 2: MPIV_DLRAW(2); break;
+        case 3: MPIV_DLRAW(3); break;
+        default: MPIV_DLRAW(4); break;
+    }
+#undef MPIV_DLRAW
+    return launched(nm);
+}
+
+int mpiv_plane_sweep_into(const float* img, const int64_t st[4], int B, int Hs, int Ws, int C, const float* ki,
+                          const float* proj, const float* depths, int D, int Ht, int Wt, float* out,
+                          int64_t out_bstride, int64_t out_pstride, void* stream) {
+    if (!img || !st || !ki || !proj || !depths || !out)
+        return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_into: null pointer");
+    if (B <= 0 || Hs <= 0 || Ws <= 0 || C <= 0 || C > 4 || D <= 0 || Ht <= 0 || Wt <= 0)
+        return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_into: bad shape");
+    return sweep_raw_into("mpiv_plane_sweep_into", img, st, B, Hs, Ws, C, ki, proj, depths, D, Ht, Wt, out,
+                          out_bstride, out_pstride, stream);
+}
+
 int mpiv_plane_sweep(const float* img, const int64_t st[4], int B, int Hs, int Ws, int C, const float* ki,
                      const float* proj, const float* depths, int D, int Ht, int Wt, float* out, void* stream) {
     if (!img || !st || !ki || !proj || !depths || !out) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep: null pointer");
     if (B <= 0 || Hs <= 0 || Ws <= 0 || C <= 0 || D <= 0 || Ht <= 0 || Wt <= 0)
         return fail(MPIV_ERR_ARG, "mpiv_plane_sweep: bad shape");
+    // C <= 4: the depth-per-lane LDS kernel reading the source in place (sweep_dlane=0: the
+    // generic one-sample-per-thread kernel, as for C > 4)
+    if (C <= 4 && opt(kOptSweepDlane) != 0)
+        return sweep_raw_into("mpiv_plane_sweep", img, st, B, Hs, Ws, C, ki, proj, depths, D, Ht, Wt, out,
+                              (int64_t)Ht * Wt * D * C, (int64_t)D * C, stream);
     const int64_t per_view = (int64_t)Ht * Wt * D;
     if (B > kMaxGridYZ || blocks(per_view, 256) > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep: too large");
     const ImgStrides s{st[0], st[1], st[2], st[3]};
@@ -627,9 +674,10 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
         const int shrink = opt(kOptBoxShrink);
         const FastDiv fd_b = make_fastdiv((unsigned)(16 * NG));
         if (opt(kOptSweepDlane) != 0) {
-#define MPIV_DLANE(CC)                                                                                           \
-    plane_sweep_dlane_kernel<CC><<<lgrid, kDLThreads, 0, q>>>(im, sp, pg, rc_hs, rc_ws, ki, proj, depths, out,   \
-                                                              out_bstride, out_pstride, (int)vec, shrink)
+#define MPIV_DLANE(CC)                                                                                          \
+    plane_sweep_dlane_kernel<CC, false><<<lgrid, kDLThreads, 0, q>>>(im, pg, nullptr, ImgStrides{0, 0, 0, 0}, sp, \
+                                                                     rc_hs, rc_ws, ki, proj, depths, out,          \
+                                                                     out_bstride, out_pstride, (int)vec, shrink)
             switch (C) {
                 case 1: MPIV_DLANE(1); break;
                 case 2: MPIV_DLANE(2); break;

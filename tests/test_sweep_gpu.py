@@ -84,17 +84,24 @@ def test_format_network_input(small, dev):
     assert_bits(out.cpu().numpy(), small["fni_out"])
 
 
-@pytest.mark.parametrize("store", [None, "shrink", "tile", "0", "1", "2"])
-def test_plane_sweep_store_modes(store, small, meta, dev, kopts):
-    """The LDS-staged sweep (default; "shrink" forces its per-sample global fallback),
-    the tile kernel, and every output-store path of the grouped kernel (scalar, 16-B per
-    lane, LDS-staged dense run; debug option sweep_store selects it) give the reference bits,
-    incl. a partial last depth group (D = 6, 5)."""
-    if store == "shrink":
+@pytest.mark.parametrize("store", [None, "shrink", "padded", "pixlane", "pixlane-shrink", "tile", "0", "1", "2"])
+def test_plane_sweep_store_modes(store, small, meta, dev, kopts, monkeypatch):
+    """Every sweep kernel through the drop-ins gives the reference bits, incl. a partial last
+    depth group (D = 6, 5): the default depth-per-lane kernel on the source in place ("shrink"
+    forces its per-sample global fallback) and, on a padded texel copy (the drop-ins routed
+    through _lib.plane_sweep_padded), the same kernel, the pixel-per-lane LDS kernel, the tile
+    kernel and every output-store path of the grouped kernel (scalar, 16-B per lane,
+    LDS-staged dense run; debug option sweep_store)."""
+    from mpi_vision_amd import _lib
+    if store not in (None, "shrink"):
+        monkeypatch.setattr(_lib, "plane_sweep", _lib.plane_sweep_padded)
+    if store in ("shrink", "pixlane-shrink"):
         kopts(box_shrink=2)
+    if store in ("pixlane", "pixlane-shrink"):
+        kopts(sweep_dlane=0)
     elif store == "tile":
         kopts(sweep_tile=1)
-    elif store is not None:
+    elif store in ("0", "1", "2"):
         kopts(sweep_store=store)
     img = psv_case_input(meta["small"], "psv_a")
     out = mv.plane_sweep_torch(img.to(dev), list(small["psv_a_depths"]), _t(small, "psv_a_pose", dev),
@@ -130,15 +137,15 @@ def test_plane_sweep_many_depths_vs_oracle(dev):
 
 @pytest.mark.parametrize("C", [1, 2, 3, 4])
 @pytest.mark.parametrize("shrink", ["0", "3"])
-@pytest.mark.parametrize("dlane", ["1", "0"])
-def test_plane_sweep_lds_vs_oracle(C, shrink, dlane, dev, kopts):
+@pytest.mark.parametrize("path", ["raw", "padded", "pixlane"])
+def test_plane_sweep_lds_vs_oracle(C, shrink, path, dev, kopts):
     """The LDS-staged sweep with C = 1 and 4, a target size whose rows end in a partial
     64-pixel segment, separate source / target intrinsics and sizes (the _one2 geometry):
     bit-exact to the oracle, also with every staged box shrunk (box_shrink: most
     samples take the per-sample global fallback)."""
     from mpi_vision_amd import _host, _lib
     from oracle import oracle
-    kopts(box_shrink=shrink, sweep_dlane=dlane)
+    kopts(box_shrink=shrink, sweep_dlane=0 if path == "pixlane" else 1)
     g = torch.Generator().manual_seed(31 + C)
     B, Hs, Ws, D, Ht, Wt = 2, 45, 97, 11, 38, 131
     img = torch.rand((B, Hs, Ws, C), generator=g)
@@ -149,8 +156,9 @@ def test_plane_sweep_lds_vs_oracle(C, shrink, dlane, dev, kopts):
     depths = configs.inv_depths(0.8, 40, D)
     ki, proj = _host.psv_matrices(Ks, Kt, poses)
     want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Ht, Wt)
-    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Ht, Wt)
-    assert_bits(out.cpu().numpy(), want, f"C={C} shrink={shrink}")
+    sweep = _lib.plane_sweep if path == "raw" else _lib.plane_sweep_padded
+    out = sweep(img.to(dev), depths, ki, proj, Ht, Wt)
+    assert_bits(out.cpu().numpy(), want, f"C={C} shrink={shrink} {path}")
 
 
 @pytest.mark.parametrize("dlane", ["1", "0"])
@@ -167,7 +175,8 @@ def test_plane_sweep_more_depths_than_lds_table(dlane, dev, kopts):
     depths = configs.inv_depths(0.5, 50, 1030)
     ki, proj = _host.psv_matrices(K, K, pose)
     want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, 9, 13)
-    assert_bits(_lib.plane_sweep(img.to(dev), depths, ki, proj, 9, 13).cpu().numpy(), want)
+    sweep = _lib.plane_sweep if dlane == "1" else _lib.plane_sweep_padded
+    assert_bits(sweep(img.to(dev), depths, ki, proj, 9, 13).cpu().numpy(), want)
 
 
 @pytest.mark.parametrize("C", [3, 4])
@@ -237,7 +246,7 @@ def test_plane_sweep_pixel_interleaved_store_all_channels(C, dlane, dev, kopts):
     different row rotation for C = 3 than for C = 1, 2, 4), bit-exact to the oracle."""
     from mpi_vision_amd import _host, _lib
     from oracle import oracle
-    kopts(sweep_dlane=dlane)  # 0: the pixel-per-lane kernel's pixel-interleaved store path
+    kopts(sweep_dlane=dlane)  # 0: the pixel-per-lane kernel's pixel-interleaved store path (padded input)
     g = torch.Generator().manual_seed(90 + C)
     B, Hs, Ws, D, Ht, Wt = 2, 40, 96, 32, 12, 128
     img = torch.rand((B, Hs, Ws, C), generator=g)
@@ -248,7 +257,7 @@ def test_plane_sweep_pixel_interleaved_store_all_channels(C, dlane, dev, kopts):
     depths = configs.inv_depths(1.0, 40, D)
     ki, proj = _host.psv_matrices(Ks, Kt, poses)
     want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Ht, Wt)
-    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Ht, Wt)
+    out = (_lib.plane_sweep_padded if dlane == "0" else _lib.plane_sweep)(img.to(dev), depths, ki, proj, Ht, Wt)
     assert_bits(out.cpu().numpy(), want, f"C={C}")
 
 
@@ -333,15 +342,22 @@ def test_plane_sweep_depth_lanes_off_image(C, dev):
 
 def test_format_network_input_depth_lanes_strided(small, dev, kopts):
     """format_network_input_torch with 64 planes: every source swept by the depth-per-lane
-    kernel straight into its channel slice of the network input (strided output rows),
-    bit-identical to the pixel-per-lane kernel (itself pinned by the reference golden of
-    test_format_network_input)."""
-    t = {k: torch.tensor(small[f"fni_{k}"]).to(dev) for k in ("ref", "src", "ref_pose", "src_poses", "K")}
+    kernel straight from its strided channel slice into its channel slice of the network
+    input (mpiv_plane_sweep_into), bit-identical to per-source volumes of the pixel-per-lane
+    kernel on padded copies (itself pinned by the reference golden of
+    test_format_network_input) concatenated after the reference image."""
+    from mpi_vision_amd import _host, _lib
+    t = {k: torch.tensor(small[f"fni_{k}"]) for k in ("ref", "src", "ref_pose", "src_poses", "K")}
     planes = configs.inv_depths(1.0, 100.0, 64)
-    outs = []
-    for dl in ("1", "0"):
-        kopts(sweep_dlane=dl)
-        outs.append(mv.format_network_input_torch(None, t["ref"], t["src"], t["ref_pose"], t["src_poses"], planes,
-                                                  t["K"]).cpu().numpy())
-    assert outs[0].shape == outs[1].shape
-    assert_bits(outs[0], outs[1])
+    got = mv.format_network_input_torch(None, t["ref"].to(dev), t["src"].to(dev), t["ref_pose"].to(dev),
+                                        t["src_poses"].to(dev), planes, t["K"].to(dev)).cpu()
+    kopts(sweep_dlane=0)
+    S = t["src_poses"].shape[1]
+    inv_ref = torch.inverse(t["ref_pose"])
+    H, W = t["ref"].shape[1], t["ref"].shape[2]
+    parts = [t["ref"]]
+    for i in range(S):
+        ki, proj = _host.psv_matrices(t["K"], t["K"], torch.matmul(t["src_poses"][:, i], inv_ref))
+        src = t["src"][..., i * 3:(i + 1) * 3].contiguous().to(dev)
+        parts.append(_lib.plane_sweep_padded(src, planes, ki, proj, H, W).cpu())
+    assert_bits(got.numpy(), torch.cat(parts, dim=-1).numpy())

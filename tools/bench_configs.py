@@ -112,9 +112,6 @@ def c3(dev, it, wu):
     fn = lambda: _lib._call("mpiv_plane_sweep", img, _lib._strides(img), S, H, W, 3, ki, proj, d, D, H, W, out,  # noqa: E731
                             _lib._stream(dev))
     alg = S * H * W * 12 + S * D * H * W * 12
-    ms, mn = timed(fn, it, wu)
-    report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, generic strided kernel", ms, mn, alg,
-           extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
     img4 = _lib.pad_texels(img)  # [S, H+4, W+4, 4]
     pad = lambda: _lib.pad_texels(img, out=img4)  # noqa: E731
     sweep = lambda: _lib._call("mpiv_plane_sweep_padded", img4, S, H, W, 3, ki, proj, d, D, H, W, out,  # noqa: E731
@@ -143,8 +140,16 @@ def c3(dev, it, wu):
         with _lib.debug(**opts):
             ms, mn = timed(sweep10, it, wu)
         report(f"c3 sources, 10 planes (notebook dataset PSV), {label}", ms, mn, alg10)
+    ms, mn = timed(fn, it, wu)
+    report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, mpiv_plane_sweep: depth-per-lane on the source in place "
+           "(the plane_sweep_torch path)", ms, mn, alg,
+           extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
+    with _lib.debug(sweep_dlane=0):
+        ms, mn = timed(fn, it, wu)
+    report(f"c3 PSV {S}x{H}x{W}x3 -> {D} planes, mpiv_plane_sweep with sweep_dlane=0: generic strided kernel",
+           ms, mn, alg)
     ms, mn = timed(lambda: (pad(), sweep()), it, wu)
-    report("c3 PSV plane_sweep_torch path (pad + padded kernel)", ms, mn, alg,
+    report("c3 PSV pad + padded depth-per-lane kernel", ms, mn, alg,
            extra={"Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1)})
 
 
