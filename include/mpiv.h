@@ -90,6 +90,13 @@ int mpiv_pack_planes(const float *mpi_view, const int64_t strides[4], int H, int
 int mpiv_render_packed(const float *packed, int H, int W, int P, const float *homs, int V,
                        float *out, void *stream);
 
+/* mpiv_render_packed through the counting build of render_rows_kernel (same frames): adds to
+ * *census (device, caller-zeroed) the number of 64-lane 16-B gather instructions the launch
+ * issues -- the texture path's real work, which vertical tap reuse makes smaller than 4 per
+ * plane-sample (bench.py's roofline).  Fails unless the launch routes to the rows kernel. */
+int mpiv_render_packed_census(const float *packed, int H, int W, int P, const float *homs, int V, float *out,
+                              unsigned long long *census, void *stream);
+
 /* The same with the LDS-staged kernel (per-tile plane footprints staged by LDS-DMA):
  * identical output; kept for A/B measurement. */
 int mpiv_render_packed_lds(const float *packed, int H, int W, int P, const float *homs, int V,

@@ -50,6 +50,7 @@ _SIGS = {
     "mpiv_deprocess_u8": [_vp, _i64, _vp, _vp],
     "mpiv_render_backward": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp],
     "mpiv_render_train": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp],
+    "mpiv_render_packed_census": [_vp, _int, _int, _int, _vp, _int, _vp, _vp, _vp],
     "mpiv_plane_sweep_into": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,
                               _vp],
     "mpiv_plane_sweep_padded_into": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,

@@ -85,6 +85,10 @@ int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
+// mpiv_render_packed_census: set for the duration of one call on this thread; the rows-kernel
+// launch takes it (and clears it) to launch the counting build
+thread_local unsigned long long* g_census = nullptr;
+
 constexpr int64_t kMaxGridYZ = 65535;
 constexpr int kNativeLdsMaxP = 16;
 constexpr int kChunkMaxLds = 65536;  // render_chunk_kernel: slots + P homographies, default LDS limit
@@ -334,7 +338,16 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
         const bool vs = vs_opt > 0 || (vs_opt == 0 && vs_auto && !rows_opt);
         if (rows == 2) MPIV_ROWS(2);
         else if (rows == 4) MPIV_ROWS(4);
-        else if (rows == 8 && vs) {
+        else if (rows == 8 && g_census && !ct) {  // the counting build (mpiv_render_packed_census)
+            unsigned long long* cn = g_census;
+            g_census = nullptr;
+            if (vs)
+                render_rows_kernel<false, 8, true, true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1,
+                                                                                       homs, out, cn);
+            else
+                render_rows_kernel<false, 8, false, true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end,
+                                                                                        1, homs, out, cn);
+        } else if (rows == 8 && vs) {
             if (ct)
                 render_rows_kernel<true, 8, true><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs,
                                                                                  out);
@@ -363,6 +376,18 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
 int mpiv_render_packed(const float* packed, int H, int W, int P, const float* homs, int V, float* out,
                        void* stream) {
     return render_packed_impl(packed, H, W, P, 0, P, 1, homs, V, out, false, 0, stream);
+}
+
+int mpiv_render_packed_census(const float* packed, int H, int W, int P, const float* homs, int V, float* out,
+                              unsigned long long* census, void* stream) {
+    if (!census) return fail(MPIV_ERR_ARG, "mpiv_render_packed_census: null census");
+    g_census = census;  // render_packed_impl launches the counting build of the rows kernel
+    const int rc = render_packed_impl(packed, H, W, P, 0, P, 1, homs, V, out, false, 0, stream);
+    const bool used = g_census == nullptr;
+    g_census = nullptr;
+    if (rc != MPIV_OK) return rc;
+    if (!used) return fail(MPIV_ERR_ARG, "mpiv_render_packed_census: this launch does not route to render_rows_kernel");
+    return MPIV_OK;
 }
 
 int mpiv_render_packed_lds(const float* packed, int H, int W, int P, const float* homs, int V, float* out,

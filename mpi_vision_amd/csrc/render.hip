@@ -326,7 +326,8 @@ template <bool CT, bool GUARD, int R>
 __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__ planes, int64_t plane_stride,
                                                       const RenderGeom& g, int p_begin, int p_end, int back,
                                                       const float* __restrict__ hv, int x, int y0,
-                                                      float* cr, float* cg, float* cb, float* tt) {
+                                                      float* cr, float* cg, float* cb, float* tt,
+                                                      unsigned& nvm) {
     static_assert(R % 2 == 0, "R must be even");
     struct RowTaps {
         f32x4 a, b, c, d;  // NW, NE (own, when not shared), SW, SE
@@ -362,6 +363,7 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
         t.a = f32x4{0.f, 0.f, 0.f, 0.f};  // defined on both paths (lets the allocator keep one register set)
         t.b = t.a;
         t.own = __builtin_amdgcn_ballot_w64(!t.sh) != 0;
+        nvm += t.own ? 4u : 2u;  // gather instructions this wave issues (census builds only)
         if (t.own) {  // wave-uniform: some lane needs its own north taps
             t.a = llvm_raw_buffer_load_v4f32(r, t.sh ? kOOB : off, 0, 0);
             t.b = llvm_raw_buffer_load_v4f32(r, (t.sh ? kOOB - 16 : off) + 16, 0, 0);
@@ -528,10 +530,13 @@ __global__ __launch_bounds__(256) void render_rows_lds_kernel(const float4* __re
 // render_packed_kernel's contract (FAST recipe: H, W >= 2); a 256-thread block = 64 x 4R
 // tile, wave w owns rows w*R .. w*R+R-1; XCD-aware (tile, view) order, tile-level
 // division proof.
-template <bool CT, int R, bool VS = false>
+// COUNT (census build, mpiv_render_packed_census): the same kernel also adds up the gather
+// instructions its waves issue (the texture path's real work, for bench.py's roofline).
+template <bool CT, int R, bool VS = false, bool COUNT = false>
 __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restrict__ planes, int64_t plane_stride,
                                                           RenderGeom g, int V, int p_begin, int p_end, int back,
-                                                          const float* __restrict__ homs, float* __restrict__ out) {
+                                                          const float* __restrict__ homs, float* __restrict__ out,
+                                                          unsigned long long* __restrict__ census = nullptr) {
     constexpr int TY = 4 * R;
     const int tiles_x = (g.W + kTileX - 1) / kTileX;
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
@@ -556,17 +561,25 @@ __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restri
         cr[k] = -0.0f; cg[k] = -0.0f; cb[k] = -0.0f; tt[k] = 1.0f;  // render_packed_pixel: plane 0 replaces
     }
     if (!proven) {  // rare (w near 0 over the tile): the guarded one-pixel recipe, row by row
-        for (int k = 0; k < R && y0 + k < g.H; ++k) {
+        int rows = 0;
+        for (int k = 0; k < R && y0 + k < g.H; ++k, ++rows) {
             const int64_t o = ((int64_t)v * g.H + y0 + k) * g.W + x;
             render_packed_pixel<CT, 1>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0 + k,
                                        CT ? out + o * 4 : out + o * 3);
         }
+        // ~(P + 1) issues of 4 gathers per row (render_packed_pixel's ping-pong)
+        if (COUNT && (threadIdx.x & (kWave - 1)) == 0)
+            atomicAdd(census, (unsigned long long)rows * 4ull * (unsigned long long)(p_end - p_begin + 1));
         return;
     }
+    unsigned nvm = 0;
     if (VS)
-        render_rows_vs_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
-    else
+        render_rows_vs_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt,
+                                            nvm);
+    else  // 4 gathers per issue: R per plane plus the first
         render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
+    if (!VS) nvm = 4u * (unsigned)(R * (p_end - p_begin) + 1);
+    if (COUNT && (threadIdx.x & (kWave - 1)) == 0) atomicAdd(census, (unsigned long long)nvm);
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const int y = y0 + k;

@@ -399,3 +399,31 @@ def test_default_routing_square_camera_path(V, dev):
     want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.numpy())
     got = _lib.render_packed(_lib.pack_planes(mpi[0].to(dev)), homs)
     assert_bits(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("vs", ["-1", "1"])
+def test_gather_census(vs, dev, kopts):
+    """mpiv_render_packed_census (the counting build of render_rows_kernel, bench.py's texture
+    roofline): same frames as the production launch; without vertical reuse exactly
+    4 x (R*P + 1) gathers per wave, with it between 2 and 4 per plane-sample."""
+    from mpi_vision_amd import _host
+    kopts(render_tile=8, render_vshare=vs)
+    H, W, P, V = 64, 128, 12, 5
+    mpi = configs.synthetic_mpi(1, H, W, P, 4)
+    f = configs.focal_from_fov(W)
+    poses = configs.f32(configs.sway_path(1000)[40:40 + V])
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * V)
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(1, 100, P)), K, V).to(dev)
+    packed = _lib.pack_planes(mpi[0].to(dev))
+    want = _lib.render_packed(packed, homs)
+    out = torch.empty_like(want)
+    census = torch.zeros(1, dtype=torch.int64, device=dev)
+    _lib._call("mpiv_render_packed_census", packed, H, W, P, homs, V, out, census, _lib._stream(dev))
+    torch.cuda.synchronize()
+    assert_bits(out.cpu().numpy(), want.cpu().numpy())
+    waves = V * (W // 64) * (H // 8)
+    n = int(census.item())
+    if vs == "-1":
+        assert n == waves * 4 * (8 * P + 1)
+    else:
+        assert waves * (2 * 8 * P + 2) <= n < waves * 4 * (8 * P + 1)
