@@ -385,15 +385,16 @@ def main():
         one_sha = sha16(one[0])
         peak_gbs = gather_peak_gbs(dev, stream)
         # the texture path's real work in the timed launches: the counting build of the same
-        # kernel (mpiv_render_packed_census) re-renders the last timed step and adds up the
+        # kernel (mpiv_render_packed_census) re-renders the timed steps and adds up the
         # 64-lane 16-B gather instructions its waves issue (vertical tap reuse gathers fewer
         # than the four taps per plane-sample of the direct kernel)
         if packed is not None and entry == "mpiv_render_packed":
             census = torch.zeros(1, dtype=torch.int64, device=dev)
-            hl = host_homs(last).to(dev)
-            try:
-                _lib._call("mpiv_render_packed_census", packed, H, W, P, hl, V, out, census, _lib._stream(dev))
-                gathers = int(census.item())
+            try:  # every timed step's views (the count depends on the poses), averaged per launch
+                for s_ in range(args.warmup, args.warmup + args.steps):
+                    _lib._call("mpiv_render_packed_census", packed, H, W, P, host_homs(s_).to(dev), V, out, census,
+                               _lib._stream(dev))
+                gathers = int(census.item()) // args.steps
             except RuntimeError:  # this view count does not route to the rows kernel
                 gathers = None
 
