@@ -361,3 +361,24 @@ def test_format_network_input_depth_lanes_strided(small, dev, kopts):
         src = t["src"][..., i * 3:(i + 1) * 3].contiguous().to(dev)
         parts.append(_lib.plane_sweep_padded(src, planes, ki, proj, H, W).cpu())
     assert_bits(got.numpy(), torch.cat(parts, dim=-1).numpy())
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1, 1), (2, 3, 1, 2), (5, 4, 3, 65)])
+def test_plane_sweep_tiny_targets(shape, dev):
+    """Tiny targets and depth counts through the default (depth-per-lane, in-place) sweep:
+    1x1 target with one depth and one channel, 2x3 targets, 65 depths (a one-depth second
+    chunk) into a 5x4 target: bit-exact to the oracle."""
+    from mpi_vision_amd import _host, _lib
+    from oracle import oracle
+    Ht, Wt, C, D = shape
+    g = torch.Generator().manual_seed(200 + D)
+    B, Hs, Ws = 2, 9, 11
+    img = torch.rand((B, Hs, Ws, C), generator=g)
+    Ks = configs.f32([configs.intrinsics_matrix(9.0, 9.5, 5.0, 4.0)] * B)
+    Kt = configs.f32([configs.intrinsics_matrix(3.0, 3.0, Wt / 2.0, Ht / 2.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(3.0 * k - 1.0), (0.1 * k, 0.02, 0.0)) for k in range(B)])
+    depths = configs.inv_depths(1.0, 20, D) if D > 1 else [2.5]
+    ki, proj = _host.psv_matrices(Ks, Kt, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Ht, Wt)
+    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Ht, Wt)
+    assert_bits(out.cpu().numpy(), want, str(shape))
