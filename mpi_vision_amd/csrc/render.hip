@@ -360,8 +360,13 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
         const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes);
         t.c = llvm_raw_buffer_load_v4f32(r, off, g.row, 0);
         t.d = llvm_raw_buffer_load_v4f32(r, off + 16, g.row, 0);
-        t.a = f32x4{0.f, 0.f, 0.f, 0.f};  // defined on both paths (lets the allocator keep one register set)
-        t.b = t.a;
+#ifndef MPIV_VS_ZINIT
+#define MPIV_VS_ZINIT 0
+#endif
+        if (MPIV_VS_ZINIT) {  // defined on both paths (lets the allocator keep one register set)
+            t.a = f32x4{0.f, 0.f, 0.f, 0.f};
+            t.b = t.a;
+        }
         t.own = __builtin_amdgcn_ballot_w64(!t.sh) != 0;
         nvm += t.own ? 4u : 2u;  // gather instructions this wave issues (census builds only)
         if (t.own) {  // wave-uniform: some lane needs its own north taps
@@ -376,6 +381,10 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
 #define MPIV_VS_BRANCH 1
 #endif
         if (!MPIV_VS_BRANCH || t.own) {
+#ifndef MPIV_VS_ASMBR
+#define MPIV_VS_ASMBR 1
+#endif
+            if (MPIV_VS_ASMBR) asm volatile("");  // keeps this a real (wave-uniform) branch: if-converted, its 8 selects ran always
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 na[c] = t.sh ? pc[c] : t.a[c];
