@@ -296,20 +296,24 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             render_pair_kernel<false, false><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
         return launched(nm);
     }
-    // R rows per work-item, planes outermost (render.hip render_rows_kernel).  Automatic for a
-    // near-square MPI (the reference's swapped x/(H-1), y/(W-1) normalisation stretches the
-    // footprints by W/(H-1) and H/(W-1); stretched ones lose) at one or two
-    // views (single-view 0.435 vs 0.48-0.51 ms) and at >= 32 views per launch (camera-path
-    // launches: 30.7 vs 31.6 ms at 125 views); 8 views measured 2 % slower.
+    // R rows per work-item, planes outermost (render.hip render_rows_kernel), automatic:
+    //  * near-square MPIs: R = 8 at one or two views (HBM-bound; single view 0.435 vs 0.48-0.51 ms
+    //    for the one-row kernel), with vertical tap reuse from three views per launch up (the
+    //    texture path binds: 125 views 28.1 vs 30.7 ms, 8 views 1.92 vs 2.33);
+    //  * stretched MPIs (the reference's swapped x/(H-1), y/(W-1) normalisation: footprints
+    //    stretched by W/(H-1) and H/(W-1)): R = 8 only WITH the reuse, and only when its 64x32
+    //    tiles fill the chip (>= 2048 blocks): config 5's plane shard 0.81 vs 0.88 ms, config 2
+    //    at 64 / 8 views 2.15 vs 2.40 / 0.278 vs 0.302 ms; config 2 at one view (288 blocks)
+    //    0.100 vs 0.054 ms, so the one-row kernel keeps small launches.
     const float sxr = (float)W / (float)(H > 1 ? H - 1 : 1), syr = (float)H / (float)(W > 1 ? W - 1 : 1);
     const bool square = sxr >= 0.8f && sxr <= 1.25f && syr >= 0.8f && syr <= 1.25f;
     const int rows_opt = opt(kOptRenderTile);
-    // R = 8 with vertical tap reuse from three views per launch up (the texture path, not HBM,
-    // binds there: 125 views 28.0 vs 30.7 ms, 8 views 1.98 vs 2.33 for the one-row kernel); at one
-    // or two views (HBM-bound) the reuse's extra dependency costs (0.51 vs 0.46 ms)
-    const int rows_auto = (square && !opt(kOptRenderMv) && !opt(kOptRenderPair)) ? 8 : 0;
+    const int64_t rows_blocks = (int64_t)blocks(W, kTileX) * blocks(H, 4 * 8) * V;
+    const bool stretched_vs = !square && rows_blocks >= 2048;
+    const bool variants_off = !opt(kOptRenderMv) && !opt(kOptRenderPair);
+    const int rows_auto = ((square || stretched_vs) && variants_off) ? 8 : 0;
     const int vs_opt = opt(kOptRenderVshare);
-    const bool vs_auto = V >= 3;
+    const bool vs_auto = square ? V >= 3 : stretched_vs;
     const int rows_sel = fast ? (rows_opt ? rows_opt : rows_auto) : 0;
     if (const int rows = rows_sel; rows == 108 || rows == 116 || rows == 132) {
         // R rows with the compositing state in LDS (render_rows_lds_kernel)

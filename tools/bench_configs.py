@@ -87,10 +87,20 @@ def c2(dev, it, wu):
     packed = _lib.pack_planes(mpi[0])
     out = torch.empty((V, H, W, 3), device=dev)
     per_view = P * H * W * 16 + H * W * 12
-    for label, opts in (("direct gathers (default)", {}), ("multi-view LDS kernel", {"render_mv": 1})):
+    for label, opts in (("default routing", {}), ("direct gathers", {"render_tile": -1}),
+                        ("multi-view LDS kernel", {"render_mv": 1}), ("rows x8 per lane", {"render_tile": 8}),
+                        ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1})):
         with _lib.debug(**opts):
             ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it, wu)
         report(f"c2 1024x576x32, {V} views, packed, {label}", ms, mn, V * per_view, V * H * W / 1e6)
+    for V1 in (1, 8):
+        h1 = homs[:V1].contiguous()
+        o1 = out[:V1]
+        for label, opts in (("default routing", {}), ("direct gathers", {"render_tile": -1}),
+                            ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1})):
+            with _lib.debug(**opts):
+                ms, mn = timed(lambda: _lib.render_packed(packed, h1, o1), it, wu)
+            report(f"c2 1024x576x32, {V1} views, packed, {label}", ms, mn, V1 * per_view, V1 * H * W / 1e6)
     ms, mn = timed(lambda: _lib.pack_planes(mpi[0]), it, wu)
     report("c2 pack (one-time per MPI)", ms, mn, 2 * P * H * W * 16)
     mpi5 = mpi.expand(V, H, W, P, 4)
