@@ -237,3 +237,45 @@ def test_view_sharded_hip_ranks_gather_bit_exact(world, tmp_path):
     out = str(tmp_path / "frames.npy")
     mp.spawn(_view_worker_gpu, args=(world, _free_port(), out), nprocs=world, join=True)
     np.testing.assert_array_equal(np.load(out), np.load(out + ".seq.npy"))
+
+
+def _rccl_worker(rank, world, port, out_path):
+    """Both sharded paths with the device collectives on RCCL ("nccl"): world 1 is the
+    most a one-GPU box allows (RCCL refuses two ranks on one device: "Duplicate GPU
+    detected"), so this checks the RCCL calls themselves -- all_to_all_single and gather
+    on device tensors, no host staging -- that the 8-GPU node runs at world 8."""
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    from mpi_vision_amd import _host, _lib, configs, parallel
+    assert dist.get_backend() == "nccl"
+    H, W, P, V = 37, 53, 11, 5
+    mpi = configs.synthetic_mpi(1, H, W, P, 5)
+    K = configs.f32([configs.intrinsics_matrix(50.0, 52.0, 26.0, 18.0)] * V)
+    poses = configs.f32([configs.pose_from(configs.rot_y(1.5 - v), (0.05 * v, -0.02, 0.03)) for v in range(V)])
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(1, 20, P)), K, V).to(dev)
+    packed = _lib.pack_planes(mpi[0].to(dev))
+    frames = parallel.render_view_sharded(packed, homs, gather=True)
+    p0, p1 = parallel.shard_range(P, rank, world)
+    local = _lib.pack_planes(mpi[0, :, :, p0:p1].contiguous().to(dev))
+    frame = parallel.render_plane_sharded(local, homs[:1, p0:p1].contiguous(), H)
+    if rank == 0:
+        assert frames.is_cuda and frame.is_cuda
+        np.save(out_path, frames.cpu().numpy())
+        np.save(out_path + ".plane.npy", frame.cpu().numpy())
+        np.save(out_path + ".seq.npy", _lib.render_packed(packed, homs).cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_paths_over_rccl_world1(tmp_path):
+    """View- and plane-sharded renders through RCCL device collectives (world 1 on the
+    one-GPU box): bit-identical to one launch of all views / all planes."""
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_rccl_worker, args=(1, _free_port(), out), nprocs=1, join=True)
+    seq = np.load(out + ".seq.npy")
+    np.testing.assert_array_equal(np.load(out), seq)
+    np.testing.assert_array_equal(np.load(out + ".plane.npy"), seq[:1])
