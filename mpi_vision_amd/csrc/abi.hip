@@ -60,8 +60,9 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (render_rows_kernel; 100+R: state in LDS, render_rows_lds_kernel);
 //                      -1: off (one row per work-item), 0: automatic (R = 8 where it pays)
 //   sweep_tile=1       the sweep uses the tile kernel; sweep_store=k (k >= 0) the grouped one
-//   render_vshare=-1|0|1  render_rows_kernel (R = 8) without / automatic (>= 3 views) / with
-//                      vertical tap reuse
+//   render_vshare=-1|0|1  render_rows_kernel without vertical tap reuse (R = render_tile or 8) /
+//                      automatic / with it, two rows in flight (R = 8); 3..9: with it and the
+//                      (R, rows in flight) of abi.hip's table (A/B)
 //   sweep_dlane=0      the LDS sweep runs pixel-per-lane (plane_sweep_lds_kernel) instead of
 //                      depth-per-lane (plane_sweep_dlane_kernel)
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
@@ -296,15 +297,18 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             render_pair_kernel<false, false><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
         return launched(nm);
     }
-    // R rows per work-item, planes outermost (render.hip render_rows_kernel), automatic:
-    //  * near-square MPIs: R = 8 at one or two views (HBM-bound; single view 0.435 vs 0.48-0.51 ms
-    //    for the one-row kernel), with vertical tap reuse from three views per launch up (the
-    //    texture path binds: 125 views 28.1 vs 30.7 ms, 8 views 1.92 vs 2.33);
+    // R rows per work-item, planes outermost (render.hip render_rows_kernel), automatic
+    // (bench_configs.py A/B, profiles/r02_vshare_ab.txt), all with vertical tap reuse and a ring
+    // of D rows in flight:
+    //  * up to 8 views per launch: R = 8, D = 4 (single view, HBM-bound: 0.41 vs 0.44 ms for
+    //    plain R = 8 and 0.48-0.51 for the one-row kernel; 8 views 1.83-1.87 vs 1.94 ms with D = 2);
+    //  * more views (the texture path binds): near-square MPIs R = 6, D = 3 (125 views 26.5-26.9
+    //    vs 27.4-28.3 ms with D = 2, 30.8 without reuse); stretched MPIs R = 9, D = 3 (config 2 at
+    //    64 views 2.04-2.09 vs 2.11-2.17 ms for (8, 4), 2.33-2.39 one-row);
     //  * stretched MPIs (the reference's swapped x/(H-1), y/(W-1) normalisation: footprints
-    //    stretched by W/(H-1) and H/(W-1)): R = 8 only WITH the reuse, and only when its 64x32
-    //    tiles fill the chip (>= 2048 blocks): config 5's plane shard 0.81 vs 0.88 ms, config 2
-    //    at 64 / 8 views 2.15 vs 2.40 / 0.278 vs 0.302 ms; config 2 at one view (288 blocks)
-    //    0.100 vs 0.054 ms, so the one-row kernel keeps small launches.
+    //    stretched by W/(H-1) and H/(W-1)) only when the tiles fill the chip (>= 2048 blocks of
+    //    64x32): config 5's plane shard 0.80 vs 0.87 ms one-row; config 2 at one view (288
+    //    blocks) is latency-bound (0.079 vs 0.054 ms), so the one-row kernel keeps small launches.
     const float sxr = (float)W / (float)(H > 1 ? H - 1 : 1), syr = (float)H / (float)(W > 1 ? W - 1 : 1);
     const bool square = sxr >= 0.8f && sxr <= 1.25f && syr >= 0.8f && syr <= 1.25f;
     const int rows_opt = opt(kOptRenderTile);
@@ -313,7 +317,6 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     const bool variants_off = !opt(kOptRenderMv) && !opt(kOptRenderPair);
     const int rows_auto = ((square || stretched_vs) && variants_off) ? 8 : 0;
     const int vs_opt = opt(kOptRenderVshare);
-    const bool vs_auto = square ? V >= 3 : stretched_vs;
     const int rows_sel = fast ? (rows_opt ? rows_opt : rows_auto) : 0;
     if (const int rows = rows_sel; rows == 108 || rows == 116 || rows == 132) {
         // R rows with the compositing state in LDS (render_rows_lds_kernel)
@@ -331,6 +334,48 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
 #undef MPIV_ROWSL
         return launched(nm);
     }
+    // vertical tap reuse with D rows in flight, (R, D) by table index: 3: (8, 4), 4: (6, 3),
+    // 5: (9, 3) (the automatic choices), 6: (12, 4), 7: (12, 3), 8: (16, 4), 9: (10, 5) (A/B only,
+    // render_vshare = index)
+    int vsd = 0;
+    if (fast && vs_opt >= 3 && vs_opt <= 9)
+        vsd = vs_opt;
+    else if (fast && vs_opt == 0 && !rows_opt && rows_auto == 8)
+        vsd = V <= 8 ? 3 : square ? 4 : 5;
+    if (vsd) {
+        static const int kR[] = {8, 6, 9, 12, 12, 16, 10};
+        const int R = kR[vsd - 3];
+        const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
+        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+        // the counting build (mpiv_render_packed_census) exists for the automatic choices
+        unsigned long long* cn = (g_census && !ct && vsd <= 5) ? g_census : nullptr;
+        if (cn) g_census = nullptr;
+#define MPIV_VSD(R, D)                                                                                              \
+    if (ct)                                                                                                        \
+        render_rows_kernel<true, R, true, false, D><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end,    \
+                                                                                   back, homs, out);               \
+    else                                                                                                           \
+        render_rows_kernel<false, R, true, false, D><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, \
+                                                                                    homs, out)
+#define MPIV_VSDC(R, D)                                                                                                \
+    if (cn)                                                                                                           \
+        render_rows_kernel<false, R, true, true, D><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, \
+                                                                                  out, cn);                           \
+    else                                                                                                              \
+        MPIV_VSD(R, D)
+        switch (vsd) {
+            case 3: MPIV_VSDC(8, 4); break;
+            case 4: MPIV_VSDC(6, 3); break;
+            case 5: MPIV_VSDC(9, 3); break;
+            case 6: MPIV_VSD(12, 4); break;
+            case 7: MPIV_VSD(12, 3); break;
+            case 8: MPIV_VSD(16, 4); break;
+            default: MPIV_VSD(10, 5); break;
+        }
+#undef MPIV_VSDC
+#undef MPIV_VSD
+        return launched(nm);
+    }
     if (const int rows = rows_sel; rows == 2 || rows == 4 || rows == 8 || rows == 16) {
         const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * rows) * V;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
@@ -339,7 +384,7 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
         render_rows_kernel<true, R><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out); \
     else                                                                                                          \
         render_rows_kernel<false, R><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out)
-        const bool vs = vs_opt > 0 || (vs_opt == 0 && vs_auto && !rows_opt);
+        const bool vs = vs_opt == 1;  // two rows in flight (A/B; the automatic routes are above)
         if (rows == 2) MPIV_ROWS(2);
         else if (rows == 4) MPIV_ROWS(4);
         else if (rows == 8 && g_census && !ct) {  // the counting build (mpiv_render_packed_census)

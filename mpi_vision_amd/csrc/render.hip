@@ -322,13 +322,13 @@ __device__ __forceinline__ void render_rows_pixels(const float4* __restrict__ pl
 // that continue get the buffer's zero range there and take the previous row's south taps).
 // The texture path charges per wave instruction, so its work drops from 4 to ~2.5 gathers per
 // sample on a camera path; the result is bit-identical.
-template <bool CT, bool GUARD, int R>
+template <bool CT, bool GUARD, int R, int D = 2>
 __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__ planes, int64_t plane_stride,
                                                       const RenderGeom& g, int p_begin, int p_end, int back,
                                                       const float* __restrict__ hv, int x, int y0,
                                                       float* cr, float* cg, float* cb, float* tt,
                                                       unsigned& nvm) {
-    static_assert(R % 2 == 0, "R must be even");
+    static_assert(D != 2 || R % 2 == 0, "R must be even");
     struct RowTaps {
         f32x4 a, b, c, d;  // NW, NE (own, when not shared), SW, SE
         float nw, ne, sw, se;
@@ -410,9 +410,37 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
         asm volatile("" : "+v"(cr[k]), "+v"(cg[k]), "+v"(cb[k]));
         if (CT) asm volatile("" : "+v"(tt[k]));
     };
-    RowTaps A, B;
     f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sd = sc;  // the previous row's south taps
     Hom9 h = hom(p_begin), hn = hom(p_begin + 1);
+    if constexpr (D != 2) {  // D rows in flight (a ring of D tap sets; A/B)
+        static_assert(R % D == 0 && D > 2, "ring depth must divide R");
+        RowTaps T[D];
+        issue(p_begin, 0, h, 0, false, T[0]);
+#pragma unroll
+        for (int k = 1; k < D - 1; ++k) issue(p_begin, k, h, T[k - 1].off, true, T[k]);
+        for (int p = p_begin; p < p_end; ++p) {
+            const bool first = replace_first && p == p_begin;
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const int kk = k + D - 1;  // the row issued now, D - 1 ahead of the one consumed
+                if (kk < R)
+                    issue(p, kk, h, T[(kk - 1) % D].off, true, T[kk % D]);
+                else if (kk == R)
+                    issue(p + 1, 0, hn, 0, false, T[kk % D]);  // past the end: the last plane again (unused)
+                else
+                    issue(p + 1, kk - R, hn, T[(kk - 1) % D].off, true, T[kk % D]);
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                consume(T[k % D], sc, sd, k, first);
+                sc = T[k % D].c;
+                sd = T[k % D].d;
+            }
+            h = hn;
+            hn = hom(p + 2);
+        }
+        return;
+    }
+    RowTaps A, B;
     issue(p_begin, 0, h, 0, false, A);
     for (int p = p_begin; p < p_end; ++p) {
         const bool first = replace_first && p == p_begin;
@@ -541,7 +569,7 @@ __global__ __launch_bounds__(256) void render_rows_lds_kernel(const float4* __re
 // division proof.
 // COUNT (census build, mpiv_render_packed_census): the same kernel also adds up the gather
 // instructions its waves issue (the texture path's real work, for bench.py's roofline).
-template <bool CT, int R, bool VS = false, bool COUNT = false>
+template <bool CT, int R, bool VS = false, bool COUNT = false, int D = 2>
 __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restrict__ planes, int64_t plane_stride,
                                                           RenderGeom g, int V, int p_begin, int p_end, int back,
                                                           const float* __restrict__ homs, float* __restrict__ out,
@@ -582,9 +610,9 @@ __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restri
         return;
     }
     unsigned nvm = 0;
-    if (VS)
-        render_rows_vs_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt,
-                                            nvm);
+    if constexpr (VS)
+        render_rows_vs_pixels<CT, false, R, D>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb,
+                                               tt, nvm);
     else  // 4 gathers per issue: R per plane plus the first
         render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
     if (!VS) nvm = 4u * (unsigned)(R * (p_end - p_begin) + 1);

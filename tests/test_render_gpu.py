@@ -252,13 +252,17 @@ def _variant_env(kopts, mv):
     tap-sharing kernel with two / one planes in flight (A/B); "ring<k>": the LDS-DMA ring
     kernel with tile geometry k (render_ring.hip); "tile<R>": R rows per work-item
     (render_rows_kernel), "tile8vs": with vertical tap sharing."""
+    if mv.startswith("vsd"):  # vertical reuse with 4 / 3 / 3 rows in flight (render_vshare 3 / 4 / 5)
+        kopts(render_vshare=int(mv[3:]))
+        return
     kopts(render_mv=1 if mv == "1" else 0, render_pair={"pair": 1, "pair1": 2}.get(mv, 0),
           render_ring=int(mv[4:]) if mv.startswith("ring") else -1,
           render_tile=int(mv[4:].replace("vs", "")) if mv.startswith("tile") else -1,
           render_vshare=1 if mv.endswith("vs") else 0)
 
 
-RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile8vs", "tile16",
+RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile8vs", "vsd3", "vsd4", "vsd5", "vsd6", "vsd7", "vsd8", "vsd9",
+        "tile16",
         "tile108", "tile116", "tile132"]
 
 
@@ -384,11 +388,11 @@ def test_ring_kernel_golden_cases(ring, name, small, meta, dev, kopts):
     assert_bits(_lib.render_packed(_lib.pack_planes(mpi[0].to(dev)), homs).cpu().numpy(), want, "extreme views")
 
 
-@pytest.mark.parametrize("V", [1, 3, 40])
+@pytest.mark.parametrize("V", [1, 3, 9, 40])
 def test_default_routing_square_camera_path(V, dev):
-    """Default routing on a square MPI (render_rows_kernel, R = 8; with vertical tap reuse
-    from 3 views per launch up) along the sway path, a frame height that is not a multiple
-    of the 32-row block tile: bit-exact to the oracle."""
+    """Default routing on a square MPI (render_rows_kernel with vertical tap reuse: R = 8 with
+    4 rows in flight up to 8 views, R = 6 with 3 above) along the sway path, a frame height
+    that is not a multiple of the block tile: bit-exact to the oracle."""
     from mpi_vision_amd import _host
     H, W, P = 100, 100, 16
     mpi = configs.synthetic_mpi(1, H, W, P, 21)
@@ -427,3 +431,43 @@ def test_gather_census(vs, dev, kopts):
         assert n == waves * 4 * (8 * P + 1)
     else:
         assert waves * (2 * 8 * P + 2) <= n < waves * 4 * (8 * P + 1)
+
+
+@pytest.mark.parametrize("V,R,D", [(1, 8, 4), (12, 6, 3)])
+def test_gather_census_default_routing(V, R, D, dev):
+    """The counting build of the default route (vertical reuse, R rows with D in flight; a frame
+    height that leaves a partial last tile): the production frames, and between 2 and 4
+    gathers per computed plane-sample."""
+    from mpi_vision_amd import _host
+    H, W, P = 128, 128, 12  # square: the stretched route of a launch this small is the one-row kernel
+    mpi = configs.synthetic_mpi(1, H, W, P, 4)
+    f = configs.focal_from_fov(W)
+    poses = configs.f32(configs.sway_path(1000)[40:40 + V])
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * V)
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(1, 100, P)), K, V).to(dev)
+    packed = _lib.pack_planes(mpi[0].to(dev))
+    want = _lib.render_packed(packed, homs)
+    out = torch.empty_like(want)
+    census = torch.zeros(1, dtype=torch.int64, device=dev)
+    _lib._call("mpiv_render_packed_census", packed, H, W, P, homs, V, out, census, _lib._stream(dev))
+    torch.cuda.synchronize()
+    assert_bits(out.cpu().numpy(), want.cpu().numpy())
+    waves = V * (W // 64) * ((H + R - 1) // R)  # waves whose first row is inside the frame
+    n = int(census.item())
+    assert waves * 2 * R * P <= n <= waves * 4 * (R * P + D)
+
+
+def test_default_routing_stretched_many_views(dev):
+    """Default routing on a stretched MPI (x footprints stretched by W/(H-1)) with enough views
+    for the rows kernel (>= 2048 tiles of 64x32): R = 9 with 3 rows in flight, a frame height
+    that leaves a partial tile: bit-exact to the oracle."""
+    from mpi_vision_amd import _host
+    H, W, P, V = 70, 256, 4, 200
+    mpi = configs.synthetic_mpi(1, H, W, P, 23)
+    f = configs.focal_from_fov(W)
+    poses = configs.f32(configs.sway_path(1000)[500:500 + V])
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * V)
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(1, 100, P)), K, V)
+    want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.numpy())
+    got = _lib.render_packed(_lib.pack_planes(mpi[0].to(dev)), homs)
+    assert_bits(got.cpu().numpy(), want)

@@ -89,7 +89,9 @@ def c2(dev, it, wu):
     per_view = P * H * W * 16 + H * W * 12
     for label, opts in (("default routing", {}), ("direct gathers", {"render_tile": -1}),
                         ("multi-view LDS kernel", {"render_mv": 1}), ("rows x8 per lane", {"render_tile": 8}),
-                        ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1})):
+                        ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1}),
+                        ("rows x8, vertical reuse, 4 rows in flight", {"render_vshare": 3}),
+                        ("rows x9, vertical reuse, 3 rows in flight", {"render_vshare": 5})):
         with _lib.debug(**opts):
             ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it, wu)
         report(f"c2 1024x576x32, {V} views, packed, {label}", ms, mn, V * per_view, V * H * W / 1e6)
@@ -97,7 +99,8 @@ def c2(dev, it, wu):
         h1 = homs[:V1].contiguous()
         o1 = out[:V1]
         for label, opts in (("default routing", {}), ("direct gathers", {"render_tile": -1}),
-                            ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1})):
+                            ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1}),
+                            ("rows x8, vertical reuse, 4 rows in flight", {"render_vshare": 3})):
             with _lib.debug(**opts):
                 ms, mn = timed(lambda: _lib.render_packed(packed, h1, o1), it, wu)
             report(f"c2 1024x576x32, {V1} views, packed, {label}", ms, mn, V1 * per_view, V1 * H * W / 1e6)
@@ -178,6 +181,14 @@ def c4(dev, it, wu):
                             ("multi-view LDS kernel", {"render_mv": 1}),
                             ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("rows x8 per lane", {"render_tile": 8}),
                             ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1}),
+                            ("rows x8, vertical reuse, 4 rows in flight", {"render_vshare": 3}),
+                            ("rows x6, vertical reuse, 3 rows in flight", {"render_vshare": 4}),
+                            ("rows x9, vertical reuse, 3 rows in flight", {"render_vshare": 5}),
+                            ("rows x12, vertical reuse, 4 rows in flight", {"render_vshare": 6}),
+                            ("rows x12, vertical reuse, 3 rows in flight", {"render_vshare": 7}),
+                            ("rows x16, vertical reuse, 4 rows in flight", {"render_vshare": 8}),
+                            ("rows x10, vertical reuse, 5 rows in flight", {"render_vshare": 9}),
+                            ("rows x8, vertical tap reuse (again)", {"render_tile": 8, "render_vshare": 1}),
                             ("rows x16 per lane", {"render_tile": 16})):
             if V == 125 and ("ring" in label or "LDS kernel" in label):
                 continue
@@ -276,6 +287,9 @@ def c5(dev, it, wu):
     for label, opts in (("default routing", {}), ("direct gathers", {"render_tile": -1}),
                         ("LDS-DMA ring 8w 64x8/2", {"render_ring": 4}), ("rows x8 per lane", {"render_tile": 8}),
                             ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1}),
+                            ("rows x8, vertical reuse, 4 rows in flight", {"render_vshare": 3}),
+                            ("rows x9, vertical reuse, 3 rows in flight", {"render_vshare": 5}),
+                            ("rows x12, vertical reuse, 3 rows in flight", {"render_vshare": 7}),
                             ("rows x16 per lane", {"render_tile": 16})):
         with _lib.debug(**opts):
             ms, mn = timed(lambda: _lib.render_packed_ct(packed, homs_local, back=True, out=ct), it, wu)
