@@ -300,8 +300,9 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     // R rows per work-item, planes outermost (render.hip render_rows_kernel), automatic
     // (bench_configs.py A/B, profiles/r02_vshare_ab.txt), all with vertical tap reuse and a ring
     // of D rows in flight:
-    //  * up to 8 views per launch: R = 8, D = 4 (single view, HBM-bound: 0.41 vs 0.44 ms for
-    //    plain R = 8 and 0.48-0.51 for the one-row kernel; 8 views 1.83-1.87 vs 1.94 ms with D = 2);
+    //  * one or two views (HBM-bound): R = 4, D = 4 (single view 0.383 ms vs 0.40-0.41 for (8, 4),
+    //    0.44 for plain R = 8, 0.48-0.51 for the one-row kernel; config-5 shard 0.776 vs 0.80);
+    //  * 3 to 8 views: R = 8, D = 4 (8 views 1.80-1.87 vs 1.93-1.98 ms with D = 2, 1.90 for (4, 4));
     //  * more views (the texture path binds): near-square MPIs R = 6, D = 3 (125 views 26.5-26.9
     //    vs 27.4-28.3 ms with D = 2, 30.8 without reuse); stretched MPIs R = 9, D = 3 (config 2 at
     //    64 views 2.04-2.09 vs 2.11-2.17 ms for (8, 4), 2.33-2.39 one-row);
@@ -334,21 +335,21 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
 #undef MPIV_ROWSL
         return launched(nm);
     }
-    // vertical tap reuse with D rows in flight, (R, D) by table index: 3: (8, 4), 4: (6, 3),
-    // 5: (9, 3) (the automatic choices), 6: (12, 4), 7: (12, 3), 8: (16, 4), 9: (10, 5) (A/B only,
-    // render_vshare = index)
+    // vertical tap reuse with D rows in flight, (R, D) by table index: 11: (4, 4), 3: (8, 4),
+    // 4: (6, 3), 5: (9, 3) (the automatic choices), 6: (12, 4), 7: (12, 3), 8: (16, 4), 9: (10, 5), 10: (6, 2),
+    // 11: (4, 4), 12: (3, 3), 13: (4, 2), 14: (5, 5) (A/B only, render_vshare = index)
     int vsd = 0;
-    if (fast && vs_opt >= 3 && vs_opt <= 9)
+    if (fast && vs_opt >= 3 && vs_opt <= 14)
         vsd = vs_opt;
     else if (fast && vs_opt == 0 && !rows_opt && rows_auto == 8)
-        vsd = V <= 8 ? 3 : square ? 4 : 5;
+        vsd = V <= 2 ? 11 : V <= 8 ? 3 : square ? 4 : 5;
     if (vsd) {
-        static const int kR[] = {8, 6, 9, 12, 12, 16, 10};
+        static const int kR[] = {8, 6, 9, 12, 12, 16, 10, 6, 4, 3, 4, 5};
         const int R = kR[vsd - 3];
         const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
         // the counting build (mpiv_render_packed_census) exists for the automatic choices
-        unsigned long long* cn = (g_census && !ct && vsd <= 5) ? g_census : nullptr;
+        unsigned long long* cn = (g_census && !ct && (vsd <= 5 || vsd == 11)) ? g_census : nullptr;
         if (cn) g_census = nullptr;
 #define MPIV_VSD(R, D)                                                                                              \
     if (ct)                                                                                                        \
@@ -370,7 +371,12 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             case 6: MPIV_VSD(12, 4); break;
             case 7: MPIV_VSD(12, 3); break;
             case 8: MPIV_VSD(16, 4); break;
-            default: MPIV_VSD(10, 5); break;
+            case 9: MPIV_VSD(10, 5); break;
+            case 10: MPIV_VSD(6, 2); break;
+            case 11: MPIV_VSDC(4, 4); break;
+            case 12: MPIV_VSD(3, 3); break;
+            case 13: MPIV_VSD(4, 2); break;
+            default: MPIV_VSD(5, 5); break;
         }
 #undef MPIV_VSDC
 #undef MPIV_VSD

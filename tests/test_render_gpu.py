@@ -261,7 +261,7 @@ def _variant_env(kopts, mv):
           render_vshare=1 if mv.endswith("vs") else 0)
 
 
-RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile8vs", "vsd3", "vsd4", "vsd5", "vsd6", "vsd7", "vsd8", "vsd9",
+RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile8vs", "vsd3", "vsd4", "vsd5", "vsd6", "vsd7", "vsd8", "vsd9", "vsd10", "vsd11", "vsd12", "vsd13", "vsd14",
         "tile16",
         "tile108", "tile116", "tile132"]
 
@@ -388,11 +388,11 @@ def test_ring_kernel_golden_cases(ring, name, small, meta, dev, kopts):
     assert_bits(_lib.render_packed(_lib.pack_planes(mpi[0].to(dev)), homs).cpu().numpy(), want, "extreme views")
 
 
-@pytest.mark.parametrize("V", [1, 3, 9, 40])
+@pytest.mark.parametrize("V", [1, 2, 3, 9, 40])
 def test_default_routing_square_camera_path(V, dev):
-    """Default routing on a square MPI (render_rows_kernel with vertical tap reuse: R = 8 with
-    4 rows in flight up to 8 views, R = 6 with 3 above) along the sway path, a frame height
-    that is not a multiple of the block tile: bit-exact to the oracle."""
+    """Default routing on a square MPI (render_rows_kernel with vertical tap reuse, (R, rows in
+    flight) = (4, 4) at 1-2 views, (8, 4) up to 8, (6, 3) above) along the sway path, a frame
+    height that is not a multiple of the block tile: bit-exact to the oracle."""
     from mpi_vision_amd import _host
     H, W, P = 100, 100, 16
     mpi = configs.synthetic_mpi(1, H, W, P, 21)
@@ -433,7 +433,7 @@ def test_gather_census(vs, dev, kopts):
         assert waves * (2 * 8 * P + 2) <= n < waves * 4 * (8 * P + 1)
 
 
-@pytest.mark.parametrize("V,R,D", [(1, 8, 4), (12, 6, 3)])
+@pytest.mark.parametrize("V,R,D", [(1, 4, 4), (5, 8, 4), (12, 6, 3)])
 def test_gather_census_default_routing(V, R, D, dev):
     """The counting build of the default route (vertical reuse, R rows with D in flight; a frame
     height that leaves a partial last tile): the production frames, and between 2 and 4
