@@ -91,7 +91,9 @@ def c2(dev, it, wu):
                         ("multi-view LDS kernel", {"render_mv": 1}), ("rows x8 per lane", {"render_tile": 8}),
                         ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1}),
                         ("rows x8, vertical reuse, 4 rows in flight", {"render_vshare": 3}),
-                        ("rows x9, vertical reuse, 3 rows in flight", {"render_vshare": 5})):
+                        ("rows x9, vertical reuse, 3 rows in flight", {"render_vshare": 5}),
+                        ("rows x6, vertical reuse, 3 rows in flight", {"render_vshare": 4}),
+                        ("rows x9, vertical reuse, 3 rows in flight (again)", {"render_vshare": 5})):
         with _lib.debug(**opts):
             ms, mn = timed(lambda: _lib.render_packed(packed, homs, out), it, wu)
         report(f"c2 1024x576x32, {V} views, packed, {label}", ms, mn, V * per_view, V * H * W / 1e6)
@@ -100,7 +102,8 @@ def c2(dev, it, wu):
         o1 = out[:V1]
         for label, opts in (("default routing", {}), ("direct gathers", {"render_tile": -1}),
                             ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1}),
-                            ("rows x8, vertical reuse, 4 rows in flight", {"render_vshare": 3})):
+                            ("rows x8, vertical reuse, 4 rows in flight", {"render_vshare": 3}),
+                            ("rows x4, vertical reuse, 4 rows in flight", {"render_vshare": 11})):
             with _lib.debug(**opts):
                 ms, mn = timed(lambda: _lib.render_packed(packed, h1, o1), it, wu)
             report(f"c2 1024x576x32, {V1} views, packed, {label}", ms, mn, V1 * per_view, V1 * H * W / 1e6)
