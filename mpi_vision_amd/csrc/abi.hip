@@ -61,8 +61,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      -1: off (one row per work-item), 0: automatic (R = 8 where it pays)
 //   sweep_tile=1       the sweep uses the tile kernel; sweep_store=k (k >= 0) the grouped one
 //   render_vshare=-1|0|1  render_rows_kernel without vertical tap reuse (R = render_tile or 8) /
-//                      automatic / with it, two rows in flight (R = 8); 3..9: with it and the
-//                      (R, rows in flight) of abi.hip's table (A/B)
+//                      automatic / with it, two rows in flight (R = 8); 3|4|5|11: with it and
+//                      (R, rows in flight) = (8, 4) / (6, 3) / (9, 3) / (4, 4)
 //   sweep_dlane=0      the LDS sweep runs pixel-per-lane (plane_sweep_lds_kernel) instead of
 //                      depth-per-lane (plane_sweep_dlane_kernel)
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
@@ -335,21 +335,20 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
 #undef MPIV_ROWSL
         return launched(nm);
     }
-    // vertical tap reuse with D rows in flight, (R, D) by table index: 11: (4, 4), 3: (8, 4),
-    // 4: (6, 3), 5: (9, 3) (the automatic choices), 6: (12, 4), 7: (12, 3), 8: (16, 4), 9: (10, 5), 10: (6, 2),
-    // 11: (4, 4), 12: (3, 3), 13: (4, 2), 14: (5, 5) (A/B only, render_vshare = index)
+    // vertical tap reuse with D rows in flight; render_vshare forces one of the automatic
+    // choices: 3: (R, D) = (8, 4), 4: (6, 3), 5: (9, 3), 11: (4, 4) (the other (R, D) points of
+    // profiles/r02_vshare_ab.txt were A/B builds and are not shipped)
     int vsd = 0;
-    if (fast && vs_opt >= 3 && vs_opt <= 14)
+    if (fast && (vs_opt == 3 || vs_opt == 4 || vs_opt == 5 || vs_opt == 11))
         vsd = vs_opt;
     else if (fast && vs_opt == 0 && !rows_opt && rows_auto == 8)
         vsd = V <= 2 ? 11 : V <= 8 ? 3 : square ? 4 : 5;
     if (vsd) {
-        static const int kR[] = {8, 6, 9, 12, 12, 16, 10, 6, 4, 3, 4, 5};
-        const int R = kR[vsd - 3];
+        const int R = vsd == 3 ? 8 : vsd == 4 ? 6 : vsd == 5 ? 9 : 4;
         const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
         // the counting build (mpiv_render_packed_census) exists for the automatic choices
-        unsigned long long* cn = (g_census && !ct && (vsd <= 5 || vsd == 11)) ? g_census : nullptr;
+        unsigned long long* cn = (g_census && !ct) ? g_census : nullptr;
         if (cn) g_census = nullptr;
 #define MPIV_VSD(R, D)                                                                                              \
     if (ct)                                                                                                        \
@@ -368,15 +367,7 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             case 3: MPIV_VSDC(8, 4); break;
             case 4: MPIV_VSDC(6, 3); break;
             case 5: MPIV_VSDC(9, 3); break;
-            case 6: MPIV_VSD(12, 4); break;
-            case 7: MPIV_VSD(12, 3); break;
-            case 8: MPIV_VSD(16, 4); break;
-            case 9: MPIV_VSD(10, 5); break;
-            case 10: MPIV_VSD(6, 2); break;
-            case 11: MPIV_VSDC(4, 4); break;
-            case 12: MPIV_VSD(3, 3); break;
-            case 13: MPIV_VSD(4, 2); break;
-            default: MPIV_VSD(5, 5); break;
+            default: MPIV_VSDC(4, 4); break;
         }
 #undef MPIV_VSDC
 #undef MPIV_VSD

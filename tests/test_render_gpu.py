@@ -252,7 +252,7 @@ def _variant_env(kopts, mv):
     tap-sharing kernel with two / one planes in flight (A/B); "ring<k>": the LDS-DMA ring
     kernel with tile geometry k (render_ring.hip); "tile<R>": R rows per work-item
     (render_rows_kernel), "tile8vs": with vertical tap sharing."""
-    if mv.startswith("vsd"):  # vertical reuse with 4 / 3 / 3 rows in flight (render_vshare 3 / 4 / 5)
+    if mv.startswith("vsd"):  # vertical reuse, (R, rows in flight) = (8, 4) / (6, 3) / (9, 3) / (4, 4)
         kopts(render_vshare=int(mv[3:]))
         return
     kopts(render_mv=1 if mv == "1" else 0, render_pair={"pair": 1, "pair1": 2}.get(mv, 0),
@@ -261,7 +261,7 @@ def _variant_env(kopts, mv):
           render_vshare=1 if mv.endswith("vs") else 0)
 
 
-RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile8vs", "vsd3", "vsd4", "vsd5", "vsd6", "vsd7", "vsd8", "vsd9", "vsd10", "vsd11", "vsd12", "vsd13", "vsd14",
+RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile8vs", "vsd3", "vsd4", "vsd5", "vsd11",
         "tile16",
         "tile108", "tile116", "tile132"]
 

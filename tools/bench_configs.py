@@ -187,15 +187,7 @@ def c4(dev, it, wu):
                             ("rows x8, vertical reuse, 4 rows in flight", {"render_vshare": 3}),
                             ("rows x6, vertical reuse, 3 rows in flight", {"render_vshare": 4}),
                             ("rows x9, vertical reuse, 3 rows in flight", {"render_vshare": 5}),
-                            ("rows x12, vertical reuse, 4 rows in flight", {"render_vshare": 6}),
-                            ("rows x12, vertical reuse, 3 rows in flight", {"render_vshare": 7}),
-                            ("rows x16, vertical reuse, 4 rows in flight", {"render_vshare": 8}),
-                            ("rows x10, vertical reuse, 5 rows in flight", {"render_vshare": 9}),
-                            ("rows x6, vertical reuse, 2 rows in flight", {"render_vshare": 10}),
                             ("rows x4, vertical reuse, 4 rows in flight", {"render_vshare": 11}),
-                            ("rows x3, vertical reuse, 3 rows in flight", {"render_vshare": 12}),
-                            ("rows x4, vertical reuse, 2 rows in flight", {"render_vshare": 13}),
-                            ("rows x5, vertical reuse, 5 rows in flight", {"render_vshare": 14}),
                             ("rows x4, vertical reuse, 4 rows in flight (again)", {"render_vshare": 11}),
                             ("rows x8, vertical reuse, 4 rows in flight (again)", {"render_vshare": 3}),
                             ("rows x6, vertical reuse, 3 rows in flight (again)", {"render_vshare": 4}),
@@ -300,9 +292,7 @@ def c5(dev, it, wu):
                             ("rows x8, vertical tap reuse", {"render_tile": 8, "render_vshare": 1}),
                             ("rows x8, vertical reuse, 4 rows in flight", {"render_vshare": 3}),
                             ("rows x9, vertical reuse, 3 rows in flight", {"render_vshare": 5}),
-                            ("rows x12, vertical reuse, 3 rows in flight", {"render_vshare": 7}),
                             ("rows x4, vertical reuse, 4 rows in flight", {"render_vshare": 11}),
-                            ("rows x5, vertical reuse, 5 rows in flight", {"render_vshare": 14}),
                             ("rows x8, vertical reuse, 4 rows in flight (again)", {"render_vshare": 3}),
                             ("rows x16 per lane", {"render_tile": 16})):
         with _lib.debug(**opts):
