@@ -1066,20 +1066,29 @@ static int render_u8_impl(const uint32_t* packed, int H, int W, int P, int p_beg
     ug.row = g.Wp * 4;
     ug.org = (kPad * g.Wp + kPad) * 4;
     ug.plane_bytes = (int)(npix * 4);
-    // two rows per work-item: measured faster than 8 for u8 texels at 1, 8 and 125 views and
-    // on the config-5 shard (0.36 vs 0.44 ms single view); render_tile=8 A/B
-    const int R = opt(kOptRenderTile) == 8 ? 8 : 2;
+    // automatic: 4 rows per work-item with vertical tap reuse (the north taps' u8 -> float
+    // conversions are reused too): 8 views 1.93 vs 2.17 ms, 125 views 30.0 vs 33.2 ms, single
+    // view 0.337 vs 0.340, config-5 shard 0.611 vs 0.620 for 2 plain rows (profiles/r02_u8_render.jsonl).
+    // A/B: render_tile=2|8 plain rows; render_tile=4|8 with render_vshare=1: reuse, that many rows
+    const int rt = opt(kOptRenderTile), vso = opt(kOptRenderVshare);
+    const bool vs = (rt == 0 && vso != -1) || (vso == 1 && (rt == 4 || rt == 8));
+    const int R = rt == 0 ? (vs ? 4 : 2) : vs ? rt : rt == 8 ? 8 : 2;
     const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const unsigned* pk = reinterpret_cast<const unsigned*>(packed);
     hipStream_t q = S(stream);
-#define MPIV_U8(CT, RR)                                                                                      \
-    render_u8_kernel<CT, RR><<<(unsigned)nb, 256, 0, q>>>(pk, npix, g, ug, V, p_begin, p_end, CT ? back : 1, \
-                                                          homs, out)
-    if (ct && R == 8) MPIV_U8(true, 8);
-    else if (ct) MPIV_U8(true, 2);
-    else if (R == 8) MPIV_U8(false, 8);
-    else MPIV_U8(false, 2);
+#define MPIV_U8(CT, RR, VV)                                                                                       \
+    render_u8_kernel<CT, RR, VV><<<(unsigned)nb, 256, 0, q>>>(pk, npix, g, ug, V, p_begin, p_end, CT ? back : 1, \
+                                                              homs, out)
+    if (vs) {
+        if (ct && R == 8) MPIV_U8(true, 8, true);
+        else if (ct) MPIV_U8(true, 4, true);
+        else if (R == 8) MPIV_U8(false, 8, true);
+        else MPIV_U8(false, 4, true);
+    } else if (ct && R == 8) MPIV_U8(true, 8, false);
+    else if (ct) MPIV_U8(true, 2, false);
+    else if (R == 8) MPIV_U8(false, 8, false);
+    else MPIV_U8(false, 2, false);
 #undef MPIV_U8
     return launched(nm);
 }

@@ -116,10 +116,120 @@ __device__ __forceinline__ void render_u8_pixels(const unsigned* __restrict__ pl
     }
 }
 
+// The same with vertical tap reuse (render.hip render_rows_vs_pixels on u8 texels): row k's
+// north taps are row k-1's south taps (same clamped offset + one padded row: the same memory
+// words) -- and so are their CONVERTED values, so a continuing row converts 2 taps instead of
+// 4 (the u8 -> RN(u8/255) conversion is most of this kernel's VALU).  North taps are gathered
+// only when some lane of the wave does not continue (wave-uniform branch).
+template <bool CT, bool GUARD, int R>
+__device__ __forceinline__ void render_u8_vs_pixels(const unsigned* __restrict__ planes, int64_t plane_stride,
+                                                    const RenderGeom& g, const U8Geom& ug, int p_begin, int p_end,
+                                                    int back, const float* __restrict__ hv, int x, int y0, float* cr,
+                                                    float* cg, float* cb, float* tt) {
+    static_assert(R % 2 == 0, "R must be even");
+    struct RowU8 {
+        unsigned a, b, c, d;  // NW, NE (own, when not shared), SW, SE texels
+        float wx, wy;
+        int off;
+        bool sh, own;
+    };
+    const float fx = (float)x;
+    const bool replace_first = !CT || back;
+    const int last = p_end - 1;
+    auto hom = [&](int p) { return load_hom(hv + (int64_t)(p < last ? p : last) * 9); };
+    auto issue = [&](int p, int k, const Hom9& h, int prev_off, bool can_share, RowU8& t) {
+        const int q = p < last ? p : last;
+        float px, py;
+        render_pos_fast<GUARD>(h.h, fx, (float)(y0 + k), g, px, py);
+        const float fx0 = floorf(px), fy0 = floorf(py);
+        t.wx = px - fx0;
+        t.wy = py - fy0;
+        const int cx = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)g.W);
+        const int cy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)g.H);
+        const int off = (__mul24(cy, g.Wp) + cx) * 4 + ug.org;
+        t.off = off;
+        t.sh = can_share && off == prev_off + ug.row;
+        const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)q * plane_stride, ug.plane_bytes);
+        t.c = __builtin_bit_cast(unsigned, llvm_raw_buffer_load_f32(r, off + ug.row, 0, 0));
+        t.d = __builtin_bit_cast(unsigned, llvm_raw_buffer_load_f32(r, off + ug.row + 4, 0, 0));
+        t.own = __builtin_amdgcn_ballot_w64(!t.sh) != 0;
+        if (t.own) {  // wave-uniform: some lane needs its own north taps
+            t.a = __builtin_bit_cast(unsigned, llvm_raw_buffer_load_f32(r, t.sh ? kOOB : off, 0, 0));
+            t.b = __builtin_bit_cast(unsigned, llvm_raw_buffer_load_f32(r, (t.sh ? kOOB - 4 : off) + 4, 0, 0));
+        }
+    };
+    // pc, pd: the previous row's converted south taps; sc, sd: this row's (out)
+    auto consume = [&](const RowU8& t, const f32x4& pc, const f32x4& pd, int k, bool first, f32x4& sc,
+                       f32x4& sd) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            sc[c] = u8_unit((t.c >> (8 * c)) & 255u);
+            sd[c] = u8_unit((t.d >> (8 * c)) & 255u);
+        }
+        f32x4 na = pc, nb = pd;
+        if (t.own) {
+            asm volatile("");  // a real wave-uniform branch (render.hip MPIV_VS_ASMBR)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float ua = u8_unit((t.a >> (8 * c)) & 255u), ub = u8_unit((t.b >> (8 * c)) & 255u);
+                na[c] = t.sh ? pc[c] : ua;
+                nb[c] = t.sh ? pd[c] : ub;
+            }
+        }
+        const float ex = 1.0f - t.wx, sy = 1.0f - t.wy;
+        const float nw = sy * ex, ne = sy * t.wx, sw = t.wy * ex, se = t.wy * t.wx;
+        f32x4 s;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {  // blend_taps_u8's fma chain
+            float acc = na[c] * nw;
+            acc = __builtin_fmaf(nb[c], ne, acc);
+            acc = __builtin_fmaf(sc[c], sw, acc);
+            acc = __builtin_fmaf(sd[c], se, acc);
+            s[c] = acc;
+        }
+        const float a = first ? 1.0f : s[3];
+        const float om = 1.0f - a;
+        cr[k] = over(s[0], a, om, cr[k]);
+        cg[k] = over(s[1], a, om, cg[k]);
+        cb[k] = over(s[2], a, om, cb[k]);
+        if (CT) tt[k] = tt[k] * om;
+        asm volatile("" : "+v"(cr[k]), "+v"(cg[k]), "+v"(cb[k]));  // pinned here (render.hip)
+        if (CT) asm volatile("" : "+v"(tt[k]));
+    };
+    RowU8 A, B;
+    f32x4 pc = {0.f, 0.f, 0.f, 0.f}, pd = pc;
+    Hom9 h = hom(p_begin), hn = hom(p_begin + 1);
+    issue(p_begin, 0, h, 0, false, A);
+    for (int p = p_begin; p < p_end; ++p) {
+        const bool first = replace_first && p == p_begin;
+#pragma unroll
+        for (int k = 0; k < R; k += 2) {  // A holds (p, k)
+            issue(p, k + 1, h, A.off, true, B);
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            f32x4 sc, sd;
+            consume(A, pc, pd, k, first, sc, sd);
+            pc = sc;
+            pd = sd;
+            if (k + 2 < R)
+                issue(p, k + 2, h, B.off, true, A);
+            else
+                issue(p + 1, 0, hn, 0, false, A);  // past the end: the last plane again (cached, unused)
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            consume(B, pc, pd, k + 1, first, sc, sd);
+            pc = sc;
+            pd = sd;
+        }
+        h = hn;
+        hn = hom(p + 2);
+    }
+}
+
 // render_rows_kernel's contract on the packed u8 layout (FAST recipe: H, W >= 2): a
 // 256-thread block = 64 x 4R tile, XCD-aware (tile, view) order, tile-level division
 // proof; a tile where the proof fails runs the per-sample guarded recipe (GUARD).
-template <bool CT, int R>
+template <bool CT, int R, bool VS = false>
 __global__ __launch_bounds__(256) void render_u8_kernel(const unsigned* __restrict__ planes, int64_t plane_stride,
                                                         RenderGeom g, U8Geom ug, int V, int p_begin, int p_end,
                                                         int back, const float* __restrict__ homs,
@@ -148,7 +258,12 @@ __global__ __launch_bounds__(256) void render_u8_kernel(const unsigned* __restri
         cr[k] = -0.0f; cg[k] = -0.0f; cb[k] = -0.0f; tt[k] = 1.0f;  // render_packed_pixel: plane 0 replaces
     }
     if (proven) {
-        render_u8_pixels<CT, false, R>(planes, plane_stride, g, ug, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
+        if constexpr (VS)
+            render_u8_vs_pixels<CT, false, R>(planes, plane_stride, g, ug, p_begin, p_end, back, hv, x, y0, cr, cg, cb,
+                                              tt);
+        else
+            render_u8_pixels<CT, false, R>(planes, plane_stride, g, ug, p_begin, p_end, back, hv, x, y0, cr, cg, cb,
+                                           tt);
     } else {  // rare (w near 0 over the tile): the guarded recipe two rows at a time (few VGPRs)
 #pragma unroll
         for (int k = 0; k < R; k += 2)

@@ -28,12 +28,21 @@ def _u8_to_float(u8: np.ndarray) -> np.ndarray:
     return u8.astype(np.float32) / np.float32(255.0)  # correctly rounded fp32 division
 
 
-@pytest.mark.parametrize("rows", [0, 2, 8])
+
+def _rows_opts(kopts, rows):
+    """rows: 2 / 8 rows per lane, or "4vs" / "8vs": that many with vertical tap reuse (A/B)."""
+    if isinstance(rows, str):
+        kopts(render_tile=int(rows[:-2]), render_vshare=1)
+    else:
+        kopts(render_tile=rows)
+
+
+@pytest.mark.parametrize("rows", [0, 2, 8, "4vs", "8vs"])
 def test_u8_render_reference_test_mpi(rows, large, meta, dev, kopts):
     """Config 1: the reference's 10-plane uint8 test MPI, two poses, against the goldens
     the reference produced from u8 / 255 (tools/gen_goldens.py)."""
     if rows:
-        kopts(render_tile=rows)
+        _rows_opts(kopts, rows)
     u8 = _test_mpi_u8().to(dev)
     pose = torch.tensor(large["c1_pose"]).to(dev)
     K = torch.tensor(large["c1_K"]).to(dev)
@@ -59,12 +68,12 @@ def _extreme_case(V, H, W, P, seed):
     return u8, homs
 
 
-@pytest.mark.parametrize("rows", [2, 8])
+@pytest.mark.parametrize("rows", [2, 8, "4vs", "8vs"])
 @pytest.mark.parametrize("shape", [(70, 150, 9), (37, 203, 7), (64, 66, 16)])
 def test_u8_render_random_vs_oracle(rows, shape, dev, kopts):
     """Random bytes (every value 0..255 occurs), odd sizes, partial tiles, planes partly
     behind the camera: bit-exact vs the oracle on u8 / 255."""
-    kopts(render_tile=rows)
+    _rows_opts(kopts, rows)
     H, W, P = shape
     V = 7
     u8, homs = _extreme_case(V, H, W, P, seed=H * W + P)
@@ -76,11 +85,11 @@ def test_u8_render_random_vs_oracle(rows, shape, dev, kopts):
     assert_bits(_lib.render_packed(_lib.pack_planes(fl[0].to(dev)), homs).cpu().numpy(), want, "float path")
 
 
-@pytest.mark.parametrize("rows", [2, 8])
+@pytest.mark.parametrize("rows", [2, 8, "4vs", "8vs"])
 def test_u8_ct_partials(rows, dev, kopts):
     """Plane-range (C, T) partials of a u8 MPI equal the oracle's; their ordered combine
     equals the sequential render within 1e-5 (north_star)."""
-    kopts(render_tile=rows)
+    _rows_opts(kopts, rows)
     H, W, P, V = 45, 130, 11, 4
     u8, homs = _extreme_case(V, H, W, P, seed=5)
     full = np.broadcast_to(_u8_to_float(u8.numpy()), (V, H, W, P, 4)).copy()

@@ -256,7 +256,9 @@ def u8(dev, it, wu):
                                          configs.f32([c["K"]] * V), V).to(dev)
         out = torch.empty((V, H, W, 3), device=dev)
         for label, opts in (("default routing", {}), ("2 rows per lane", {"render_tile": 2}),
-                            ("8 rows per lane", {"render_tile": 8})):
+                            ("8 rows per lane", {"render_tile": 8}),
+                            ("4 rows, vertical tap reuse", {"render_tile": 4, "render_vshare": 1}),
+                            ("8 rows, vertical tap reuse", {"render_tile": 8, "render_vshare": 1})):
             with _lib.debug(**opts):
                 ms, mn = timed(lambda: _lib.render_packed_u8(packed, homs, out), it if V < 125 else 3, 1)
             report(f"u8 c4 1024^2x128 u8 texels, {label}, {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
@@ -268,7 +270,9 @@ def u8(dev, it, wu):
     homs = _host.render_homographies(configs.f32(c5c["poses"]), configs.f32(c5c["depths"]),
                                      configs.f32([c5c["K"]]), 1)[:, :PL].contiguous().to(dev)
     ct = torch.empty((1, H, W, 4), device=dev)
-    for label, opts in (("default routing", {}), ("8 rows per lane", {"render_tile": 8})):
+    for label, opts in (("default routing", {}), ("8 rows per lane", {"render_tile": 8}),
+                        ("4 rows, vertical tap reuse", {"render_tile": 4, "render_vshare": 1}),
+                        ("8 rows, vertical tap reuse", {"render_tile": 8, "render_vshare": 1})):
         with _lib.debug(**opts):
             ms, mn = timed(lambda: _lib.render_packed_u8_ct(packed, homs, back=True, out=ct), it, wu)
         report(f"u8 c5 plane shard: {PL} of {P} planes, 4096x2160 u8 texels, (C,T), {label}", ms, mn,
