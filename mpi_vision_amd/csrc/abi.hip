@@ -1070,8 +1070,14 @@ static int render_u8_impl(const uint32_t* packed, int H, int W, int P, int p_beg
     // conversions are reused too): 8 views 1.93 vs 2.17 ms, 125 views 30.0 vs 33.2 ms, single
     // view 0.337 vs 0.340, config-5 shard 0.611 vs 0.620 for 2 plain rows (profiles/r02_u8_render.jsonl).
     // A/B: render_tile=2|8 plain rows; render_tile=4|8 with render_vshare=1: reuse, that many rows
+    // Stretched MPIs (swapped x/(H-1) normalisation) take it only when the launch fills the chip
+    // (>= 2048 tiles of 64x32, as the float route): config 2 at one view 0.080-0.089 vs 0.065 ms
+    // for 2 plain rows, at 64 views 2.35 vs 2.40-2.49.
+    const float sxr = (float)W / (float)(H - 1), syr = (float)H / (float)(W - 1);
+    const bool square = sxr >= 0.8f && sxr <= 1.25f && syr >= 0.8f && syr <= 1.25f;
+    const bool big = (int64_t)blocks(W, kTileX) * blocks(H, 4 * 8) * V >= 2048;
     const int rt = opt(kOptRenderTile), vso = opt(kOptRenderVshare);
-    const bool vs = (rt == 0 && vso != -1) || (vso == 1 && (rt == 4 || rt == 8));
+    const bool vs = (rt == 0 && vso != -1 && (square || big)) || (vso == 1 && (rt == 4 || rt == 8));
     const int R = rt == 0 ? (vs ? 4 : 2) : vs ? rt : rt == 8 ? 8 : 2;
     const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);

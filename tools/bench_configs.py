@@ -277,6 +277,23 @@ def u8(dev, it, wu):
             ms, mn = timed(lambda: _lib.render_packed_u8_ct(packed, homs, back=True, out=ct), it, wu)
         report(f"u8 c5 plane shard: {PL} of {P} planes, 4096x2160 u8 texels, (C,T), {label}", ms, mn,
                PL * H * W * 4 + H * W * 16, H * W / 1e6)
+    del packed
+    c2c = configs.config2()  # a stretched MPI (x step W/(H-1) = 1.78), small and large launches
+    H, W, P = c2c["H"], c2c["W"], c2c["P"]
+    packed = _lib.synth_mpi_packed_u8(0, H, W, 0, P, dev)
+    per_view = P * H * W * 4 + H * W * 12
+    V2 = len(c2c["poses"])
+    homs_all = _host.render_homographies(configs.f32(c2c["poses"]), configs.f32(c2c["depths"]),
+                                         configs.f32([c2c["K"]] * V2), V2).to(dev)
+    for V in (1, 8, V2):
+        homs = homs_all[:V].contiguous()
+        out = torch.empty((V, H, W, 3), device=dev)
+        for label, opts in (("default routing", {}), ("2 rows per lane", {"render_tile": 2}),
+                            ("4 rows, vertical tap reuse", {"render_tile": 4, "render_vshare": 1}),
+                            ("2 rows per lane (again)", {"render_tile": 2})):
+            with _lib.debug(**opts):
+                ms, mn = timed(lambda: _lib.render_packed_u8(packed, homs, out), it, wu)
+            report(f"u8 c2 {W}x{H}x{P} u8 texels, {label}, {V} views/launch", ms, mn, V * per_view, V * H * W / 1e6)
 
 
 def c5(dev, it, wu):
