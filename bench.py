@@ -2,38 +2,57 @@
 """Headline benchmark: rendered Mpix/s of the fused MPI warp + over-composite on
 BASELINE.json config 4 (128-plane 1024x1024 MPI, 1000-pose camera path,
 view-sharded), with the dominant kernel's roofline and the CPU restatement timed on
-the same host, plus a config-5 leg (256-plane 4096x2160 MPI, plane-sharded).
+the same host, plus one leg per other BASELINE config and the notebook's own shape.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--views V] [--no-config5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--views V] [--legs c4,sv,...]
 
-One process per GPU (torchrun for N > 1).  Each rank holds a full MPI replica in
-HBM (packed plane-major once, outside the timed region) and every step renders
-V views of the camera path (rank r renders path poses r*V .. r*V+V-1 modulo the
-path), so per-GPU work is fixed as N grows ("weak"); at N = 8 and V = 125 one step
-is exactly the 1000-pose path.  There is no collective on the data path.
+Launch.  One process per GPU.  `--gpus N > 1` without a torchrun environment starts
+N ranks itself (a `torch.distributed.run` child, before this process touches the GPU)
+and exits with its status; with WORLD_SIZE set (the driver's own torchrun launch) it
+must equal --gpus.  Ranks talk over RCCL ("nccl"); MPIV_BENCH_BACKEND=gloo +
+MPIV_BENCH_ONE_DEVICE=1 rehearse the multi-rank logic on a one-GPU box.
 
-Per step (inside the timed region): host-side homographies for the NEXT step
-(torch-CPU fp32, the reference's op order) overlap the current launch; then one
-render launch writes V frames [V,1024,1024,3] fp32 that stay in HBM.
+Headline (config 4, "weak").  Each rank holds a full MPI replica in HBM (packed
+plane-major once, outside the timed region) and every step renders V views of the
+camera path (rank r renders path poses r*V .. r*V+V-1 modulo the path), so per-GPU
+work is fixed as N grows; at N = 8 and V = 125 one step is exactly the 1000-pose path.
+There is no collective on the data path.  Per step (inside the timed region):
+host-side homographies for the NEXT step (the reference's torch-CPU fp32 op order)
+overlap the current launch; then one render launch writes V frames [V,1024,1024,3]
+fp32 that stay in HBM.
 
 Roofline.  The V views of one launch share one MPI, so the texels
-they gather come from L2 (hit rate ~0.99): what bounds the kernel is the vector-memory
-("texture") path that serves the gathers, not HBM.  `roofline` therefore prices the
-launch against that path: bytes = the 16-B gather instructions the launch issues x 1 KiB
-(four per plane-sample for the direct kernel; fewer with the rows kernel's vertical tap
-reuse, counted live by its census build), peak = the gather rate the same device reaches
-with the render's access shape (mpiv_probe_gather, measured live).  HBM is reported separately, with fractions
-that cannot exceed 1: `hbm_traffic_frac` (PMC bytes actually moved per launch, from the
-committed rocprofv3 summary of this same command, only if its build id / kernel / shape
-match) and `single_view` (one view per launch: every texel is read once, so its
-algorithmic bytes P*H*W*16 + H*W*12 really cross HBM -- the north-star 0.60 bar).
+they gather come from L2: what bounds the launch is the vector-memory ("texture")
+path that serves the gathers, not HBM.  `roofline` prices the launch against that
+path: bytes = the 16-B gather instructions the launch issues x 1 KiB (counted live by
+the kernel's census build), peak = the gather rate the same device reaches with the
+render's access shape (mpiv_probe_gather, measured live: a TA ceiling, not a spec
+peak).  HBM is reported per leg with fractions that cannot exceed 1: `single_view`
+(one view per launch: every texel crosses HBM once, the north-star 0.60 bar), the
+PSV (config 3) and the config-5 shard.
+
+rocprofv3 evidence.  tools/profile.sh runs this script under rocprofv3 and
+tools/parse_prof.py groups the dispatches by (kernel, grid size) into
+profiles/prof_summary.json, tagged with the library build id.  Every leg names the
+kernel and grid its launch routes to (mpiv_route) and, when the summary's build id
+matches this library, quotes rocprof's average duration and the PMC HBM traffic of
+exactly those dispatches next to its own HIP-event time.
+
+Legs (--legs, default all): c4 (headline), sv (single view), c2 (config 2: 64 views
+of a 1024x576x32 MPI), c3 (config 3: PSV of 5 sources into 64 planes through
+plane_sweep_torch), nb (the notebook's 224x224x10 render + training step + PSV),
+train (config-4-size training forward + backward), c5 (config 5, plane-sharded),
+cpu (the CPU baseline, rank 0 at N = 1).
 """
 from __future__ import annotations
 
 import argparse
 import hashlib
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -48,6 +67,11 @@ from mpi_vision_amd import _host, _lib, configs, parallel  # noqa: E402
 METRIC = "rendered Mpix/sec (node) + achieved HBM GB/s fraction, 1024²×128-plane MPI"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 kWaveBytes = 64 * 16   # one 64-lane 16-B gather instruction
+ALL_LEGS = ("c4", "sv", "c2", "c3", "nb", "train", "c5", "cpu")
+# SURVEY.md §6 / BASELINE.md: the reference utils.py on torch-CPU (MKL), 8 Xeon cores,
+# measured in the survey container (the reference cannot run on the GPU box)
+REF_CPU = {"c4_Mpix_s": 0.37, "c4_s_per_view": 2.8727, "c3_s": 5.858, "c2_proxy_Mpix_s": 1.49,
+           "cores": 8, "source": "SURVEY.md §6: reference utils.py on torch 2.10 CPU, 8 Xeon cores, survey container"}
 
 
 def parse():
@@ -57,26 +81,49 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--views", type=int, default=125, help="views rendered per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
-    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 plane-sharded leg")
-    ap.add_argument("--no-training", action="store_true",
-                    help="skip the training (render backward) leg: its gated cooperative fallback launch makes "
-                         "rocprofv3 --kernel-trace crash in its own teardown (DESIGN.md section 7)")
-    ap.add_argument("--no-extras", action="store_true",
-                    help="only the timed config-4 launches (rocprofv3 runs: tools/profile.sh), no frame check, "
-                         "single-view leg, gather probe or config-5 leg")
-    ap.add_argument("--kernel", choices=["packed", "packed_mv", "packed_lds", "native"], default="packed",
-                    help="packed: direct-gather kernel on the packed MPI (default); packed_mv: multi-view "
-                         "LDS kernel (A/B); packed_lds: single-view LDS variant (A/B); native: reference "
-                         "layout read in place")
-    return ap.parse_args()
+    ap.add_argument("--legs", default=",".join(ALL_LEGS), help="comma list of " + ",".join(ALL_LEGS))
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 leg")
+    ap.add_argument("--no-training", action="store_true", help="skip the training leg")
+    ap.add_argument("--no-extras", action="store_true", help="only the timed config-4 launches")
+    ap.add_argument("--kernel", choices=["packed", "native"], default="packed",
+                    help="packed: the production packed-MPI route (default); native: the reference layout "
+                         "read in place (mpiv_render)")
+    a = ap.parse_args()
+    legs = [x for x in a.legs.split(",") if x]
+    bad = [x for x in legs if x not in ALL_LEGS]
+    if bad:
+        ap.error(f"unknown legs {bad}")
+    if a.no_extras:
+        legs = [x for x in legs if x == "c4"]
+    if a.no_config5:
+        legs = [x for x in legs if x != "c5"]
+    if a.no_training:
+        legs = [x for x in legs if x != "train"]
+    if a.cpu_seconds <= 0:
+        legs = [x for x in legs if x != "cpu"]
+    a.legs = legs
+    return a
+
+
+def spawn_ranks(n: int) -> int:
+    """--gpus N > 1 outside torchrun: run this script as N ranks under a
+    torch.distributed.run child (127.0.0.1 rendezvous on a free port) and wait.  Called
+    before anything touches the GPU; rank 0's JSON line reaches stdout directly."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
 def dist_setup(args):
-    """One process per GPU (torchrun env).  MPIV_BENCH_BACKEND=gloo + MPIV_BENCH_ONE_DEVICE=1
-    rehearse the multi-rank logic on a single-GPU box (all ranks on cuda:0, CPU collectives)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     local = 0 if os.environ.get("MPIV_BENCH_ONE_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", "0"))
+    backend = None
     if world > 1:
         torch.cuda.set_device(local)
         import torch.distributed as dist
@@ -85,7 +132,9 @@ def dist_setup(args):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    return world, rank, torch.device("cuda", local)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    return world, rank, torch.device("cuda", local), backend
 
 
 def max_over_ranks(x: float, world: int, dev) -> float:
@@ -98,27 +147,77 @@ def max_over_ranks(x: float, world: int, dev) -> float:
     return float(t.item())
 
 
+def all_ranks(x: float, world: int, dev) -> list:
+    if world == 1:
+        return [x]
+    import torch.distributed as dist
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.float64, device=dev if on_dev else "cpu")
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
+
+
 def barrier(world):
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
 
 
-def load_pmc(profile_dir: str, kernel: str, views: int, shape):
-    """The committed rocprofv3 PMC summary of this bench command (tools/profile.sh ->
-    tools/parse_pmc.py -> profiles/render_pmc.json), or None unless it was taken from the
-    same library build (source hash), kernel, views per launch and MPI shape."""
-    path = os.path.join(profile_dir, "render_pmc.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        d = json.load(f)
-    want = {"build_id": _lib.load().mpiv_build_id().decode(), "kernel": kernel, "views": views,
-            "shape": list(shape)}
-    if any(d.get(k) != v for k, v in want.items()):
-        return None
-    return d
+# ---------------------------------------------------------------------------
+# rocprofv3 evidence (tools/profile.sh -> tools/parse_prof.py)
+# ---------------------------------------------------------------------------
 
+_PROF = None
+
+
+def prof_summary():
+    """profiles/prof_summary.json when it was taken from this library build, else None."""
+    global _PROF
+    if _PROF is None:
+        path = os.path.join(REPO, "profiles", "prof_summary.json")
+        _PROF = {}
+        if os.path.exists(path):
+            with open(path) as f:
+                d = json.load(f)
+            if d.get("build_id") == _lib.load().mpiv_build_id().decode():
+                _PROF = d
+    return _PROF or None
+
+
+def prof_for(kernel: str, grid: int):
+    """The summary's entry for the dispatches of `kernel` with `grid` work-items."""
+    d = prof_summary()
+    if not d:
+        return None
+    for e in d.get("launches", []):
+        if e["kernel"] == kernel and e["grid"] == grid:
+            return e
+    return None
+
+
+def prof_fields(kernel: str, grid: int, alg_bytes: float, ms: float):
+    """rocprof average and PMC traffic of this leg's launch, with the ratios the verdict
+    recomputes: rocprof ms vs the bench's own HIP-event ms, HBM traffic vs algorithmic bytes."""
+    e = prof_for(kernel, grid)
+    res = {"kernel": kernel, "grid_workitems": grid,
+           "prof_source": "profiles/prof_summary.json (same build id)" if e else "no rocprof summary of this build"}
+    if e:
+        res["rocprof_avg_ms"] = round(e["avg_ns"] / 1e6, 4)
+        res["rocprof_calls"] = e["calls"]
+        if e.get("hbm_bytes") is not None:
+            res["traffic"] = e["hbm_bytes"]
+            res["traffic_over_alg"] = round(e["hbm_bytes"] / alg_bytes, 3)
+            res["traffic_frac"] = round(e["hbm_bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        for k in ("fetch_kib", "write_kib", "l2_hit_rate", "ta_busy_frac", "valu_issue_frac"):
+            if e.get(k) is not None:
+                res[k] = e[k]
+    return res
+
+
+# ---------------------------------------------------------------------------
+# timing helpers
+# ---------------------------------------------------------------------------
 
 def event_ms(fn, n, stream):
     """Average device time of fn() over n calls, HIP events on the launch stream."""
@@ -131,24 +230,77 @@ def event_ms(fn, n, stream):
     return float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
 
+def span_ms(fn, n, stream):
+    """Device time of n back-to-back calls / n (host work between launches overlaps)."""
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(n):
+        fn()
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / n
+
+
 def gather_peak_gbs(dev, stream):
     """The texture path's gather ceiling on this device (mpiv_probe_gather: 16-B-per-lane
     buffer loads with the render's access shape from an L1/L2-resident window)."""
     window = torch.zeros(4096, device=dev)
     sink = torch.zeros(4, device=dev)
     blocks, iters = 2048, 2048
-    fn = lambda: _lib._call("mpiv_probe_gather", window, iters, blocks, sink, _lib._stream(dev))  # noqa: E731
+    fn = lambda: _lib._call("mpiv_probe_gather", window, window.numel() * 4, iters, blocks, sink,  # noqa: E731
+                            _lib._stream(dev))
     fn()
     ms = event_ms(fn, 5, stream)
     return blocks * 256 * iters * 128 / (ms * 1e-3) / 1e9
 
 
-def cpu_baseline(mpi_dev: torch.Tensor, homs_all: torch.Tensor, budget_s: float, check_frames):
-    """The oracle's C restatement (bit-exact to the reference) on this host's cores,
-    on a bounded sample: whole views of the same MPI, as many as fit ~budget_s."""
+def sha16(t: torch.Tensor) -> str:
+    return hashlib.sha256(t.detach().cpu().contiguous().numpy().tobytes()).hexdigest()[:16]
+
+
+def gen_view(H, W, P, seed, dev):
+    """Synthetic MPI view [H,W,P,4] on the device: rgb U[-1,1), alpha U[0,1), plane-0 alpha 1."""
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    v = torch.rand((H, W, P, 4), generator=gen, device=dev, dtype=torch.float32)
+    v[..., :3].mul_(2.0).sub_(1.0)
+    v[:, :, 0, 3] = 1.0
+    return v
+
+
+def hbm(alg_bytes, ms):
+    gbs = alg_bytes / (ms * 1e-3) / 1e9
+    return round(gbs, 1), round(gbs / HBM_PEAK_GBS, 4)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline
+# ---------------------------------------------------------------------------
+
+def host_cores():
+    """(threads to use, description): the cores this process may run on (affinity, cgroup
+    CPU quota) -- the box's CPU share -- capped by OMP_NUM_THREADS when the box sets it."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    usable = min(aff, quota) if quota else aff
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(usable, omp) if omp > 0 else usable
+    return threads, {"host_nproc": nproc, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                     "omp_num_threads_env": omp or None, "threads_used": threads}
+
+
+def cpu_baseline(view_dev: torch.Tensor, homs_all: torch.Tensor, budget_s: float, check_frames):
+    """The oracle's C restatement (bit-exact to the reference) on this host's cores, on a
+    bounded sample: whole views of the same MPI, as many as fit ~budget_s."""
     from oracle import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    mpi = mpi_dev.cpu().numpy()[None]          # [1,H,W,P,4]
+    threads, cores = host_cores()
+    mpi = view_dev.cpu().numpy()[None]          # [1,H,W,P,4]
     H, W = mpi.shape[1], mpi.shape[2]
     views, t_total, outs = 0, 0.0, []
     while views == 0 or (t_total < budget_s and views < homs_all.shape[0]):
@@ -158,18 +310,163 @@ def cpu_baseline(mpi_dev: torch.Tensor, homs_all: torch.Tensor, budget_s: float,
         t_total += time.perf_counter() - t0
         outs.append(o)
         views += 1
-    mism = 0
-    for i, o in enumerate(outs[:len(check_frames)]):
-        if not np.array_equal(o, check_frames[i]):
-            mism += 1
+    mism = sum(1 for i, o in enumerate(outs[:len(check_frames)]) if not np.array_equal(o, check_frames[i]))
     return {"value": views * H * W / 1e6 / t_total, "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "sample": f"{views} full view(s) of the 1024x1024x128 MPI with the oracle's C restatement "
-                      f"(oracle/mpiv_oracle.c, {threads} OpenMP threads), {t_total:.1f} s",
-            "gpu_frames_bit_exact_vs_cpu": mism == 0}
+            "sample": f"{views} full view(s) of the config-4 1024x1024x128 MPI (camera-path poses 0..{views - 1}) "
+                      f"with the oracle's C restatement (oracle/mpiv_oracle.c, {threads} OpenMP threads), "
+                      f"{t_total:.1f} s",
+            "host": cores, "gpu_frames_bit_exact_vs_cpu": mism == 0,
+            "reference_cpu": {"value": REF_CPU["c4_Mpix_s"], "unit": "Mpix/s", "cores": REF_CPU["cores"],
+                              "s_per_view": REF_CPU["c4_s_per_view"], "source": REF_CPU["source"]}}
 
 
-def sha16(t: torch.Tensor) -> str:
-    return hashlib.sha256(t.detach().cpu().contiguous().numpy().tobytes()).hexdigest()[:16]
+# ---------------------------------------------------------------------------
+# legs
+# ---------------------------------------------------------------------------
+
+def single_view_leg(packed, H, W, P, h_sv, dev, stream):
+    """One view per launch (every texel crosses HBM once): the north-star HBM bar."""
+    one = torch.empty((1, H, W, 3), device=dev)
+    launch = lambda: _lib._call("mpiv_render_packed", packed, H, W, P, h_sv, 1, one, _lib._stream(dev))  # noqa: E731
+    for _ in range(50):  # ~20 ms of untimed launches: the clocks leave their idle state first
+        launch()
+    ms = event_ms(launch, 20, stream)
+    alg = P * H * W * 16 + H * W * 12
+    gbs, frac = hbm(alg, ms)
+    kname, grid = _lib.route("render_packed", H, W, P, 1)
+    res = {"workload": "config 4 MPI, one view per launch", "kernel_ms": round(ms, 4), "alg_bytes": alg,
+           "alg_def": "P*H*W*16 + H*W*12", "achieved_gbs": gbs, "peak": HBM_PEAK_GBS, "frac": frac, "bound": "hbm"}
+    res.update(prof_fields(kname, grid, alg, ms))
+    return res
+
+
+def config2_leg(dev, stream, n=20):
+    """BASELINE config 2: a 32-plane 1024x576 MPI broadcast to 64 target views, one launch
+    of all 64 from the packed MPI (the drop-in packs a stride-0 batch once)."""
+    c = configs.config2()
+    H, W, P = c["H"], c["W"], c["P"]
+    V = len(c["poses"])
+    packed = _lib.pack_planes(gen_view(H, W, P, c["seed"], dev))
+    homs = _host.render_homographies(configs.f32(c["poses"]), configs.f32(c["depths"]),
+                                     configs.f32([c["K"]] * V), V).to(dev)
+    out = torch.empty((V, H, W, 3), device=dev)
+    launch = lambda: _lib._call("mpiv_render_packed", packed, H, W, P, homs, V, out, _lib._stream(dev))  # noqa: E731
+    for _ in range(3):
+        launch()
+    ms = event_ms(launch, n, stream)
+    alg = V * (P * H * W * 16 + H * W * 12)
+    gbs, frac = hbm(alg, ms)
+    kname, grid = _lib.route("render_packed", H, W, P, V)
+    res = {"workload": "BASELINE config 2: 32-plane 1024x576 MPI, 64 target views in one launch",
+           "kernel_ms": round(ms, 4), "Mpix_per_s": round(V * H * W / 1e6 / (ms * 1e-3), 1),
+           "baseline_bar_Mpix_s": 9160, "alg_bytes": alg, "alg_def": "V*(P*H*W*16 + H*W*12) (SURVEY §8d)",
+           "alg_gbs": gbs, "alg_frac": frac,
+           "alg_frac_note": "the 64 views share one MPI through L2, so the per-view formula can exceed 1 of HBM"}
+    res.update(prof_fields(kname, grid, alg, ms))
+    del packed, out
+    return res
+
+
+def config3_leg(dev, stream, n=20):
+    """BASELINE config 3: plane-sweep volume of 5 source 1024x768 images into 64 planes through
+    the drop-in plane_sweep_torch (host Ki/proj + one mpiv_plane_sweep launch), and that
+    launch alone."""
+    import mpi_vision_amd as mv
+    c = configs.config3()
+    S, H, W, D = c["S"], c["H"], c["W"], c["D"]
+    g = torch.Generator(device=dev).manual_seed(c["seed"])
+    img = torch.rand((S, H, W, 3), generator=g, device=dev)
+    K = configs.f32([c["K"]] * S).to(dev)
+    pose = configs.f32(c["poses"]).to(dev)
+    depths = list(c["depths"])
+    vol = mv.plane_sweep_torch(img, depths, pose, K)
+    for _ in range(3):
+        mv.plane_sweep_torch(img, depths, pose, K)
+    dropin_ms = span_ms(lambda: mv.plane_sweep_torch(img, depths, pose, K), n, stream)
+    ki, proj = _host.psv_matrices(K.cpu(), K.cpu(), pose.cpu())
+    ki, proj = ki.to(dev), proj.to(dev)
+    dd = configs.f32(depths).to(dev)
+    out = torch.empty((S, H, W, D * 3), device=dev)
+    launch = lambda: _lib._call("mpiv_plane_sweep", img, _lib._strides(img), S, H, W, 3, ki, proj, dd, D, H, W,  # noqa: E731
+                                out, _lib._stream(dev))
+    launch()
+    same = bool(torch.equal(out.view(torch.int32), vol.view(torch.int32)))
+    ms = event_ms(launch, n, stream)
+    alg = S * H * W * 12 + S * D * H * W * 12
+    gbs, frac = hbm(alg, ms)
+    kname, grid = _lib.route("plane_sweep", S, H, W, 3, D, H, W)
+    res = {"workload": "BASELINE config 3: PSV of 5 source 1024x768x3 images into 64 depth planes "
+                       "(plane_sweep_torch, utils.py:452-471)",
+           "kernel_ms": round(ms, 4), "dropin_ms": round(dropin_ms, 4),
+           "Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1),
+           "alg_bytes": alg, "alg_def": "S*Hs*Ws*C*4 + S*D*Ht*Wt*C*4 (SURVEY §8d)", "achieved_gbs": gbs,
+           "peak": HBM_PEAK_GBS, "frac": frac, "bound": "hbm", "baseline_bar_ms": 0.64,
+           "dropin_equals_kernel": same,
+           "reference_cpu": {"s": REF_CPU["c3_s"], "cores": REF_CPU["cores"], "source": REF_CPU["source"]}}
+    res.update(prof_fields(kname, grid, alg, ms))
+    del img, out, vol
+    return res
+
+
+def notebook_leg(dev, stream, n=50):
+    """The reference's only real caller at its own size (fast-torch-stereo-vision.ipynb
+    cell 8 L89-90: img_size 224, num_planes 10, bs 1): the dataset's PSV
+    (plane_sweep_torch_one at inv_depths(1, 100, 10), cell 8 L73-75), the loss's render
+    (mpi_render_view_torch, cell 12 L42) and the render's training step (forward with
+    autograd + backward), all through the drop-in functions."""
+    import mpi_vision_amd as mv
+    S = N = 224
+    P = 10
+    depths = mv.inv_depths(1, 100, P)
+    f = configs.focal_from_fov(N)
+    K = configs.f32(configs.intrinsics_matrix(f, f, N / 2.0, N / 2.0)).to(dev)
+    pose = configs.f32(configs.pose_from(configs.rot_y(1.0), (0.05, -0.02, 0.03))).to(dev)
+    g = torch.Generator(device=dev).manual_seed(5)
+    img = torch.rand((S, N, 3), generator=g, device=dev)
+    psv = lambda: mv.plane_sweep_torch_one(img, depths, pose, K)  # noqa: E731
+    for _ in range(5):
+        psv()
+    psv_ms = span_ms(psv, n, stream)
+    ki, proj = _host.psv_matrices(K.cpu()[None], K.cpu()[None], pose.cpu()[None])
+    ki, proj = ki.to(dev), proj.to(dev)
+    dd = configs.f32(depths).to(dev)
+    out = torch.empty((1, S, N, P * 3), device=dev)
+    img4 = img[None]
+    launch = lambda: _lib._call("mpiv_plane_sweep", img4, _lib._strides(img4), 1, S, N, 3, ki, proj, dd, P, S, N,  # noqa: E731
+                                out, _lib._stream(dev))
+    launch()
+    psv_kernel_ms = event_ms(launch, n, stream)
+    psv_alg = S * N * 12 + P * S * N * 12
+    mpi = configs.synthetic_mpi(1, S, N, P, 9).to(dev)
+    planes = configs.f32(depths).to(dev)
+    poses = pose[None]
+    Kb = K[None]
+    rend = lambda: mv.mpi_render_view_torch(mpi, poses, planes, Kb)  # noqa: E731
+    for _ in range(5):
+        rend()
+    render_ms = span_ms(rend, n, stream)
+    leaf = mpi.clone().requires_grad_(True)
+    dout = torch.rand((1, S, N, 3), generator=g, device=dev)
+
+    def train_step():
+        o = mv.mpi_render_view_torch(leaf, poses, planes, Kb)
+        o.backward(dout)
+        leaf.grad = None
+    for _ in range(5):
+        train_step()
+    train_ms = span_ms(train_step, n, stream)
+    kname, grid = _lib.route("plane_sweep", 1, S, N, 3, P, S, N)
+    r_alg = P * S * N * 16 + S * N * 12
+    res = {"workload": "notebook shape (ipynb cell 8 L89-90): 224x224, 10 planes, bs 1",
+           "psv_dropin_ms": round(psv_ms, 4), "psv_kernel_ms": round(psv_kernel_ms, 4),
+           "psv_alg_bytes": psv_alg, "psv_frac": hbm(psv_alg, psv_kernel_ms)[1],
+           "render_dropin_ms": round(render_ms, 4), "render_alg_bytes": r_alg,
+           "train_step_ms": round(train_ms, 4),
+           "train_step_def": "mpi_render_view_torch forward (autograd, checkpoints) + backward through the drop-in",
+           "note": "8 MB of texels: launch-latency-bound at this size", "psv": prof_fields(kname, grid, psv_alg,
+                                                                                             psv_kernel_ms)}
+    del mpi, leaf, out
+    return res
 
 
 def training_leg(dev, stream, n=10):
@@ -188,6 +485,7 @@ def training_leg(dev, stream, n=10):
     ws = torch.empty(_lib.load().mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
     _, ck = _lib.render_train(mpi, homs)
     fwd_ms = event_ms(lambda: _lib.render_train(mpi, homs), n, stream)
+    inf_ms = event_ms(lambda: _lib.render(mpi, homs), n, stream)
     g1 = _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)
     bwd_ms = event_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck), n, stream)
     g2 = _lib.render_backward(mpi, homs, dout, workspace=ws)
@@ -195,14 +493,19 @@ def training_leg(dev, stream, n=10):
     flag = int(ws[_lib.bwd_flag_offset(H, W, P):][:4].view(torch.int32).item())
     same = bool(torch.equal(g1.view(torch.int32), g2.view(torch.int32)))
     mpi_bytes = P * H * W * 16
+    f_alg = mpi_bytes + H * W * 12
+    b_alg = 2 * mpi_bytes + H * W * 12
+    kname, grid = _lib.route("render", 1, H, W, P)
     res = {"workload": "BASELINE config 4 MPI (1024x1024x128), one non-broadcast view: training forward + backward",
+           "inference_ms": round(inf_ms, 4), "inference_frac": hbm(f_alg, inf_ms)[1],
            "forward_ms": round(fwd_ms, 4), "backward_ms": round(bwd_ms, 4),
            "backward_no_ckpt_ms": round(bwd2_ms, 4), "step_ms": round(fwd_ms + bwd_ms, 4),
-           "backward_alg_bytes": 2 * mpi_bytes + H * W * 12,
+           "forward_alg_bytes": f_alg, "forward_hbm_frac": hbm(f_alg, fwd_ms)[1],
+           "backward_alg_bytes": b_alg,
            "backward_alg_def": "MPI read + d MPI written + d frame read (workspace traffic not counted)",
-           "backward_hbm_frac": round((2 * mpi_bytes + H * W * 12) / (bwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "backward_hbm_frac": hbm(b_alg, bwd_ms)[1],
            "workspace_GB": round(ws.numel() / 1e9, 3), "fallback_flag": flag,
-           "ckpt_grad_bit_identical": same}
+           "ckpt_grad_bit_identical": same, "inference": prof_fields(kname, grid, f_alg, inf_ms)}
     del mpi, ws, g1, g2, ck
     torch.cuda.empty_cache()
     return res
@@ -231,12 +534,15 @@ def config5_leg(world, rank, dev, steps, warmup):
             launch()
             return out
         shard_bytes = P * H * W * 16 + H * W * 12
+        kname, grid = _lib.route("render_packed", H, W, P, 1)
     else:
         ct = torch.empty((1, H, W, 4), device=dev)
         launch = lambda: _lib._call("mpiv_render_packed_ct", packed, H, W, p1 - p0, 0, p1 - p0,  # noqa: E731
                                     int(rank == 0), hl, 1, ct, _lib._stream(dev))
         step = lambda: parallel.render_plane_sharded(packed, hl, H)  # noqa: E731
         shard_bytes = (p1 - p0) * H * W * 16 + H * W * 16
+        kname, grid = _lib.route("render_packed_ct", H, W, p1 - p0, 1)
+    launch()
     kern_ms = event_ms(launch, 3, stream)
     for _ in range(warmup):
         step()
@@ -249,17 +555,19 @@ def config5_leg(world, rank, dev, steps, warmup):
     torch.cuda.synchronize()
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
-    kern_ms = max_over_ranks(kern_ms, world, dev)
+    kern_all = all_ranks(kern_ms, world, dev)
     res = {"workload": "BASELINE config 5: 256-plane 4096x2160 MPI (36.2 GB), 1 pose, plane-sharded",
            "value": round(steps * H * W / 1e6 / elapsed, 2), "unit": "Mpix/s", "n_gpus": world,
            "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "scaling": "strong",
            "data": "synthetic (counter-based per-shard generator, synth.hip, seed 0)",
-           "planes_per_gpu": p1 - p0, "shard_kernel_ms": round(kern_ms, 3),
+           "planes_per_gpu": p1 - p0, "shard_kernel_ms": round(max(kern_all), 3),
+           "per_rank_shard_kernel_ms": [round(x, 3) for x in kern_all],
            "shard_alg_bytes": shard_bytes,
-           "shard_hbm_frac": round(shard_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "shard_hbm_frac": hbm(shard_bytes, max(kern_all))[1],
            "parallelism": "single GPU, sequential render" if world == 1 else
            f"plane-sharded x{world}: (C,T) partials + band all-to-all + ordered combine + gather",
            "frame_sha16": sha16(frame) if rank == 0 else None}
+    res.update(prof_fields(kname, grid, shard_bytes, max(kern_all)))
     del packed
     torch.cuda.empty_cache()
     return res
@@ -267,37 +575,27 @@ def config5_leg(world, rank, dev, steps, warmup):
 
 def main():
     args = parse()
-    if args.kernel == "packed_mv":
-        _lib.load().mpiv_debug_set(b"render_mv", 1)  # libmpiv's debug option (A/B)
-    world, rank, dev = dist_setup(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))  # before any GPU call in this process
+    world, rank, dev, backend = dist_setup(args)
     torch.cuda.set_device(dev)
+    legs = args.legs
     c4 = configs.config4()
     H, W, P = c4["H"], c4["W"], c4["P"]
     V = args.views
     n_path = len(c4["poses"])
 
-    def make_view():
-        gen = torch.Generator(device=dev).manual_seed(c4["seed"])
-        v = torch.rand((H, W, P, 4), generator=gen, device=dev, dtype=torch.float32)
-        v[..., :3].mul_(2.0).sub_(1.0)
-        v[:, :, 0, 3] = 1.0
-        return v
-
     # --- resident inputs: one MPI replica per GPU (generated on device), packed once
-    view = make_view()
+    view = gen_view(H, W, P, c4["seed"], dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    packed = _lib.pack_planes(view) if args.kernel.startswith("packed") else None
-    # mpiv_render_packed's routing (abi.hip render_packed_impl): a near-square MPI at 1-2 or
-    # >= 32 views per launch goes to the R-rows-per-lane kernel, other view counts gather
-    # one row per work-item
-    rows = abs(W / (H - 1) - 1.0) <= 0.25 and (V <= 2 or V >= 32)
-    kernel_name = {"packed": "render_rows_kernel" if rows else "render_packed_kernel",
-                   "packed_lds": "render_lds_kernel", "native": "render_chunk_kernel",
-                   "packed_mv": "render_mv_kernel" if V >= 4 else "render_packed_kernel"}[args.kernel]
-    entry = "mpiv_render_packed_lds" if args.kernel == "packed_lds" else "mpiv_render_packed"
+    packed = _lib.pack_planes(view) if args.kernel == "packed" else None
     torch.cuda.synchronize()
     pack_ms = (time.perf_counter() - t0) * 1e3
+    if packed is not None:
+        kernel_name, grid = _lib.route("render_packed", H, W, P, V)
+    else:
+        kernel_name, grid = _lib.route("render", V, H, W, P)
 
     poses = configs.f32(c4["poses"])
     K = configs.f32(c4["K"])
@@ -318,7 +616,7 @@ def main():
 
     def launch(h_dev, n, o):
         if packed is not None:
-            _lib._call(entry, packed, H, W, P, h_dev, n, o, _lib._stream(dev))
+            _lib._call("mpiv_render_packed", packed, H, W, P, h_dev, n, o, _lib._stream(dev))
         else:
             mpi5 = view.unsqueeze(0).expand(n, H, W, P, 4)
             _lib._call("mpiv_render", mpi5, _lib._strides(mpi5), n, H, W, P, h_dev, o, _lib._stream(dev))
@@ -346,16 +644,9 @@ def main():
             if s + 1 < first + n_steps:
                 upload(s + 1)  # host-side homographies of the next step overlap this launch
 
-    # single-view leg (one view per launch: every texel crosses HBM once, the north-star
-    # 0.60 bar), measured before the sustained multi-view load so it does not inherit a
-    # lowered clock from it
-    one = torch.empty((1, H, W, 3), device=dev)
-    sv_ms = float("nan")
-    if not args.no_extras:
-        h_sv = host_homs(0, 1).to(dev)
-        for _ in range(50):  # ~25 ms of untimed launches: the clocks leave their idle state first
-            launch(h_sv, 1, one)
-        sv_ms = event_ms(lambda: launch(h_sv, 1, one), 20, stream)
+    # single-view leg first, so it does not inherit a clock lowered by the sustained load
+    sv = single_view_leg(packed, H, W, P, host_homs(0, 1).to(dev), dev, stream) \
+        if ("sv" in legs and packed is not None) else None
 
     run(args.warmup, 0)
     torch.cuda.synchronize()
@@ -369,28 +660,30 @@ def main():
     barrier(world)
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, world, dev)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kern_ms_local = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kern_all = all_ranks(kern_ms_local, world, dev)
+    kern_ms = max(kern_all)
 
     # --- after the timed region: the last timed launch's first frame against a one-view
-    # launch of the same pose (bit-exact), the single-view leg, the gather ceiling
+    # launch of the same pose (bit-exact), the gather ceiling, the census
+    extras = len(legs) > 1 or legs != ["c4"]
     last = args.warmup + args.steps - 1
     timed_frame_sha = one_sha = None
     peak_gbs = float("nan")
     gathers = None
-    if not args.no_extras:
+    if extras:
+        one = torch.empty((1, H, W, 3), device=dev)
         timed_frame_sha = sha16(out[0])
-        h1 = host_homs(last, 1).to(dev)
-        launch(h1, 1, one)
+        launch(host_homs(last, 1).to(dev), 1, one)
         torch.cuda.synchronize()
         one_sha = sha16(one[0])
         peak_gbs = gather_peak_gbs(dev, stream)
         # the texture path's real work in the timed launches: the counting build of the same
         # kernel (mpiv_render_packed_census) re-renders the timed steps and adds up the
-        # 64-lane 16-B gather instructions its waves issue (vertical tap reuse gathers fewer
-        # than the four taps per plane-sample of the direct kernel)
-        if packed is not None and entry == "mpiv_render_packed":
+        # 64-lane 16-B gather instructions its waves issue
+        if packed is not None:
             census = torch.zeros(1, dtype=torch.int64, device=dev)
-            try:  # every timed step's views (the count depends on the poses), averaged per launch
+            try:
                 for s_ in range(args.warmup, args.warmup + args.steps):
                     _lib._call("mpiv_render_packed_census", packed, H, W, P, host_homs(s_).to(dev), V, out, census,
                                _lib._stream(dev))
@@ -400,20 +693,38 @@ def main():
 
     mpix_total = world * args.steps * V * H * W / 1e6
     value = mpix_total / elapsed
-    tap_bytes = V * P * H * W * 64            # four 16-B taps per plane-sample (direct kernel)
+    tap_bytes = V * P * H * W * 64            # four 16-B taps per plane-sample (one-row kernel)
     hbm_alg_bytes = V * (P * H * W * 16 + H * W * 12)  # every view reading its MPI once (§8d)
-    sv_bytes = P * H * W * 16 + H * W * 12
-    gather_bytes = gathers * kWaveBytes if gathers else tap_bytes  # what the texture path moves
+    gather_bytes = gathers * kWaveBytes if gathers else tap_bytes
     achieved = gather_bytes / (kern_ms * 1e-3) / 1e9
-    pmc = load_pmc(os.path.join(REPO, "profiles"), kernel_name, V, (H, W, P))
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    pf = prof_fields(kernel_name, grid, hbm_alg_bytes, kern_ms)
+    traffic = pf.get("traffic")
 
+    cpu_frames, cpu_view = None, None
+    if "cpu" in legs and world == 1 and rank == 0 and packed is not None:
+        one = torch.empty((1, H, W, 3), device=dev)
+        launch(host_homs(0, 1).to(dev), 1, one)
+        torch.cuda.synchronize()
+        cpu_frames = [one.cpu().numpy()]
+        cpu_view = view.cpu()
     del out
     if packed is not None:
-        del view
+        del view, packed
     torch.cuda.empty_cache()
-    train = training_leg(dev, stream) if (world == 1 and not args.no_extras and not args.no_training) else None
-    c5 = None if (args.no_config5 or args.no_extras) else config5_leg(world, rank, dev, max(3, args.steps // 2), 1)
+
+    c2 = config2_leg(dev, stream) if "c2" in legs else None
+    torch.cuda.empty_cache()
+    c3 = config3_leg(dev, stream) if "c3" in legs else None
+    torch.cuda.empty_cache()
+    nb = notebook_leg(dev, stream) if "nb" in legs else None
+    torch.cuda.empty_cache()
+    train = training_leg(dev, stream) if "train" in legs else None
+    c5 = config5_leg(world, rank, dev, max(3, args.steps // 2), 1) if "c5" in legs else None
+    ranks = {"world_size_seen": world, "backend": backend, "per_rank_kernel_ms": [round(x, 4) for x in kern_all]}
+    if world > 1:
+        import torch.distributed as dist
+        ranks["world_size_seen"] = dist.get_world_size()
+        ranks["one_device_rehearsal"] = os.environ.get("MPIV_BENCH_ONE_DEVICE") == "1"
 
     if rank == 0:
         res = {
@@ -424,46 +735,48 @@ def main():
             "config": {"workload": "BASELINE config 4: 128-plane 1024x1024 MPI, 1000-pose camera path, view-sharded",
                        "H": H, "W": W, "planes": P, "views_per_gpu_per_step": V, "kernel": args.kernel,
                        "parallelism": f"view-sharded x{world} (replicas, no data-path collective)",
-                       "views_per_s": round(value / (H * W / 1e6), 2), "pack_ms_once": round(pack_ms, 2)},
+                       "views_per_s": round(value / (H * W / 1e6), 2), "pack_ms_once": round(pack_ms, 2),
+                       "build_id": _lib.load().mpiv_build_id().decode()},
+            "ranks": ranks,
             "roofline": {
                 "bound": "texture", "achieved": round(achieved, 1),
                 "peak": round(peak_gbs, 1) if peak_gbs == peak_gbs else None, "unit": "GB/s",
                 "frac": round(achieved / peak_gbs, 4) if peak_gbs == peak_gbs else None, "traffic": traffic,
-                "kernel": kernel_name, "kernel_ms_per_launch": round(kern_ms, 3),
+                "kernel": kernel_name, "grid_workitems": grid, "kernel_ms_per_launch": round(kern_ms, 3),
                 "alg_bytes_per_launch": gather_bytes,
                 "alg_bytes_def": ("gather instructions the launch issues (counted live by the kernel's census build, "
                                   "mpiv_render_packed_census) x 64 lanes x 16 B" if gathers else
                                   "V*P*H*W*64: four 16-B bilinear taps per plane-sample through the vector-memory path"),
                 "gathers_per_plane_sample": round(gathers * 64 / (V * P * H * W), 3) if gathers else 4.0,
                 "alg_bytes_4tap": tap_bytes,
-                "peak_def": "mpiv_probe_gather on this device: 16-B/lane buffer loads, render access shape, "
-                            "L1/L2-resident window (MI355X_MICROARCH.md L2: 34.5-36.9 TB/s)",
-                "ta_busy_frac": pmc.get("ta_busy_frac") if pmc else None,
-                "l2_hit_rate": pmc.get("l2_hit_rate") if pmc else None,
-                "hbm_traffic_frac": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                "peak_def": "mpiv_probe_gather on this device: 16-B/lane buffer loads from an L1/L2-resident "
+                            "window with the render's access shape -- a measured TA ceiling, not a spec peak "
+                            "(MI355X_MICROARCH.md L2: 34.5-36.9 TB/s)",
+                "hbm_alg_bytes_per_launch": hbm_alg_bytes,
+                "hbm_traffic_frac": pf.get("traffic_frac"),
+                "hbm_traffic_over_compulsory": round(traffic / (P * (H + 4) * (W + 4) * 16 + V * H * W * 12), 2)
+                if traffic else None,
+                "compulsory_def": "packed MPI read once + V frames written",
                 "mpi_reuse_per_launch": round(hbm_alg_bytes / traffic, 1) if traffic else None,
-                "single_view": None if args.no_extras else {
-                    "kernel_ms": round(sv_ms, 4), "alg_bytes": sv_bytes,
-                    "achieved_gbs": round(sv_bytes / (sv_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                    "frac": round(sv_bytes / (sv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bound": "hbm"},
-                "pmc_source": "profiles/render_pmc.json (same build id / kernel / views / shape)" if pmc else
-                              "no matching profiles/render_pmc.json for this build",
+                "rocprof": {k: v for k, v in pf.items() if k not in ("kernel", "grid_workitems")},
+                "single_view": sv,
             },
             "timed_frame_check": {"frame": "view 0 of the last timed launch vs a 1-view launch of its pose",
-                                  "sha16": timed_frame_sha, "bit_exact": timed_frame_sha == one_sha},
+                                  "sha16": timed_frame_sha, "bit_exact": timed_frame_sha == one_sha}
+            if extras else None,
             "cpu_baseline": None,
-            "config5_plane_sharded": c5,
+            "config2": c2,
+            "config3_psv": c3,
+            "notebook": nb,
             "training_render_backward": train,
+            "config5_plane_sharded": c5,
         }
-        if world == 1 and args.cpu_seconds > 0 and not args.no_extras:
-            # the GPU frame of the first view of step 0, to cross-check the CPU sample bit-exactly
-            hs = host_homs(0)
-            launch(hs[:1].to(dev), 1, one)
-            torch.cuda.synchronize()
-            res["cpu_baseline"] = cpu_baseline(make_view(), hs, args.cpu_seconds, [one.cpu().numpy()])
+        if cpu_frames is not None:
+            res["cpu_baseline"] = cpu_baseline(cpu_view, host_homs(0), args.cpu_seconds, cpu_frames)
         print(json.dumps(res), flush=True)
     if world > 1:
         import torch.distributed as dist
+        dist.barrier()
         dist.destroy_process_group()
 
 

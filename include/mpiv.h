@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 9
+#define MPIV_ABI_VERSION 10
 
 enum {
     MPIV_OK = 0,
@@ -48,9 +48,21 @@ const char *mpiv_build_id(void);
 
 /* Debug / A/B hook, never needed in production: selects a non-default kernel variant
  * by name ("render_mv", "render_pair", "render_native_lds", "render_chunk", "render_ring",
- * "render_tile", "sweep_tile", "sweep_store", "box_shrink"; "reset" restores every default).  Process-wide;
- * returns MPIV_ERR_ARG for an unknown name. */
+ * "render_tile", "render_vshare", "sweep_tile", "sweep_store", "sweep_dlane", "box_shrink",
+ * "bwd_fallback", "bwd_margin"; "reset" restores every default; abi.hip documents the
+ * values).  Process-wide; returns MPIV_ERR_ARG for an unknown name. */
 int mpiv_debug_set(const char *name, int value);
+
+/* Dry run of an entry point's production dispatch (no device memory touched, nothing
+ * launched): writes the name of the kernel the call WOULD launch (as it appears in
+ * rocprofv3's kernel names, template arguments included) into name[name_cap] and its grid
+ * size in work-items into *grid_threads (may be NULL).  bench.py uses it to find its
+ * launches in rocprofv3 summaries.  entry / args:
+ *   "render_packed", "render_packed_ct"  {H, W, P, V}        (mpiv_render_packed[_ct])
+ *   "render"                             {B, H, W, P}        (mpiv_render, contiguous MPI)
+ *   "plane_sweep"                        {B, Hs, Ws, C, D, Ht, Wt} (mpiv_plane_sweep)
+ * Fails while a debug option is set (it reports production routes only). */
+int mpiv_route(const char *entry, const int64_t *args, int nargs, char *name, int name_cap, int64_t *grid_threads);
 
 /* ---- MPI render -------------------------------------------------------- */
 
@@ -321,10 +333,10 @@ int mpiv_synth_mpi_packed_u8(uint32_t seed, int H, int W, int p_begin, int p_end
 
 /* Gather-rate probe (bench.py's texture-path roofline): `blocks` x 256 work-items each
  * issue iters x 8 16-B buffer loads (1 KiB per wave instruction, the render's tap shape)
- * from a 16 KiB L1/L2-resident window (>= 16 KiB of zeros, device, 16-B aligned);
- * bytes moved = blocks * 256 * iters * 128.  `sink` (>= 4 floats) is never written for a
- * zero window. */
-int mpiv_probe_gather(const float *window, int iters, int blocks, float *sink, void *stream);
+ * from a 16 KiB L1/L2-resident window (window_bytes >= 16384 bytes of zeros, device, 16-B
+ * aligned; smaller windows are refused); bytes moved = blocks * 256 * iters * 128.  `sink`
+ * (>= 4 floats) is never written for a zero window. */
+int mpiv_probe_gather(const float *window, size_t window_bytes, int iters, int blocks, float *sink, void *stream);
 
 /* Exhaustive self-check of the render's launch-constant division (x / (H-1),
  * x / (W-1) via a precomputed reciprocal + two residual corrections) against IEEE

@@ -43,7 +43,8 @@ _SIGS = {
     "mpiv_cam2pixel": [_vp, _vp, _int, _i64, _vp, _vp],
     "mpiv_plane_coords": [_vp, _int, _i64, _vp, _int, _int, _vp, _vp],
     "mpiv_selftest_div_const": [_int, _vp, _vp],
-    "mpiv_probe_gather": [_vp, _int, _int, _vp, _vp],
+    "mpiv_probe_gather": [_vp, ctypes.c_size_t, _int, _int, _vp, _vp],
+    "mpiv_route": [ctypes.c_char_p, _c_i64p, _int, ctypes.c_char_p, _int, _c_i64p],
     "mpiv_pad_texels": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_plane_sweep_padded": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
     "mpiv_preprocess": [_vp, _i64, _vp, _vp],
@@ -70,7 +71,7 @@ _SIGS = {
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
                           "mpiv_build_id", "mpiv_debug_set")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lib = None
 
@@ -187,6 +188,19 @@ def debug(**opts):
         yield
     finally:
         L.mpiv_debug_set(b"reset", 0)
+
+
+def route(entry: str, *args: int) -> tuple[str, int]:
+    """(kernel name, grid work-items) of the kernel an entry point's production dispatch
+    would launch for these sizes (mpiv_route: a dry run, nothing launched, no GPU needed)."""
+    L = load()
+    buf = ctypes.create_string_buffer(160)
+    grid = ctypes.c_int64(0)
+    a = (ctypes.c_int64 * len(args))(*args)
+    rc = L.mpiv_route(entry.encode(), a, len(args), buf, len(buf), ctypes.byref(grid))
+    if rc != 0:
+        raise RuntimeError(f"mpiv_route failed ({rc}): {L.mpiv_last_error().decode()}")
+    return buf.value.decode(), grid.value
 
 
 def _strides(t: torch.Tensor, dims=None):

@@ -90,6 +90,23 @@ int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 // launch takes it (and clears it) to launch the counting build
 thread_local unsigned long long* g_census = nullptr;
 
+// mpiv_route: set for the duration of one dry-run call on this thread; the entry point fills
+// in the kernel (and grid size in work-items) it WOULD launch, and launches nothing
+struct RouteNote {
+    char name[160];
+    int64_t threads;
+};
+thread_local RouteNote* g_route = nullptr;
+
+int note_route(int64_t blocks_, int threads, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_route->name, sizeof(g_route->name), fmt, ap);
+    va_end(ap);
+    g_route->threads = blocks_ * threads;
+    return MPIV_OK;
+}
+
 constexpr int64_t kMaxGridYZ = 65535;
 constexpr int kNativeLdsMaxP = 16;
 constexpr int kChunkMaxLds = 65536;  // render_chunk_kernel: slots + P homographies, default LDS limit
@@ -149,6 +166,7 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
         const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * B;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_render: too many blocks");
         const ChunkGeom cg{(int)(s.y / 4), (int)(s.x / 4), (int)rec};
+        if (g_route) return note_route(nb, 256, "render_chunk_kernel<%d, %d>", CH, SPLIT);
         if (CH == 8 && SPLIT == 2)
             render_chunk_kernel<8, 2><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out, nullptr);
         else if (CH == 8)
@@ -165,9 +183,13 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
     if (vec && fast && P <= kNativeLdsMaxP && opt(kOptNativeLds)) {
         const int64_t nb = (int64_t)blocks(W, kLTX) * blocks(H, kLTY) * B;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_render: too many blocks");
+        if (g_route) return note_route(nb, kLThreads, "render_lds_native_kernel<true>");
         render_lds_native_kernel<true><<<(unsigned)nb, kLThreads, 0, q>>>(mpi, s, g, B, homs, out);
         return launched("mpiv_render");
     }
+    if (g_route)
+        return note_route((int64_t)grid.x * grid.y * grid.z, 256, "render_native_kernel<%s, %s>", vec ? "true" : "false",
+                          fast ? "true" : "false");
     if (vec && fast) render_native_kernel<true, true><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
     else if (vec) render_native_kernel<true, false><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
     else if (fast) render_native_kernel<false, true><<<grid, 256, 0, q>>>(mpi, s, g, homs, out);
@@ -348,6 +370,9 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
         const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
         // the counting build (mpiv_render_packed_census) exists for the automatic choices
+        if (g_route)
+            return note_route(nb, 256, "render_rows_kernel<%s, %d, true, false, %d>", ct ? "true" : "false", R,
+                              vsd == 3 || vsd == 11 ? 4 : 3);
         unsigned long long* cn = (g_census && !ct) ? g_census : nullptr;
         if (cn) g_census = nullptr;
 #define MPIV_VSD(R, D)                                                                                              \
@@ -408,6 +433,8 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     const int64_t nblocks = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;
     if (nblocks > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const dim3 grid((unsigned)nblocks), blk(256);
+    if (g_route)
+        return note_route(nblocks, 256, "render_packed_kernel<%s, %s>", ct ? "true" : "false", fast ? "true" : "false");
     if (ct && fast)
         render_packed_kernel<true, true><<<grid, blk, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, homs, out);
     else if (ct)
@@ -641,6 +668,7 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
     const dim3 lgrid((unsigned)tiles, B, 1);
     const int shrink = opt(kOptBoxShrink);
     hipStream_t q = S(stream);
+    if (g_route) return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true>", C < 4 ? C : 4);
 #define MPIV_DLRAW(CC)                                                                                         \
     plane_sweep_dlane_kernel<CC, true><<<lgrid, kDLThreads, 0, q>>>(nullptr, PadGeom{0, 0, 0, 0}, img, is, sp, \
                                                                     rc_hs, rc_ws, ki, proj, depths, out,       \
@@ -680,6 +708,7 @@ int mpiv_plane_sweep(const float* img, const int64_t st[4], int B, int Hs, int W
     if (B > kMaxGridYZ || blocks(per_view, 256) > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep: too large");
     const ImgStrides s{st[0], st[1], st[2], st[3]};
     dim3 grid(blocks(per_view, 256), B, 1);
+    if (g_route) return note_route((int64_t)grid.x * B, 256, "plane_sweep_kernel");
     plane_sweep_kernel<<<grid, 256, 0, S(stream)>>>(img, s, sweep_params(B, Hs, Ws, C, D, Ht, Wt), ki, proj, depths,
                                                     out);
     return launched("mpiv_plane_sweep");
@@ -1109,12 +1138,49 @@ int mpiv_render_packed_u8_ct(const uint32_t* packed, int H, int W, int P, int p_
     return render_u8_impl(packed, H, W, P, p_begin, p_end, back, homs, V, ct, true, stream);
 }
 
-int mpiv_probe_gather(const float* window, int iters, int blocks_, float* sink, void* stream) {
+int mpiv_probe_gather(const float* window, size_t window_bytes, int iters, int blocks_, float* sink, void* stream) {
     if (!window || !sink) return fail(MPIV_ERR_ARG, "mpiv_probe_gather: null pointer");
+    if (window_bytes < (size_t)kProbeWindow)
+        return fail(MPIV_ERR_ARG, "mpiv_probe_gather: the window must hold >= %d bytes", (int)kProbeWindow);
     if (iters <= 0 || blocks_ <= 0) return fail(MPIV_ERR_ARG, "mpiv_probe_gather: bad size");
     if (!aligned16(window)) return fail(MPIV_ERR_ARG, "mpiv_probe_gather: window must be 16-byte aligned");
     probe_gather_kernel<<<blocks_, 256, 0, S(stream)>>>(reinterpret_cast<const float4*>(window), iters, sink);
     return launched("mpiv_probe_gather");
+}
+
+int mpiv_route(const char* entry, const int64_t* a, int na, char* name, int name_cap, int64_t* grid_threads) {
+    if (!entry || !a || !name || name_cap <= 0) return fail(MPIV_ERR_ARG, "mpiv_route: null pointer");
+    for (int i = 0; i < kNumOpts; ++i)
+        if (opt((DebugOpt)i) != kOptDefaults[i])
+            return fail(MPIV_ERR_ARG, "mpiv_route: reports the production routes only (debug options are set)");
+    // nothing is dereferenced or launched in a dry run: any 256-B aligned address passes the checks
+    alignas(256) static float dummy[64];
+    float* d = dummy;
+    RouteNote note{};
+    int rc;
+    g_route = &note;
+    if (strcmp(entry, "render_packed") == 0 && na == 4)
+        rc = render_packed_impl(d, (int)a[0], (int)a[1], (int)a[2], 0, (int)a[2], 1, d, (int)a[3], d, false, 0, nullptr);
+    else if (strcmp(entry, "render_packed_ct") == 0 && na == 4)
+        rc = render_packed_impl(d, (int)a[0], (int)a[1], (int)a[2], 0, (int)a[2], 1, d, (int)a[3], d, true, 0, nullptr);
+    else if (strcmp(entry, "plane_sweep") == 0 && na == 7) {
+        const int64_t C = a[3], D = a[4], st[4] = {a[1] * a[2] * C, a[2] * C, C, 1};
+        rc = mpiv_plane_sweep(d, st, (int)a[0], (int)a[1], (int)a[2], (int)C, d, d, d, (int)D, (int)a[5], (int)a[6], d,
+                              nullptr);
+    } else if (strcmp(entry, "render") == 0 && na == 4) {
+        const int64_t P = a[3], st[5] = {a[1] * a[2] * P * 4, a[2] * P * 4, P * 4, 4, 1};
+        rc = mpiv_render(d, st, (int)a[0], (int)a[1], (int)a[2], (int)P, d, d, nullptr);
+    } else {
+        g_route = nullptr;
+        return fail(MPIV_ERR_ARG, "mpiv_route: unknown entry '%s' or wrong argument count %d", entry, na);
+    }
+    g_route = nullptr;
+    if (rc != MPIV_OK) return rc;
+    if (!note.name[0]) return fail(MPIV_ERR_ARG, "mpiv_route: '%s' has no reportable route", entry);
+    snprintf(name, (size_t)name_cap, "%s", note.name);
+    if (grid_threads) *grid_threads = note.threads;
+    g_err[0] = '\0';
+    return MPIV_OK;
 }
 
 int mpiv_selftest_div_const(int divisor, unsigned long long* mismatches, void* stream) {

@@ -1,0 +1,89 @@
+"""bench.py's host logic on CPU: leg selection, the N-rank launcher (it must start the
+ranks itself when the driver runs `bench.py --gpus N` outside torchrun, and refuse a
+WORLD_SIZE that disagrees with --gpus), the host-core report of the CPU baseline, and
+the library's route dry run that ties every leg to its rocprof dispatches."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+from mpi_vision_amd import _lib  # noqa: E402
+
+
+def _parse(monkeypatch, *argv):
+    monkeypatch.setattr(sys, "argv", ["bench.py", *argv])
+    return bench.parse()
+
+
+def test_leg_selection(monkeypatch):
+    assert _parse(monkeypatch).legs == list(bench.ALL_LEGS)
+    assert _parse(monkeypatch, "--no-extras").legs == ["c4"]
+    a = _parse(monkeypatch, "--no-config5", "--no-training", "--cpu-seconds", "0")
+    assert a.legs == ["c4", "sv", "c2", "c3", "nb"]
+    assert _parse(monkeypatch, "--legs", "c3").legs == ["c3"]
+    with pytest.raises(SystemExit):
+        _parse(monkeypatch, "--legs", "c9")
+
+
+def test_spawn_ranks_runs_torchrun_child(monkeypatch):
+    seen = {}
+
+    def fake_run(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return subprocess.CompletedProcess(cmd, 3)
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    assert bench.spawn_ranks(4) == 3
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    assert cmd[-5].endswith("bench.py")
+
+
+def test_main_spawns_before_touching_the_gpu(monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    monkeypatch.setattr(bench, "spawn_ranks", lambda n: 7)
+    monkeypatch.setattr(bench, "dist_setup", lambda a: (_ for _ in ()).throw(AssertionError("touched the GPU")))
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 7
+
+
+def test_world_size_must_match_gpus(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
+    with pytest.raises(SystemExit, match="WORLD_SIZE=2"):
+        bench.dist_setup(bench.parse())
+
+
+def test_host_cores_report():
+    threads, d = bench.host_cores()
+    assert threads >= 1 and d["threads_used"] == threads
+    assert d["host_nproc"] == os.cpu_count()
+    assert threads <= d["affinity_cpus"]
+
+
+def test_route_dry_run_names_the_launched_kernels():
+    """mpiv_route reports the production kernel and grid without a GPU (no launch)."""
+    assert _lib.route("render_packed", 1024, 1024, 128, 125) == ("render_rows_kernel<false, 6, true, false, 3>",
+                                                                 16 * 43 * 125 * 256)
+    assert _lib.route("render_packed", 1024, 1024, 128, 1)[0] == "render_rows_kernel<false, 4, true, false, 4>"
+    assert _lib.route("render_packed", 576, 1024, 32, 64)[0] == "render_rows_kernel<false, 9, true, false, 3>"
+    # a stretched MPI in a small launch keeps the one-row kernel
+    assert _lib.route("render_packed", 576, 1024, 32, 1)[0] == "render_packed_kernel<false, true>"
+    assert _lib.route("plane_sweep", 5, 768, 1024, 3, 64, 768, 1024) == ("plane_sweep_dlane_kernel<3, true>",
+                                                                         16 * 192 * 5 * 512)
+    assert _lib.route("render", 1, 1024, 1024, 128)[0] == "render_chunk_kernel<8, 1>"
+    with pytest.raises(RuntimeError, match="unknown entry"):
+        _lib.route("nope", 1)
+    with _lib.debug(render_tile=-1):
+        with pytest.raises(RuntimeError, match="debug options"):
+            _lib.route("render_packed", 64, 64, 4, 1)

@@ -60,7 +60,8 @@ int main() {
     EXPECT(mpiv_assemble_mpi_packed(f, st4, f, st4, -1, 4, 4, 2, f, nullptr) == MPIV_ERR_ARG);
     EXPECT(mpiv_assemble_mpi_backward(f, st5, f, st4, f, st4, 1, 4, 4, 2, nullptr, nullptr, nullptr) == MPIV_ERR_ARG);
     EXPECT(mpiv_synth_mpi_packed(1, 4, 4, 3, 3, f, nullptr) == MPIV_ERR_ARG);
-    EXPECT(mpiv_probe_gather(f, 0, 1, f, nullptr) == MPIV_ERR_ARG);
+    EXPECT(mpiv_probe_gather(f, 16384, 0, 1, f, nullptr) == MPIV_ERR_ARG);
+    EXPECT(mpiv_probe_gather(f, 4096, 1, 1, f, nullptr) == MPIV_ERR_ARG);
     EXPECT(mpiv_selftest_div_const(0, nullptr, nullptr) == MPIV_ERR_ARG);
     // debug options
     EXPECT(mpiv_debug_set("render_mv", 1) == MPIV_OK);

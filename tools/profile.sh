@@ -1,25 +1,27 @@
 #!/bin/bash
-# rocprofv3 evidence for the bench's dominant kernel (run on the GPU box):
-#   1. kernel-trace --stats of bench.py --no-extras (only the timed config-4 launches)
+# rocprofv3 evidence for every bench.py leg (run on the GPU box):
+#   1. kernel-trace --stats of bench.py (all legs but the CPU baseline)
 #   2-6. separate --pmc passes (FETCH_SIZE | WRITE_SIZE | TCC_HIT,TCC_MISS | VALU | TA busy)
-# then tools/parse_pmc.py writes profiles/<tag>_render_pmc.json + profiles/render_pmc.json.
+# then, locally in the same tree: python tools/parse_prof.py gpurun_out/prof <tag>
+# (groups the dispatches by kernel and grid size -> profiles/prof_summary.json).
 # Each pass has its own time limit; any failure ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-OUT=$ROOT/gpurun_out/pmc
-TAG=${TAG:-r02}
-ARGS=${PROF_ARGS:---steps 2 --warmup 1 --no-extras}
+OUT=$ROOT/gpurun_out/prof
+ARGS=${PROF_ARGS:---steps 3 --warmup 1 --cpu-seconds 0 --no-training}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
-    -- python -u "$ROOT/bench.py" $ARGS > "$OUT/trace.log" 2>&1 || { echo "trace pass failed"; tail -5 "$OUT/trace.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
+    -- python3 -u "$ROOT/bench.py" $ARGS > "$OUT/trace.log" 2>&1 || { echo "trace pass failed"; tail -5 "$OUT/trace.log"; exit 1; }
+echo "trace pass ok"
 for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" \
             "TA_BUSY_avr GRBM_GUI_ACTIVE"; do
     name=$(echo "$pass" | tr ' ' '_')
     [ "$pass" = "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" ] && name=VALU
     [ "$pass" = "TA_BUSY_avr GRBM_GUI_ACTIVE" ] && name=TA
-    timeout -s KILL 240 rocprofv3 --pmc $pass --output-format csv -d "$OUT/$name" -o run \
-        -- python -u "$ROOT/bench.py" $ARGS > "$OUT/$name.log" 2>&1 || { echo "pmc pass $pass failed"; tail -5 "$OUT/$name.log"; exit 1; }
+    timeout -s KILL 300 rocprofv3 --pmc $pass --output-format csv -d "$OUT/$name" -o run \
+        -- python3 -u "$ROOT/bench.py" $ARGS > "$OUT/$name.log" 2>&1 || { echo "pmc pass $pass failed"; tail -5 "$OUT/$name.log"; exit 1; }
+    echo "pmc pass $name ok"
 done
-echo "profile passes done; summarise locally: python tools/parse_pmc.py gpurun_out/pmc $TAG"
+echo "profile passes done; summarise locally: python tools/parse_prof.py gpurun_out/prof <tag>"
