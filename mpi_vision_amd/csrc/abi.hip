@@ -506,7 +506,7 @@ size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
     char* inv = take((size_t)P * 12 * 4);
     char* truth = take(kCtrSlots * 8);
     char* found = take(kCtrSlots * 8);
-    char* flag = take(4);
+    char* flag = take(16);
     const size_t ntiles = (size_t)((W + kGTW - 1) / kGTW) * ((H + kGTH - 1) / kGTH);
     char* box = take((size_t)P * ntiles * 16);
     char* key = take((size_t)pc * hw * 4);
@@ -580,7 +580,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const int force = opt(kOptBwdFallback) != 0 || !fast;
     const float margin = (float)opt(kOptBwdMargin) / 64.0f;
     hipStream_t q = S(stream);
-    // fallback grid: every block resident (cooperative launch), at most 4 per CU; queried
+    // fallback grid: every block resident (its phases meet at grid barriers), at most 4 per CU; queried
     // once per device (relaxed atomics: racing first calls store the same value)
     static int s_fb_blocks[64] = {};
     int dev = 0;
@@ -621,14 +621,11 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
             bwd_gather_kernel<<<(unsigned)gather_blocks, 256, 0, q>>>(g, hv, ws, gv, margin);
         }
         bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force);
-        // fallback: one cooperative launch, returns at once unless flagged
-        const float* hvc = hv;
-        void* args[] = {(void*)&g, (void*)&hvc, (void*)&ws, (void*)&gv};
-        const hipError_t e = fast ? hipLaunchCooperativeKernel(bwd_fallback_kernel<true>, dim3(fb_blocks), dim3(256),
-                                                               args, 0, q)
-                                  : hipLaunchCooperativeKernel(bwd_fallback_kernel<false>, dim3(fb_blocks), dim3(256),
-                                                               args, 0, q);
-        if (e != hipSuccess) return fail(MPIV_ERR_HIP, "%s: cooperative fallback launch failed: %s", nm, hipGetErrorString(e));
+        // fallback: one launch of resident blocks, returns at once unless flagged
+        if (fast)
+            bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv);
+        else
+            bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv);
     }
     return launched(nm);
 }

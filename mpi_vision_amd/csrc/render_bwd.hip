@@ -41,8 +41,6 @@
 //            chunks so its workspace stays a fraction of d s.
 // Every product and sum is a single fp32 rounding written out explicitly (the library
 // builds with -ffp-contract=off).
-#include <hip/hip_cooperative_groups.h>
-
 #include "mpiv_common.hpp"
 
 namespace mpiv {
@@ -81,7 +79,8 @@ struct BwdWs {
     int4* box;     // [P][tiles] gather pixel box (x0, x1, y0, y1); x0 = -2: the block cannot gather
     unsigned long long* truth;  // [kCtrSlots] (sample, in-image tap) pairs
     unsigned long long* found;  // [kCtrSlots] (texel, contributor) pairs gathered
-    int* flag;     // 1: the fallback recomputes every plane of the view
+    int* flag;     // [0] 1: the fallback recomputes every plane of the view; [1] the fallback's grid
+                   // barrier counter; [2] 1 after a barrier wait timed out (a bug, never expected)
     // fallback: bucket pipeline over chunks of pc planes
     int pc;
     int* key;      // [pc][HW] nw-tap bucket in the (H+1) x (W+1) grid, -1 = no tap in the image;
@@ -673,13 +672,19 @@ __global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force) {
     }
     ws.truth[l] = 0;
     ws.found[l] = 0;
-    if (l == 0) *ws.flag = (force || t != f) ? 1 : 0;
+    if (l == 0) {
+        ws.flag[0] = (force || t != f) ? 1 : 0;
+        ws.flag[1] = 0;  // the fallback's barrier counter
+    }
 }
 
 // ---- fallback: the general bucket pipeline (runs only when *flag is set) -------------
-// One cooperative launch per view (bwd_fallback_kernel, hipLaunchCooperativeKernel: every
-// block resident, so grid.sync() separates the phases); it returns at once while the flag
-// is clear.  Per chunk of ws.pc planes: nw-tap bucket of every sample and bucket sizes,
+// One launch per view (bwd_fallback_kernel) whose grid is sized so every block is resident
+// (<= 4 blocks per CU and the occupancy the device reports; the stream runs nothing beside
+// it), so a grid barrier separates the phases; it returns at once while the flag is clear.
+// (A normal launch, not hipLaunchCooperativeKernel: rocprofv3's kernel tracer crashes in its
+// teardown after a cooperative launch, and this one was issued on every backward.)
+// Per chunk of ws.pc planes: nw-tap bucket of every sample and bucket sizes,
 // exclusive scan of the sizes, pixel ids into their buckets, each bucket sorted by pixel
 // id, then per texel the four buckets merged in the reference's order.  Each phase is a
 // grid-stride loop over blocks `bid` of `nblk`.
@@ -700,6 +705,31 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* s_tmp, int& tota
     return incl - v;
 }
 
+// Grid-wide barrier: arrive = one device-scope atomic per block after a release fence, wait
+// = poll the counter until every block of this phase has arrived, then an acquire fence (the
+// fences write back / invalidate the XCD's L2, so the next phase sees every block's stores).
+// Targets grow by the block count per phase, so the counter (zeroed by bwd_check_kernel) is
+// never reset inside a launch.  A wait that outlasts ~2^24 polls (seconds) gives up and
+// records flag[2] instead of hanging the device.
+__device__ __forceinline__ void grid_barrier(int* flag, unsigned target) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* ctr = reinterpret_cast<unsigned*>(flag + 1);
+        __threadfence();
+        atomicAdd(ctr, 1u);
+        unsigned spins = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 24)) {
+                atomicExch(flag + 2, 1);
+                break;
+            }
+        }
+        __threadfence();
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ unsigned order_key(int pix, int corner) {
     return ((unsigned)(pix / kGridVec) << 5) | ((unsigned)corner << 3) | (unsigned)(pix % kGridVec);
 }
@@ -708,17 +738,17 @@ template <bool FAST>
 __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
                                                            float4* __restrict__ dmpi) {
     __shared__ int s_tmp[kScanBlock];
-    if (*ws.flag == 0) return;  // uniform over the grid: the tile gather was complete
-    namespace cgr = cooperative_groups;
-    cgr::grid_group grid = cgr::this_grid();
+    if (ws.flag[0] == 0) return;  // uniform over the grid: the tile gather was complete
     const int bid = blockIdx.x, nblk = gridDim.x, tid = threadIdx.x;
+    unsigned phase = 0;
+    auto sync = [&]() { grid_barrier(ws.flag, ++phase * (unsigned)nblk); };
     const int64_t gtid = (int64_t)bid * 256 + tid, gstride = (int64_t)nblk * 256;
     const int64_t HW = (int64_t)g.H * g.W;
     const int K1 = g.W + 1;
     const int64_t K = (int64_t)(g.H + 1) * K1;
     // bucket sizes start at zero (the fill returns them to zero for the next chunk)
     for (int64_t i = gtid; i < (int64_t)ws.pc * K; i += gstride) ws.count[i] = 0;
-    grid.sync();
+    sync();
     for (int pc0 = 0; pc0 < g.P; pc0 += ws.pc) {
         const int pcn = min(ws.pc, g.P - pc0);
         const int64_t nq = pcn * HW, nk = pcn * K;
@@ -737,7 +767,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
             ws.key[q] = k;
             if (in) atomicAdd(&ws.count[pl * K + k], 1);
         }
-        grid.sync();
+        sync();
         // exclusive scan of the sizes: tile sums, their scan (block 0), per-tile apply
         for (int tb = bid; tb < nb; tb += nblk) {
             const int64_t base = (int64_t)tb * kScanTile + (int64_t)tid * kScanItems;
@@ -748,7 +778,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
             block_exclusive_scan(sum, s_tmp, total);
             if (tid == 0) ws.bsum[tb] = total;
         }
-        grid.sync();
+        sync();
         if (bid == 0) {
             int carry = 0;
             for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
@@ -761,7 +791,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
             }
             if (tid == 0) ws.big[0] = 0;
         }
-        grid.sync();
+        sync();
         for (int tb = bid; tb < nb; tb += nblk) {
             const int64_t base = (int64_t)tb * kScanTile + (int64_t)tid * kScanItems;
             int v[kScanItems];
@@ -780,7 +810,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
             }
             if (tb == nb - 1 && tid == kScanBlock - 1) ws.offs[nk] = run;  // grand total
         }
-        grid.sync();
+        sync();
         // pixel ids into their buckets (atomic slot claim; sizes return to zero)
         for (int64_t q = gtid; q < nq; q += gstride) {
             const int k = ws.key[q];
@@ -790,7 +820,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
             const int slot = atomicSub(&ws.count[pk], 1) - 1;
             ws.ids[ws.offs[pk] + slot] = (int)(q - pl * HW);
         }
-        grid.sync();
+        sync();
         // each bucket sorted by pixel id: <= kSmallBucket ids by one thread (insertion
         // sort), larger ones (minification, degenerate homographies) listed for a block
         for (int64_t pk = gtid; pk < nk; pk += gstride) {
@@ -809,7 +839,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
                 ws.ids[jx + 1] = v;
             }
         }
-        grid.sync();
+        sync();
         // the large buckets: one block each, merge sort with all threads (runs of width w
         // merged pairwise per pass, output element k of a pair found by a merge-path binary
         // search; ids within a bucket are distinct).  Scratch: the bucket's range of `key`
@@ -848,7 +878,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
                 for (int k0 = tid; k0 < n; k0 += 256) ws.ids[b + k0] = src[k0];
             __syncthreads();
         }
-        grid.sync();
+        sync();
         // texel t of plane pc0 + pl: its four nw-tap buckets (the samples having it as nw,
         // ne, sw, se tap) merged by the reference's order key; fractions from the position
         for (int64_t q = gtid; q < nq; q += gstride) {
@@ -902,7 +932,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
             }
             dmpi[(int64_t)t * g.P + pc0 + pl] = make_float4(a0, a1, a2, a3);
         }
-        grid.sync();  // the chunk's arrays are reused by the next one
+        sync();  // the chunk's arrays are reused by the next one
     }
 }
 

@@ -47,7 +47,10 @@ def _backward_flag(mpi, homs, dout, dev):
     ws = torch.zeros(L.mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
     got = _lib.render_backward(mpi, homs, dout, workspace=ws)
     off = _lib.bwd_flag_offset(H, W, P)
-    return got, int(ws[off:off + 4].view(torch.int32).item())
+    words = ws[off:off + 12].view(torch.int32).tolist()
+    # words[1]: the fallback's grid-barrier counter; words[2]: a barrier wait that timed out
+    assert words[2] == 0, "the fallback's grid barrier timed out"
+    return got, words[0]
 
 
 def _inputs(grad, name, dev):
