@@ -149,17 +149,35 @@ def render_homographies_torch(pose: torch.Tensor, depths: torch.Tensor, intrinsi
     return H.permute(1, 0, 2, 3).reshape(batch, P, 9).contiguous()
 
 
-def psv_matrices(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pose: torch.Tensor):
+def _cpu32_together(*ts: torch.Tensor):
+    """fp32 CPU copies of several tensors with ONE device-to-host transfer when any of them
+    lives on a device (the PSV drop-in's caller keeps K and the pose on the GPU, ipynb cell 8
+    L49-75: one blocking copy instead of three)."""
+    if not any(t.device.type != "cpu" for t in ts):
+        return [_cpu32(t) for t in ts]
+    dev = next(t.device for t in ts if t.device.type != "cpu")
+    flat = torch.cat([t.detach().to(device=dev, dtype=_F32).reshape(-1) for t in ts]).cpu()
+    out, o = [], 0
+    for t in ts:
+        n = t.numel()
+        out.append(flat[o:o + n].reshape(t.shape))
+        o += n
+    return out
+
+
+def psv_matrices(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pose: torch.Tensor, pin: bool = False):
     """Matrices for projective_inverse_warp_torch[2] (utils.py:428-438, 747-757):
         Ki   = inverse(K_tgt)                       [B, 9]
         proj = [[K_src, 0], [0, 0, 0, 1]] @ pose    [B, 16]
-    computed on CPU in fp32 with the reference's ops."""
-    Ks = _cpu32(src_intrinsics)
-    Kt = _cpu32(tgt_intrinsics)
-    pose = _cpu32(pose)
+    computed on CPU in fp32 with the reference's ops (page-locked with pin=True, ready for
+    an asynchronous upload)."""
+    Ks, Kt, pose = _cpu32_together(src_intrinsics, tgt_intrinsics, pose)
     B = pose.shape[0]
     ki = torch.inverse(Kt)
     k4 = torch.cat([Ks, torch.zeros(B, 3, 1)], dim=2)
     k4 = torch.cat([k4, torch.tensor([[[0.0, 0.0, 0.0, 1.0]]]).repeat(B, 1, 1)], dim=1)
     proj = torch.matmul(k4, pose)
-    return ki.reshape(B, 9).contiguous(), proj.reshape(B, 16).contiguous()
+    ki, proj = ki.reshape(B, 9).contiguous(), proj.reshape(B, 16).contiguous()
+    if pin:
+        ki, proj = ki.pin_memory(), proj.pin_memory()
+    return ki, proj

@@ -625,6 +625,29 @@ class AssembleFunction(torch.autograd.Function):
 # plane sweep / inverse warp
 # ---------------------------------------------------------------------------
 
+_DEPTHS_DEV: dict = {}
+
+
+def _depths_on(depth_planes, dev) -> torch.Tensor:
+    """The sweep depths as a contiguous fp32 tensor on `dev`.  The reference iterates
+    `for depth in depth_planes` and adds each to an fp32 zero map (utils.py:466-467), so a
+    list of floats and a tensor (the notebook passes torch.Tensor(inv_depths(...)).to(device),
+    ipynb cell 8 L73) both mean their values rounded to fp32.  A device tensor is used where
+    it is (no per-element reads back to the host); a list is uploaded once per distinct value
+    list and device (memoised)."""
+    if isinstance(depth_planes, torch.Tensor):
+        return depth_planes.detach().to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+    vals = tuple(float(x) for x in depth_planes)
+    key = (vals, str(dev))
+    d = _DEPTHS_DEV.get(key)
+    if d is None:
+        if len(_DEPTHS_DEV) >= 64:
+            _DEPTHS_DEV.clear()
+        d = torch.tensor(vals, dtype=torch.float32).to(dev)
+        _DEPTHS_DEV[key] = d
+    return d
+
+
 def _require_depths(depth_planes) -> None:
     # the reference concatenates one slice per depth (utils.py:466-470): no depths is
     # torch.cat.s ValueError, raised here before anything is launched
@@ -640,10 +663,10 @@ def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.T
     _require_depths(depth_planes)
     dev = _dev(img)
     B, Hs, Ws, C = img.shape
-    d = torch.tensor([float(x) for x in depth_planes], dtype=torch.float32)
-    D = d.shape[0]
+    dd = _depths_on(depth_planes, dev)
+    D = dd.shape[0]
     out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
-    kid, projd, dd = _up(ki, dev), _up(proj, dev), _up(d, dev)
+    kid, projd = _up(ki, dev), _up(proj, dev)
     _call("mpiv_plane_sweep", img, _strides(img), B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out, _stream(dev))
     return out
 
@@ -656,11 +679,11 @@ def plane_sweep_padded(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: 
     _require_depths(depth_planes)
     dev = _dev(img)
     B, Hs, Ws, C = img.shape
-    d = torch.tensor([float(x) for x in depth_planes], dtype=torch.float32)
-    D = d.shape[0]
+    dd = _depths_on(depth_planes, dev)
+    D = dd.shape[0]
     out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
     img4 = pad_texels(img)
-    _call("mpiv_plane_sweep_padded", img4, B, Hs, Ws, C, _up(ki, dev), _up(proj, dev), _up(d, dev), D, tgt_h,
+    _call("mpiv_plane_sweep_padded", img4, B, Hs, Ws, C, _up(ki, dev), _up(proj, dev), dd, D, tgt_h,
           tgt_w, out, _stream(dev))
     return out
 
@@ -704,15 +727,14 @@ def network_input(ref_image, psv_src_images, rel_poses, depth_planes, intrinsics
     dev = _dev(ref_image, psv_src_images)
     B, H, W, _ = ref_image.shape
     S = len(rel_poses)
-    d = torch.tensor([float(x) for x in depth_planes], dtype=torch.float32)
-    D = d.shape[0]
+    dd = _depths_on(depth_planes, dev) if S else None
+    D = dd.shape[0] if S else len(depth_planes)
     Ctot = 3 + S * D * 3
     out = torch.empty((B, H, W, Ctot), device=dev, dtype=torch.float32)
     out[..., :3].copy_(ref_image)  # the concat's first slice is a plain copy (utils.py:491)
-    dd = _up(d, dev)
     for i, pose in enumerate(rel_poses):
         src = psv_src_images[:, :, :, i * 3:(i + 1) * 3]  # a strided channel slice, read in place
-        ki, proj = psv_matrices(intrinsics, intrinsics, pose)
+        ki, proj = psv_matrices(intrinsics, intrinsics, pose, pin=True)
         _call("mpiv_plane_sweep_into", src, _strides(src), B, H, W, 3, _up(ki, dev), _up(proj, dev), dd, D, H, W,
               out[..., 3 + i * D * 3:], H * W * Ctot, Ctot, _stream(dev))
     return out

@@ -243,7 +243,7 @@ def plane_sweep_torch(img, depth_planes, pose, intrinsics):
     """Plane-sweep volume [B, H, W, D*C] (channel d*C+c) of img [B, H, W, C] at the
     listed depths (utils.py:452-471).  One HIP launch writes the whole volume."""
     batch, height, width, _ = img.shape
-    ki, proj = _host.psv_matrices(intrinsics, intrinsics, pose)
+    ki, proj = _host.psv_matrices(intrinsics, intrinsics, pose, pin=img.is_cuda)
     return _lib.plane_sweep(img, depth_planes, ki, proj, height, width)
 
 
@@ -280,5 +280,5 @@ def plane_sweep_torch_one2(img, depth_planes, pose, src_intrinsics, tgt_intrinsi
     """PSV of img [H_s, W_s, C] into a (tgt_height, tgt_width) target grid with separate
     intrinsics; returns [1, tgt_height, tgt_width, D*C] (utils.py:771-799)."""
     ki, proj = _host.psv_matrices(src_intrinsics.unsqueeze(0), tgt_intrinsics.unsqueeze(0),
-                                  pose.unsqueeze(0))
+                                  pose.unsqueeze(0), pin=img.is_cuda)
     return _lib.plane_sweep(img.unsqueeze(0), depth_planes, ki, proj, tgt_height, tgt_width)

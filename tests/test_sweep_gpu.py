@@ -31,6 +31,21 @@ def test_plane_sweep_one(small, meta, dev):
     assert_bits(out.cpu().numpy(), small["psv_one_out"])
 
 
+def test_plane_sweep_one_notebook_call_pattern(small, meta, dev):
+    """The notebook's dataset call (ipynb cell 8 L73-75): the depths are a DEVICE tensor
+    (torch.Tensor(inv_depths(...)).to(device)) and pose / intrinsics live on the device; the
+    reference iterates the tensor element by element -- same volume as the depth list.
+    Repeated calls (the memoised depth upload, the single pinned matrix upload) stay equal."""
+    img = psv_case_input(meta["small"], "psv_one").to(dev)
+    planes = torch.Tensor(list(small["psv_one_depths"])).to(dev)
+    pose, K = _t(small, "psv_one_pose", dev), _t(small, "psv_one_K", dev)
+    for _ in range(3):
+        out = mv.plane_sweep_torch_one(img, planes, pose, K)
+        assert_bits(out.cpu().numpy(), small["psv_one_out"])
+        out = mv.plane_sweep_torch_one(img, list(small["psv_one_depths"]), pose, K)
+        assert_bits(out.cpu().numpy(), small["psv_one_out"])
+
+
 def test_plane_sweep_one2_separate_intrinsics(small, meta, dev):
     img = psv_case_input(meta["small"], "psv_two")
     m = meta["small"]["psv_two"]

@@ -9,7 +9,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof
-ARGS=${PROF_ARGS:---steps 3 --warmup 1 --cpu-seconds 0 --no-training}
+ARGS=${PROF_ARGS:---steps 3 --warmup 1 --cpu-seconds 0}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
