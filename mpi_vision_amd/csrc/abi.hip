@@ -65,6 +65,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (R, rows in flight) = (8, 4) / (6, 3) / (9, 3) / (4, 4)
 //   sweep_dlane=0      the LDS sweep runs pixel-per-lane (plane_sweep_lds_kernel) instead of
 //                      depth-per-lane (plane_sweep_dlane_kernel)
+//   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
+//                      wave (0 = automatic)
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
 //                      forces their per-sample global fallback (tests)
 //   bwd_fallback=1     mpiv_render_backward skips the tile gather and runs its bucket
@@ -76,13 +78,13 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 // launches is a test-harness race on which kernel runs, never on memory.
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
-                kOptRenderVshare, kNumOpts };
+                kOptRenderVshare, kOptChunkRows, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
-                                         "render_vshare"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0};
+                                         "render_vshare", "chunk_rows"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -111,11 +113,38 @@ constexpr int64_t kMaxGridYZ = 65535;
 constexpr int kNativeLdsMaxP = 16;
 constexpr int kChunkMaxLds = 65536;  // render_chunk_kernel: slots + P homographies, default LDS limit
 constexpr int kChunkSplit = 1;       // composite phases per chunk (render_chunk.hip SPLIT)
+
 constexpr int64_t kMaxGridX = 2147483647;
 
 }  // namespace
 
 using namespace mpiv;
+
+namespace {
+
+// rows per wave of render_chunk_kernel (chunk_rows option; automatic: 1)
+int chunk_rows() {
+    const int o = opt(kOptChunkRows);
+    return (o == 2 || o == 4) ? o : 1;
+}
+
+// launch render_chunk_kernel<CH, SPLIT, R> with the block count of its 64 x 4R tiles
+template <int CH, int SPLIT>
+int launch_chunk(int R, const float* mpi, int64_t vstride, const RenderGeom& g, const ChunkGeom& cg, int B,
+                 const float* homs, float* out, float4* ck, size_t lds, hipStream_t q, const char* nm) {
+    const int64_t nb = (int64_t)blocks(g.W, kTileX) * blocks(g.H, kTileY * R) * B;
+    if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+    if (g_route) return note_route(nb, 256, "render_chunk_kernel<%d, %d, %d>", CH, SPLIT, R);
+    if (R == 4)
+        render_chunk_kernel<CH, SPLIT, SPLIT == 1 ? 4 : 1><<<(unsigned)nb, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
+    else if (R == 2)
+        render_chunk_kernel<CH, SPLIT, SPLIT == 1 ? 2 : 1><<<(unsigned)nb, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
+    else
+        render_chunk_kernel<CH, SPLIT, 1><<<(unsigned)nb, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
+    return launched(nm);
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -163,19 +192,14 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
     const size_t ch_lds = (size_t)4 * (kWave / SPLIT) * (CH + 1) * 16 + (size_t)P * 36;
     if (vec && fast && s.p == 4 && ch_opt >= 0 && (CH == 4 || CH == 8) && rec < (int64_t)kOOB &&
         s.y / 4 < (1 << 22) && s.x / 4 < (1 << 22) && ch_lds <= (size_t)kChunkMaxLds) {
-        const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * B;
-        if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_render: too many blocks");
         const ChunkGeom cg{(int)(s.y / 4), (int)(s.x / 4), (int)rec};
-        if (g_route) return note_route(nb, 256, "render_chunk_kernel<%d, %d>", CH, SPLIT);
+        const int R = SPLIT == 1 ? chunk_rows() : 1;
         if (CH == 8 && SPLIT == 2)
-            render_chunk_kernel<8, 2><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out, nullptr);
-        else if (CH == 8)
-            render_chunk_kernel<8, 1><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out, nullptr);
-        else if (SPLIT == 2)
-            render_chunk_kernel<4, 2><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out, nullptr);
-        else
-            render_chunk_kernel<4, 1><<<(unsigned)nb, 256, ch_lds, q>>>(mpi, s.b, g, cg, B, homs, out, nullptr);
-        return launched("mpiv_render");
+            return launch_chunk<8, 2>(1, mpi, s.b, g, cg, B, homs, out, nullptr, ch_lds, q, "mpiv_render");
+        if (CH == 8) return launch_chunk<8, 1>(R, mpi, s.b, g, cg, B, homs, out, nullptr, ch_lds, q, "mpiv_render");
+        if (SPLIT == 2)
+            return launch_chunk<4, 2>(1, mpi, s.b, g, cg, B, homs, out, nullptr, ch_lds, q, "mpiv_render");
+        return launch_chunk<4, 1>(R, mpi, s.b, g, cg, B, homs, out, nullptr, ch_lds, q, "mpiv_render");
     }
     // footprints staged through LDS, read in place (render_lds.hip render_lds_native_kernel):
     // measured faster for few planes (P = 10: 0.031 vs 0.039 ms), slower for many (P = 128:
@@ -209,12 +233,9 @@ int mpiv_render_train(const float* mpi, const int64_t st[5], int B, int H, int W
         st[2] / 4 >= (1 << 22) || ch_lds > (size_t)kChunkMaxLds)
         return fail(MPIV_ERR_ARG, "%s: rgba_layers must be read in place (16-byte texels, planes contiguous per "
                     "pixel, one view below 2 GiB, P <= 796)", nm);
-    const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * B;
-    if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const ChunkGeom cg{(int)(st[1] / 4), (int)(st[2] / 4), (int)rec};
-    render_chunk_kernel<8, 1><<<(unsigned)nb, 256, ch_lds, S(stream)>>>(mpi, st[0], make_geom(H, W, P), cg, B, homs,
-                                                                        out, reinterpret_cast<float4*>(ckpt));
-    return launched(nm);
+    return launch_chunk<8, 1>(chunk_rows(), mpi, st[0], make_geom(H, W, P), cg, B, homs, out,
+                              reinterpret_cast<float4*>(ckpt), ch_lds, S(stream), nm);
 }
 
 int mpiv_pack_planes(const float* mpi, const int64_t st[4], int H, int W, int P, float* packed, void* stream) {
@@ -572,7 +593,6 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const ChunkGeom cg{(int)(st[1] / 4), (int)(st[2] / 4), (int)rec};
     const bool fast = H >= 2 && W >= 2;
     const int64_t HW = (int64_t)H * W;
-    const unsigned chain_blocks = blocks(W, kTileX) * blocks(H, kTileY);
     const int tiles_x = (int)blocks(W, kGTW);
     const int64_t ntiles = (int64_t)tiles_x * blocks(H, kGTH);
     const int64_t gather_blocks = ntiles * blocks(P, kGPl);
@@ -608,12 +628,19 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         float4* gv = reinterpret_cast<float4*>(dmpi) + (int64_t)v * HW * P;
         const float4* ck = ckpt ? reinterpret_cast<const float4*>(ckpt) + (int64_t)v * ((P + kBwdCH - 1) / kBwdCH) * HW
                                 : nullptr;
-        if (fast && ck)
-            bwd_chain_kernel<1, true><<<chain_blocks, 256, chain_lds, q>>>(mv, g, cg, hv, dv, ck, ws);
-        else if (fast)
-            bwd_chain_kernel<1, false><<<chain_blocks, 256, chain_lds, q>>>(mv, g, cg, hv, dv, nullptr, ws);
-        else
-            bwd_chain_kernel<0, false><<<chain_blocks, 256, chain_lds, q>>>(mv, g, cg, hv, dv, nullptr, ws);
+        const int R = fast ? chunk_rows() : 1;
+        const unsigned cb = blocks(W, kTileX) * blocks(H, kTileY * R);
+#define MPIV_CHAIN(CKB, RR)                                                                                  \
+    bwd_chain_kernel<1, CKB, RR><<<cb, 256, chain_lds, q>>>(mv, g, cg, hv, dv, CKB ? ck : nullptr, ws)
+        if (!fast)
+            bwd_chain_kernel<0, false, 1><<<cb, 256, chain_lds, q>>>(mv, g, cg, hv, dv, nullptr, ws);
+        else if (ck && R == 4) MPIV_CHAIN(true, 4);
+        else if (ck && R == 2) MPIV_CHAIN(true, 2);
+        else if (ck) MPIV_CHAIN(true, 1);
+        else if (R == 4) MPIV_CHAIN(false, 4);
+        else if (R == 2) MPIV_CHAIN(false, 2);
+        else MPIV_CHAIN(false, 1);
+#undef MPIV_CHAIN
         if (!force) {
             bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
             bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x, margin,
@@ -1164,6 +1191,9 @@ int mpiv_route(const char* entry, const int64_t* a, int na, char* name, int name
         const int64_t C = a[3], D = a[4], st[4] = {a[1] * a[2] * C, a[2] * C, C, 1};
         rc = mpiv_plane_sweep(d, st, (int)a[0], (int)a[1], (int)a[2], (int)C, d, d, d, (int)D, (int)a[5], (int)a[6], d,
                               nullptr);
+    } else if (strcmp(entry, "render_train") == 0 && na == 4) {
+        const int64_t P = a[3], st[5] = {a[1] * a[2] * P * 4, a[2] * P * 4, P * 4, 4, 1};
+        rc = mpiv_render_train(d, st, (int)a[0], (int)a[1], (int)a[2], (int)P, d, d, d, nullptr);
     } else if (strcmp(entry, "render") == 0 && na == 4) {
         const int64_t P = a[3], st[5] = {a[1] * a[2] * P * 4, a[2] * P * 4, P * 4, 4, 1};
         rc = mpiv_render(d, st, (int)a[0], (int)a[1], (int)a[2], (int)P, d, d, nullptr);

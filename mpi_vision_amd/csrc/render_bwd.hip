@@ -108,20 +108,22 @@ __device__ __forceinline__ void bwd_pos(const float* h, float fx, float fy, cons
 
 // CK: the forward's checkpoints (mpiv_render_train, [nchunk][HW] of this view) replace
 // pass 1; every sample is then issued (and its taps counted) in pass 2 only.
-template <int MODE, bool CK>
+// R rows per wave (render_chunk.hip's row grouping): rows y0 .. y0+R-1 of the wave's 64
+// columns with the chunk loop outside the row loop (row r+1's north taps come from L1/L2);
+// rows past the frame (nrows < R, wave-uniform) re-sample the last row, uncounted and unstored.
+template <int MODE, bool CK, int R>
 __device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, const RenderGeom& g,
                                                const ChunkGeom& cg, const float* __restrict__ hs,
-                                               f32x4* __restrict__ slot, int tx0, int y, int lane,
+                                               f32x4* __restrict__ slot, int tx0, int y0, int nrows_, int lane,
                                                const float* __restrict__ dout, const float4* __restrict__ ck,
                                                const BwdWs& ws) {
     constexpr int CH = kBwdCH, PPS = kWave / CH;
+    const int nrows = R == 1 ? 1 : nrows_;  // wave-uniform
     const int j = lane % CH, i = lane / CH;
-    const float fy = (float)y;
     const int n = (g.P + CH - 1) / CH;
     const int64_t HW = (int64_t)g.H * g.W;
     const int x = tx0 + lane;  // this lane's pixel in the composite phases
     const bool xin = x < g.W;
-    const int64_t pix = (int64_t)y * g.W + x;
     float h[9];
     auto load_h = [&](int c, float* d) {
         const int p = min(c * CH + j, g.P - 1);
@@ -130,29 +132,31 @@ __device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, c
     };
     auto rsrc = [&](int c) { return make_rsrc(view + (int64_t)c * CH * 4, cg.rec_bytes); };
     int ntap = 0;
-    // sub-step k of chunk c: pixel tx0 + k*PPS + i, plane c*CH + j (taps counted in pass 1)
-    auto issue = [&](int c, int k, const float* hh, ChunkTaps& ts, bool cnt) {
+    // sub-step k of row r, chunk c: pixel tx0 + k*PPS + i, plane c*CH + j (taps counted once)
+    auto issue = [&](int c, int r, int k, const float* hh, ChunkTaps& ts, bool cnt) {
         const int xs = tx0 + k * PPS + i;
         float px, py;
-        bwd_pos<MODE>(hh, (float)xs, fy, g, px, py);
+        bwd_pos<MODE>(hh, (float)xs, (float)(y0 + min(r, nrows - 1)), g, px, py);
         const int nt = issue_taps_chunk(rsrc(c), g, cg, j, c * CH + j < g.P, px, py, ts);
-        if (cnt && xs < g.W) ntap += nt;
+        if (cnt && xs < g.W && r < nrows) ntap += nt;
     };
     auto put = [&](int k, const ChunkTaps& ts) { slot[(k * PPS + i) * (CH + 1) + j] = blend_chunk(ts); };
     ChunkTaps A, B;
-    // chunk c's samples into the slot; A holds its sub-step 0 on entry and sub-step 0 of
-    // chunk cn (issued ahead, with cn's homography in h) on exit
-    auto sample_chunk = [&](int c, int cn, bool cnt, bool cnt_next) {
+    // row r of chunk c into the slot; A holds its sub-step 0 on entry and, on exit, sub-step 0
+    // of the next row (r + 1 < R) or of row 0 of chunk cn (issued ahead, cn's homography in h)
+    auto sample_row = [&](int c, int r, int cn, bool cnt, bool cnt_next) {
 #pragma unroll
         for (int k = 0; k < CH; k += 2) {
-            issue(c, k + 1, h, B, cnt);
+            issue(c, r, k + 1, h, B, cnt);
             __builtin_amdgcn_sched_barrier(0);
             put(k, A);
             if (k + 2 < CH) {
-                issue(c, k + 2, h, A, cnt);
+                issue(c, r, k + 2, h, A, cnt);
+            } else if (r + 1 < R) {
+                issue(c, r + 1, 0, h, A, cnt);
             } else {
                 load_h(cn, h);
-                issue(cn, 0, h, A, cnt_next);
+                issue(cn, 0, 0, h, A, cnt_next);
             }
             __builtin_amdgcn_sched_barrier(0);
             put(k + 1, B);
@@ -161,92 +165,117 @@ __device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, c
     const f32x4* row = slot + lane * (CH + 1);
     // ---- pass 1: planes 0 .. P-1 like the forward (plane 0 replaces the -0 start
     // exactly, render.hip), the colour checkpointed before every chunk.  The last chunk
-    // stays in the slot for pass 2; chunk n-2 is issued ahead.
-    float cr = -0.0f, cgc = -0.0f, cb = -0.0f;
+    // stays in the slot for pass 2 (R == 1); chunk n-2 is issued ahead.
+    float cr[R], cgc[R], cb[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) cr[r] = cgc[r] = cb[r] = -0.0f;
     if (CK) {
         load_h(n - 1, h);
-        issue(n - 1, 0, h, A, true);
+        issue(n - 1, 0, 0, h, A, true);
     } else {
         load_h(0, h);
-        issue(0, 0, h, A, true);
+        issue(0, 0, 0, h, A, true);
         for (int c = 0; c < n; ++c) {
             const bool last = c == n - 1;
-            sample_chunk(c, last ? max(n - 2, 0) : c + 1, true, !last);
-            if (last) break;
+            // R == 1: the last chunk stays in the slot for pass 2, chunk n-2's first sub-step is
+            // issued ahead; R > 1: pass 2 re-samples the last chunk (row 0 issued ahead)
 #pragma unroll
-            for (int k = 0; k < CH; ++k) {  // a chunk before the last is full
-                const f32x4 s = row[k];
-                const float a = (c == 0 && k == 0) ? 1.0f : s[3];
-                const float om = 1.0f - a;
-                cr = over(s[0], a, om, cr);
-                cgc = over(s[1], a, om, cgc);
-                cb = over(s[2], a, om, cb);
+            for (int r = 0; r < R; ++r) {
+                sample_row(c, r, last ? (R == 1 ? max(n - 2, 0) : n - 1) : c + 1, true, !last);
+                if (!last && r < nrows) {
+#pragma unroll
+                    for (int k = 0; k < CH; ++k) {  // a chunk before the last is full
+                        const f32x4 s = row[k];
+                        const float a = (c == 0 && k == 0) ? 1.0f : s[3];
+                        const float om = 1.0f - a;
+                        cr[r] = over(s[0], a, om, cr[r]);
+                        cgc[r] = over(s[1], a, om, cgc[r]);
+                        cb[r] = over(s[2], a, om, cb[r]);
+                    }
+                    if (xin) ws.ckpt[(int64_t)(c + 1) * HW + (int64_t)(y0 + r) * g.W + x] =
+                        make_float4(cr[r], cgc[r], cb[r], 0.0f);
+                }
+                if (R > 1) asm volatile("" : "+v"(cr[r]), "+v"(cgc[r]), "+v"(cb[r])::"memory");
             }
-            if (xin) ws.ckpt[(int64_t)(c + 1) * HW + pix] = make_float4(cr, cgc, cb, 0.0f);
+            if (last) break;
         }
     }
     // ---- pass 2: chunks back to front; over_composite backward (utils.py:149-156 under
     // autograd), planes P-1 .. 0
-    float g0 = 0.0f, g1 = 0.0f, g2 = 0.0f;
-    if (xin) {
-        const float* d = dout + pix * 3;
-        g0 = d[0];
-        g1 = d[1];
-        g2 = d[2];
+    float g0[R], g1[R], g2[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        g0[r] = g1[r] = g2[r] = 0.0f;
+        if (xin && r < nrows) {
+            const float* d = dout + ((int64_t)(y0 + r) * g.W + x) * 3;
+            g0[r] = d[0];
+            g1[r] = d[1];
+            g2[r] = d[2];
+        }
     }
     for (int c = n - 1; c >= 0; --c) {
-        float4 pre = make_float4(cr, cgc, cb, 0.0f);  // c = n-1: pass 1's colour
-        if (CK || c < n - 1) {
-            if (c == 0)
-                pre = make_float4(-0.0f, -0.0f, -0.0f, 0.0f);
-            else if (xin)
-                pre = CK ? ck[(int64_t)c * HW + pix] : ws.ckpt[(int64_t)c * HW + pix];
-            sample_chunk(c, c > 0 ? c - 1 : 0, CK, CK && c > 0);
-        }
-        // prefixes out_{p-1} of the chunk's planes, recomputed in the forward's order
-        float pr[CH][3];
-        pr[0][0] = pre.x;
-        pr[0][1] = pre.y;
-        pr[0][2] = pre.z;
 #pragma unroll
-        for (int k = 0; k + 1 < CH; ++k) {
-            const int p = c * CH + k;
-            float r = pr[k][0], gr = pr[k][1], b = pr[k][2];
-            if (p < g.P) {
-                const f32x4 s = row[k];
-                const float a = p == 0 ? 1.0f : s[3];
-                const float om = 1.0f - a;
-                r = over(s[0], a, om, r);
-                gr = over(s[1], a, om, gr);
-                b = over(s[2], a, om, b);
+        for (int r = 0; r < R; ++r) {
+            const int64_t pix = (int64_t)(y0 + r) * g.W + x;
+            float4 pre = make_float4(cr[r], cgc[r], cb[r], 0.0f);  // R == 1, c = n-1: pass 1's colour
+            const bool resample = CK || R > 1 || c < n - 1;
+            if (resample) {
+                if (c == 0)
+                    pre = make_float4(-0.0f, -0.0f, -0.0f, 0.0f);
+                else if (xin && r < nrows)
+                    pre = CK ? ck[(int64_t)c * HW + pix] : ws.ckpt[(int64_t)c * HW + pix];
+                // the sample issued ahead for row 0 of chunk c-1 is counted only when every
+                // sample is issued here (CK); without checkpoints pass 1 counted it
+                sample_row(c, r, c > 0 ? c - 1 : 0, CK, CK && c > 0);
             }
-            pr[k + 1][0] = r;
-            pr[k + 1][1] = gr;
-            pr[k + 1][2] = b;
-        }
+            if (r < nrows) {
+                // prefixes out_{p-1} of the chunk's planes, recomputed in the forward's order
+                float pr[CH][3];
+                pr[0][0] = pre.x;
+                pr[0][1] = pre.y;
+                pr[0][2] = pre.z;
 #pragma unroll
-        for (int k = CH - 1; k >= 0; --k) {
-            const int p = c * CH + k;
-            if (p < g.P) {
-                const f32x4 s = row[k];
-                float4 d;
-                if (p >= 1) {
-                    const float a = s[3], om = 1.0f - a;
-                    float s1 = g0 * s[0];
-                    s1 = s1 + g1 * s[1];
-                    s1 = s1 + g2 * s[2];
-                    float s2 = g0 * pr[k][0];
-                    s2 = s2 + g1 * pr[k][1];
-                    s2 = s2 + g2 * pr[k][2];
-                    d = make_float4(g0 * a, g1 * a, g2 * a, s1 + (-s2));
-                    g0 = g0 * om;
-                    g1 = g1 * om;
-                    g2 = g2 * om;
-                } else {
-                    d = make_float4(g0, g1, g2, 0.0f);  // plane 0: output = rgb_0, alpha unused
+                for (int k = 0; k + 1 < CH; ++k) {
+                    const int p = c * CH + k;
+                    float rr = pr[k][0], gr = pr[k][1], b = pr[k][2];
+                    if (p < g.P) {
+                        const f32x4 s = row[k];
+                        const float a = p == 0 ? 1.0f : s[3];
+                        const float om = 1.0f - a;
+                        rr = over(s[0], a, om, rr);
+                        gr = over(s[1], a, om, gr);
+                        b = over(s[2], a, om, b);
+                    }
+                    pr[k + 1][0] = rr;
+                    pr[k + 1][1] = gr;
+                    pr[k + 1][2] = b;
                 }
-                if (xin) ws.ds[(int64_t)p * HW + pix] = d;
+#pragma unroll
+                for (int k = CH - 1; k >= 0; --k) {
+                    const int p = c * CH + k;
+                    if (p < g.P) {
+                        const f32x4 s = row[k];
+                        float4 d;
+                        if (p >= 1) {
+                            const float a = s[3], om = 1.0f - a;
+                            float s1 = g0[r] * s[0];
+                            s1 = s1 + g1[r] * s[1];
+                            s1 = s1 + g2[r] * s[2];
+                            float s2 = g0[r] * pr[k][0];
+                            s2 = s2 + g1[r] * pr[k][1];
+                            s2 = s2 + g2[r] * pr[k][2];
+                            d = make_float4(g0[r] * a, g1[r] * a, g2[r] * a, s1 + (-s2));
+                            g0[r] = g0[r] * om;
+                            g1[r] = g1[r] * om;
+                            g2[r] = g2[r] * om;
+                        } else {
+                            d = make_float4(g0[r], g1[r], g2[r], 0.0f);  // plane 0: output = rgb_0, alpha unused
+                        }
+                        if (xin) ws.ds[(int64_t)p * HW + pix] = d;
+                    }
+                }
             }
+            if (R > 1) asm volatile("" : "+v"(g0[r]), "+v"(g1[r]), "+v"(g2[r])::"memory");
         }
     }
 #pragma unroll
@@ -254,38 +283,41 @@ __device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, c
     if (lane == 0 && ntap) atomicAdd(&ws.truth[blockIdx.x % kCtrSlots], (unsigned long long)ntap);
 }
 
-// One block = 4 waves = a 64x4 output tile of one view.  Dynamic LDS: 4 per-wave sample
-// slots (64 x (CH+1) float4) + the view's P homographies.  MODE 0: generic recipe
-// (H or W < 2); 1: fast recipe, the tile's division proof picks the unguarded path.
-template <int MODE, bool CK>
-__global__ __launch_bounds__(256) void bwd_chain_kernel(const float* __restrict__ view, RenderGeom g, ChunkGeom cg,
-                                                        const float* __restrict__ homs,
-                                                        const float* __restrict__ dout,
-                                                        const float4* __restrict__ ck, BwdWs ws) {
+// One block = 4 waves = a 64 x 4R output tile of one view (wave w: rows w*R .. w*R+R-1).
+// Dynamic LDS: 4 per-wave sample slots (64 x (CH+1) float4) + the view's P homographies.
+// MODE 0: generic recipe (H or W < 2); 1: fast recipe, the tile's division proof picks the
+// unguarded path.
+template <int MODE, bool CK, int R>
+__global__ __launch_bounds__(256, R == 1 ? 1 : 4) void bwd_chain_kernel(const float* __restrict__ view, RenderGeom g, ChunkGeom cg,
+                                                           const float* __restrict__ homs,
+                                                           const float* __restrict__ dout,
+                                                           const float4* __restrict__ ck, BwdWs ws) {
     extern __shared__ float4 bwd_lds[];
     f32x4* slots = reinterpret_cast<f32x4*>(bwd_lds);
     float* hs = reinterpret_cast<float*>(bwd_lds) + 4 * kWave * (kBwdCH + 1) * 4;
+    constexpr int TH = kTileY * R;
     const int tiles_x = (g.W + kTileX - 1) / kTileX;
     const int tile = xcd_logical_block(blockIdx.x, gridDim.x);
-    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * kTileY;
+    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * TH;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     for (int k = threadIdx.x; k < g.P * 9; k += 256) hs[k] = homs[k];
     bool ok = MODE != 0;
     if (MODE != 0) {
         const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
-        const float y0 = (float)ty0, y1 = (float)min(ty0 + kTileY - 1, g.H - 1);
+        const float y0 = (float)ty0, y1 = (float)min(ty0 + TH - 1, g.H - 1);
         for (int p = (int)threadIdx.x; p < g.P; p += 256) ok = ok && div2_rect_safe(homs + (int64_t)p * 9, x0, x1, y0, y1);
     }
     const bool proven = __syncthreads_and(ok);  // also publishes hs
-    const int y = ty0 + wave;
+    const int y = ty0 + wave * R;
     if (y >= g.H) return;  // whole wave; no barrier follows
+    const int nrows = min(R, g.H - y);
     f32x4* slot = slots + wave * kWave * (kBwdCH + 1);
     if (MODE == 0)
-        bwd_chain_wave<0, CK>(view, g, cg, hs, slot, tx0, y, lane, dout, ck, ws);
+        bwd_chain_wave<0, CK, R>(view, g, cg, hs, slot, tx0, y, nrows, lane, dout, ck, ws);
     else if (proven)
-        bwd_chain_wave<2, CK>(view, g, cg, hs, slot, tx0, y, lane, dout, ck, ws);
+        bwd_chain_wave<2, CK, R>(view, g, cg, hs, slot, tx0, y, nrows, lane, dout, ck, ws);
     else
-        bwd_chain_wave<1, CK>(view, g, cg, hs, slot, tx0, y, lane, dout, ck, ws);
+        bwd_chain_wave<1, CK, R>(view, g, cg, hs, slot, tx0, y, nrows, lane, dout, ck, ws);
 }
 
 // ---- 2. gather: per-texel sums in the reference's order ------------------------------

@@ -106,15 +106,22 @@ constexpr int chunk_slot_floats() {
     return 4 * (kWave / SPLIT) * (CH + 1) * 4;
 }
 
-template <int CH, int SPLIT, bool GUARD>
+// R rows per wave (R > 1: SPLIT == 1): the wave renders rows y0 .. y0+R-1 of its 64 columns
+// with the chunk loop OUTSIDE the row loop, so row r+1's north taps are the texels row r
+// gathered moments before (L1/L2 hits instead of HBM re-reads: a 64 x 4R block tile re-reads
+// only its outer halo).  The A/B tap pipeline runs on across rows and chunks.  Rows past the
+// frame (nrows < R, wave-uniform) re-sample the last row and are neither composited nor
+// stored.
+template <int CH, int SPLIT, int R, bool GUARD>
 __device__ __forceinline__ void render_chunk_wave(const float* __restrict__ view, const RenderGeom& g,
                                                   const ChunkGeom& cg, const float* __restrict__ hs,
-                                                  f32x4* __restrict__ slot, int tx0, int y, int lane,
-                                                  float& cr, float& cg_, float& cb, float4* __restrict__ ck,
-                                                  int64_t ck_stride) {
+                                                  f32x4* __restrict__ slot, int tx0, int y0, int nrows_, int lane,
+                                                  float (&cr)[R], float (&cg_)[R], float (&cb)[R],
+                                                  float4* __restrict__ ck, int64_t ck_stride) {
+    static_assert(R == 1 || SPLIT == 1, "R rows per wave composite whole chunks");
     constexpr int PPS = kWave / CH;  // pixels per sub-step
+    const int nrows = R == 1 ? 1 : nrows_;  // wave-uniform
     const int j = lane % CH, i = lane / CH;
-    const float fy = (float)y;
     const int nchunk = (g.P + CH - 1) / CH;
     float h[9];
     auto load_h = [&](int c, float* d) {
@@ -125,26 +132,27 @@ __device__ __forceinline__ void render_chunk_wave(const float* __restrict__ view
     auto rsrc = [&](int c) {
         return make_rsrc(view + (int64_t)c * CH * 4, cg.rec_bytes);
     };
-    // sub-step k of chunk c: pixel tx0 + k*PPS + i, plane c*CH + j
-    auto issue = [&](int c, int k, const float* hh, ChunkTaps& ts) {
+    // sub-step k of row r, chunk c: pixel (tx0 + k*PPS + i, row r), plane c*CH + j
+    auto issue = [&](int c, int r, int k, const float* hh, ChunkTaps& ts) {
         float px, py;
+        const float fy = (float)(y0 + min(r, nrows - 1));
         chunk_pos<GUARD>(hh, (float)(tx0 + k * PPS + i), fy, g, px, py);
         issue_taps_chunk(rsrc(c), g, cg, j, c * CH + j < g.P, px, py, ts);
     };
     constexpr int QP = kWave / SPLIT;  // pixels per composite phase
     constexpr int KP = CH / SPLIT;     // sub-steps per composite phase
     auto put = [&](int k, const ChunkTaps& ts) { slot[((k * PPS + i) % QP) * (CH + 1) + j] = blend_chunk(ts); };
-    // composite phase h: lane = pixel tx0 + lane (lanes of that phase only), planes
+    // composite phase h of row r: lane = pixel tx0 + lane (lanes of that phase only), planes
     // c*CH .. c*CH+CH-1 back to front
-    auto over_px = [&](const f32x4& s, bool first) {
-        const float a = first ? 1.0f : s[3];  // plane 0 replaces (render_packed_pixel)
-        const float om = 1.0f - a;
-        cr = over(s[0], a, om, cr);
-        cg_ = over(s[1], a, om, cg_);
-        cb = over(s[2], a, om, cb);
-    };
-    auto composite = [&](int c, int h) {
-        if (SPLIT == 1 || lane / QP == h) {
+    auto composite = [&](int c, int hph, int r) {
+        auto over_px = [&](const f32x4& s, bool first) {
+            const float a = first ? 1.0f : s[3];  // plane 0 replaces (render_packed_pixel)
+            const float om = 1.0f - a;
+            cr[r] = over(s[0], a, om, cr[r]);
+            cg_[r] = over(s[1], a, om, cg_[r]);
+            cb[r] = over(s[2], a, om, cb[r]);
+        };
+        if (SPLIT == 1 || lane / QP == hph) {
             const f32x4* row = slot + (lane % QP) * (CH + 1);
             if (c * CH + CH <= g.P) {  // full chunk: reads in flight 4 at a time, no branches
 #pragma unroll
@@ -162,33 +170,44 @@ __device__ __forceinline__ void render_chunk_wave(const float* __restrict__ view
     };
     ChunkTaps A, B;
     load_h(0, h);
-    issue(0, 0, h, A);
+    issue(0, 0, 0, h, A);
     for (int c = 0; c < nchunk; ++c) {
         const int cn = c + 1 < nchunk ? c + 1 : c;  // past the end: re-issue (cached, unused)
         // training: the colour before chunk c, the render backward's checkpoint (render_bwd.hip)
-        if (ck && c > 0) ck[c * ck_stride] = make_float4(cr, cg_, cb, 0.0f);
+        if (ck && c > 0) {
 #pragma unroll
-        for (int k = 0; k < CH; k += 2) {  // A holds sub-step k
-            issue(c, k + 1, h, B);
-            __builtin_amdgcn_sched_barrier(0);
-            put(k, A);
-            if (k + 2 < CH) {
-                issue(c, k + 2, h, A);
-            } else {
-                load_h(cn, h);  // the next chunk's homography (LDS) replaces this one's
-                issue(cn, 0, h, A);
+            for (int r = 0; r < R; ++r)
+                if (r < nrows) ck[c * ck_stride + (int64_t)r * g.W] = make_float4(cr[r], cg_[r], cb[r], 0.0f);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int k = 0; k < CH; k += 2) {  // A holds sub-step k of row r
+                issue(c, r, k + 1, h, B);
+                __builtin_amdgcn_sched_barrier(0);
+                put(k, A);
+                if (k + 2 < CH) {
+                    issue(c, r, k + 2, h, A);
+                } else if (r + 1 < R) {
+                    issue(c, r + 1, 0, h, A);
+                } else {
+                    load_h(cn, h);  // the next chunk's homography (LDS) replaces this one's
+                    issue(cn, 0, 0, h, A);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                put(k + 1, B);
+                if ((k + 2) % KP == 0 && r < nrows) composite(c, (k + 1) / KP, r);
+                if (R > 1) asm volatile("" : "+v"(cr[r]), "+v"(cg_[r]), "+v"(cb[r])::"memory");  // pinned here
             }
-            __builtin_amdgcn_sched_barrier(0);
-            put(k + 1, B);
-            if ((k + 2) % KP == 0) composite(c, (k + 1) / KP);
         }
     }
 }
 
-// One block = 4 waves = a 64x4 output tile of one view; blocks in render_packed_kernel's
-// XCD-aware (tile, view) order.  Dynamic LDS: chunk_slot_floats<CH, SPLIT>() + P*9 floats.
-template <int CH, int SPLIT>
-__global__ __launch_bounds__(256, SPLIT == 2 ? 6 : 1) void render_chunk_kernel(const float* __restrict__ mpi, int64_t view_stride,
+// One block = 4 waves = a 64 x 4R output tile of one view (wave w: rows w*R .. w*R+R-1 of
+// the tile); blocks in render_packed_kernel's XCD-aware (tile, view) order.  Dynamic LDS:
+// chunk_slot_floats<CH, SPLIT>() + P*9 floats.
+template <int CH, int SPLIT, int R>
+__global__ __launch_bounds__(256, SPLIT == 2 ? 6 : 4) void render_chunk_kernel(const float* __restrict__ mpi, int64_t view_stride,
                                                            RenderGeom g, ChunkGeom cg, int V,
                                                            const float* __restrict__ homs,
                                                            float* __restrict__ out,
@@ -196,38 +215,47 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 6 : 1) void render_chunk_kernel(c
     extern __shared__ float4 chunk_lds[];
     f32x4* slots = reinterpret_cast<f32x4*>(chunk_lds);
     float* hs = reinterpret_cast<float*>(chunk_lds) + chunk_slot_floats<CH, SPLIT>();
+    constexpr int TH = kTileY * R;
     const int tiles_x = (g.W + kTileX - 1) / kTileX;
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
     const int v = lb % V;
     const int tile = lb / V;
-    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * kTileY;
+    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * TH;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     const float* hv = homs + (int64_t)v * g.P * 9;
     for (int k = threadIdx.x; k < g.P * 9; k += 256) hs[k] = hv[k];
     // block prologue: prove the fast division for the tile, all planes at once
     const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
-    const float y0 = (float)ty0, y1 = (float)min(ty0 + kTileY - 1, g.H - 1);
+    const float y0 = (float)ty0, y1 = (float)min(ty0 + TH - 1, g.H - 1);
     bool ok = true;
     for (int p = (int)threadIdx.x; p < g.P; p += 256) ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, y0, y1);
     const bool proven = __syncthreads_and(ok);  // also publishes hs
-    const int y = ty0 + wave;
+    const int y = ty0 + wave * R;
     if (y >= g.H) return;  // whole wave; no barrier follows
+    const int nrows = min(R, g.H - y);
     const float* view = mpi + (int64_t)v * view_stride;
     f32x4* slot = slots + wave * (kWave / SPLIT) * (CH + 1);
-    float cr = -0.0f, cgr = -0.0f, cb = -0.0f;
+    float cr[R], cgr[R], cb[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) cr[r] = cgr[r] = cb[r] = -0.0f;
     const int x = tx0 + lane;
     // checkpoints [V][nchunk][H][W] (nullptr: inference; SPLIT = 1 only: lane = pixel)
     const int64_t HW = (int64_t)g.H * g.W;
     float4* ck = (ckpt && x < g.W) ? ckpt + ((int64_t)v * ((g.P + CH - 1) / CH)) * HW + (int64_t)y * g.W + x : nullptr;
     if (proven)
-        render_chunk_wave<CH, SPLIT, false>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb, ck, HW);
+        render_chunk_wave<CH, SPLIT, R, false>(view, g, cg, hs, slot, tx0, y, nrows, lane, cr, cgr, cb, ck, HW);
     else
-        render_chunk_wave<CH, SPLIT, true>(view, g, cg, hs, slot, tx0, y, lane, cr, cgr, cb, ck, HW);
+        render_chunk_wave<CH, SPLIT, R, true>(view, g, cg, hs, slot, tx0, y, nrows, lane, cr, cgr, cb, ck, HW);
     if (x < g.W) {
-        float* o = out + (((int64_t)v * g.H + y) * g.W + x) * 3;
-        o[0] = cr;
-        o[1] = cgr;
-        o[2] = cb;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r < nrows) {
+                float* o = out + (((int64_t)v * g.H + y + r) * g.W + x) * 3;
+                o[0] = cr[r];
+                o[1] = cgr[r];
+                o[2] = cb[r];
+            }
+        }
     }
 }
 

@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Kernel A/B timings on the GPU box (round 3): each experiment times the production
+entry point under a set of libmpiv debug options, alternating the variants twice so a
+drifting clock shows up as disagreement between the two passes.  One JSON line per
+measurement (median of --iters launches, HIP events on the launch stream).
+
+    python tools/ab.py --only chunk,train,bwd,sweep,sweep10,u8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from mpi_vision_amd import _host, _lib, configs  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, iters, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        fn()
+        b.record(s)
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return statistics.median(ts), min(ts)
+
+
+def run(name, variants, fn, alg, iters, passes=2):
+    for p in range(passes):
+        for label, opts in variants:
+            with _lib.debug(**opts):
+                ms, mn = timed(fn, iters)
+            print(json.dumps({"exp": name, "variant": label, "pass": p, "ms": round(ms, 4), "ms_min": round(mn, 4),
+                              "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK, 4)}), flush=True)
+
+
+def c4_mpi(dev, B=1):
+    c = configs.config4()
+    H, W, P = c["H"], c["W"], c["P"]
+    g = torch.Generator(device=dev).manual_seed(0)
+    mpi = torch.rand((B, H, W, P, 4), generator=g, device=dev)
+    homs = _host.render_homographies(configs.f32(c["poses"][100:100 + B]), configs.f32(c["depths"]),
+                                     configs.f32([c["K"]] * B), B).to(dev)
+    return mpi, homs, H, W, P
+
+
+ROWS = [("rows1", {"chunk_rows": 1}), ("rows2", {"chunk_rows": 2}), ("rows4", {"chunk_rows": 4})]
+
+
+def chunk(dev, it):
+    mpi, homs, H, W, P = c4_mpi(dev)
+    out = torch.empty((1, H, W, 3), device=dev)
+    fn = lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out, _lib._stream(dev))  # noqa: E731
+    run("c4 in-place render (render_chunk_kernel), 1 view", ROWS, fn, P * H * W * 16 + H * W * 12, it)
+
+
+def train(dev, it):
+    mpi, homs, H, W, P = c4_mpi(dev)
+    fn = lambda: _lib.render_train(mpi, homs)  # noqa: E731
+    run("c4 training forward (frame + checkpoints), 1 view", ROWS, fn, P * H * W * 16 + H * W * 12, it)
+
+
+def bwd(dev, it):
+    mpi, homs, H, W, P = c4_mpi(dev)
+    g = torch.Generator(device=dev).manual_seed(1)
+    dout = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    ws = torch.empty(_lib.load().mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    _, ck = _lib.render_train(mpi, homs)
+    fn = lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)  # noqa: E731
+    run("c4 render backward with checkpoints, 1 view", ROWS, fn, 2 * P * H * W * 16 + H * W * 12, it)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="chunk,train,bwd")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    for name in a.only.split(","):
+        globals()[name](dev, a.iters)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
