@@ -18,6 +18,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MPIV_LIB: another build of the same ABI (kernel A/B tools only, tools/gpu_ab_lib.sh);
 # its build id is not checked against the sources in this tree
 LIB_PATH = os.environ.get("MPIV_LIB") or os.path.join(_HERE, "libmpiv.so")
+# the A/B flavour of the same sources (Makefile: -DMPIV_AB=1): the production kernels plus the
+# variants kept for measurement; loaded only while a debug option selects one of them
+AB_PATH = os.path.join(_HERE, "libmpiv_ab.so")
 _CSRC = os.path.join(_HERE, "csrc")
 
 _c_i64p = ctypes.POINTER(ctypes.c_int64)
@@ -74,6 +77,8 @@ EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_ba
 ABI_VERSION = 10
 
 _lib = None
+_lib_ab = None
+_override = None  # the A/B library while a debug option selects an A/B kernel
 
 # How mpi_render_view_torch renders a non-broadcast MPI batch: "auto" (the in-place
 # chunked kernel when the layout allows it, else pack per view when P >= 8, else read in
@@ -114,35 +119,56 @@ def source_hash() -> str | None:
         return None
 
 
-def load():
-    """Load libmpiv.so (raises if it has not been built, or was built from other sources
-    than the ones in this tree)."""
+def _open(path: str, check_id: bool):
+    if not os.path.exists(path):
+        raise RuntimeError(f"mpi_vision_amd: {path} is missing -- build it first "
+                           "(python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(path)
+    L.mpiv_build_id.restype = ctypes.c_char_p
+    want = source_hash()
+    if check_id and want is not None and L.mpiv_build_id().decode() != want:
+        raise RuntimeError(f"mpi_vision_amd: {path} was built from other sources (build id "
+                           f"{L.mpiv_build_id().decode()}, sources {want}) -- rebuild it "
+                           "(python -c 'import __graft_entry__ as g; g.build()')")
+    L.mpiv_debug_set.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    L.mpiv_debug_set.restype = ctypes.c_int
+    for name, args in _SIGS.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    L.mpiv_abi_version.restype = ctypes.c_int
+    L.mpiv_last_error.restype = ctypes.c_char_p
+    L.mpiv_render_backward_workspace_size.argtypes = [_int, _int, _int]
+    L.mpiv_render_backward_workspace_size.restype = ctypes.c_size_t
+    if L.mpiv_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"mpi_vision_amd: {path} ABI version mismatch")
+    return L
+
+
+def load_main():
+    """The production libmpiv.so (raises if it has not been built, or was built from other
+    sources than the ones in this tree)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"mpi_vision_amd: {LIB_PATH} is missing -- build it first "
-                               "(python -c 'import __graft_entry__ as g; g.build()')")
-        L = ctypes.CDLL(LIB_PATH)
-        L.mpiv_build_id.restype = ctypes.c_char_p
-        want = source_hash()
-        if not os.environ.get("MPIV_LIB") and want is not None and L.mpiv_build_id().decode() != want:
-            raise RuntimeError(f"mpi_vision_amd: {LIB_PATH} was built from other sources (build id "
-                               f"{L.mpiv_build_id().decode()}, sources {want}) -- rebuild it "
-                               "(python -c 'import __graft_entry__ as g; g.build()')")
-        L.mpiv_debug_set.argtypes = [ctypes.c_char_p, ctypes.c_int]
-        L.mpiv_debug_set.restype = ctypes.c_int
-        for name, args in _SIGS.items():
-            fn = getattr(L, name)
-            fn.argtypes = args
-            fn.restype = ctypes.c_int
-        L.mpiv_abi_version.restype = ctypes.c_int
-        L.mpiv_last_error.restype = ctypes.c_char_p
-        L.mpiv_render_backward_workspace_size.argtypes = [_int, _int, _int]
-        L.mpiv_render_backward_workspace_size.restype = ctypes.c_size_t
-        if L.mpiv_abi_version() != ABI_VERSION:
-            raise RuntimeError("mpi_vision_amd: libmpiv.so ABI version mismatch")
-        _lib = L
+        _lib = _open(LIB_PATH, not os.environ.get("MPIV_LIB"))
     return _lib
+
+
+def load_ab():
+    """libmpiv_ab.so, the A/B flavour (same sources, -DMPIV_AB=1).  Under MPIV_LIB (an A/B
+    tool's own build, which compiles every variant) that library serves both roles."""
+    global _lib_ab
+    if os.environ.get("MPIV_LIB"):
+        return load_main()
+    if _lib_ab is None:
+        _lib_ab = _open(AB_PATH, True)
+    return _lib_ab
+
+
+def load():
+    """The library entry points run through: libmpiv.so, or libmpiv_ab.so while a debug
+    option selects an A/B kernel (set_debug)."""
+    return _override if _override is not None else load_main()
 
 
 # MPIV_ROCTX=1: every entry-point call is wrapped in a roctx range named after it, so
@@ -157,11 +183,15 @@ if os.environ.get("MPIV_ROCTX") == "1":
         _ROCTX = None
 
 
+# entry points whose only kernels are A/B variants (libmpiv.so refuses them)
+_AB_ENTRIES = frozenset({"mpiv_render_packed_lds"})
+
+
 def _call(name, *args):
-    """Call an entry point.  Tensor arguments are passed as their device pointers and
+    """Call an entry point (an A/B-only one on libmpiv_ab.so).  Tensor arguments are passed as their device pointers and
     stay referenced (alive) for the duration of the call, so temporaries built inline
     cannot be freed and their memory reused by a later argument's allocation."""
-    L = load()
+    L = load_ab() if name in _AB_ENTRIES else load()
     cargs = [ctypes.c_void_p(a.data_ptr()) if isinstance(a, torch.Tensor) else a for a in args]
     if _ROCTX is not None:
         _ROCTX.roctxRangePushA(name.encode())
@@ -175,25 +205,55 @@ def _call(name, *args):
         raise RuntimeError(f"{name} failed ({rc}): {L.mpiv_last_error().decode()}")
 
 
+def set_debug(**opts):
+    """Select non-default kernel variants (tests and A/B tools only; mpiv_debug_set).
+    Options that pick a kernel kept for A/B measurement are refused by the production
+    library; then the A/B flavour takes them and runs every entry point until reset_debug()."""
+    global _override
+    L = load_main()
+    need_ab = False
+    for k, v in opts.items():
+        if L.mpiv_debug_set(k.encode(), int(v)) != 0:
+            msg = L.mpiv_last_error().decode()
+            if "libmpiv_ab.so" not in msg:
+                L.mpiv_debug_set(b"reset", 0)
+                raise ValueError(msg)
+            need_ab = True
+    if need_ab:
+        L.mpiv_debug_set(b"reset", 0)
+        A = load_ab()
+        for k, v in opts.items():
+            if A.mpiv_debug_set(k.encode(), int(v)) != 0:
+                msg = A.mpiv_last_error().decode()
+                A.mpiv_debug_set(b"reset", 0)
+                raise ValueError(msg)
+        _override = A
+
+
+def reset_debug():
+    """Every option back to its production default; entry points back on libmpiv.so."""
+    global _override
+    for L in (_lib, _lib_ab):
+        if L is not None:
+            L.mpiv_debug_set(b"reset", 0)
+    _override = None
+
+
 @contextlib.contextmanager
 def debug(**opts):
-    """Select non-default kernel variants for the duration of the block (tests and A/B
-    tools only; mpiv_debug_set): e.g. ``with _lib.debug(render_mv=1, box_shrink=2): ...``.
-    Every option is restored to its production default on exit."""
-    L = load()
+    """set_debug(**opts) for the duration of the block, e.g.
+    ``with _lib.debug(render_mv=1, box_shrink=2): ...``; reset_debug() on exit."""
     try:
-        for k, v in opts.items():
-            if L.mpiv_debug_set(k.encode(), int(v)) != 0:
-                raise ValueError(L.mpiv_last_error().decode())
+        set_debug(**opts)
         yield
     finally:
-        L.mpiv_debug_set(b"reset", 0)
+        reset_debug()
 
 
 def route(entry: str, *args: int) -> tuple[str, int]:
     """(kernel name, grid work-items) of the kernel an entry point's production dispatch
     would launch for these sizes (mpiv_route: a dry run, nothing launched, no GPU needed)."""
-    L = load()
+    L = load_main()
     buf = ctypes.create_string_buffer(160)
     grid = ctypes.c_int64(0)
     a = (ctypes.c_int64 * len(args))(*args)

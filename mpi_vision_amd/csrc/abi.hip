@@ -10,6 +10,11 @@
 #include <algorithm>
 
 #include "../../include/mpiv.h"
+
+// MPIV_AB=1 (libmpiv_ab.so): also compile the kernel variants kept for A/B measurement
+#ifndef MPIV_AB
+#define MPIV_AB 0
+#endif
 #include "render.hip"
 #include "render_lds.hip"
 #include "render_chunk.hip"
@@ -88,6 +93,22 @@ int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
+// Option values that select a kernel kept for A/B measurement only: those kernels are
+// compiled into libmpiv_ab.so (-DMPIV_AB=1, Makefile) and left out of libmpiv.so, whose
+// mpiv_debug_set refuses these values (the Python layer then switches to the A/B build).
+bool ab_only(int o, int v) {
+    switch (o) {
+        case kOptRenderMv: case kOptRenderPair: case kOptSweepTile: return v != 0;
+        case kOptRenderRing: return v > 0;
+        case kOptRenderTile: return v != 0 && v != -1;
+        case kOptRenderVshare: return v == -1 || v == 1;
+        case kOptSweepStore: return v >= 0;
+        case kOptRenderChunk: return v >= 100;
+        case kOptSweepDlane: return v == 0;
+        default: return false;
+    }
+}
+
 // mpiv_render_packed_census: set for the duration of one call on this thread; the rows-kernel
 // launch takes it (and clears it) to launch the counting build
 thread_local unsigned long long* g_census = nullptr;
@@ -160,6 +181,9 @@ int mpiv_debug_set(const char* name, int value) {
     if (!name) return fail(MPIV_ERR_ARG, "mpiv_debug_set: null name");
     for (int i = 0; i < kNumOpts; ++i) {
         if (strcmp(name, kOptNames[i]) == 0) {
+            if (!MPIV_AB && ab_only(i, value))
+                return fail(MPIV_ERR_ARG, "mpiv_debug_set: %s=%d selects an A/B kernel, built only into libmpiv_ab.so",
+                            name, value);
             __atomic_store_n(&g_opts[i], value, __ATOMIC_RELAXED);
             return MPIV_OK;
         }
@@ -194,11 +218,13 @@ int mpiv_render(const float* mpi, const int64_t st[5], int B, int H, int W, int 
         s.y / 4 < (1 << 22) && s.x / 4 < (1 << 22) && ch_lds <= (size_t)kChunkMaxLds) {
         const ChunkGeom cg{(int)(s.y / 4), (int)(s.x / 4), (int)rec};
         const int R = SPLIT == 1 ? chunk_rows() : 1;
+#if MPIV_AB  // two composite phases per chunk (A/B)
         if (CH == 8 && SPLIT == 2)
             return launch_chunk<8, 2>(1, mpi, s.b, g, cg, B, homs, out, nullptr, ch_lds, q, "mpiv_render");
-        if (CH == 8) return launch_chunk<8, 1>(R, mpi, s.b, g, cg, B, homs, out, nullptr, ch_lds, q, "mpiv_render");
         if (SPLIT == 2)
             return launch_chunk<4, 2>(1, mpi, s.b, g, cg, B, homs, out, nullptr, ch_lds, q, "mpiv_render");
+#endif
+        if (CH == 8) return launch_chunk<8, 1>(R, mpi, s.b, g, cg, B, homs, out, nullptr, ch_lds, q, "mpiv_render");
         return launch_chunk<4, 1>(R, mpi, s.b, g, cg, B, homs, out, nullptr, ch_lds, q, "mpiv_render");
     }
     // footprints staged through LDS, read in place (render_lds.hip render_lds_native_kernel):
@@ -268,6 +294,7 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     const RenderGeom g = make_geom(H, W, P);
     const bool fast = H >= 2 && W >= 2;  // div_const needs divisors >= 1
     hipStream_t st = S(stream);
+#if MPIV_AB
     if (variant == 1 && fast && p_end - p_begin <= kLMaxP) {
         // footprints staged through LDS (render_lds.hip)
         const int64_t nb = (int64_t)blocks(W, kLTX) * blocks(H, kLTY) * V;
@@ -340,6 +367,8 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
             render_pair_kernel<false, false><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, out);
         return launched(nm);
     }
+#endif  // MPIV_AB
+
     // R rows per work-item, planes outermost (render.hip render_rows_kernel), automatic
     // (bench_configs.py A/B, profiles/r02_vshare_ab.txt), all with vertical tap reuse and a ring
     // of D rows in flight:
@@ -361,7 +390,8 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     const bool variants_off = !opt(kOptRenderMv) && !opt(kOptRenderPair);
     const int rows_auto = ((square || stretched_vs) && variants_off) ? 8 : 0;
     const int vs_opt = opt(kOptRenderVshare);
-    const int rows_sel = fast ? (rows_opt ? rows_opt : rows_auto) : 0;
+    [[maybe_unused]] const int rows_sel = fast ? (rows_opt ? rows_opt : rows_auto) : 0;
+#if MPIV_AB
     if (const int rows = rows_sel; rows == 108 || rows == 116 || rows == 132) {
         // R rows with the compositing state in LDS (render_rows_lds_kernel)
         const int R = rows - 100;
@@ -378,6 +408,8 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
 #undef MPIV_ROWSL
         return launched(nm);
     }
+#endif  // MPIV_AB
+
     // vertical tap reuse with D rows in flight; render_vshare forces one of the automatic
     // choices: 3: (R, D) = (8, 4), 4: (6, 3), 5: (9, 3), 11: (4, 4) (the other (R, D) points of
     // profiles/r02_vshare_ab.txt were A/B builds and are not shipped)
@@ -419,6 +451,7 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
 #undef MPIV_VSD
         return launched(nm);
     }
+#if MPIV_AB
     if (const int rows = rows_sel; rows == 2 || rows == 4 || rows == 8 || rows == 16) {
         const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * rows) * V;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
@@ -451,6 +484,8 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
 #undef MPIV_ROWS
         return launched(nm);
     }
+#endif  // MPIV_AB
+
     const int64_t nblocks = (int64_t)blocks(W, kTileX) * blocks(H, kTileY) * V;
     if (nblocks > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const dim3 grid((unsigned)nblocks), blk(256);
@@ -486,6 +521,10 @@ int mpiv_render_packed_census(const float* packed, int H, int W, int P, const fl
 
 int mpiv_render_packed_lds(const float* packed, int H, int W, int P, const float* homs, int V, float* out,
                            void* stream) {
+#if !MPIV_AB
+    (void)packed, (void)H, (void)W, (void)P, (void)homs, (void)V, (void)out, (void)stream;
+    return fail(MPIV_ERR_ARG, "mpiv_render_packed_lds: an A/B kernel, built only into libmpiv_ab.so");
+#endif
     return render_packed_impl(packed, H, W, P, 0, P, 1, homs, V, out, false, 1, stream);
 }
 
@@ -645,7 +684,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
             bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
             bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x, margin,
                                                                            ws.box);
-            bwd_gather_kernel<<<(unsigned)gather_blocks, 256, 0, q>>>(g, hv, ws, gv, margin);
+            bwd_gather_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
         }
         bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force);
         // fallback: one launch of resident blocks, returns at once unless flagged
@@ -768,7 +807,7 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
     const int NG = (D + kSweepDG - 1) / kSweepDG;
     const int64_t per_view = (int64_t)Ht * Wt * NG;
     if (B > kMaxGridYZ || per_view >= (1ll << 31)) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: too large");
-    const FastDiv fd_g = make_fastdiv((unsigned)NG), fd_w = make_fastdiv((unsigned)Wt);
+    [[maybe_unused]] const FastDiv fd_g = make_fastdiv((unsigned)NG), fd_w = make_fastdiv((unsigned)Wt);
     const SweepParams sp = sweep_params(B, Hs, Ws, C, D, Ht, Wt);
     const float rc_hs = 1.0f / sp.fhs, rc_ws = 1.0f / sp.fws;
     PadGeom pg;
@@ -796,7 +835,7 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
         if (tiles > kMaxGridX) return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: too large");
         const dim3 lgrid((unsigned)tiles, B, 1);
         const int shrink = opt(kOptBoxShrink);
-        const FastDiv fd_b = make_fastdiv((unsigned)(16 * NG));
+        [[maybe_unused]] const FastDiv fd_b = make_fastdiv((unsigned)(16 * NG));
         if (opt(kOptSweepDlane) != 0) {
 #define MPIV_DLANE(CC)                                                                                          \
     plane_sweep_dlane_kernel<CC, false><<<lgrid, kDLThreads, 0, q>>>(im, pg, nullptr, ImgStrides{0, 0, 0, 0}, sp, \
@@ -811,6 +850,7 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
 #undef MPIV_DLANE
             return launched("mpiv_plane_sweep_padded");
         }
+#if MPIV_AB  // pixel-per-lane LDS, tile and grouped sweeps (A/B)
 #define MPIV_LDS(CC)                                                                                          \
     plane_sweep_lds_kernel<CC><<<lgrid, kSLThreads, 0, q>>>(im, sp, pg, rc_hs, rc_ws, fd_g, fd_b, ki, proj, depths, \
                                                      out, out_bstride, out_pstride, (int)vec, shrink)
@@ -857,6 +897,10 @@ int mpiv_plane_sweep_padded_into(const float* img4, int B, int Hs, int Ws, int C
 #undef MPIV_SWEEP_C
 #undef MPIV_SWEEP
     return launched("mpiv_plane_sweep_padded");
+#else
+    }
+    return fail(MPIV_ERR_ARG, "mpiv_plane_sweep_padded: an A/B sweep kernel, built only into libmpiv_ab.so");
+#endif
 }
 
 int mpiv_plane_sweep_padded(const float* img4, int B, int Hs, int Ws, int C, const float* ki, const float* proj,
@@ -1139,14 +1183,19 @@ static int render_u8_impl(const uint32_t* packed, int H, int W, int P, int p_beg
 #define MPIV_U8(CT, RR, VV)                                                                                       \
     render_u8_kernel<CT, RR, VV><<<(unsigned)nb, 256, 0, q>>>(pk, npix, g, ug, V, p_begin, p_end, CT ? back : 1, \
                                                               homs, out)
+#if MPIV_AB  // 8 rows per work-item (A/B)
+    if (R == 8) {
+        if (vs && ct) MPIV_U8(true, 8, true);
+        else if (vs) MPIV_U8(false, 8, true);
+        else if (ct) MPIV_U8(true, 8, false);
+        else MPIV_U8(false, 8, false);
+        return launched(nm);
+    }
+#endif
     if (vs) {
-        if (ct && R == 8) MPIV_U8(true, 8, true);
-        else if (ct) MPIV_U8(true, 4, true);
-        else if (R == 8) MPIV_U8(false, 8, true);
+        if (ct) MPIV_U8(true, 4, true);
         else MPIV_U8(false, 4, true);
-    } else if (ct && R == 8) MPIV_U8(true, 8, false);
-    else if (ct) MPIV_U8(true, 2, false);
-    else if (R == 8) MPIV_U8(false, 8, false);
+    } else if (ct) MPIV_U8(true, 2, false);
     else MPIV_U8(false, 2, false);
 #undef MPIV_U8
     return launched(nm);

@@ -48,7 +48,11 @@ namespace mpiv {
 constexpr int kGridVec = 8;        // grid_sampler_2d_backward chunk width (oracle.GRID_VEC)
 constexpr int kBwdCH = 8;          // chain: planes per chunk
 constexpr int kGTW = 64;           // gather: texel tile width (a wave = one tile row)
-constexpr int kGTH = 4;            // gather: tile rows (4 waves)
+#ifndef MPIV_GTH
+#define MPIV_GTH 4
+#endif
+constexpr int kGTH = MPIV_GTH;     // gather: tile rows (one wave each)
+constexpr int kGThreads = kGTW * kGTH;
 // gather tile constants (overridable for A/B builds, tools/gpu_ab_lib.sh); measured on
 // config 4 (profiles/r02_bwd_gather_ab.txt): 4 planes x 736 staged pixels at 6 waves/SIMD
 // 2.97 ms per backward, 8 planes x 1024 at 4 waves 3.40, 8 waves (any shape) spills
@@ -468,7 +472,7 @@ constexpr int kGBCap = 2;                   // entries per bucket list (more: th
 // reference's order (pixel/8, corner, pixel%8), and the staged index rides in the low bits.
 // A bucket with more entries (magnification: several pixels per texel) makes the block
 // scan per-texel windows of the inverse map instead (one 8-pixel chunk at a time).
-__global__ __launch_bounds__(256, MPIV_GLB) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
+__global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
                                                          float4* __restrict__ dmpi, float margin) {
     __shared__ int s_code[kGCap];     // local nw-tap bucket of the staged pixel, -1 = none
     __shared__ float2 s_fr[kGCap];    // its bilinear fractions (px - floor px, py - floor py)
@@ -487,7 +491,7 @@ __global__ __launch_bounds__(256, MPIV_GLB) void bwd_gather_kernel(RenderGeom g,
     const bool tin = tx < g.W && ty < g.H;
     const int64_t HW = (int64_t)g.H * g.W;
     const int bt = (ty - ty0 + 1) * TB + (tx - tx0 + 1);  // bucket of the texel as an nw tap
-    for (int b = threadIdx.x; b < 2 * kGNB; b += 256) (&s_bcnt[0][0])[b] = 0;
+    for (int b = threadIdx.x; b < 2 * kGNB; b += kGThreads) (&s_bcnt[0][0])[b] = 0;
     if (threadIdx.x < 2) s_ovf[threadIdx.x] = 0;
     int par = 0;
     unsigned hits = 0;    // (texel, contributor) pairs found by this thread
@@ -519,7 +523,7 @@ __global__ __launch_bounds__(256, MPIV_GLB) void bwd_gather_kernel(RenderGeom g,
                 // order keys hold (chunk - gbase) in 16 bits
                 if (threadIdx.x == 0 && (int64_t)(rb - ra + 1) * g.W >= ((int64_t)1 << 19)) s_ovf[par] = 1;
                 const float rbw = 1.0f / (float)bw;
-                for (int q = threadIdx.x; q < np; q += 256) {
+                for (int q = threadIdx.x; q < np; q += kGThreads) {
                     const int r = (int)(((float)q + 0.5f) * rbw);  // q / bw: q, bw <= 1024, error << 0.5/bw
                     const int yy = ra + r, xx = bx0 + (q - r * bw);
                     float px, py;
@@ -545,7 +549,7 @@ __global__ __launch_bounds__(256, MPIV_GLB) void bwd_gather_kernel(RenderGeom g,
                             s_ovf[par] = 1;
                     }
                 }
-                for (int b = threadIdx.x; b < kGNB; b += 256) s_bcnt[par ^ 1][b] = 0;  // for the next pass
+                for (int b = threadIdx.x; b < kGNB; b += kGThreads) s_bcnt[par ^ 1][b] = 0;  // for the next pass
                 if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
             }
             __syncthreads();

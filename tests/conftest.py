@@ -50,14 +50,9 @@ def kopts():
     """Select non-default kernel variants for one test (libmpiv's debug options,
     mpiv_debug_set); every option is restored to its production default afterwards."""
     from mpi_vision_amd import _lib
-    L = _lib.load()
 
-    def set_(**opts):
-        for k, v in opts.items():
-            assert L.mpiv_debug_set(k.encode(), int(v)) == 0, L.mpiv_last_error()
-
-    yield set_
-    L.mpiv_debug_set(b"reset", 0)
+    yield _lib.set_debug  # A/B-only variants run on libmpiv_ab.so until the reset
+    _lib.reset_debug()
 
 
 def sha256(a) -> str:

@@ -83,6 +83,33 @@ def test_debug_options():
             pass
 
 
+def test_ab_kernels_live_in_the_ab_library():
+    """The production libmpiv.so carries only the routed kernels: options that pick a variant
+    kept for A/B measurement are refused there, and _lib.debug() runs such blocks on
+    libmpiv_ab.so (same sources, same build id, -DMPIV_AB=1), then returns to libmpiv.so."""
+    L = _lib.load_main()
+    for name, val in (("render_mv", 1), ("render_ring", 4), ("render_pair", 1), ("render_tile", 8),
+                      ("render_vshare", 1), ("sweep_tile", 1), ("sweep_store", 2), ("render_chunk", 108),
+                      ("sweep_dlane", 0)):
+        assert L.mpiv_debug_set(name.encode(), val) == -1, name
+        assert b"libmpiv_ab.so" in L.mpiv_last_error()
+    for name, val in (("render_tile", -1), ("render_vshare", 11), ("render_chunk", 4), ("chunk_rows", 2),
+                      ("bwd_fallback", 1), ("box_shrink", 2)):  # production kernels / test hooks
+        assert L.mpiv_debug_set(name.encode(), val) == 0, name
+    L.mpiv_debug_set(b"reset", 0)
+    p = ctypes.c_void_p(256)
+    assert L.mpiv_render_packed_lds(p, 8, 8, 2, p, 1, p, None) == -1
+    assert b"libmpiv_ab.so" in L.mpiv_last_error()
+    A = _lib.load_ab()
+    assert A.mpiv_build_id().decode() == _lib.source_hash()
+    with _lib.debug(render_mv=1):
+        assert _lib.load() is A
+    assert _lib.load() is L
+    with _lib.debug(chunk_rows=2):
+        assert _lib.load() is L
+    assert os.path.getsize(_lib.LIB_PATH) < os.path.getsize(_lib.AB_PATH)
+
+
 def test_output_buffers_validated():
     """Caller-supplied outputs of the packed render / pack must be dense fp32 tensors of the
     exact shape on the same device, else a Python error (not out-of-bounds device writes)."""
