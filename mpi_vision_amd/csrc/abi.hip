@@ -70,6 +70,10 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (R, rows in flight) = (8, 4) / (6, 3) / (9, 3) / (4, 4)
 //   sweep_dlane=0      the LDS sweep runs pixel-per-lane (plane_sweep_lds_kernel) instead of
 //                      depth-per-lane (plane_sweep_dlane_kernel)
+//   sweep_rows=4|6|8   mpiv_plane_sweep[_into]'s depth-per-lane kernel with tiles of that many
+//                      target rows (staging 3072 / 4096 / 4096 texels; 0 = automatic)
+//   chunk_flight=2|4   render_chunk_kernel with that many sub-steps' taps in flight per wave
+//                      (0 = automatic)
 //   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
 //                      wave (0 = automatic)
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
@@ -83,13 +87,13 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 // launches is a test-harness race on which kernel runs, never on memory.
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
-                kOptRenderVshare, kOptChunkRows, kNumOpts };
+                kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
-                                         "render_vshare", "chunk_rows"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0};
+                                         "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -155,8 +159,11 @@ int launch_chunk(int R, const float* mpi, int64_t vstride, const RenderGeom& g, 
                  const float* homs, float* out, float4* ck, size_t lds, hipStream_t q, const char* nm) {
     const int64_t nb = (int64_t)blocks(g.W, kTileX) * blocks(g.H, kTileY * R) * B;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
-    if (g_route) return note_route(nb, 256, "render_chunk_kernel<%d, %d, %d>", CH, SPLIT, R);
-    if (R == 4)
+    const int NT = (opt(kOptChunkFlight) == 4 && R == 1 && SPLIT == 1) ? 4 : 2;
+    if (g_route) return note_route(nb, 256, "render_chunk_kernel<%d, %d, %d, %d>", CH, SPLIT, R, NT);
+    if (NT == 4)
+        render_chunk_kernel<CH, SPLIT, 1, 4><<<(unsigned)nb, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
+    else if (R == 4)
         render_chunk_kernel<CH, SPLIT, SPLIT == 1 ? 4 : 1><<<(unsigned)nb, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
     else if (R == 2)
         render_chunk_kernel<CH, SPLIT, SPLIT == 1 ? 2 : 1><<<(unsigned)nb, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
@@ -722,7 +729,10 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
         (int64_t)Ht * Wt >= (1ll << 31))
         return fail(MPIV_ERR_ARG, "%s: bad output strides", nm);
     if (Hs >= (1 << 22) || Ws >= (1 << 22)) return fail(MPIV_ERR_ARG, "%s: a source side >= 2^22", nm);
-    const int64_t tiles = (int64_t)((Wt + kSLP - 1) / kSLP) * ((Ht + kSLR - 1) / kSLR);
+    // tile rows: sweep_rows option, else 4 (automatic)
+    const int so = opt(kOptSweepRows);
+    const int SLR = (so == 6 || so == 8) ? so : 4;
+    const int64_t tiles = (int64_t)((Wt + kSLP - 1) / kSLP) * ((Ht + SLR - 1) / SLR);
     if (B > kMaxGridYZ || tiles > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too large", nm);
     const SweepParams sp = sweep_params(B, Hs, Ws, C, D, Ht, Wt);
     const float rc_hs = 1.0f / sp.fhs, rc_ws = 1.0f / sp.fws;
@@ -731,17 +741,28 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
     const dim3 lgrid((unsigned)tiles, B, 1);
     const int shrink = opt(kOptBoxShrink);
     hipStream_t q = S(stream);
-    if (g_route) return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true>", C < 4 ? C : 4);
-#define MPIV_DLRAW(CC)                                                                                         \
-    plane_sweep_dlane_kernel<CC, true><<<lgrid, kDLThreads, 0, q>>>(nullptr, PadGeom{0, 0, 0, 0}, img, is, sp, \
-                                                                    rc_hs, rc_ws, ki, proj, depths, out,       \
-                                                                    out_bstride, out_pstride, (int)vec, shrink)
-    switch (C) {
-        case 1: MPIV_DLRAW(1); break;
-        case 2: MPIV_DLRAW(2); break;
-        case 3: MPIV_DLRAW(3); break;
-        default: MPIV_DLRAW(4); break;
+    if (g_route)
+        return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true, %d, %d>", C < 4 ? C : 4, SLR,
+                          SLR == 4 ? kSLCap : 4096);
+#define MPIV_DLRAW(CC, RR, CAP)                                                                              \
+    plane_sweep_dlane_kernel<CC, true, RR, CAP><<<lgrid, kDLThreads, 0, q>>>(nullptr, PadGeom{0, 0, 0, 0}, img, is, \
+                                                                            sp, rc_hs, rc_ws, ki, proj, depths, out, \
+                                                                            out_bstride, out_pstride, (int)vec, shrink)
+#define MPIV_DLRAW_C(RR, CAP)                  \
+    switch (C) {                               \
+        case 1: MPIV_DLRAW(1, RR, CAP); break; \
+        case 2: MPIV_DLRAW(2, RR, CAP); break; \
+        case 3: MPIV_DLRAW(3, RR, CAP); break; \
+        default: MPIV_DLRAW(4, RR, CAP); break; \
     }
+    if (SLR == 8) {
+        MPIV_DLRAW_C(8, 4096)
+    } else if (SLR == 6) {
+        MPIV_DLRAW_C(6, 4096)
+    } else {
+        MPIV_DLRAW_C(4, kSLCap)
+    }
+#undef MPIV_DLRAW_C
 #undef MPIV_DLRAW
     return launched(nm);
 }

@@ -203,10 +203,84 @@ __device__ __forceinline__ void render_chunk_wave(const float* __restrict__ view
     }
 }
 
+// NT sub-steps in flight (NT divides CH; R = 1, SPLIT = 1): a ring of NT tap sets, sub-step
+// s + NT - 1 issued while sub-step s blends, the issue running into the next chunk (whose
+// homography is then held beside the current one).  The kernel is latency-bound with its
+// occupancy pinned at 4 waves/SIMD by the LDS slots, so VGPRs up to 128 cost nothing: more
+// loads in flight per wave is the lever the A/B ping-pong (NT = 2) leaves unused.
+template <int CH, int NT, bool GUARD>
+__device__ __forceinline__ void render_chunk_wave_ring(const float* __restrict__ view, const RenderGeom& g,
+                                                       const ChunkGeom& cg, const float* __restrict__ hs,
+                                                       f32x4* __restrict__ slot, int tx0, int y, int lane, float& cr,
+                                                       float& cg_, float& cb, float4* __restrict__ ck,
+                                                       int64_t ck_stride) {
+    static_assert(CH % NT == 0 && NT >= 2, "the ring position of a sub-step must be static");
+    constexpr int PPS = kWave / CH;
+    const int j = lane % CH, i = lane / CH;
+    const float fy = (float)y;
+    const int nchunk = (g.P + CH - 1) / CH;
+    float hc[9];  // this chunk's homography (per lane: plane c*CH + j); the next one's is re-read from LDS
+    auto load_h = [&](int c, float* d) {
+        const int p = min(c * CH + j, g.P - 1);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) d[k] = hs[p * 9 + k];
+    };
+    auto issue = [&](int c, int k, const float* hh, ChunkTaps& ts) {
+        float px, py;
+        chunk_pos<GUARD>(hh, (float)(tx0 + k * PPS + i), fy, g, px, py);
+        issue_taps_chunk(make_rsrc(view + (int64_t)c * CH * 4, cg.rec_bytes), g, cg, j, c * CH + j < g.P, px, py, ts);
+    };
+    auto put = [&](int k, const ChunkTaps& ts) { slot[(k * PPS + i) * (CH + 1) + j] = blend_chunk(ts); };
+    auto over_px = [&](const f32x4& s, bool first) {
+        const float a = first ? 1.0f : s[3];
+        const float om = 1.0f - a;
+        cr = over(s[0], a, om, cr);
+        cg_ = over(s[1], a, om, cg_);
+        cb = over(s[2], a, om, cb);
+    };
+    ChunkTaps T[NT];
+    load_h(0, hc);
+#pragma unroll
+    for (int k = 0; k + 1 < NT; ++k) issue(0, k, hc, T[k]);
+    for (int c = 0; c < nchunk; ++c) {
+        const int cn = c + 1 < nchunk ? c + 1 : c;  // past the end: re-issue (cached, unused)
+        if (ck && c > 0) ck[c * ck_stride] = make_float4(cr, cg_, cb, 0.0f);
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int ka = k + NT - 1;  // the sub-step issued now
+            if (ka < CH) {
+                issue(c, ka, hc, T[ka % NT]);
+            } else {
+                float hn[9];
+                load_h(cn, hn);
+                issue(cn, ka - CH, hn, T[ka % NT]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            put(k, T[k % NT]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // composite (lane = pixel): planes c*CH .. c*CH+CH-1, back to front
+        const f32x4* row = slot + lane * (CH + 1);
+        if (c * CH + CH <= g.P) {
+#pragma unroll
+            for (int j0 = 0; j0 < CH; j0 += 4) {
+                f32x4 sv[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) sv[jj] = row[j0 + jj];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) over_px(sv[jj], c == 0 && j0 + jj == 0);
+            }
+        } else {
+            for (int jj = 0; c * CH + jj < g.P; ++jj) over_px(row[jj], c * CH + jj == 0);
+        }
+        load_h(cn, hc);
+    }
+}
+
 // One block = 4 waves = a 64 x 4R output tile of one view (wave w: rows w*R .. w*R+R-1 of
 // the tile); blocks in render_packed_kernel's XCD-aware (tile, view) order.  Dynamic LDS:
 // chunk_slot_floats<CH, SPLIT>() + P*9 floats.
-template <int CH, int SPLIT, int R>
+template <int CH, int SPLIT, int R, int NT = 2>
 __global__ __launch_bounds__(256, SPLIT == 2 ? 6 : 4) void render_chunk_kernel(const float* __restrict__ mpi, int64_t view_stride,
                                                            RenderGeom g, ChunkGeom cg, int V,
                                                            const float* __restrict__ homs,
@@ -242,10 +316,16 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 6 : 4) void render_chunk_kernel(c
     // checkpoints [V][nchunk][H][W] (nullptr: inference; SPLIT = 1 only: lane = pixel)
     const int64_t HW = (int64_t)g.H * g.W;
     float4* ck = (ckpt && x < g.W) ? ckpt + ((int64_t)v * ((g.P + CH - 1) / CH)) * HW + (int64_t)y * g.W + x : nullptr;
-    if (proven)
+    if constexpr (NT > 2 && R == 1 && SPLIT == 1) {
+        if (proven)
+            render_chunk_wave_ring<CH, NT, false>(view, g, cg, hs, slot, tx0, y, lane, cr[0], cgr[0], cb[0], ck, HW);
+        else
+            render_chunk_wave_ring<CH, NT, true>(view, g, cg, hs, slot, tx0, y, lane, cr[0], cgr[0], cb[0], ck, HW);
+    } else if (proven) {
         render_chunk_wave<CH, SPLIT, R, false>(view, g, cg, hs, slot, tx0, y, nrows, lane, cr, cgr, cb, ck, HW);
-    else
+    } else {
         render_chunk_wave<CH, SPLIT, R, true>(view, g, cg, hs, slot, tx0, y, nrows, lane, cr, cgr, cb, ck, HW);
+    }
     if (x < g.W) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {

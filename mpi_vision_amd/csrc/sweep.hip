@@ -736,7 +736,7 @@ struct SweepBox {
 __device__ __forceinline__ SweepBox sweep_tile_box(const float* __restrict__ k9, const float* __restrict__ m,
                                                    const SweepParams& sp, float rc_hs, float rc_ws, int x0, int y0,
                                                    int np, int nr, float dmin, float dmax, float dbad, int shrink,
-                                                   int lane) {
+                                                   int lane, int cap = kSLCap) {
     // vertex = lane % 8: (first | last pixel) x (first | last row) x (min | max depth)
     const int vtx = lane & 7;
     float rx, ry, rz;
@@ -787,7 +787,7 @@ __device__ __forceinline__ SweepBox sweep_tile_box(const float* __restrict__ k9,
         yh = yl + 2;
     }
     const int width = xh - xl + 1, rows = yh - yl + 1;
-    const bool fits = ok && width >= 2 && rows >= 2 && width <= kSLCap && rows <= kSLCap && width * rows <= kSLCap;
+    const bool fits = ok && width >= 2 && rows >= 2 && width <= cap && rows <= cap && width * rows <= cap;
     bx.xl = xl;
     bx.yl = yl;
     bx.rows = rows;
@@ -825,10 +825,10 @@ __device__ __forceinline__ void sweep_zero_tile(float* __restrict__ out, int64_t
 
 // Register-staged box fill (the non-persistent kernel): box texel idx = row * pitch + col
 // <- padded-plane texel.
-template <int NT>
+template <int NT, int CAP = kSLCap>
 __device__ __forceinline__ void sweep_fill_box(float4* __restrict__ s_src, __amdgpu_buffer_rsrc_t r,
                                                const PadGeom& pg, const SweepBox& bx) {
-    constexpr int kFill = kSLCap / NT;  // staged texels per thread
+    constexpr int kFill = CAP / NT;  // staged texels per thread
     const int nfp = bx.rows * bx.pitch;
     const float rp = 1.0f / (float)bx.pitch;
     const int org = (bx.yl + kPad) * pg.Wp + bx.xl + kPad;  // >= 0: boxes start at -2
@@ -891,10 +891,10 @@ __device__ __forceinline__ f32x4 raw_texel(const float* __restrict__ t, int64_t 
 // exactly the padded buffer's values (mpiv_pad_texels writes the image inside a zero border).
 // (CONTIG is decided once per fill, outside the unrolled loop: a branch per texel kept the
 // loads from being in flight together)
-template <int C, int NT, bool CONTIG>
+template <int C, int NT, bool CONTIG, int CAP = kSLCap>
 __device__ __forceinline__ void sweep_fill_box_raw(float4* __restrict__ s_src, const float* __restrict__ img,
                                                    const ImgStrides& is, int Hs, int Ws, const SweepBox& bx) {
-    constexpr int kFill = kSLCap / NT;
+    constexpr int kFill = CAP / NT;
     const int nfp = bx.rows * bx.pitch;
     const float rp = 1.0f / (float)bx.pitch;
     f32x4 stg[kFill];
@@ -940,21 +940,24 @@ __device__ __forceinline__ f32x4 raw_sample(const float* __restrict__ img, const
     return blend_taps(t);
 }
 
-// RAW: the source is the caller's strided tensor (img, is) instead of padded texels (img4, pg)
-template <int C, bool RAW>
+// RAW: the source is the caller's strided tensor (img, is) instead of padded texels (img4, pg).
+// SLR target rows per tile, CAP staged texels: (4, 3072) by default; few depths take taller
+// tiles (more samples per staged box, abi.hip sweep_tile_rows) with a larger box.
+template <int C, bool RAW, int SLR = kSLR, int CAP = kSLCap>
 __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     const float4* __restrict__ img4, PadGeom pg, const float* __restrict__ img, ImgStrides is, SweepParams sp,
     float rc_hs, float rc_ws, const float* __restrict__ ki, const float* __restrict__ proj,
     const float* __restrict__ depths, float* __restrict__ out, int64_t out_bstride, int64_t out_pstride, int vec,
     int shrink) {
-    __shared__ __attribute__((aligned(16))) float4 s_src[kSLCap];
+    static_assert(CAP % kDLThreads == 0, "the box fill writes every staging slot");
+    __shared__ __attribute__((aligned(16))) float4 s_src[CAP];
     __shared__ SweepBox s_box;
 
     const int segs = (sp.Wt + kSLP - 1) / kSLP;
     const int b = blockIdx.y;
     const int ty = blockIdx.x / segs;
-    const int y0 = ty * kSLR, x0 = (blockIdx.x - ty * segs) * kSLP;
-    const int np = min(kSLP, sp.Wt - x0), nr = min(kSLR, sp.Ht - y0);
+    const int y0 = ty * SLR, x0 = (blockIdx.x - ty * segs) * kSLP;
+    const int np = min(kSLP, sp.Wt - x0), nr = min(SLR, sp.Ht - y0);
     const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const float* k9 = ki + (int64_t)b * 9;
     const float* m = proj + (int64_t)b * 16;
@@ -965,7 +968,7 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     if (wave == 0) {
         float dmin, dmax, dbad;
         sweep_depth_range(depths, sp.D, lane, dmin, dmax, dbad);
-        const SweepBox bx = sweep_tile_box(k9, m, sp, rc_hs, rc_ws, x0, y0, np, nr, dmin, dmax, dbad, shrink, lane);
+        const SweepBox bx = sweep_tile_box(k9, m, sp, rc_hs, rc_ws, x0, y0, np, nr, dmin, dmax, dbad, shrink, lane, CAP);
         if (lane == 0) s_box = bx;
     }
     __syncthreads();
@@ -982,11 +985,11 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     }
     if (bx.pitch > 0) {
         if (RAW && is.c == 1 && C > 1)
-            sweep_fill_box_raw<C, kDLThreads, true>(s_src, imb, is, sp.Hs, sp.Ws, bx);
+            sweep_fill_box_raw<C, kDLThreads, true, CAP>(s_src, imb, is, sp.Hs, sp.Ws, bx);
         else if (RAW)
-            sweep_fill_box_raw<C, kDLThreads, false>(s_src, imb, is, sp.Hs, sp.Ws, bx);
+            sweep_fill_box_raw<C, kDLThreads, false, CAP>(s_src, imb, is, sp.Hs, sp.Ws, bx);
         else
-            sweep_fill_box<kDLThreads>(s_src, r, pg, bx);
+            sweep_fill_box<kDLThreads, CAP>(s_src, r, pg, bx);
     }
     __syncthreads();
 

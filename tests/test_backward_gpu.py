@@ -229,14 +229,14 @@ def test_backward_full_size_tile_equals_fallback(cfg, dev, kopts):
     assert torch.equal(fast.view(torch.int32), slow.view(torch.int32))
 
 
-@pytest.mark.parametrize("rows", [1, 2, 4])
+@pytest.mark.parametrize("rows", [1, 2, 4, "f4"])
 @pytest.mark.parametrize("cfg", ["config2", "config4"])
 def test_training_forward_checkpoints(cfg, rows, dev, kopts):
     """mpiv_render_train: frames bit-identical to the inference render; the backward fed its
     checkpoints (one pass) is bit-identical to the backward that recomputes them (two
     passes); two views in one launch (non-broadcast [2,H,W,P,4]); the forward at 1, 2 and 4
     rows per wave (chunk_rows) writes the same frames and checkpoints."""
-    kopts(chunk_rows=rows)
+    kopts(**({"chunk_flight": 4} if rows == "f4" else {"chunk_rows": rows}))
     c = getattr(configs, cfg)()
     H, W, P = c["H"], c["W"], c["P"]
     if cfg == "config4":

@@ -31,6 +31,27 @@ def test_plane_sweep_one(small, meta, dev):
     assert_bits(out.cpu().numpy(), small["psv_one_out"])
 
 
+@pytest.mark.parametrize("rows", [6, 8])
+@pytest.mark.parametrize("D", [3, 10, 64])
+def test_plane_sweep_tall_tiles_vs_oracle(rows, D, dev, kopts):
+    """The depth-per-lane sweep with 6- and 8-row tiles (sweep_rows; 4096-texel staging box):
+    partial tiles, off-image footprints and the swapped normalisation, bit-exact vs the oracle."""
+    from mpi_vision_amd import _host
+    from oracle import oracle
+    kopts(sweep_rows=rows)
+    g = torch.Generator().manual_seed(D + rows)
+    B, H, W = 2, 45, 100
+    img = torch.rand((B, H, W, 3), generator=g)
+    K = configs.f32([configs.intrinsics_matrix(80.0, 85.0, W / 2.0, H / 2.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(3.0), (0.2, 0.03, 0.0)),
+                         configs.pose_from(configs.rot_y(-1.0), (-0.1, 0.0, 0.05))])
+    depths = configs.inv_depths(1, 100, D)
+    ki, proj = _host.psv_matrices(K, K, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, H, W)
+    out = mv.plane_sweep_torch(img.to(dev), depths, poses.to(dev), K.to(dev))
+    assert_bits(out.cpu().numpy(), want)
+
+
 def test_plane_sweep_one_notebook_call_pattern(small, meta, dev):
     """The notebook's dataset call (ipynb cell 8 L73-75): the depths are a DEVICE tensor
     (torch.Tensor(inv_depths(...)).to(device)) and pose / intrinsics live on the device; the

@@ -85,6 +85,38 @@ def bwd(dev, it):
     run("c4 render backward with checkpoints, 1 view", ROWS, fn, 2 * P * H * W * 16 + H * W * 12, it)
 
 
+FLIGHT = [("flight2", {}), ("flight4", {"chunk_flight": 4})]
+
+
+def chunkf(dev, it):
+    mpi, homs, H, W, P = c4_mpi(dev)
+    out = torch.empty((1, H, W, 3), device=dev)
+    fn = lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out, _lib._stream(dev))  # noqa: E731
+    run("c4 in-place render (render_chunk_kernel), 1 view", FLIGHT, fn, P * H * W * 16 + H * W * 12, it)
+    fn2 = lambda: _lib.render_train(mpi, homs)  # noqa: E731
+    run("c4 training forward (frame + checkpoints), 1 view", FLIGHT, fn2, P * H * W * 16 + H * W * 12, it)
+
+
+SWROWS = [("rows4", {}), ("rows6", {"sweep_rows": 6}), ("rows8", {"sweep_rows": 8})]
+
+
+def sweep(dev, it):
+    c = configs.config3()
+    S, H, W = c["S"], c["H"], c["W"]
+    g = torch.Generator(device=dev).manual_seed(1)
+    img = torch.rand((S, H, W, 3), generator=g, device=dev)
+    K = configs.f32([c["K"]] * S)
+    ki, proj = _host.psv_matrices(K, K, configs.f32(c["poses"]))
+    ki, proj = ki.to(dev), proj.to(dev)
+    for D in (64, 10):
+        d = configs.f32(configs.inv_depths(1, 100, D)).to(dev)
+        out = torch.empty((S, H, W, D * 3), device=dev)
+        fn = lambda: _lib._call("mpiv_plane_sweep", img, _lib._strides(img), S, H, W, 3, ki, proj, d, D, H, W,  # noqa: E731
+                                out, _lib._stream(dev))
+        run(f"c3 sources -> {D} planes (mpiv_plane_sweep)", SWROWS, fn, S * H * W * 12 + S * D * H * W * 12, it)
+        del out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
