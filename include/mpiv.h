@@ -151,7 +151,8 @@ size_t mpiv_render_backward_workspace_size(int H, int W, int P);
  * grid_sampler_2d_backward's scatter, summed per texel in ATen's order.
  * mpi:     the forward's [V,H,W,P,4] rgba_layers IN PLACE, element strides mpi_strides[5]
  *          with 16-byte aligned texels and planes contiguous per pixel (strides[3] == 4,
- *          strides[4] == 1; a stride-0 broadcast batch is fine); P <= 796;
+ *          strides[4] == 1; a stride-0 broadcast batch is fine); any P (more than 796 planes
+ *          read their homographies from global memory instead of LDS);
  * homs:    [V][P][9] (the forward's); dout: [V,H,W,3] contiguous incoming gradient;
  * ckpt:    NULL, or the checkpoints mpiv_render_train wrote in the forward of these views
  *          (then the adjoint skips recomputing the forward composite);

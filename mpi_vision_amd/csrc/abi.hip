@@ -109,6 +109,9 @@ bool ab_only(int o, int v) {
         case kOptSweepStore: return v >= 0;
         case kOptRenderChunk: return v >= 100;
         case kOptSweepDlane: return v == 0;
+        case kOptChunkRows: return v == 2 || v == 4;
+        case kOptChunkFlight: return v == 4;
+        case kOptSweepRows: return v == 6 || v == 8;
         default: return false;
     }
 }
@@ -161,6 +164,7 @@ int launch_chunk(int R, const float* mpi, int64_t vstride, const RenderGeom& g, 
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const int NT = (opt(kOptChunkFlight) == 4 && R == 1 && SPLIT == 1) ? 4 : 2;
     if (g_route) return note_route(nb, 256, "render_chunk_kernel<%d, %d, %d, %d>", CH, SPLIT, R, NT);
+#if MPIV_AB  // R rows per wave / 4 sub-steps in flight: measured slower
     if (NT == 4)
         render_chunk_kernel<CH, SPLIT, 1, 4><<<(unsigned)nb, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
     else if (R == 4)
@@ -168,6 +172,7 @@ int launch_chunk(int R, const float* mpi, int64_t vstride, const RenderGeom& g, 
     else if (R == 2)
         render_chunk_kernel<CH, SPLIT, SPLIT == 1 ? 2 : 1><<<(unsigned)nb, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
     else
+#endif
         render_chunk_kernel<CH, SPLIT, 1><<<(unsigned)nb, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
     return launched(nm);
 }
@@ -622,9 +627,11 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                     "(strides[3] == 4, strides[4] == 1)", nm);
     if (st[1] < 0 || st[2] < 0 || rec >= (int64_t)kOOB || st[1] / 4 >= (1 << 22) || st[2] / 4 >= (1 << 22))
         return fail(MPIV_ERR_ARG, "%s: one view's MPI must span less than 2 GiB", nm);
-    const size_t chain_lds = (size_t)4 * kWave * (kBwdCH + 1) * 16 + (size_t)P * 36;
-    if (chain_lds > (size_t)kChunkMaxLds) return fail(MPIV_ERR_ARG, "%s: more than %d planes", nm,
-                                                      (int)((kChunkMaxLds - 4 * kWave * (kBwdCH + 1) * 16) / 36));
+    // the chain's homographies go to LDS beside its sample slots when they fit (P <= 796),
+    // else it reads them from global memory
+    const size_t slots_lds = (size_t)4 * kWave * (kBwdCH + 1) * 16;
+    const int h_lds = slots_lds + (size_t)P * 36 <= (size_t)kChunkMaxLds;
+    const size_t chain_lds = slots_lds + (h_lds ? (size_t)P * 36 : 0);
     if (ckpt && (!aligned16(ckpt) || H < 2 || W < 2))
         return fail(MPIV_ERR_ARG, "%s: checkpoints must be 16-byte aligned (and come from mpiv_render_train)", nm);
     if (!aligned16(dmpi) || (reinterpret_cast<uintptr_t>(workspace) & 255))
@@ -677,14 +684,16 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         const int R = fast ? chunk_rows() : 1;
         const unsigned cb = blocks(W, kTileX) * blocks(H, kTileY * R);
 #define MPIV_CHAIN(CKB, RR)                                                                                  \
-    bwd_chain_kernel<1, CKB, RR><<<cb, 256, chain_lds, q>>>(mv, g, cg, hv, dv, CKB ? ck : nullptr, ws)
+    bwd_chain_kernel<1, CKB, RR><<<cb, 256, chain_lds, q>>>(mv, g, cg, hv, dv, CKB ? ck : nullptr, ws, h_lds)
         if (!fast)
-            bwd_chain_kernel<0, false, 1><<<cb, 256, chain_lds, q>>>(mv, g, cg, hv, dv, nullptr, ws);
+            bwd_chain_kernel<0, false, 1><<<cb, 256, chain_lds, q>>>(mv, g, cg, hv, dv, nullptr, ws, h_lds);
+#if MPIV_AB  // R rows per wave: measured slower
         else if (ck && R == 4) MPIV_CHAIN(true, 4);
         else if (ck && R == 2) MPIV_CHAIN(true, 2);
+        else if (!ck && R == 4) MPIV_CHAIN(false, 4);
+        else if (!ck && R == 2) MPIV_CHAIN(false, 2);
+#endif
         else if (ck) MPIV_CHAIN(true, 1);
-        else if (R == 4) MPIV_CHAIN(false, 4);
-        else if (R == 2) MPIV_CHAIN(false, 2);
         else MPIV_CHAIN(false, 1);
 #undef MPIV_CHAIN
         if (!force) {
@@ -755,11 +764,14 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
         case 3: MPIV_DLRAW(3, RR, CAP); break; \
         default: MPIV_DLRAW(4, RR, CAP); break; \
     }
+#if MPIV_AB  // taller tiles: measured within noise
     if (SLR == 8) {
         MPIV_DLRAW_C(8, 4096)
     } else if (SLR == 6) {
         MPIV_DLRAW_C(6, 4096)
-    } else {
+    } else
+#endif
+    {
         MPIV_DLRAW_C(4, kSLCap)
     }
 #undef MPIV_DLRAW_C
@@ -1195,6 +1207,9 @@ static int render_u8_impl(const uint32_t* packed, int H, int W, int P, int p_beg
     const bool square = sxr >= 0.8f && sxr <= 1.25f && syr >= 0.8f && syr <= 1.25f;
     const bool big = (int64_t)blocks(W, kTileX) * blocks(H, 4 * 8) * V >= 2048;
     const int rt = opt(kOptRenderTile), vso = opt(kOptRenderVshare);
+    // render_tile: 0 automatic, -1 / 2 two plain rows, 8 eight plain rows, 4 | 8 with render_vshare=1
+    if (!(rt == 0 || rt == -1 || rt == 2 || rt == 8 || (rt == 4 && vso == 1)))
+        return fail(MPIV_ERR_ARG, "%s: render_tile=%d (render_vshare=%d) is not a u8 render variant", nm, rt, vso);
     const bool vs = (rt == 0 && vso != -1 && (square || big)) || (vso == 1 && (rt == 4 || rt == 8));
     const int R = rt == 0 ? (vs ? 4 : 2) : vs ? rt : rt == 8 ? 8 : 2;
     const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;

@@ -21,15 +21,15 @@
 //            -(sum(g*out_{p-1})), g *= (1 - a).  Only d s_p (16 B per plane-pixel) is
 //            written.  It also counts every (sample, in-image tap) pair: the number of
 //            (texel, contributor) pairs step 2 must find.
-//  2. gather (bwd_gather_kernel): a block owns a 64x4 texel tile of 8 planes.  Per plane
+//  2. gather (bwd_gather_kernel): a block owns a 64x4 texel tile of kGPl = 4 planes.  Per plane
 //            it maps the tile (one texel margin) back through the inverse homography to a
 //            box of output pixels, recomputes their sample positions with the forward's
 //            recipe (bit-identical) and stages (nw-tap bucket, fractions, d s) in LDS; each
 //            texel then scans the pixels of ITS window (the inverse image of the 2x2 texels
 //            whose samples can touch it) in pixel order, collects the hits of one 8-pixel
 //            chunk in a 32-bit mask indexed (corner, pixel%8) and adds them in mask-bit
-//            order -- exactly the reference's key order.  A texel's 8 planes leave as one
-//            128-B run.  Found pairs are counted.
+//            order -- exactly the reference's key order.  A texel's kGPl planes leave as one
+//            16*kGPl-B run (64 B).  Found pairs are counted.
 //  3. check  (bwd_check_kernel): the windows come from float inverse maps, so they are a
 //            guess that the count makes exact: every found pair is genuine and found at
 //            most once, so found == truth iff nothing was missed.  On a mismatch (or a
@@ -295,16 +295,20 @@ template <int MODE, bool CK, int R>
 __global__ __launch_bounds__(256, R == 1 ? 1 : 4) void bwd_chain_kernel(const float* __restrict__ view, RenderGeom g, ChunkGeom cg,
                                                            const float* __restrict__ homs,
                                                            const float* __restrict__ dout,
-                                                           const float4* __restrict__ ck, BwdWs ws) {
+                                                           const float4* __restrict__ ck, BwdWs ws, int h_lds) {
     extern __shared__ float4 bwd_lds[];
     f32x4* slots = reinterpret_cast<f32x4*>(bwd_lds);
-    float* hs = reinterpret_cast<float*>(bwd_lds) + 4 * kWave * (kBwdCH + 1) * 4;
+    // the view's homographies: staged in LDS, or (h_lds == 0: more planes than the LDS holds
+    // beside the slots) read from global memory through the caches
+    float* hl = reinterpret_cast<float*>(bwd_lds) + 4 * kWave * (kBwdCH + 1) * 4;
+    const float* hs = h_lds ? hl : homs;
     constexpr int TH = kTileY * R;
     const int tiles_x = (g.W + kTileX - 1) / kTileX;
     const int tile = xcd_logical_block(blockIdx.x, gridDim.x);
     const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * TH;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
-    for (int k = threadIdx.x; k < g.P * 9; k += 256) hs[k] = homs[k];
+    if (h_lds)
+        for (int k = threadIdx.x; k < g.P * 9; k += 256) hl[k] = homs[k];
     bool ok = MODE != 0;
     if (MODE != 0) {
         const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
@@ -689,7 +693,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     for (int off = 32; off >= 1; off >>= 1) hits += __shfl_xor(hits, off);
     const unsigned long long tot = (unsigned long long)hits + (__any(unsafe) ? kUnsafe : 0ull);
     if ((threadIdx.x & (kWave - 1)) == 0 && tot) atomicAdd(&ws.found[blockIdx.x % kCtrSlots], tot);
-    if (tin) {  // the texel's kGPl planes: one 128-B run
+    if (tin) {  // the texel's kGPl planes: one 16*kGPl-B run
         float4* o = dmpi + ((int64_t)ty * g.W + tx) * g.P + p0;
 #pragma unroll
         for (int jj = 0; jj < kGPl; ++jj)

@@ -208,6 +208,25 @@ def test_backward_strided_layout_vs_oracle(dev):
     assert flag == 0
 
 
+def test_backward_more_planes_than_lds_holds(dev):
+    """P = 900 (> 796: the chain's homographies no longer fit beside its LDS slots, so it reads
+    them from global memory; the training forward falls back to the plain render and the
+    backward recomputes the composite): the drop-in's autograd equals the oracle bit for bit."""
+    H, W, P = 12, 40, 900
+    mpi = configs.synthetic_mpi(1, H, W, P, 6)
+    c = configs.config4()
+    K = configs.intrinsics_matrix(30.0, 30.0, 20.0, 6.0)
+    planes = configs.f32(configs.inv_depths(1, 60, P))
+    pose = configs.f32([c["poses"][120]])
+    homs = _host.render_homographies(pose, planes, configs.f32([K]), 1)
+    dout = torch.rand((1, H, W, 3), generator=torch.Generator().manual_seed(9)) * 2 - 1
+    want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
+    leaf = mpi.to(dev).requires_grad_(True)
+    out = mv.mpi_render_view_torch(leaf, pose.to(dev), planes.to(dev), configs.f32([K]).to(dev))
+    out.backward(dout.to(dev))
+    assert_bits(leaf.grad.cpu().numpy(), want, "P = 900")
+
+
 @pytest.mark.parametrize("cfg", ["config2", "config4"])
 def test_backward_full_size_tile_equals_fallback(cfg, dev, kopts):
     """BASELINE config 2 (1024x576x32, the stretched normalisation) and config 4

@@ -128,3 +128,15 @@ def test_u8_synth_shards_equal_whole(dev):
     assert torch.all((w[0, 2:2 + H, 2:2 + W] >> 24) == 255)
     assert torch.all(w[:, :2] == 0) and torch.all(w[:, :, -2:] == 0)
     assert len(torch.unique(w[1:, 2:2 + H, 2:2 + W] & 255)) == 256
+
+
+def test_u8_render_rejects_unknown_row_variants(dev, kopts):
+    """render_tile values the u8 render has no kernel for (4 rows without vertical reuse, 16)
+    are refused instead of being silently remapped to another variant."""
+    P, H, W = 3, 16, 70
+    packed = _lib.synth_mpi_packed_u8(1, H, W, 0, P, dev)
+    homs = torch.zeros((1, P, 9), device=dev)
+    for rows in (4, 16):
+        kopts(render_tile=rows)
+        with pytest.raises(RuntimeError, match="not a u8 render variant"):
+            _lib.render_packed_u8(packed, homs)
