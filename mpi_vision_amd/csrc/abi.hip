@@ -72,6 +72,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      depth-per-lane (plane_sweep_dlane_kernel)
 //   sweep_rows=4|6|8   mpiv_plane_sweep[_into]'s depth-per-lane kernel with tiles of that many
 //                      target rows (staging 3072 / 4096 / 4096 texels; 0 = automatic)
+//   bwd_gather=0|1     render backward gather: block tiles (bwd_gather_kernel) / one texel row per
+//                      wave, no block barriers (bwd_gather_wave_kernel)
 //   chunk_flight=2|4   render_chunk_kernel with that many sub-steps' taps in flight per wave
 //                      (0 = automatic)
 //   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
@@ -87,13 +89,13 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 // launches is a test-harness race on which kernel runs, never on memory.
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
-                kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kNumOpts };
+                kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
-                                         "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0};
+                                         "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -698,9 +700,13 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
 #undef MPIV_CHAIN
         if (!force) {
             bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
-            bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x, margin,
-                                                                           ws.box);
-            bwd_gather_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
+            if (opt(kOptBwdGather) == 1) {
+                bwd_gather_wave_kernel<<<(unsigned)gather_blocks, 256, 0, q>>>(g, hv, ws, gv, margin);
+            } else {
+                bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x,
+                                                                               margin, ws.box);
+                bwd_gather_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
+            }
         }
         bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force);
         // fallback: one launch of resident blocks, returns at once unless flagged

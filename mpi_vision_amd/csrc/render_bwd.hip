@@ -701,6 +701,262 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     }
 }
 
+// ---- 2b. gather, one texel row per wave (bwd_gather=1) ---------------------------------
+// The same per-texel sums and keys as bwd_gather_kernel, but every wave works alone on its
+// 64-texel row: it maps its own bucket region [tx0-1, tx0+63] x [ty-1, ty] (nw taps) back to a
+// box of pixels, stages their sample positions in wave-private LDS and reads the d samples of
+// the contributors it finds straight from memory -- no block barriers, so the waves of a CU
+// drift apart and one wave's memory round trip hides behind another's arithmetic.
+constexpr int kWCap = 256;              // staged pixels per wave pass
+constexpr int kWNB = kGTB * 2;          // bucket rows: nw-tap y = ty - 1, ty
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#ifndef MPIV_GLBW
+#define MPIV_GLBW 6
+#endif
+__global__ __launch_bounds__(256, MPIV_GLBW) void bwd_gather_wave_kernel(RenderGeom g, const float* __restrict__ homs,
+                                                                   BwdWs ws, float4* __restrict__ dmpi, float margin) {
+    __shared__ int s_code_a[4][kWCap];   // local nw-tap bucket of the staged pixel, -1 = none
+    __shared__ float2 s_fr_a[4][kWCap];  // its bilinear fractions
+    __shared__ int s_pix_a[4][kWCap];    // its pixel index (y*W + x)
+    __shared__ uint2 s_bent_a[4][kWNB];  // bucket lists (kGBCap entries)
+    __shared__ int s_bcnt_a[4][kWNB];    // bucket sizes
+    constexpr int TB = kGTB;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+    int* s_code = s_code_a[wave];
+    float2* s_fr = s_fr_a[wave];
+    int* s_pix = s_pix_a[wave];
+    uint2* s_bent = s_bent_a[wave];
+    int* s_bcnt = s_bcnt_a[wave];
+    const int tiles_x = (g.W + kGTW - 1) / kGTW;
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int ngroups = (g.P + kGPl - 1) / kGPl;
+    const int tile = lb / ngroups, p0 = (lb % ngroups) * kGPl;
+    const int tx0 = (tile % tiles_x) * kGTW, ty = (tile / tiles_x) * kGTH + wave;
+    if (ty >= g.H) return;  // whole wave; no block barrier anywhere below
+    const int tx = tx0 + lane;
+    const bool tin = tx < g.W;
+    const int64_t HW = (int64_t)g.H * g.W;
+    const int bt = TB + lane + 1;  // bucket of the texel as an nw tap (row 1: nw-tap y = ty)
+    for (int b = lane; b < kWNB; b += kWave) s_bcnt[b] = 0;
+    unsigned hits = 0;
+    bool unsafe = false;
+    f32x4 acc[kGPl];
+#pragma unroll
+    for (int jj = 0; jj < kGPl; ++jj) {
+        acc[jj] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const int p = p0 + jj;
+        if (p >= g.P) continue;  // wave-uniform
+        // the box of pixels whose samples can have their nw tap in the bucket region:
+        // samples in [tx0-1, tx0+kGTW) x [ty-1, ty+1), inverse image of the corners + margin
+        const float* iv = ws.inv + (int64_t)p * 12;
+        bool bad = iv[9] == 0.0f;
+        float xmn = __builtin_inff(), xmx = -__builtin_inff(), ymn = __builtin_inff(), ymx = -__builtin_inff();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float mb[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) mb[k] = iv[k];
+            float xx, yy;
+            const bool okc = inv_map(mb, (float)((c & 1) ? tx0 + kGTW : tx0 - 1), (float)((c & 2) ? ty + 1 : ty - 1), xx, yy);
+            bad = bad || !okc;
+            xmn = __builtin_fminf(xmn, xx);
+            xmx = __builtin_fmaxf(xmx, xx);
+            ymn = __builtin_fminf(ymn, yy);
+            ymx = __builtin_fmaxf(ymx, yy);
+        }
+        int bx0 = 0, bx1 = -1, by0 = 0, by1 = -1;
+        if (!bad) {
+            pix_range(xmn, xmx, margin, 0, g.W - 1, bx0, bx1);
+            pix_range(ymn, ymx, margin, 0, g.H - 1, by0, by1);
+            const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
+            if (bw > 0 && bh > 0) {
+                const int rpp = bw <= kWCap ? kWCap / bw : 1;
+                bad = bw > kWCap || (int64_t)bw * bh > 64 * kWCap ||
+                      (bh > rpp && (g.W & 7) && bx0 <= 6 && bx1 >= g.W - 7);
+            }
+        }
+        if (bad) {  // this wave cannot gather the plane: the check sends the view to the fallback
+            unsafe = true;
+            continue;
+        }
+        const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
+        if (bw <= 0 || bh <= 0) continue;  // no pixel samples the row: zero gradient (counted)
+        const float* hp = homs + (int64_t)p * 9;
+        const bool proven = div2_rect_safe(hp, (float)bx0, (float)bx1, (float)by0, (float)by1);
+        const int rpp = kWCap / bw;
+        const float4* dsp = ws.ds + (int64_t)p * HW;
+        for (int ra = by0; ra <= by1; ra += rpp) {
+            const int rb = min(by1 + 1, ra + rpp);
+            const int np = (rb - ra) * bw;
+            const int gbase = (ra * g.W) >> 3;
+            bool ovf = (int64_t)(rb - ra + 1) * g.W >= ((int64_t)1 << 19);  // keys hold chunk - gbase in 16 bits
+            const float rbw = 1.0f / (float)bw;
+            for (int q = lane; q < np; q += kWave) {
+                const int r = (int)(((float)q + 0.5f) * rbw);  // q / bw
+                const int yy = ra + r, xx = bx0 + (q - r * bw);
+                float px, py;
+                if (proven)
+                    render_pos_fast<false>(hp, (float)xx, (float)yy, g, px, py);
+                else
+                    render_pos<true>(hp, (float)xx, (float)yy, g, px, py);
+                const float fx0 = floorf(px), fy0 = floorf(py);
+                const float lx = fx0 - (float)(tx0 - 1), ly = fy0 - (float)(ty - 1);
+                const bool in = lx >= 0.0f && lx <= (float)kGTW && ly >= 0.0f && ly <= 1.0f;
+                const int code = in ? (int)ly * TB + (int)lx : -1;
+                const int pix = yy * g.W + xx;
+                s_code[q] = code;
+                if (in) {
+                    s_fr[q] = make_float2(px - fx0, py - fy0);
+                    s_pix[q] = pix;
+                    const unsigned e = ((unsigned)((pix >> 3) - gbase) << 16) | ((unsigned)(pix & 7) << 11) | (unsigned)q;
+                    const int slot = atomicAdd(&s_bcnt[code], 1);
+                    if (slot < kGBCap)
+                        (slot == 0 ? s_bent[code].x : s_bent[code].y) = e;
+                    else
+                        ovf = true;
+                }
+            }
+            wave_lds_fence();
+            ovf = __any(ovf);
+            if (tin && !ovf) {
+                unsigned key[8];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int b = bt - (c & 1) - (c >> 1) * TB;
+                    const int n = s_bcnt[b];
+                    const uint2 e = s_bent[b];
+                    key[2 * c] = n > 0 ? (e.x | ((unsigned)c << 14)) : 0xFFFFFFFFu;
+                    key[2 * c + 1] = n > 1 ? (e.y | ((unsigned)c << 14)) : 0xFFFFFFFFu;
+                }
+                bool two = false;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) two = two || key[2 * c + 1] != 0xFFFFFFFFu;
+                if (__any(two)) {
+                    sort8(key);
+                } else {
+                    sort4(key[0], key[2], key[4], key[6]);
+                    key[1] = key[2];
+                    key[2] = key[4];
+                    key[3] = key[6];
+                    key[4] = key[5] = key[6] = key[7] = 0xFFFFFFFFu;
+                }
+#pragma unroll
+                for (int k0 = 0; k0 < 8; k0 += 4) {
+                    if (key[k0] == 0xFFFFFFFFu) break;
+                    float2 f[4];
+                    float4 d[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (key[k0 + k] != 0xFFFFFFFFu) {
+                            const int q = (int)(key[k0 + k] & 0x7FF);
+                            f[k] = s_fr[q];
+                            d[k] = dsp[s_pix[q]];
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (key[k0 + k] != 0xFFFFFFFFu) {
+                            const float wx = f[k].x, ex = 1.0f - wx;
+                            const float wy = f[k].y, sy = 1.0f - wy;
+                            const unsigned c = key[k0 + k] >> 14;
+                            const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
+                            acc[jj][0] = acc[jj][0] + w * d[k].x;
+                            acc[jj][1] = acc[jj][1] + w * d[k].y;
+                            acc[jj][2] = acc[jj][2] + w * d[k].z;
+                            acc[jj][3] = acc[jj][3] + w * d[k].w;
+                            ++hits;
+                        }
+                    }
+                }
+            } else if (tin) {
+                // window scan (magnification): bwd_gather_kernel's, on this wave's staging
+                float m[9];  // the inverse map again (not kept live through the fill)
+#pragma unroll
+                for (int k = 0; k < 9; ++k) m[k] = iv[k];
+                int wx0 = 0, wx1 = -1, wy0 = 0, wy1 = -1;
+                float a0 = __builtin_inff(), a1 = -__builtin_inff(), b0 = __builtin_inff(), b1 = -__builtin_inff();
+                bool lbad = false;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    float xx, yy;
+                    const bool okc = inv_map(m, (float)(tx + ((c & 1) ? 1 : -1)), (float)(ty + ((c & 2) ? 1 : -1)), xx, yy);
+                    lbad = lbad || !okc;
+                    a0 = __builtin_fminf(a0, xx);
+                    a1 = __builtin_fmaxf(a1, xx);
+                    b0 = __builtin_fminf(b0, yy);
+                    b1 = __builtin_fmaxf(b1, yy);
+                }
+                if (!lbad) {
+                    pix_range(a0, a1, margin, bx0, bx1, wx0, wx1);
+                    pix_range(b0, b1, margin, by0, by1, wy0, wy1);
+                    if ((g.W & 7) && wy1 > wy0 && wx1 >= g.W - 7 && wx0 <= 6) lbad = true;
+                }
+                if (lbad) {
+                    unsafe = true;
+                    wy1 = wy0 - 1;
+                }
+                const int ya = max(wy0, ra), yb = min(wy1, rb - 1);
+                for (int yy = ya; yy <= yb; ++yy) {
+                    const int rowbase = (yy - ra) * bw - bx0;
+                    const int pixrow = yy * g.W;
+                    int cur = -1;
+                    unsigned msk = 0;
+                    auto flush = [&]() {
+                        while (msk) {
+                            const int b = __builtin_ctz(msk);
+                            msk &= msk - 1;
+                            const int idx = rowbase + (cur * kGridVec + (b & 7) - pixrow);
+                            const float2 f = s_fr[idx];
+                            const float4 d = dsp[s_pix[idx]];
+                            const float wx = f.x, ex = 1.0f - wx;
+                            const float wy = f.y, sy = 1.0f - wy;
+                            const int c = b >> 3;
+                            const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
+                            acc[jj][0] = acc[jj][0] + w * d.x;
+                            acc[jj][1] = acc[jj][1] + w * d.y;
+                            acc[jj][2] = acc[jj][2] + w * d.z;
+                            acc[jj][3] = acc[jj][3] + w * d.w;
+                            ++hits;
+                        }
+                    };
+                    for (int xx = wx0; xx <= wx1; ++xx) {
+                        const int code = s_code[rowbase + xx];
+                        const int dd = bt - code;  // 0: nw tap, 1: ne, TB: sw, TB+1: se
+                        const int c = code < 0 ? -1 : dd == 0 ? 0 : dd == 1 ? 1 : dd == TB ? 2 : dd == TB + 1 ? 3 : -1;
+                        if (c >= 0) {
+                            const int px = pixrow + xx;
+                            if ((px >> 3) != cur) {
+                                flush();
+                                cur = px >> 3;
+                            }
+                            msk |= 1u << (c * 8 + (px & 7));
+                        }
+                    }
+                    flush();
+                }
+            }
+            wave_lds_fence();  // every lane has read the lists before they are cleared
+            for (int b = lane; b < kWNB; b += kWave) s_bcnt[b] = 0;
+            wave_lds_fence();
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) hits += __shfl_xor(hits, off);
+    const unsigned long long tot = (unsigned long long)hits + (__any(unsafe) ? kUnsafe : 0ull);
+    if (lane == 0 && tot) atomicAdd(&ws.found[blockIdx.x % kCtrSlots], tot);
+    if (tin) {
+        float4* o = dmpi + ((int64_t)ty * g.W + tx) * g.P + p0;
+#pragma unroll
+        for (int jj = 0; jj < kGPl; ++jj)
+            if (p0 + jj < g.P) o[jj] = make_float4(acc[jj][0], acc[jj][1], acc[jj][2], acc[jj][3]);
+    }
+}
+
 // ---- 3. check: found == truth, else the fallback runs; counters reset for the next view
 __global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force) {
     const int l = threadIdx.x;

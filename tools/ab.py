@@ -117,6 +117,27 @@ def sweep(dev, it):
         del out
 
 
+GATHER = [("block", {}), ("wave", {"bwd_gather": 1})]
+
+
+def bwdg(dev, it):
+    mpi, homs, H, W, P = c4_mpi(dev)
+    g = torch.Generator(device=dev).manual_seed(1)
+    dout = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    ws = torch.empty(_lib.load().mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    _, ck = _lib.render_train(mpi, homs)
+    ref = _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)
+    flag_off = _lib.bwd_flag_offset(H, W, P)
+    for label, opts in GATHER:
+        with _lib.debug(**opts):
+            got = _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)
+            flag = int(ws[flag_off:flag_off + 4].view(torch.int32).item())
+        print(json.dumps({"exp": "bwd gather parity", "variant": label, "bit_identical":
+                          bool(torch.equal(got.view(torch.int32), ref.view(torch.int32))), "fallback_flag": flag}))
+    fn = lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)  # noqa: E731
+    run("c4 render backward with checkpoints, 1 view", GATHER, fn, 2 * P * H * W * 16 + H * W * 12, it)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
