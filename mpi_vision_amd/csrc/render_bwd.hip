@@ -65,6 +65,9 @@ constexpr int kGThreads = kGTW * kGTH;
 #ifndef MPIV_GLB
 #define MPIV_GLB 6
 #endif
+#ifndef MPIV_GPF
+#define MPIV_GPF 0
+#endif
 constexpr int kGPl = MPIV_GPL;     // gather: planes per block (a texel's kGPl planes are one 16*kGPl-B run)
 constexpr int kGCap = MPIV_GCAP;   // gather: output pixels staged per pass
 constexpr int kGMaxBox = 64 * kGCap;  // gather: larger boxes (extreme magnification) -> fallback
@@ -460,6 +463,18 @@ __device__ __forceinline__ void sort8(unsigned* k) {
     cx(3, 4);
 }
 
+// One LDS-DMA instruction (render_ring.hip's): 64 lanes x 16 B from the buffer at per-lane
+// byte offsets into LDS bytes [lds, lds + 1 KiB).  Inline asm: hipcc cannot tell which LDS
+// bytes a DMA writes and would drain vmcnt(0) before every ds_read; the gather waits for its
+// own fills (vmcnt(0) before the barrier that publishes them).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void gather_dma16(__amdgpu_buffer_rsrc_t r, int voff, unsigned lds) {
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(lds)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 constexpr int kGTB = kGTW + 1;              // bucket row pitch: nw taps x in [tx0-1, tx0+kGTW-1]
 constexpr int kGNB = kGTB * (kGTH + 1);     // nw-tap buckets of a tile
 constexpr int kGBCap = 2;                   // entries per bucket list (more: the window scan)
@@ -480,7 +495,15 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
                                                          float4* __restrict__ dmpi, float margin) {
     __shared__ int s_code[kGCap];     // local nw-tap bucket of the staged pixel, -1 = none
     __shared__ float2 s_fr[kGCap];    // its bilinear fractions (px - floor px, py - floor py)
+#if MPIV_GPF
+    // d samples of a pass, double-buffered by pass parity: the next plane's first pass is
+    // copied in by LDS-DMA while this plane's texels accumulate (rows padded to 256 slots:
+    // a wave's DMA instruction writes 64 consecutive slots)
+    constexpr int kGCapD = (kGCap + 255) / 256 * 256;
+    __shared__ float4 s_dsb[2][kGCapD];
+#else
     __shared__ float4 s_ds[kGCap];    // its d sample
+#endif
     __shared__ uint2 s_bent[kGNB];    // bucket lists (kGBCap entries)
     __shared__ int s_bcnt[2][kGNB];   // bucket sizes, by pass parity (one is zeroed while the other is in use)
     __shared__ int s_ovf[2];          // a list overflowed in this pass
@@ -500,6 +523,38 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     int par = 0;
     unsigned hits = 0;    // (texel, contributor) pairs found by this thread
     bool unsafe = false;  // a plane this block could not order (the view goes to the fallback)
+#if MPIV_GPF
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+    // copy the d samples of plane p's rows [ra, ra + n/bw) of box columns [bx0, bx0 + bw) into
+    // s_dsb[buf] (staged index q = row * bw + column), 64 per wave instruction
+    auto dma_pass = [&](int p, int bx0_, int bw_, int ra_, int n, int buf) {
+        const __amdgpu_buffer_rsrc_t r = make_rsrc(ws.ds + (int64_t)p * HW, (int)(HW * 16));
+        const float rbw = 1.0f / (float)bw_;
+        const unsigned base = (unsigned)(uintptr_t)&s_dsb[buf][0];
+        for (int q0 = wave * kWave; q0 < n; q0 += kGThreads) {
+            const int q = q0 + lane;
+            int rr = (int)(((float)q + 0.5f) * rbw);  // q / bw (q < 2048: exact after the +0.5)
+            const int off = q < n ? ((ra_ + rr) * g.W + bx0_ + (q - rr * bw_)) * 16 : kOOB;
+            gather_dma16(r, off, __builtin_amdgcn_readfirstlane(base + (unsigned)q0 * 16u));
+        }
+    };
+    // a plane whose box fits one pass gets its d samples prefetched during the previous
+    // plane's texel phase (pf_plane: the plane whose first pass sits in s_dsb[par ^ 1])
+    auto one_pass_box = [&](int p, int4& b) {
+        b = ws.box[(int64_t)p * ntiles + tile];
+        const int bw_ = b.y - b.x + 1, bh_ = (b.w & ~kBoxProven) - b.z + 1;
+        return b.x != -2 && bw_ > 0 && bh_ > 0 && bh_ * bw_ <= kGCap;
+    };
+    int pf_plane = -1;
+    {
+        int4 b;
+        if (p0 < g.P && one_pass_box(p0, b)) {
+            dma_pass(p0, b.x, b.y - b.x + 1, b.z, (b.y - b.x + 1) * ((b.w & ~kBoxProven) - b.z + 1), par);
+            pf_plane = p0;
+        }
+    }
+    pf_plane = pf_plane == p0 ? -2 : -1;  // -2: plane p0's first pass already sits in s_dsb[par]
+#endif
     f32x4 acc[kGPl];
 #pragma unroll
     for (int jj = 0; jj < kGPl; ++jj) {
@@ -521,7 +576,16 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
             const int rb = min(by1 + 1, ra + rpp);
             const int np = (rb - ra) * bw;
             const int gbase = (ra * g.W) >> 3;  // the pass's first 8-pixel chunk
-            __syncthreads();  // the previous pass's readers are done
+#if MPIV_GPF
+            float4* s_ds = s_dsb[par];
+            if (!(ra == by0 && pf_plane == -2)) {
+                __syncthreads();  // the previous pass's readers of this buffer are done
+                dma_pass(p, bx0, bw, ra, np, par);
+            }
+            pf_plane = -1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's fills of s_ds have landed
+#endif
+            __syncthreads();  // the previous pass's readers are done (and, MPIV_GPF, every wave's fills)
             {
                 int* cnt = s_bcnt[par];
                 // order keys hold (chunk - gbase) in 16 bits
@@ -542,7 +606,9 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
                     s_code[q] = code;
                     if (in) {
                         s_fr[q] = make_float2(px - fx0, py - fy0);
+#if !MPIV_GPF
                         s_ds[q] = ws.ds[(int64_t)p * HW + (int64_t)yy * g.W + xx];
+#endif
                         const int pix = yy * g.W + xx;
                         const unsigned e = ((unsigned)((pix >> 3) - gbase) << 16) | ((unsigned)(pix & 7) << 11) |
                                            (unsigned)q;
@@ -557,6 +623,19 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
                 if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
             }
             __syncthreads();
+#if MPIV_GPF
+            // the last pass of this plane: prefetch the next plane's first pass into the other
+            // buffer (last read by the previous pass, whose readers finished before this pass's
+            // first barrier)
+            if (rb > by1 && jj + 1 < kGPl && p + 1 < g.P) {
+                int4 b;
+                if (one_pass_box(p + 1, b)) {
+                    dma_pass(p + 1, b.x, b.y - b.x + 1, b.z, (b.y - b.x + 1) * ((b.w & ~kBoxProven) - b.z + 1),
+                             par ^ 1);
+                    pf_plane = -2;
+                }
+            }
+#endif
             const bool ovf = s_ovf[par] != 0;
             if (tin && !ovf) {
                 // the texel's <= 8 contributors: buckets t (nw), t-1 (ne), t-row (sw), t-row-1 (se)

@@ -127,6 +127,8 @@ def bwdg(dev, it):
     ws = torch.empty(_lib.load().mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
     _, ck = _lib.render_train(mpi, homs)
     ref = _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)
+    import hashlib
+    print(json.dumps({"exp": "bwd gradient sha16", "sha16": hashlib.sha256(ref.cpu().numpy().tobytes()).hexdigest()[:16]}))
     flag_off = _lib.bwd_flag_offset(H, W, P)
     for label, opts in GATHER:
         with _lib.debug(**opts):
