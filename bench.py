@@ -395,6 +395,21 @@ def config3_leg(dev, stream, n=20):
     alg = S * H * W * 12 + S * D * H * W * 12
     gbs, frac = hbm(alg, ms)
     kname, grid = _lib.route("plane_sweep", S, H, W, 3, D, H, W)
+    # the same sources into the notebook dataset's 10 planes (ipynb cell 8 L73-75: inv_depths(1, 100, 10))
+    D10 = 10
+    d10 = configs.f32(configs.inv_depths(1, 100, D10)).to(dev)
+    out10 = torch.empty((S, H, W, D10 * 3), device=dev)
+    launch10 = lambda: _lib._call("mpiv_plane_sweep", img, _lib._strides(img), S, H, W, 3, ki, proj, d10, D10,  # noqa: E731
+                                  H, W, out10, _lib._stream(dev))
+    launch10()
+    ms10 = event_ms(launch10, n, stream)
+    alg10 = S * H * W * 12 + S * D10 * H * W * 12
+    k10, g10 = _lib.route("plane_sweep", S, H, W, 3, D10, H, W)
+    ten = {"workload": "config 3 sources into 10 depth planes (the notebook dataset's depth count)",
+           "kernel_ms": round(ms10, 4), "alg_bytes": alg10, "achieved_gbs": hbm(alg10, ms10)[0],
+           "frac": hbm(alg10, ms10)[1], "bound": "hbm"}
+    ten.update(prof_fields(k10, g10, alg10, ms10))
+    del out10
     res = {"workload": "BASELINE config 3: PSV of 5 source 1024x768x3 images into 64 depth planes "
                        "(plane_sweep_torch, utils.py:452-471)",
            "kernel_ms": round(ms, 4), "dropin_ms": round(dropin_ms, 4),
@@ -404,6 +419,7 @@ def config3_leg(dev, stream, n=20):
            "dropin_equals_kernel": same,
            "reference_cpu": {"s": REF_CPU["c3_s"], "cores": REF_CPU["cores"], "source": REF_CPU["source"]}}
     res.update(prof_fields(kname, grid, alg, ms))
+    res["ten_planes"] = ten
     del img, out, vol
     return res
 
@@ -644,9 +660,17 @@ def main():
             if s + 1 < first + n_steps:
                 upload(s + 1)  # host-side homographies of the next step overlap this launch
 
-    # single-view leg first, so it does not inherit a clock lowered by the sustained load
+    # the short legs first (single view, configs 2 and 3, the notebook shape), so they do not
+    # inherit a clock lowered by the sustained config-4 load (config 3 measured 0.75 ms after it
+    # against 0.61-0.63 ms on a fresh clock, profiles/r03_sweep_few_depths_ab.txt)
     sv = single_view_leg(packed, H, W, P, host_homs(0, 1).to(dev), dev, stream) \
         if ("sv" in legs and packed is not None) else None
+    c2 = config2_leg(dev, stream) if "c2" in legs else None
+    torch.cuda.empty_cache()
+    c3 = config3_leg(dev, stream) if "c3" in legs else None
+    torch.cuda.empty_cache()
+    nb = notebook_leg(dev, stream) if "nb" in legs else None
+    torch.cuda.empty_cache()
 
     run(args.warmup, 0)
     torch.cuda.synchronize()
@@ -712,12 +736,6 @@ def main():
         del view, packed
     torch.cuda.empty_cache()
 
-    c2 = config2_leg(dev, stream) if "c2" in legs else None
-    torch.cuda.empty_cache()
-    c3 = config3_leg(dev, stream) if "c3" in legs else None
-    torch.cuda.empty_cache()
-    nb = notebook_leg(dev, stream) if "nb" in legs else None
-    torch.cuda.empty_cache()
     train = training_leg(dev, stream) if "train" in legs else None
     c5 = config5_leg(world, rank, dev, max(3, args.steps // 2), 1) if "c5" in legs else None
     ranks = {"world_size_seen": world, "backend": backend, "per_rank_kernel_ms": [round(x, 4) for x in kern_all]}

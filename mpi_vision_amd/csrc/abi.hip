@@ -78,6 +78,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (0 = automatic)
 //   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
 //                      wave (0 = automatic)
+//   sweep_direct=-1|0|1  mpiv_plane_sweep[_into] without LDS staging (plane_sweep_direct_kernel):
+//                      never / automatic (D <= 8) / for any D <= 64
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
 //                      forces their per-sample global fallback (tests)
 //   bwd_fallback=1     mpiv_render_backward skips the tile gather and runs its bucket
@@ -89,13 +91,15 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 // launches is a test-harness race on which kernel runs, never on memory.
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
-                kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kNumOpts };
+                kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
+                kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
-                                         "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0};
+                                         "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
+                                         "sweep_direct"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -756,6 +760,26 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
     const dim3 lgrid((unsigned)tiles, B, 1);
     const int shrink = opt(kOptBoxShrink);
     hipStream_t q = S(stream);
+    // few depths: no LDS staging (plane_sweep_direct_kernel); sweep_direct = -1 off, 1 for any D <= 64
+    const int od = opt(kOptSweepDirect);
+    if (od >= 0 && shrink == 0 && D <= (od == 1 ? kWave : kDirMaxD) && Ht <= (int)kMaxGridYZ) {
+        const int ppw = kWave / D;
+        const int64_t gpr = (Wt + ppw - 1) / ppw;  // pixel groups per target row
+        const dim3 dgrid((unsigned)((gpr + 4 * kDirG - 1) / (4 * kDirG)), (unsigned)Ht, (unsigned)B);
+        if (g_route) return note_route((int64_t)dgrid.x * Ht * B, 256, "plane_sweep_direct_kernel<%d>", C < 4 ? C : 4);
+        const float rD = 1.0f / (float)D;
+#define MPIV_DIRECT(CC)                                                                                      \
+    plane_sweep_direct_kernel<CC><<<dgrid, 256, 0, q>>>(img, is, sp, rc_hs, rc_ws, rD, ki, proj, depths, out, \
+                                                        out_bstride, out_pstride, (int)vec)
+        switch (C) {
+            case 1: MPIV_DIRECT(1); break;
+            case 2: MPIV_DIRECT(2); break;
+            case 3: MPIV_DIRECT(3); break;
+            default: MPIV_DIRECT(4); break;
+        }
+#undef MPIV_DIRECT
+        return launched(nm);
+    }
     if (g_route)
         return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true, %d, %d>", C < 4 ? C : 4, SLR,
                           SLR == 4 ? kSLCap : 4096);

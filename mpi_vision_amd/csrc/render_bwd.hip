@@ -55,7 +55,9 @@ constexpr int kGTH = MPIV_GTH;     // gather: tile rows (one wave each)
 constexpr int kGThreads = kGTW * kGTH;
 // gather tile constants (overridable for A/B builds, tools/gpu_ab_lib.sh); measured on
 // config 4 (profiles/r02_bwd_gather_ab.txt): 4 planes x 736 staged pixels at 6 waves/SIMD
-// 2.97 ms per backward, 8 planes x 1024 at 4 waves 3.40, 8 waves (any shape) spills
+// 2.97 ms per backward, 8 planes x 1024 at 4 waves 3.40, 8 waves (any shape) spills.  Round 3
+// (profiles/r03_bwd_gather_ab.txt): the staging's d-sample loads issued ahead of the positions
+// need 5 waves/SIMD (at 6 the allocator spills): gather 1.67 vs 1.76 ms
 #ifndef MPIV_GPL
 #define MPIV_GPL 4
 #endif
@@ -63,10 +65,13 @@ constexpr int kGThreads = kGTW * kGTH;
 #define MPIV_GCAP 736
 #endif
 #ifndef MPIV_GLB
-#define MPIV_GLB 6
+#define MPIV_GLB 5
 #endif
 #ifndef MPIV_GPF
 #define MPIV_GPF 0
+#endif
+#ifndef MPIV_GSI
+#define MPIV_GSI 2  // staged pixels per thread whose d samples are loaded ahead of the positions
 #endif
 constexpr int kGPl = MPIV_GPL;     // gather: planes per block (a texel's kGPl planes are one 16*kGPl-B run)
 constexpr int kGCap = MPIV_GCAP;   // gather: output pixels staged per pass
@@ -591,7 +596,25 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
                 // order keys hold (chunk - gbase) in 16 bits
                 if (threadIdx.x == 0 && (int64_t)(rb - ra + 1) * g.W >= ((int64_t)1 << 19)) s_ovf[par] = 1;
                 const float rbw = 1.0f / (float)bw;
-                for (int q = threadIdx.x; q < np; q += kGThreads) {
+                constexpr int kSI = (kGCap + kGThreads - 1) / kGThreads;  // staged pixels per thread
+#if !MPIV_GPF
+                // the pass's d samples first: one buffer load per staged pixel, all in flight while
+                // the sample positions are computed (issued after its pixel's position, inside the
+                // in-tile test, each load's latency was exposed: 0.32 of the kernel's 1.77 ms, r03)
+                const __amdgpu_buffer_rsrc_t rds = make_rsrc(ws.ds + (int64_t)p * HW, (int)(HW * 16));
+                f32x4 dsv[kSI];
+#pragma unroll
+                for (int i = 0; i < (kSI < MPIV_GSI ? kSI : MPIV_GSI); ++i) {
+                    const int q = (int)threadIdx.x + i * kGThreads;
+                    const int r = (int)(((float)q + 0.5f) * rbw);  // q / bw: q, bw <= 1024, error << 0.5/bw
+                    const int off = q < np ? ((ra + r) * g.W + bx0 + (q - r * bw)) * 16 : kOOB;
+                    dsv[i] = llvm_raw_buffer_load_v4f32(rds, off, 0, 0);
+                }
+#endif
+#pragma unroll
+                for (int i = 0; i < kSI; ++i) {
+                    const int q = (int)threadIdx.x + i * kGThreads;
+                    if (q >= np) break;
                     const int r = (int)(((float)q + 0.5f) * rbw);  // q / bw: q, bw <= 1024, error << 0.5/bw
                     const int yy = ra + r, xx = bx0 + (q - r * bw);
                     float px, py;
@@ -607,7 +630,9 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
                     if (in) {
                         s_fr[q] = make_float2(px - fx0, py - fy0);
 #if !MPIV_GPF
-                        s_ds[q] = ws.ds[(int64_t)p * HW + (int64_t)yy * g.W + xx];
+                        if (i >= MPIV_GSI)  // past the preloaded pixels (boxes over MPIV_GSI * 256 pixels)
+                            dsv[i] = llvm_raw_buffer_load_v4f32(rds, (yy * g.W + xx) * 16, 0, 0);
+                        s_ds[q] = make_float4(dsv[i][0], dsv[i][1], dsv[i][2], dsv[i][3]);
 #endif
                         const int pix = yy * g.W + xx;
                         const unsigned e = ((unsigned)((pix >> 3) - gbase) << 16) | ((unsigned)(pix & 7) << 11) |
@@ -661,36 +686,43 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
                     key[3] = key[6];
                     key[4] = key[5] = key[6] = key[7] = 0xFFFFFFFFu;
                 }
-                // valid keys sort first; a batch's reads are skipped when no lane of the wave
-                // has that many contributors
-#pragma unroll
-                for (int k0 = 0; k0 < 8; k0 += 4) {
-                    if (key[k0] == 0xFFFFFFFFu) break;  // this lane is done (others may go on)
+                // Valid keys sort first.  A batch of 4 is branch-free: every lane reads (an
+                // invalid key reads staged entry 0) and a select keeps the sum of an invalid
+                // key unchanged (acc + w*d would turn -0 into +0).  Per-lane ifs here cost an
+                // s_and_saveexec / s_cbranch / s_or_b64 exec triple each: PMC r03 counted 408M
+                // scalar instructions per launch beside 727M VALU, the CU's one scalar unit a
+                // co-limiter.  The second batch (5+ contributors: magnification) is a
+                // wave-uniform branch.
+                auto batch = [&](int k0) {
                     float2 f[4];
                     float4 d[4];
+                    bool v[4];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        if (key[k0 + k] != 0xFFFFFFFFu) {
-                            const int q = (int)(key[k0 + k] & 0x7FF);  // staged index: bits 0-10 (kGCap <= 2048)
-                            f[k] = s_fr[q];
-                            d[k] = s_ds[q];
-                        }
+                        v[k] = key[k0 + k] != 0xFFFFFFFFu;
+                        const int q = v[k] ? (int)(key[k0 + k] & 0x7FF) : 0;  // staged index: bits 0-10 (kGCap <= 2048)
+                        f[k] = s_fr[q];
+                        d[k] = s_ds[q];
                     }
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        if (key[k0 + k] != 0xFFFFFFFFu) {
-                            const float wx = f[k].x, ex = 1.0f - wx;
-                            const float wy = f[k].y, sy = 1.0f - wy;
-                            const unsigned c = key[k0 + k] >> 14;  // corner bits 14-15 (+ chunk bits above)
-                            const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
-                            acc[jj][0] = acc[jj][0] + w * d[k].x;
-                            acc[jj][1] = acc[jj][1] + w * d[k].y;
-                            acc[jj][2] = acc[jj][2] + w * d[k].z;
-                            acc[jj][3] = acc[jj][3] + w * d[k].w;
-                            ++hits;
-                        }
+                        const float wx = f[k].x, ex = 1.0f - wx;
+                        const float wy = f[k].y, sy = 1.0f - wy;
+                        const unsigned c = key[k0 + k] >> 14;  // corner bits 14-15 (+ chunk bits above)
+                        const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
+                        const float a0 = acc[jj][0] + w * d[k].x;
+                        const float a1 = acc[jj][1] + w * d[k].y;
+                        const float a2 = acc[jj][2] + w * d[k].z;
+                        const float a3 = acc[jj][3] + w * d[k].w;
+                        acc[jj][0] = v[k] ? a0 : acc[jj][0];
+                        acc[jj][1] = v[k] ? a1 : acc[jj][1];
+                        acc[jj][2] = v[k] ? a2 : acc[jj][2];
+                        acc[jj][3] = v[k] ? a3 : acc[jj][3];
+                        hits += v[k] ? 1u : 0u;
                     }
-                }
+                };
+                batch(0);
+                if (__any(key[4] != 0xFFFFFFFFu)) batch(4);
             } else if (tin) {
                 // window scan: the inverse image of the texels [tx-1, tx+1] x [ty-1, ty+1]
                 // whose samples have this texel as a tap, candidates in pixel order, the hits

@@ -1106,6 +1106,103 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     }
 }
 
+// Direct depth-per-lane sweep for few depths (D <= 8; abi.hip sweep_raw_into).  The LDS box
+// of plane_sweep_dlane_kernel is sized by the depth RANGE, not the depth count, so with few
+// depths it serves few samples per staged texel and the block's two serial latencies (box
+// prologue, fill) dominate (D = 10: 0.23-0.26 ms for config 3's sources, 0.25-0.28 of HBM).
+// Here nothing is staged: a wave takes ppw = 64 / D consecutive pixels x D depths with
+// plane_sweep_dlane_kernel's lane mapping (lane = pixel l / D, depth l % D; its ppw * D * C
+// results are one contiguous run of the volume) and gathers the four taps of each sample
+// straight from the caller's tensor -- for a fixed depth the wave's ppw pixels read
+// neighbouring texels, so the gathers hit L1/L2.  A wave walks kDirG pixel groups of its
+// row, two samples in flight per lane.  The per-sample arithmetic is the dlane kernel's
+// (bit-identical volume).
+constexpr int kDirG = 4;        // pixel groups per wave
+constexpr int kDirMaxD = 8;     // deepest volume routed here by default (measured: D = 6 0.15-0.18 ms
+                                // vs 0.19-0.23 staged; D >= 10 slower than the staged kernel)
+template <int C>
+__global__ __launch_bounds__(256) void plane_sweep_direct_kernel(const float* __restrict__ img, ImgStrides is,
+                                                                 SweepParams sp, float rc_hs, float rc_ws, float rD,
+                                                                 const float* __restrict__ ki,
+                                                                 const float* __restrict__ proj,
+                                                                 const float* __restrict__ depths,
+                                                                 float* __restrict__ out, int64_t out_bstride,
+                                                                 int64_t out_pstride, int vec) {
+    const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.z, y = blockIdx.y;
+    const int D = sp.D;
+    const int ppw = kWave / D;                            // pixels per group (scalar)
+    const int lp = (int)(((float)lane + 0.5f) * rD);      // lane / D (lane < 64, D <= 64: exact)
+    const int d = lane - lp * D;                          // the lane's depth
+    const bool dlive = lp < ppw;                          // lanes past ppw * D idle
+    const int gbase = (blockIdx.x * 4 + wave) * kDirG;    // this wave's first pixel group
+    if (gbase * ppw >= sp.Wt) return;                     // whole wave
+    const float dq = depths[min(d, D - 1)];
+    const float* k9 = ki + (int64_t)b * 9;
+    const float* m = proj + (int64_t)b * 16;
+    const float* imb = img + (int64_t)b * is.b;
+    float* orow = out + (int64_t)b * out_bstride + (int64_t)y * sp.Wt * out_pstride + (int64_t)d * C;
+    typedef float f32xC __attribute__((ext_vector_type(C), aligned(4)));
+    for (int gi = 0; gi < kDirG; gi += 2) {
+        if ((gbase + gi) * ppw >= sp.Wt) break;  // wave-uniform
+        float px[2], py[2], su[2], sv[2];
+        bool live[2], fast = true;
+        int xs[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int x = (gbase + gi + j) * ppw + lp;
+            live[j] = dlive && x < sp.Wt;
+            xs[j] = min(x, sp.Wt - 1);  // idle lanes recompute the last pixel (not stored)
+            float rx, ry, rz;
+            ray(k9, (float)xs[j], (float)y, rx, ry, rz);  // pixel2cam_torch, utils.py:370
+            const float X = rx * dq, Y = ry * dq, Z = rz * dq;
+            const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+            const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+            const float den = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11] + 1e-10f;
+            fast = fast && div2_safe(pu, pv, den);
+            div2_fast(pu, pv, den, su[j], sv[j]);  // cam2pixel_torch, utils.py:388-391
+        }
+        if (__builtin_amdgcn_ballot_w64(!fast)) {  // rare: a quotient outside the fast path's range
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                float rx, ry, rz;
+                ray(k9, (float)xs[j], (float)y, rx, ry, rz);
+                const float X = rx * dq, Y = ry * dq, Z = rz * dq;
+                const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+                const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+                const float den = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11] + 1e-10f;
+                if (!div2_safe(pu, pv, den)) {
+                    su[j] = div_rn(pu, den);
+                    sv[j] = div_rn(pv, den);
+                }
+            }
+        }
+        f32x4 s[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float cx = div_const(su[j] + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
+            const float cy = div_const(sv[j] + 0.5f, sp.fws, rc_ws);  //          y / W
+            px[j] = unnormalize(to_grid(cx), sp.half_ws);
+            py[j] = unnormalize(to_grid(cy), sp.half_hs);
+            s[j] = raw_sample<C>(imb, is, sp.Ws, sp.Hs, px[j], py[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (live[j]) {
+                float* o = orow + (int64_t)xs[j] * out_pstride;
+                f32xC v;
+#pragma unroll
+                for (int c = 0; c < C; ++c) v[c] = s[j][c];
+                if (vec) __builtin_nontemporal_store(v, reinterpret_cast<f32xC*>(o));
+                else {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) o[c] = v[c];
+                }
+            }
+        }
+    }
+}
+
 // projective_inverse_warp_torch[2] with a per-pixel depth map [B, Ht, Wt] (any
 // strides) -> [B, Ht, Wt, C]
 __global__ __launch_bounds__(256) void inverse_warp_kernel(const float* __restrict__ img, ImgStrides s,

@@ -418,3 +418,57 @@ def test_plane_sweep_tiny_targets(shape, dev):
     want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Ht, Wt)
     out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Ht, Wt)
     assert_bits(out.cpu().numpy(), want, str(shape))
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 4])
+@pytest.mark.parametrize("D,direct", [(1, "0"), (6, "0"), (8, "0"), (10, "0"), (10, "1"), (16, "1"), (32, "1"), (33, "1"),
+                                      (64, "1")])
+@pytest.mark.parametrize("strided", [False, True])
+def test_plane_sweep_direct_vs_oracle(C, D, direct, strided, dev, kopts):
+    """Few depths take the direct depth-per-lane kernel (no LDS staging; automatic for D <= 8,
+    sweep_direct=1 forces it up to D = 64, -1 keeps the LDS kernel): partial pixel groups
+    (64 % D idle lanes, a partial last group of a row), odd target sizes, separate source /
+    target intrinsics, a strided (channel-sliced) source: bit-exact to the oracle."""
+    from mpi_vision_amd import _host, _lib
+    from oracle import oracle
+    kopts(sweep_direct=direct)
+    g = torch.Generator().manual_seed(300 + C + D)
+    B, Hs, Ws, Ht, Wt = 2, 37, 83, 29, 71
+    full = torch.rand((B, Hs, Ws, C + 2), generator=g)
+    img = full[..., 1:C + 1] if strided else full[..., :C].contiguous()
+    Ks = configs.f32([configs.intrinsics_matrix(52.0, 55.0, 41.0, 19.0)] * B)
+    Kt = configs.f32([configs.intrinsics_matrix(48.0, 47.0, 35.0, 14.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(3.0 * k - 1.5), (0.2 * k - 0.1, -0.03, 0.02))
+                         for k in range(B)])
+    depths = configs.inv_depths(0.8, 60, D) if D > 1 else [3.0]
+    ki, proj = _host.psv_matrices(Ks, Kt, poses)
+    want = oracle.plane_sweep(img.contiguous().numpy(), ki.numpy(), proj.numpy(), depths, Ht, Wt)
+    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Ht, Wt)
+    assert_bits(out.cpu().numpy(), want, f"C={C} D={D} direct={direct} strided={strided}")
+    if direct == "0":  # mpiv_route reports production routes only
+        _lib.reset_debug()
+        route = _lib.route("plane_sweep", B, Hs, Ws, C, D, Ht, Wt)[0]
+        assert route.startswith("plane_sweep_direct_kernel" if D <= 8 else "plane_sweep_dlane_kernel"), route
+
+
+@pytest.mark.parametrize("direct", ["0", "-1"])
+def test_plane_sweep_direct_off_image(direct, dev, kopts):
+    """The notebook's 10 planes on landscape sources whose samples fall wholly or partly off
+    the image (the swapped x / H normalisation), through the direct kernel and the LDS kernel:
+    bit-exact to the oracle, zeros included."""
+    from mpi_vision_amd import _host, _lib
+    from oracle import oracle
+    kopts(sweep_direct=direct)
+    g = torch.Generator().manual_seed(321)
+    B, Hs, Ws, D = 3, 60, 160, 10
+    img = torch.rand((B, Hs, Ws, 3), generator=g) + 0.5
+    K = configs.f32([configs.intrinsics_matrix(150.0, 150.0, 80.0, 30.0)] * B)
+    poses = configs.f32([configs.pose_from(configs.rot_y(0.5), (0.1, 0.01, 0.0)),
+                         configs.pose_from(configs.rot_y(-20.0), (1.5, 0.2, 0.1)),
+                         configs.pose_from(configs.rot_y(40.0), (-2.0, -0.5, 0.3))])
+    depths = configs.inv_depths(1, 100, D)
+    ki, proj = _host.psv_matrices(K, K, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Hs, Ws)
+    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Hs, Ws)
+    assert_bits(out.cpu().numpy(), want, f"direct={direct}")
+    assert (want == 0).mean() > 0.2

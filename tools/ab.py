@@ -117,7 +117,7 @@ def sweep(dev, it):
         del out
 
 
-GATHER = [("block", {}), ("wave", {"bwd_gather": 1})]
+GATHER = [("block", {}), ("wave", {"bwd_gather": 1})]  # noqa: E501
 
 
 def bwdg(dev, it):
@@ -138,6 +138,51 @@ def bwdg(dev, it):
                           bool(torch.equal(got.view(torch.int32), ref.view(torch.int32))), "fallback_flag": flag}))
     fn = lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)  # noqa: E731
     run("c4 render backward with checkpoints, 1 view", GATHER, fn, 2 * P * H * W * 16 + H * W * 12, it)
+
+
+def sw10(dev, it):
+    """Config-3 sources into few depths (the notebook dataset's 10 planes) through
+    mpiv_plane_sweep: the direct depth-per-lane kernel (no LDS staging) against the LDS-staged
+    one (sweep_direct=1 / -1; automatic: direct for D <= 32)."""
+    c = configs.config3()
+    S, H, W = c["S"], c["H"], c["W"]
+    g = torch.Generator(device=dev).manual_seed(1)
+    img = torch.rand((S, H, W, 3), generator=g, device=dev)
+    K = configs.f32([c["K"]] * S)
+    ki, proj = _host.psv_matrices(K, K, configs.f32(c["poses"]))
+    ki, proj = ki.to(dev), proj.to(dev)
+    for D in (6, 10, 16, 32, 64):
+        d = configs.f32(configs.inv_depths(1, 100, D)).to(dev)
+        out = torch.empty((S, H, W, D * 3), device=dev)
+        alg = S * H * W * 12 + S * D * H * W * 12
+        raw = lambda: _lib._call("mpiv_plane_sweep", img, _lib._strides(img), S, H, W, 3, ki, proj, d, D, H, W,  # noqa: E731
+                                 out, _lib._stream(dev))
+        run(f"c3 sources -> {D} planes (mpiv_plane_sweep)", [("lds", {"sweep_direct": -1}), ("direct", {"sweep_direct": 1})],
+            raw, alg, it)
+        del out
+
+
+DEF = [("default", {})]
+
+
+def dflt(dev, it):
+    """The default routes of the training path (in-place render, training forward, backward with
+    checkpoints) -- for A/B across library builds (MPIV_LIB, tools/gpu_ab_any.sh)."""
+    mpi, homs, H, W, P = c4_mpi(dev)
+    out = torch.empty((1, H, W, 3), device=dev)
+    fn = lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out, _lib._stream(dev))  # noqa: E731
+    run("c4 in-place render, 1 view", DEF, fn, P * H * W * 16 + H * W * 12, it)
+    run("c4 training forward, 1 view", DEF, lambda: _lib.render_train(mpi, homs), P * H * W * 16 + H * W * 12, it)
+    g = torch.Generator(device=dev).manual_seed(1)
+    dout = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    ws = torch.empty(_lib.load().mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    _, ck = _lib.render_train(mpi, homs)
+    got = _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)
+    import hashlib
+    print(json.dumps({"exp": "bwd gradient sha16", "sha16": hashlib.sha256(got.cpu().numpy().tobytes()).hexdigest()[:16],
+                      "frame_sha16": hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]}))
+    fn = lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)  # noqa: E731
+    run("c4 render backward with checkpoints, 1 view", DEF, fn, 2 * P * H * W * 16 + H * W * 12, it)
 
 
 def main():
