@@ -48,9 +48,11 @@ const char *mpiv_build_id(void);
 
 /* Debug / A/B hook, never needed in production: selects a non-default kernel variant
  * by name ("render_mv", "render_pair", "render_native_lds", "render_chunk", "render_ring",
- * "render_tile", "render_vshare", "sweep_tile", "sweep_store", "sweep_dlane", "box_shrink",
- * "bwd_fallback", "bwd_margin"; "reset" restores every default; abi.hip documents the
- * values).  Process-wide; returns MPIV_ERR_ARG for an unknown name. */
+ * "render_tile", "render_vshare", "chunk_rows", "chunk_flight", "sweep_tile", "sweep_store",
+ * "sweep_dlane", "sweep_rows", "sweep_direct", "box_shrink", "bwd_fallback", "bwd_margin",
+ * "bwd_gather"; "reset" restores every default; abi.hip documents the values).  Values that
+ * select a kernel kept only for A/B measurement return MPIV_ERR_ARG from libmpiv.so (they are
+ * compiled into libmpiv_ab.so).  Process-wide; returns MPIV_ERR_ARG for an unknown name. */
 int mpiv_debug_set(const char *name, int value);
 
 /* Dry run of an entry point's production dispatch (no device memory touched, nothing
@@ -209,7 +211,10 @@ int mpiv_assemble_mpi_backward(const float *drgba, const int64_t drgba_strides[5
  * ki:     [B][9]  inverse(tgt intrinsics)         (utils.py:370 / :747)
  * proj:   [B][16] [[K_src,0],[0,0,0,1]] @ pose     (utils.py:431-438 / :750-757)
  * depths: [D] fp32
- * out:    [B,Ht,Wt,D*C] contiguous, channel d*C + c (torch.cat order, utils.py:470) */
+ * out:    [B,Ht,Wt,D*C] contiguous, channel d*C + c (torch.cat order, utils.py:470)
+ * C <= 4 reads img in place: D <= 8 by plane_sweep_direct_kernel (taps gathered per sample),
+ * more depths by plane_sweep_dlane_kernel (the tile's source footprint staged in LDS); C > 4 by
+ * the generic one-sample-per-thread kernel.  Every route writes the same bits. */
 int mpiv_plane_sweep(const float *img, const int64_t img_strides[4], int B, int Hs, int Ws, int C,
                      const float *ki, const float *proj, const float *depths, int D, int Ht, int Wt,
                      float *out, void *stream);
