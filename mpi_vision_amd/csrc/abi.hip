@@ -72,8 +72,9 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      depth-per-lane (plane_sweep_dlane_kernel)
 //   sweep_rows=4|6|8   mpiv_plane_sweep[_into]'s depth-per-lane kernel with tiles of that many
 //                      target rows (staging 3072 / 4096 / 4096 texels; 0 = automatic)
-//   bwd_gather=0|1     render backward gather: block tiles (bwd_gather_kernel) / one texel row per
-//                      wave, no block barriers (bwd_gather_wave_kernel)
+//   bwd_gather=0|1|2   render backward gather: block tiles (bwd_gather_kernel) / one texel row per
+//                      wave, no block barriers (bwd_gather_wave_kernel) / staging and texel waves
+//                      (bwd_gather_ws_kernel)
 //   chunk_flight=2|4   render_chunk_kernel with that many sub-steps' taps in flight per wave
 //                      (0 = automatic)
 //   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
@@ -118,6 +119,7 @@ bool ab_only(int o, int v) {
         case kOptChunkRows: return v == 2 || v == 4;
         case kOptChunkFlight: return v == 4;
         case kOptSweepRows: return v == 6 || v == 8;
+        case kOptBwdGather: return v == 1 || v == 2;
         default: return false;
     }
 }
@@ -704,12 +706,20 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
 #undef MPIV_CHAIN
         if (!force) {
             bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
+#if MPIV_AB  // one texel row per wave / staging and texel waves: measured slower
             if (opt(kOptBwdGather) == 1) {
                 bwd_gather_wave_kernel<<<(unsigned)gather_blocks, 256, 0, q>>>(g, hv, ws, gv, margin);
-            } else {
+            } else
+#endif
+            {
                 bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x,
                                                                                margin, ws.box);
-                bwd_gather_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
+#if MPIV_AB
+                if (opt(kOptBwdGather) == 2)
+                    bwd_gather_ws_kernel<<<(unsigned)gather_blocks, 2 * kGThreads, 0, q>>>(g, hv, ws, gv, margin);
+                else
+#endif
+                    bwd_gather_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
             }
         }
         bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force);

@@ -67,8 +67,8 @@ constexpr int kGThreads = kGTW * kGTH;
 #ifndef MPIV_GLB
 #define MPIV_GLB 5
 #endif
-#ifndef MPIV_GPF
-#define MPIV_GPF 0
+#ifndef MPIV_GLBS
+#define MPIV_GLBS 3  // bwd_gather_ws_kernel: 512-thread blocks per CU (50 KiB of LDS each)
 #endif
 #ifndef MPIV_GSI
 #define MPIV_GSI 2  // staged pixels per thread whose d samples are loaded ahead of the positions
@@ -468,47 +468,226 @@ __device__ __forceinline__ void sort8(unsigned* k) {
     cx(3, 4);
 }
 
-// One LDS-DMA instruction (render_ring.hip's): 64 lanes x 16 B from the buffer at per-lane
-// byte offsets into LDS bytes [lds, lds + 1 KiB).  Inline asm: hipcc cannot tell which LDS
-// bytes a DMA writes and would drain vmcnt(0) before every ds_read; the gather waits for its
-// own fills (vmcnt(0) before the barrier that publishes them).
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void gather_dma16(__amdgpu_buffer_rsrc_t r, int voff, unsigned lds) {
-    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(lds)
-                 : "memory", "m0");
-}
-#pragma clang diagnostic pop
-
 constexpr int kGTB = kGTW + 1;              // bucket row pitch: nw taps x in [tx0-1, tx0+kGTW-1]
 constexpr int kGNB = kGTB * (kGTH + 1);     // nw-tap buckets of a tile
 constexpr int kGBCap = 2;                   // entries per bucket list (more: the window scan)
+constexpr int kGSI = (kGCap + kGThreads - 1) / kGThreads;  // staged pixels per staging thread
+
+// One staging pass of plane p over box rows [ra, rb) x columns [bx0, bx0 + bw) by the kGThreads
+// threads t of a block (or of its staging waves): each box pixel's sample position with the
+// forward's recipe (bit-identical), its nw-tap bucket in the tile's (kGTW+1) x (kGTH+1) grid,
+// fractions and d sample into the staged arrays, and its order key pushed onto its bucket's
+// list (LDS atomic slot, <= kGBCap entries; more sets *ovf).  The pass's d samples are loaded
+// first (MPIV_GSI per thread in flight while the positions are computed: issued after each
+// pixel's position, inside the in-tile test, their latency was exposed -- 0.32 of the
+// kernel's 1.77 ms, r03).  cnt must be zero on entry.
+__device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const BwdWs& ws, const float* __restrict__ hp,
+                                                  int p, bool proven, int t, int tx0, int ty0, int bx0, int bw,
+                                                  int ra, int rb, int* s_code, float2* s_fr, float4* s_ds,
+                                                  uint2* s_bent, int* cnt, int* ovf) {
+    constexpr int TB = kGTB;
+    const int64_t HW = (int64_t)g.H * g.W;
+    const int np = (rb - ra) * bw;
+    const int gbase = (ra * g.W) >> 3;  // the pass's first 8-pixel chunk
+    // order keys hold (chunk - gbase) in 16 bits
+    if (t == 0 && (int64_t)(rb - ra + 1) * g.W >= ((int64_t)1 << 19)) *ovf = 1;
+    const float rbw = 1.0f / (float)bw;
+    const __amdgpu_buffer_rsrc_t rds = make_rsrc(ws.ds + (int64_t)p * HW, (int)(HW * 16));
+    f32x4 dsv[kGSI];
+#pragma unroll
+    for (int i = 0; i < (kGSI < MPIV_GSI ? kGSI : MPIV_GSI); ++i) {
+        const int q = t + i * kGThreads;
+        const int r = (int)(((float)q + 0.5f) * rbw);  // q / bw: q, bw <= 1024, error << 0.5/bw
+        const int off = q < np ? ((ra + r) * g.W + bx0 + (q - r * bw)) * 16 : kOOB;
+        dsv[i] = llvm_raw_buffer_load_v4f32(rds, off, 0, 0);
+    }
+    bool ovl = false;
+#pragma unroll
+    for (int i = 0; i < kGSI; ++i) {
+        const int q = t + i * kGThreads;
+        if (q >= np) break;
+        const int r = (int)(((float)q + 0.5f) * rbw);
+        const int yy = ra + r, xx = bx0 + (q - r * bw);
+        float px, py;
+        if (proven)
+            render_pos_fast<false>(hp, (float)xx, (float)yy, g, px, py);
+        else
+            render_pos<true>(hp, (float)xx, (float)yy, g, px, py);
+        const float fx0 = floorf(px), fy0 = floorf(py);
+        const float lx = fx0 - (float)(tx0 - 1), ly = fy0 - (float)(ty0 - 1);
+        const bool in = lx >= 0.0f && lx <= (float)kGTW && ly >= 0.0f && ly <= (float)kGTH;
+        const int code = in ? (int)ly * TB + (int)lx : -1;
+        s_code[q] = code;
+        if (in) {
+            s_fr[q] = make_float2(px - fx0, py - fy0);
+            if (i >= MPIV_GSI)  // past the preloaded pixels (boxes over MPIV_GSI * kGThreads pixels)
+                dsv[i] = llvm_raw_buffer_load_v4f32(rds, (yy * g.W + xx) * 16, 0, 0);
+            s_ds[q] = make_float4(dsv[i][0], dsv[i][1], dsv[i][2], dsv[i][3]);
+            const int pix = yy * g.W + xx;
+            const unsigned e = ((unsigned)((pix >> 3) - gbase) << 16) | ((unsigned)(pix & 7) << 11) | (unsigned)q;
+            const int slot = atomicAdd(&cnt[code], 1);
+            if (slot < kGBCap)
+                (slot == 0 ? s_bent[code].x : s_bent[code].y) = e;
+            else
+                ovl = true;
+        }
+    }
+    if (ovl) *ovf = 1;
+}
+
+// One texel-phase pass: texel (tx, ty)'s sum over the pass's contributors, added in the
+// reference's key order into a.  The texel is the nw / ne / sw / se tap of the samples in
+// buckets bt, bt-1, bt-row, bt-row-1: their <= 8 keys (pixel/8 relative to the pass, corner,
+// pixel%8, staged index in the low bits) go through a 4- or 8-input sorting network and are
+// added in order.  After a list overflow (magnification) the texel scans its window of the
+// inverse map instead, one 8-pixel chunk at a time.
+__device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const BwdWs& ws, int p, float margin, int tx,
+                                                  int ty, int bt, bool tin, bool ovf, const int* cnt,
+                                                  const uint2* s_bent, const int* s_code, const float2* s_fr,
+                                                  const float4* s_ds, int bx0, int bx1, int by0, int by1, int ra,
+                                                  int rb, f32x4& acc, unsigned& hits, bool& unsafe) {
+    constexpr int TB = kGTB;
+    const int bw = bx1 - bx0 + 1;
+    if (tin && !ovf) {
+        // the texel's <= 8 contributors: buckets t (nw), t-1 (ne), t-row (sw), t-row-1 (se)
+        unsigned key[8];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int b = bt - (c & 1) - (c >> 1) * TB;
+            const int n = cnt[b];
+            const uint2 e = s_bent[b];
+            key[2 * c] = n > 0 ? (e.x | ((unsigned)c << 14)) : 0xFFFFFFFFu;
+            key[2 * c + 1] = n > 1 ? (e.y | ((unsigned)c << 14)) : 0xFFFFFFFFu;
+        }
+        bool two = false;  // some bucket of this texel holds two pixels
+#pragma unroll
+        for (int c = 0; c < 4; ++c) two = two || key[2 * c + 1] != 0xFFFFFFFFu;
+        if (__any(two)) {
+            sort8(key);
+        } else {  // one pixel per bucket in the whole wave (no magnification): 4 keys
+            sort4(key[0], key[2], key[4], key[6]);
+            key[1] = key[2];
+            key[2] = key[4];
+            key[3] = key[6];
+            key[4] = key[5] = key[6] = key[7] = 0xFFFFFFFFu;
+        }
+        // Valid keys sort first.  A batch of 4 is branch-free: every lane reads (an invalid key
+        // reads staged entry 0) and a select keeps the sum of an invalid key unchanged (acc + w*d
+        // would turn -0 into +0).  The second batch (5+ contributors) is a wave-uniform branch.
+        auto batch = [&](int k0) {
+            float2 f[4];
+            float4 d[4];
+            bool v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                v[k] = key[k0 + k] != 0xFFFFFFFFu;
+                const int q = v[k] ? (int)(key[k0 + k] & 0x7FF) : 0;  // staged index: bits 0-10 (kGCap <= 2048)
+                f[k] = s_fr[q];
+                d[k] = s_ds[q];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float wx = f[k].x, ex = 1.0f - wx;
+                const float wy = f[k].y, sy = 1.0f - wy;
+                const unsigned c = key[k0 + k] >> 14;  // corner bits 14-15 (+ chunk bits above)
+                const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
+                const float a0 = acc[0] + w * d[k].x;
+                const float a1 = acc[1] + w * d[k].y;
+                const float a2 = acc[2] + w * d[k].z;
+                const float a3 = acc[3] + w * d[k].w;
+                acc[0] = v[k] ? a0 : acc[0];
+                acc[1] = v[k] ? a1 : acc[1];
+                acc[2] = v[k] ? a2 : acc[2];
+                acc[3] = v[k] ? a3 : acc[3];
+                hits += v[k] ? 1u : 0u;
+            }
+        };
+        batch(0);
+        if (__any(key[4] != 0xFFFFFFFFu)) batch(4);
+    } else if (tin) {
+        // window scan: the inverse image of the texels [tx-1, tx+1] x [ty-1, ty+1] whose samples
+        // have this texel as a tap, candidates in pixel order, the hits of one 8-pixel chunk
+        // collected in a mask (bit corner*8 + pixel%8) and added in bit order
+        const float* iv = ws.inv + (int64_t)p * 12;
+        float m[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) m[k] = iv[k];
+        int wx0 = 0, wx1 = -1, wy0 = 0, wy1 = -1;
+        float a0 = __builtin_inff(), a1 = -__builtin_inff(), b0 = __builtin_inff(), b1 = -__builtin_inff();
+        bool lbad = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float xx, yy;
+            const bool okc = inv_map(m, (float)(tx + ((c & 1) ? 1 : -1)), (float)(ty + ((c & 2) ? 1 : -1)), xx, yy);
+            lbad = lbad || !okc;
+            a0 = __builtin_fminf(a0, xx);
+            a1 = __builtin_fmaxf(a1, xx);
+            b0 = __builtin_fminf(b0, yy);
+            b1 = __builtin_fmaxf(b1, yy);
+        }
+        if (!lbad) {
+            pix_range(a0, a1, margin, bx0, bx1, wx0, wx1);
+            pix_range(b0, b1, margin, by0, by1, wy0, wy1);
+            // a wrapping 8-pixel chunk must not have window pixels in two rows: the per-row
+            // flush below would split its order
+            if ((g.W & 7) && wy1 > wy0 && wx1 >= g.W - 7 && wx0 <= 6) lbad = true;
+        }
+        if (lbad) {
+            unsafe = true;
+            wy1 = wy0 - 1;
+        }
+        const int ya = max(wy0, ra), yb = min(wy1, rb - 1);
+        for (int yy = ya; yy <= yb; ++yy) {
+            const int rowbase = (yy - ra) * bw - bx0;  // staged index of pixel (x, yy): rowbase + x
+            const int pixrow = yy * g.W;
+            int cur = -1;     // 8-pixel chunk (pixel / 8) of the hits in `msk`
+            unsigned msk = 0;
+            auto flush = [&]() {
+                while (msk) {
+                    const int b = __builtin_ctz(msk);
+                    msk &= msk - 1;
+                    const int idx = rowbase + (cur * kGridVec + (b & 7) - pixrow);
+                    const float2 f = s_fr[idx];
+                    const float4 d = s_ds[idx];
+                    const float wx = f.x, ex = 1.0f - wx;
+                    const float wy = f.y, sy = 1.0f - wy;
+                    const int c = b >> 3;
+                    const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
+                    acc[0] = acc[0] + w * d.x;
+                    acc[1] = acc[1] + w * d.y;
+                    acc[2] = acc[2] + w * d.z;
+                    acc[3] = acc[3] + w * d.w;
+                    ++hits;
+                }
+            };
+            for (int xx = wx0; xx <= wx1; ++xx) {
+                const int code = s_code[rowbase + xx];
+                const int dd = bt - code;  // 0: nw tap, 1: ne, TB: sw, TB+1: se
+                const int c = code < 0 ? -1 : dd == 0 ? 0 : dd == 1 ? 1 : dd == TB ? 2 : dd == TB + 1 ? 3 : -1;
+                if (c >= 0) {
+                    const int px = pixrow + xx;
+                    if ((px >> 3) != cur) {
+                        flush();
+                        cur = px >> 3;
+                    }
+                    msk |= 1u << (c * 8 + (px & 7));
+                }
+            }
+            flush();
+        }
+    }
+}
 
 // Grid: (texel tiles) x (groups of kGPl planes), XCD-aware (neighbouring tiles of one
 // plane group, whose pixel boxes overlap, share an XCD's L2).  The d-sample contribution
-// of pixel q to texel t: weight(corner) * d s_q, added in key order from +0.
-//
-// Per plane and pass: the box's pixels are staged (sample position -> nw-tap bucket,
-// fractions, d s) and pushed onto their bucket's list (LDS atomic slot, <= 2 entries, each
-// the pixel's order key without the corner: ((pixel/8 - pass base) << 16 | pixel%8 << 11 |
-// staged index)).  A texel is the nw / ne / sw / se tap of the samples in buckets t, t-1,
-// t-row, t-row-1: their <= 8 keys, or-ed with the corner (bits 14-15), sort into exactly the
-// reference's order (pixel/8, corner, pixel%8), and the staged index rides in the low bits.
-// A bucket with more entries (magnification: several pixels per texel) makes the block
-// scan per-texel windows of the inverse map instead (one 8-pixel chunk at a time).
+// of pixel q to texel t: weight(corner) * d s_q, added in key order from +0.  Per plane and
+// pass: one staging pass (gather_stage_pass) by all 4 waves, a barrier, one texel pass
+// (gather_texel_pass).  A texel's kGPl planes leave as one 16*kGPl-B run.
 __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
                                                          float4* __restrict__ dmpi, float margin) {
     __shared__ int s_code[kGCap];     // local nw-tap bucket of the staged pixel, -1 = none
     __shared__ float2 s_fr[kGCap];    // its bilinear fractions (px - floor px, py - floor py)
-#if MPIV_GPF
-    // d samples of a pass, double-buffered by pass parity: the next plane's first pass is
-    // copied in by LDS-DMA while this plane's texels accumulate (rows padded to 256 slots:
-    // a wave's DMA instruction writes 64 consecutive slots)
-    constexpr int kGCapD = (kGCap + 255) / 256 * 256;
-    __shared__ float4 s_dsb[2][kGCapD];
-#else
     __shared__ float4 s_ds[kGCap];    // its d sample
-#endif
     __shared__ uint2 s_bent[kGNB];    // bucket lists (kGBCap entries)
     __shared__ int s_bcnt[2][kGNB];   // bucket sizes, by pass parity (one is zeroed while the other is in use)
     __shared__ int s_ovf[2];          // a list overflowed in this pass
@@ -521,45 +700,12 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTH;
     const int tx = tx0 + (threadIdx.x & (kWave - 1)), ty = ty0 + (threadIdx.x >> 6);
     const bool tin = tx < g.W && ty < g.H;
-    const int64_t HW = (int64_t)g.H * g.W;
     const int bt = (ty - ty0 + 1) * TB + (tx - tx0 + 1);  // bucket of the texel as an nw tap
     for (int b = threadIdx.x; b < 2 * kGNB; b += kGThreads) (&s_bcnt[0][0])[b] = 0;
     if (threadIdx.x < 2) s_ovf[threadIdx.x] = 0;
     int par = 0;
     unsigned hits = 0;    // (texel, contributor) pairs found by this thread
     bool unsafe = false;  // a plane this block could not order (the view goes to the fallback)
-#if MPIV_GPF
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
-    // copy the d samples of plane p's rows [ra, ra + n/bw) of box columns [bx0, bx0 + bw) into
-    // s_dsb[buf] (staged index q = row * bw + column), 64 per wave instruction
-    auto dma_pass = [&](int p, int bx0_, int bw_, int ra_, int n, int buf) {
-        const __amdgpu_buffer_rsrc_t r = make_rsrc(ws.ds + (int64_t)p * HW, (int)(HW * 16));
-        const float rbw = 1.0f / (float)bw_;
-        const unsigned base = (unsigned)(uintptr_t)&s_dsb[buf][0];
-        for (int q0 = wave * kWave; q0 < n; q0 += kGThreads) {
-            const int q = q0 + lane;
-            int rr = (int)(((float)q + 0.5f) * rbw);  // q / bw (q < 2048: exact after the +0.5)
-            const int off = q < n ? ((ra_ + rr) * g.W + bx0_ + (q - rr * bw_)) * 16 : kOOB;
-            gather_dma16(r, off, __builtin_amdgcn_readfirstlane(base + (unsigned)q0 * 16u));
-        }
-    };
-    // a plane whose box fits one pass gets its d samples prefetched during the previous
-    // plane's texel phase (pf_plane: the plane whose first pass sits in s_dsb[par ^ 1])
-    auto one_pass_box = [&](int p, int4& b) {
-        b = ws.box[(int64_t)p * ntiles + tile];
-        const int bw_ = b.y - b.x + 1, bh_ = (b.w & ~kBoxProven) - b.z + 1;
-        return b.x != -2 && bw_ > 0 && bh_ > 0 && bh_ * bw_ <= kGCap;
-    };
-    int pf_plane = -1;
-    {
-        int4 b;
-        if (p0 < g.P && one_pass_box(p0, b)) {
-            dma_pass(p0, b.x, b.y - b.x + 1, b.z, (b.y - b.x + 1) * ((b.w & ~kBoxProven) - b.z + 1), par);
-            pf_plane = p0;
-        }
-    }
-    pf_plane = pf_plane == p0 ? -2 : -1;  // -2: plane p0's first pass already sits in s_dsb[par]
-#endif
     f32x4 acc[kGPl];
 #pragma unroll
     for (int jj = 0; jj < kGPl; ++jj) {
@@ -579,224 +725,14 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
         const float* hp = homs + (int64_t)p * 9;
         for (int ra = by0; ra <= by1; ra += rpp) {
             const int rb = min(by1 + 1, ra + rpp);
-            const int np = (rb - ra) * bw;
-            const int gbase = (ra * g.W) >> 3;  // the pass's first 8-pixel chunk
-#if MPIV_GPF
-            float4* s_ds = s_dsb[par];
-            if (!(ra == by0 && pf_plane == -2)) {
-                __syncthreads();  // the previous pass's readers of this buffer are done
-                dma_pass(p, bx0, bw, ra, np, par);
-            }
-            pf_plane = -1;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's fills of s_ds have landed
-#endif
-            __syncthreads();  // the previous pass's readers are done (and, MPIV_GPF, every wave's fills)
-            {
-                int* cnt = s_bcnt[par];
-                // order keys hold (chunk - gbase) in 16 bits
-                if (threadIdx.x == 0 && (int64_t)(rb - ra + 1) * g.W >= ((int64_t)1 << 19)) s_ovf[par] = 1;
-                const float rbw = 1.0f / (float)bw;
-                constexpr int kSI = (kGCap + kGThreads - 1) / kGThreads;  // staged pixels per thread
-#if !MPIV_GPF
-                // the pass's d samples first: one buffer load per staged pixel, all in flight while
-                // the sample positions are computed (issued after its pixel's position, inside the
-                // in-tile test, each load's latency was exposed: 0.32 of the kernel's 1.77 ms, r03)
-                const __amdgpu_buffer_rsrc_t rds = make_rsrc(ws.ds + (int64_t)p * HW, (int)(HW * 16));
-                f32x4 dsv[kSI];
-#pragma unroll
-                for (int i = 0; i < (kSI < MPIV_GSI ? kSI : MPIV_GSI); ++i) {
-                    const int q = (int)threadIdx.x + i * kGThreads;
-                    const int r = (int)(((float)q + 0.5f) * rbw);  // q / bw: q, bw <= 1024, error << 0.5/bw
-                    const int off = q < np ? ((ra + r) * g.W + bx0 + (q - r * bw)) * 16 : kOOB;
-                    dsv[i] = llvm_raw_buffer_load_v4f32(rds, off, 0, 0);
-                }
-#endif
-#pragma unroll
-                for (int i = 0; i < kSI; ++i) {
-                    const int q = (int)threadIdx.x + i * kGThreads;
-                    if (q >= np) break;
-                    const int r = (int)(((float)q + 0.5f) * rbw);  // q / bw: q, bw <= 1024, error << 0.5/bw
-                    const int yy = ra + r, xx = bx0 + (q - r * bw);
-                    float px, py;
-                    if (proven)
-                        render_pos_fast<false>(hp, (float)xx, (float)yy, g, px, py);
-                    else
-                        render_pos<true>(hp, (float)xx, (float)yy, g, px, py);
-                    const float fx0 = floorf(px), fy0 = floorf(py);
-                    const float lx = fx0 - (float)(tx0 - 1), ly = fy0 - (float)(ty0 - 1);
-                    const bool in = lx >= 0.0f && lx <= (float)kGTW && ly >= 0.0f && ly <= (float)kGTH;
-                    const int code = in ? (int)ly * TB + (int)lx : -1;
-                    s_code[q] = code;
-                    if (in) {
-                        s_fr[q] = make_float2(px - fx0, py - fy0);
-#if !MPIV_GPF
-                        if (i >= MPIV_GSI)  // past the preloaded pixels (boxes over MPIV_GSI * 256 pixels)
-                            dsv[i] = llvm_raw_buffer_load_v4f32(rds, (yy * g.W + xx) * 16, 0, 0);
-                        s_ds[q] = make_float4(dsv[i][0], dsv[i][1], dsv[i][2], dsv[i][3]);
-#endif
-                        const int pix = yy * g.W + xx;
-                        const unsigned e = ((unsigned)((pix >> 3) - gbase) << 16) | ((unsigned)(pix & 7) << 11) |
-                                           (unsigned)q;
-                        const int slot = atomicAdd(&cnt[code], 1);
-                        if (slot < kGBCap)
-                            (slot == 0 ? s_bent[code].x : s_bent[code].y) = e;
-                        else
-                            s_ovf[par] = 1;
-                    }
-                }
-                for (int b = threadIdx.x; b < kGNB; b += kGThreads) s_bcnt[par ^ 1][b] = 0;  // for the next pass
-                if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
-            }
+            __syncthreads();  // the previous pass's readers are done
+            gather_stage_pass(g, ws, hp, p, proven, (int)threadIdx.x, tx0, ty0, bx0, bw, ra, rb, s_code, s_fr, s_ds,
+                              s_bent, s_bcnt[par], &s_ovf[par]);
+            for (int b = threadIdx.x; b < kGNB; b += kGThreads) s_bcnt[par ^ 1][b] = 0;  // for the next pass
+            if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
             __syncthreads();
-#if MPIV_GPF
-            // the last pass of this plane: prefetch the next plane's first pass into the other
-            // buffer (last read by the previous pass, whose readers finished before this pass's
-            // first barrier)
-            if (rb > by1 && jj + 1 < kGPl && p + 1 < g.P) {
-                int4 b;
-                if (one_pass_box(p + 1, b)) {
-                    dma_pass(p + 1, b.x, b.y - b.x + 1, b.z, (b.y - b.x + 1) * ((b.w & ~kBoxProven) - b.z + 1),
-                             par ^ 1);
-                    pf_plane = -2;
-                }
-            }
-#endif
-            const bool ovf = s_ovf[par] != 0;
-            if (tin && !ovf) {
-                // the texel's <= 8 contributors: buckets t (nw), t-1 (ne), t-row (sw), t-row-1 (se)
-                const int* cnt = s_bcnt[par];
-                unsigned key[8];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int b = bt - (c & 1) - (c >> 1) * TB;
-                    const int n = cnt[b];
-                    const uint2 e = s_bent[b];
-                    key[2 * c] = n > 0 ? (e.x | ((unsigned)c << 14)) : 0xFFFFFFFFu;
-                    key[2 * c + 1] = n > 1 ? (e.y | ((unsigned)c << 14)) : 0xFFFFFFFFu;
-                }
-                bool two = false;  // some bucket of this texel holds two pixels
-#pragma unroll
-                for (int c = 0; c < 4; ++c) two = two || key[2 * c + 1] != 0xFFFFFFFFu;
-                if (__any(two)) {
-                    sort8(key);
-                } else {  // one pixel per bucket in the whole wave (no magnification): 4 keys
-                    sort4(key[0], key[2], key[4], key[6]);
-                    key[1] = key[2];
-                    key[2] = key[4];
-                    key[3] = key[6];
-                    key[4] = key[5] = key[6] = key[7] = 0xFFFFFFFFu;
-                }
-                // Valid keys sort first.  A batch of 4 is branch-free: every lane reads (an
-                // invalid key reads staged entry 0) and a select keeps the sum of an invalid
-                // key unchanged (acc + w*d would turn -0 into +0).  Per-lane ifs here cost an
-                // s_and_saveexec / s_cbranch / s_or_b64 exec triple each: PMC r03 counted 408M
-                // scalar instructions per launch beside 727M VALU, the CU's one scalar unit a
-                // co-limiter.  The second batch (5+ contributors: magnification) is a
-                // wave-uniform branch.
-                auto batch = [&](int k0) {
-                    float2 f[4];
-                    float4 d[4];
-                    bool v[4];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        v[k] = key[k0 + k] != 0xFFFFFFFFu;
-                        const int q = v[k] ? (int)(key[k0 + k] & 0x7FF) : 0;  // staged index: bits 0-10 (kGCap <= 2048)
-                        f[k] = s_fr[q];
-                        d[k] = s_ds[q];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const float wx = f[k].x, ex = 1.0f - wx;
-                        const float wy = f[k].y, sy = 1.0f - wy;
-                        const unsigned c = key[k0 + k] >> 14;  // corner bits 14-15 (+ chunk bits above)
-                        const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
-                        const float a0 = acc[jj][0] + w * d[k].x;
-                        const float a1 = acc[jj][1] + w * d[k].y;
-                        const float a2 = acc[jj][2] + w * d[k].z;
-                        const float a3 = acc[jj][3] + w * d[k].w;
-                        acc[jj][0] = v[k] ? a0 : acc[jj][0];
-                        acc[jj][1] = v[k] ? a1 : acc[jj][1];
-                        acc[jj][2] = v[k] ? a2 : acc[jj][2];
-                        acc[jj][3] = v[k] ? a3 : acc[jj][3];
-                        hits += v[k] ? 1u : 0u;
-                    }
-                };
-                batch(0);
-                if (__any(key[4] != 0xFFFFFFFFu)) batch(4);
-            } else if (tin) {
-                // window scan: the inverse image of the texels [tx-1, tx+1] x [ty-1, ty+1]
-                // whose samples have this texel as a tap, candidates in pixel order, the hits
-                // of one 8-pixel chunk collected in a mask (bit corner*8 + pixel%8) and added
-                // in bit order
-                const float* iv = ws.inv + (int64_t)p * 12;
-                float m[9];
-#pragma unroll
-                for (int k = 0; k < 9; ++k) m[k] = iv[k];
-                int wx0 = 0, wx1 = -1, wy0 = 0, wy1 = -1;
-                float a0 = __builtin_inff(), a1 = -__builtin_inff(), b0 = __builtin_inff(), b1 = -__builtin_inff();
-                bool lbad = false;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    float xx, yy;
-                    const bool okc =
-                        inv_map(m, (float)(tx + ((c & 1) ? 1 : -1)), (float)(ty + ((c & 2) ? 1 : -1)), xx, yy);
-                    lbad = lbad || !okc;
-                    a0 = __builtin_fminf(a0, xx);
-                    a1 = __builtin_fmaxf(a1, xx);
-                    b0 = __builtin_fminf(b0, yy);
-                    b1 = __builtin_fmaxf(b1, yy);
-                }
-                if (!lbad) {
-                    pix_range(a0, a1, margin, bx0, bx1, wx0, wx1);
-                    pix_range(b0, b1, margin, by0, by1, wy0, wy1);
-                    // a wrapping 8-pixel chunk must not have window pixels in two rows: the
-                    // per-row flush below would split its order
-                    if ((g.W & 7) && wy1 > wy0 && wx1 >= g.W - 7 && wx0 <= 6) lbad = true;
-                }
-                if (lbad) {
-                    unsafe = true;
-                    wy1 = wy0 - 1;
-                }
-                const int ya = max(wy0, ra), yb = min(wy1, rb - 1);
-                for (int yy = ya; yy <= yb; ++yy) {
-                    const int rowbase = (yy - ra) * bw - bx0;  // staged index of pixel (x, yy): rowbase + x
-                    const int pixrow = yy * g.W;
-                    int cur = -1;     // 8-pixel chunk (pixel / 8) of the hits in `msk`
-                    unsigned msk = 0;
-                    auto flush = [&]() {
-                        while (msk) {
-                            const int b = __builtin_ctz(msk);
-                            msk &= msk - 1;
-                            const int idx = rowbase + (cur * kGridVec + (b & 7) - pixrow);
-                            const float2 f = s_fr[idx];
-                            const float4 d = s_ds[idx];
-                            const float wx = f.x, ex = 1.0f - wx;
-                            const float wy = f.y, sy = 1.0f - wy;
-                            const int c = b >> 3;
-                            const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
-                            acc[jj][0] = acc[jj][0] + w * d.x;
-                            acc[jj][1] = acc[jj][1] + w * d.y;
-                            acc[jj][2] = acc[jj][2] + w * d.z;
-                            acc[jj][3] = acc[jj][3] + w * d.w;
-                            ++hits;
-                        }
-                    };
-                    for (int xx = wx0; xx <= wx1; ++xx) {
-                        const int code = s_code[rowbase + xx];
-                        const int dd = bt - code;  // 0: nw tap, 1: ne, TB: sw, TB+1: se
-                        const int c = code < 0 ? -1 : dd == 0 ? 0 : dd == 1 ? 1 : dd == TB ? 2 : dd == TB + 1 ? 3 : -1;
-                        if (c >= 0) {
-                            const int px = pixrow + xx;
-                            if ((px >> 3) != cur) {
-                                flush();
-                                cur = px >> 3;
-                            }
-                            msk |= 1u << (c * 8 + (px & 7));
-                        }
-                    }
-                    flush();
-                }
-            }
+            gather_texel_pass(g, ws, p, margin, tx, ty, bt, tin, s_ovf[par] != 0, s_bcnt[par], s_bent, s_code, s_fr,
+                              s_ds, bx0, bx1, by0, by1, ra, rb, acc[jj], hits, unsafe);
             par ^= 1;
         }
     }
@@ -805,6 +741,127 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     const unsigned long long tot = (unsigned long long)hits + (__any(unsafe) ? kUnsafe : 0ull);
     if ((threadIdx.x & (kWave - 1)) == 0 && tot) atomicAdd(&ws.found[blockIdx.x % kCtrSlots], tot);
     if (tin) {  // the texel's kGPl planes: one 16*kGPl-B run
+        float4* o = dmpi + ((int64_t)ty * g.W + tx) * g.P + p0;
+#pragma unroll
+        for (int jj = 0; jj < kGPl; ++jj)
+            if (p0 + jj < g.P) o[jj] = make_float4(acc[jj][0], acc[jj][1], acc[jj][2], acc[jj][3]);
+    }
+}
+
+#if MPIV_AB  // A/B variants of the gather (libmpiv_ab.so): measured slower, DESIGN.md §8
+// ---- 2a'. gather with staging and texel waves (bwd_gather=2) ---------------------------
+// bwd_gather_kernel alternates a memory phase (the staging pass: d-sample loads, positions)
+// and a compute phase (the sorted per-texel sums) behind block barriers, and the two barely
+// overlap (r03 diagnostics: 0.82 ms of memory phase alone, ~0.9 ms of texel phase on top).
+// Here a block of 8 waves splits the roles: waves 0-3 stage pass i+1 into one buffer while
+// waves 4-7 sum pass i from the other, one barrier per pass.  Both roles walk the same pass
+// sequence (planes p0.., box row passes), the texel waves one pass behind; bucket sizes are
+// triple-buffered (filled for pass i+1, read for pass i, zeroed for pass i+2).
+__global__ __launch_bounds__(2 * kGThreads, MPIV_GLBS) void bwd_gather_ws_kernel(RenderGeom g,
+                                                                          const float* __restrict__ homs, BwdWs ws,
+                                                                          float4* __restrict__ dmpi, float margin) {
+    __shared__ int s_code[2][kGCap];
+    __shared__ float2 s_fr[2][kGCap];
+    __shared__ float4 s_ds[2][kGCap];
+    __shared__ uint2 s_bent[2][kGNB];
+    __shared__ int s_bcnt[3][kGNB];
+    __shared__ int s_ovf[3];
+    constexpr int TB = kGTB;
+    const int tiles_x = (g.W + kGTW - 1) / kGTW;
+    const int ntiles = tiles_x * ((g.H + kGTH - 1) / kGTH);
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int ngroups = (g.P + kGPl - 1) / kGPl;
+    const int tile = lb / ngroups, p0 = (lb % ngroups) * kGPl;
+    const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTH;
+    const bool stager = threadIdx.x < kGThreads;  // wave-uniform
+    const int t = (int)threadIdx.x & (kGThreads - 1);
+    for (int b = threadIdx.x; b < 3 * kGNB; b += 2 * kGThreads) (&s_bcnt[0][0])[b] = 0;
+    if (threadIdx.x < 3) s_ovf[threadIdx.x] = 0;
+    // the pass sequence: (plane jj, box rows [ra, rb)); seek() finds the first pass at or after
+    // (jj, ra) (ra = INT_MIN: plane jj's first), skipping planes without pixels; the texel role
+    // notes planes it cannot order (bad boxes) as it passes them
+    struct Pass {
+        int jj, bx0, bx1, by0, by1, ra, rb;
+        bool proven;
+    };
+    bool unsafe = false;
+    auto seek = [&](int jj, int ra, Pass& ps) -> bool {
+        for (; jj < kGPl; ++jj, ra = INT_MIN) {
+            const int p = p0 + jj;
+            if (p >= g.P) return false;
+            const int4 bx = ws.box[(int64_t)p * ntiles + tile];  // bwd_box_kernel
+            if (bx.x == -2) {
+                if (ra == INT_MIN) unsafe = true;
+                continue;
+            }
+            const int by1 = bx.w & ~kBoxProven;
+            const int bw = bx.y - bx.x + 1;
+            const int start = ra == INT_MIN ? bx.z : ra;
+            if (bw <= 0 || by1 < bx.z || start > by1) continue;
+            ps.jj = jj;
+            ps.bx0 = bx.x;
+            ps.bx1 = bx.y;
+            ps.by0 = bx.z;
+            ps.by1 = by1;
+            ps.ra = start;
+            ps.rb = min(by1 + 1, start + kGCap / bw);
+            ps.proven = (bx.w & kBoxProven) != 0;
+            return true;
+        }
+        return false;
+    };
+    __syncthreads();  // counts zeroed
+    Pass cur;
+    bool have = seek(0, INT_MIN, cur);
+    if (stager) {
+        if (have)
+            gather_stage_pass(g, ws, homs + (int64_t)(p0 + cur.jj) * 9, p0 + cur.jj, cur.proven, t, tx0, ty0, cur.bx0,
+                              cur.bx1 - cur.bx0 + 1, cur.ra, cur.rb, s_code[0], s_fr[0], s_ds[0], s_bent[0],
+                              s_bcnt[0], &s_ovf[0]);
+        __syncthreads();
+        for (int i = 0; have; ++i) {
+            Pass nxt;
+            have = seek(cur.jj, cur.rb, nxt);
+            if (have)
+                gather_stage_pass(g, ws, homs + (int64_t)(p0 + nxt.jj) * 9, p0 + nxt.jj, nxt.proven, t, tx0, ty0,
+                                  nxt.bx0, nxt.bx1 - nxt.bx0 + 1, nxt.ra, nxt.rb, s_code[(i + 1) & 1],
+                                  s_fr[(i + 1) & 1], s_ds[(i + 1) & 1], s_bent[(i + 1) & 1], s_bcnt[(i + 1) % 3],
+                                  &s_ovf[(i + 1) % 3]);
+            for (int b = t; b < kGNB; b += kGThreads) s_bcnt[(i + 2) % 3][b] = 0;  // for pass i + 2
+            if (t == 0) s_ovf[(i + 2) % 3] = 0;
+            __syncthreads();
+            cur = nxt;
+        }
+        return;  // every barrier of the texel waves has been matched
+    }
+    // texel waves: planes unrolled (static accumulator per plane), passes in sequence order
+    const int tx = tx0 + (t & (kWave - 1)), ty = ty0 + (t >> 6);
+    const bool tin = tx < g.W && ty < g.H;
+    const int bt = (ty - ty0 + 1) * TB + (tx - tx0 + 1);
+    unsigned hits = 0;
+    f32x4 acc[kGPl];
+#pragma unroll
+    for (int jj = 0; jj < kGPl; ++jj) acc[jj] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    __syncthreads();  // pass 0 staged
+    int i = 0;
+#pragma unroll
+    for (int jj = 0; jj < kGPl; ++jj) {
+        while (have && cur.jj == jj) {
+            gather_texel_pass(g, ws, p0 + jj, margin, tx, ty, bt, tin, s_ovf[i % 3] != 0, s_bcnt[i % 3], s_bent[i & 1],
+                              s_code[i & 1], s_fr[i & 1], s_ds[i & 1], cur.bx0, cur.bx1, cur.by0, cur.by1, cur.ra,
+                              cur.rb, acc[jj], hits, unsafe);
+            Pass nxt;
+            have = seek(cur.jj, cur.rb, nxt);
+            __syncthreads();  // pass i + 1 staged; pass i's buffers free
+            cur = nxt;
+            ++i;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) hits += __shfl_xor(hits, off);
+    const unsigned long long tot = (unsigned long long)hits + (__any(unsafe) ? kUnsafe : 0ull);
+    if ((t & (kWave - 1)) == 0 && tot) atomicAdd(&ws.found[blockIdx.x % kCtrSlots], tot);
+    if (tin) {
         float4* o = dmpi + ((int64_t)ty * g.W + tx) * g.P + p0;
 #pragma unroll
         for (int jj = 0; jj < kGPl; ++jj)
@@ -1067,6 +1124,8 @@ __global__ __launch_bounds__(256, MPIV_GLBW) void bwd_gather_wave_kernel(RenderG
             if (p0 + jj < g.P) o[jj] = make_float4(acc[jj][0], acc[jj][1], acc[jj][2], acc[jj][3]);
     }
 }
+
+#endif  // MPIV_AB
 
 // ---- 3. check: found == truth, else the fallback runs; counters reset for the next view
 __global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force) {

@@ -860,6 +860,9 @@ __device__ __forceinline__ void sweep_fill_box(float4* __restrict__ s_src, __amd
 //    SIMD instead of 4.
 // The ray of the pixel is the same in every lane (a wave-uniform VALU value).  Per sample the
 // arithmetic is the same sequence as plane_sweep_lds_kernel's (bit-identical output).
+#ifndef MPIV_SWNT
+#define MPIV_SWNT 1  // depth-per-lane sweep: nontemporal volume stores (A/B flag)
+#endif
 constexpr int kDLThreads = 512;
 constexpr int kDLWaves = kDLThreads / kWave;
 #ifndef MPIV_DLPIX
@@ -1095,7 +1098,8 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
                 f32xC v;
 #pragma unroll
                 for (int c = 0; c < C; ++c) v[c] = s[j][c];
-                if (vec) __builtin_nontemporal_store(v, reinterpret_cast<f32xC*>(o[j]));
+                if (vec && MPIV_SWNT) __builtin_nontemporal_store(v, reinterpret_cast<f32xC*>(o[j]));
+                else if (vec) *reinterpret_cast<f32xC*>(o[j]) = v;
                 else {
 #pragma unroll
                     for (int c = 0; c < C; ++c) o[j][c] = v[c];

@@ -31,9 +31,10 @@ def grad():
 # pipeline for every view (bwd_fallback=1); "miss": windows 1.5 px too small
 # (bwd_margin=-96), so the tile gather misses contributors and the count must send every
 # such view to the fallback; "wave" / "wave_miss": the same with the one-row-per-wave gather
-# (bwd_gather=1) -- all bit-exact.
+# (bwd_gather=1); "ws" / "ws_miss": with staging and texel waves (bwd_gather=2) -- all bit-exact.
 BWD_MODES = {"tile": {}, "fallback": {"bwd_fallback": 1}, "miss": {"bwd_margin": -96},
-             "wave": {"bwd_gather": 1}, "wave_miss": {"bwd_gather": 1, "bwd_margin": -96}}
+             "wave": {"bwd_gather": 1}, "wave_miss": {"bwd_gather": 1, "bwd_margin": -96},
+             "ws": {"bwd_gather": 2}, "ws_miss": {"bwd_gather": 2, "bwd_margin": -96}}
 
 
 @pytest.fixture(params=list(BWD_MODES))
@@ -138,7 +139,7 @@ def test_backward_medium_case_vs_oracle(dev, bwd_mode):
     want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
     got, flag = _backward_flag(mpi.to(dev), homs, dout.to(dev), dev)
     assert_bits(got, want, "medium case")
-    assert flag == (0 if bwd_mode in ("tile", "wave") else 1)
+    assert flag == (0 if bwd_mode in ("tile", "wave", "ws") else 1)
 
 
 def test_backward_deterministic(grad, dev):
@@ -244,10 +245,11 @@ def test_backward_full_size_tile_equals_fallback(cfg, dev, kopts):
     dout = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
     fast, flag = _backward_flag(mpi, homs, dout, dev)
     assert flag == 0
-    kopts(bwd_gather=1)  # the one-row-per-wave gather
-    wave, flag = _backward_flag(mpi, homs, dout, dev)
-    assert flag == 0
-    assert torch.equal(fast.view(torch.int32), wave.view(torch.int32))
+    for variant in (1, 2):  # the one-row-per-wave gather; staging and texel waves
+        kopts(bwd_gather=variant)
+        other, flag = _backward_flag(mpi, homs, dout, dev)
+        assert flag == 0
+        assert torch.equal(fast.view(torch.int32), other.view(torch.int32)), variant
     kopts(bwd_gather=0, bwd_fallback=1)
     slow, flag = _backward_flag(mpi, homs, dout, dev)
     assert flag == 1

@@ -40,13 +40,30 @@ def timed(fn, iters, warmup=3):
     return statistics.median(ts), min(ts)
 
 
+def span(fn, iters, warmup=3):
+    """Back-to-back launches: device time of `iters` launches between two events / iters (a
+    write-heavy kernel's drain then lands in the next launch, as in bench.py's legs)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(iters):
+        fn()
+    b.record(s)
+    b.synchronize()
+    return a.elapsed_time(b) / iters
+
+
 def run(name, variants, fn, alg, iters, passes=2):
     for p in range(passes):
         for label, opts in variants:
             with _lib.debug(**opts):
                 ms, mn = timed(fn, iters)
+                b2b = span(fn, iters)
             print(json.dumps({"exp": name, "variant": label, "pass": p, "ms": round(ms, 4), "ms_min": round(mn, 4),
-                              "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK, 4)}), flush=True)
+                              "ms_b2b": round(b2b, 4), "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK, 4)}), flush=True)
 
 
 def c4_mpi(dev, B=1):
@@ -117,7 +134,7 @@ def sweep(dev, it):
         del out
 
 
-GATHER = [("block", {}), ("wave", {"bwd_gather": 1})]  # noqa: E501
+GATHER = [("block", {}), ("ws", {"bwd_gather": 2})]
 
 
 def bwdg(dev, it):
@@ -160,6 +177,22 @@ def sw10(dev, it):
         run(f"c3 sources -> {D} planes (mpiv_plane_sweep)", [("lds", {"sweep_direct": -1}), ("direct", {"sweep_direct": 1})],
             raw, alg, it)
         del out
+
+
+def c3(dev, it):
+    """BASELINE config 3 through mpiv_plane_sweep (the default route), isolated and back to back."""
+    c = configs.config3()
+    S, H, W, D = c["S"], c["H"], c["W"], c["D"]
+    g = torch.Generator(device=dev).manual_seed(1)
+    img = torch.rand((S, H, W, 3), generator=g, device=dev)
+    K = configs.f32([c["K"]] * S)
+    ki, proj = _host.psv_matrices(K, K, configs.f32(c["poses"]))
+    ki, proj = ki.to(dev), proj.to(dev)
+    d = configs.f32(c["depths"]).to(dev)
+    out = torch.empty((S, H, W, D * 3), device=dev)
+    fn = lambda: _lib._call("mpiv_plane_sweep", img, _lib._strides(img), S, H, W, 3, ki, proj, d, D, H, W,  # noqa: E731
+                            out, _lib._stream(dev))
+    run("c3 (mpiv_plane_sweep)", [("default", {})], fn, S * H * W * 12 + S * D * H * W * 12, it)
 
 
 DEF = [("default", {})]
