@@ -219,8 +219,11 @@ def set_debug(**opts):
                 L.mpiv_debug_set(b"reset", 0)
                 raise ValueError(msg)
             need_ab = True
-    if need_ab:
-        L.mpiv_debug_set(b"reset", 0)
+    if need_ab or (_override is not None and _override is not L):
+        # the A/B flavour runs (now, or still from an earlier call): the options go to it too,
+        # so successive calls accumulate on whichever library serves the entry points
+        if need_ab:
+            L.mpiv_debug_set(b"reset", 0)
         A = load_ab()
         for k, v in opts.items():
             if A.mpiv_debug_set(k.encode(), int(v)) != 0:

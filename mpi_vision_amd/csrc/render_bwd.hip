@@ -477,14 +477,14 @@ constexpr int kGSI = (kGCap + kGThreads - 1) / kGThreads;  // staged pixels per 
 // threads t of a block (or of its staging waves): each box pixel's sample position with the
 // forward's recipe (bit-identical), its nw-tap bucket in the tile's (kGTW+1) x (kGTH+1) grid,
 // fractions and d sample into the staged arrays, and its order key pushed onto its bucket's
-// list (LDS atomic slot, <= kGBCap entries; more sets *ovf).  The pass's d samples are loaded
-// first (MPIV_GSI per thread in flight while the positions are computed: issued after each
-// pixel's position, inside the in-tile test, their latency was exposed -- 0.32 of the
-// kernel's 1.77 ms, r03).  cnt must be zero on entry.
+// list (two entries per bucket, ~0 = free, claimed by LDS compare-and-swap; a third sets
+// *ovf).  The pass's d samples are loaded first (MPIV_GSI per thread in flight while the
+// positions are computed: issued after each pixel's position, inside the in-tile test, their
+// latency was exposed -- 0.32 of the kernel's 1.77 ms, r03).  s_ent must be all ~0 on entry.
 __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const BwdWs& ws, const float* __restrict__ hp,
                                                   int p, bool proven, int t, int tx0, int ty0, int bx0, int bw,
-                                                  int ra, int rb, int* s_code, float2* s_fr, float4* s_ds,
-                                                  uint2* s_bent, int* cnt, int* ovf) {
+                                                  int ra, int rb, int* s_code, f32x4* s_w, float4* s_ds,
+                                                  unsigned* s_ent, int* ovf) {
     constexpr int TB = kGTB;
     const int64_t HW = (int64_t)g.H * g.W;
     const int np = (rb - ra) * bw;
@@ -519,17 +519,20 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
         const int code = in ? (int)ly * TB + (int)lx : -1;
         s_code[q] = code;
         if (in) {
-            s_fr[q] = make_float2(px - fx0, py - fy0);
+            // the four bilinear weights (issue_taps_padded's products, corner order nw, ne, sw, se):
+            // the texel pass reads the one of its corner instead of re-deriving it from fractions
+            const float wx = px - fx0, ex = 1.0f - wx;
+            const float wy = py - fy0, sy = 1.0f - wy;
+            s_w[q] = f32x4{sy * ex, sy * wx, wy * ex, wy * wx};
             if (i >= MPIV_GSI)  // past the preloaded pixels (boxes over MPIV_GSI * kGThreads pixels)
                 dsv[i] = llvm_raw_buffer_load_v4f32(rds, (yy * g.W + xx) * 16, 0, 0);
             s_ds[q] = make_float4(dsv[i][0], dsv[i][1], dsv[i][2], dsv[i][3]);
             const int pix = yy * g.W + xx;
+            // order key (never ~0: bits 14-15 are clear) into the first free slot of the bucket
+            // (~0 = free; any order: the texel pass sorts)
             const unsigned e = ((unsigned)((pix >> 3) - gbase) << 16) | ((unsigned)(pix & 7) << 11) | (unsigned)q;
-            const int slot = atomicAdd(&cnt[code], 1);
-            if (slot < kGBCap)
-                (slot == 0 ? s_bent[code].x : s_bent[code].y) = e;
-            else
-                ovl = true;
+            unsigned* ent = s_ent + 2 * code;
+            if (atomicCAS(ent, ~0u, e) != ~0u && atomicCAS(ent + 1, ~0u, e) != ~0u) ovl = true;
         }
     }
     if (ovl) *ovf = 1;
@@ -542,22 +545,21 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
 // added in order.  After a list overflow (magnification) the texel scans its window of the
 // inverse map instead, one 8-pixel chunk at a time.
 __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const BwdWs& ws, int p, float margin, int tx,
-                                                  int ty, int bt, bool tin, bool ovf, const int* cnt,
-                                                  const uint2* s_bent, const int* s_code, const float2* s_fr,
-                                                  const float4* s_ds, int bx0, int bx1, int by0, int by1, int ra,
-                                                  int rb, f32x4& acc, unsigned& hits, bool& unsafe) {
+                                                  int ty, int bt, bool tin, bool ovf, const unsigned* s_ent,
+                                                  const int* s_code, const f32x4* s_w, const float4* s_ds, int bx0,
+                                                  int bx1, int by0, int by1, int ra, int rb, f32x4& acc,
+                                                  unsigned& hits, bool& unsafe) {
     constexpr int TB = kGTB;
     const int bw = bx1 - bx0 + 1;
     if (tin && !ovf) {
         // the texel's <= 8 contributors: buckets t (nw), t-1 (ne), t-row (sw), t-row-1 (se)
-        unsigned key[8];
+        unsigned key[8];  // a free slot (~0) stays ~0 after the corner is or-ed in
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const int b = bt - (c & 1) - (c >> 1) * TB;
-            const int n = cnt[b];
-            const uint2 e = s_bent[b];
-            key[2 * c] = n > 0 ? (e.x | ((unsigned)c << 14)) : 0xFFFFFFFFu;
-            key[2 * c + 1] = n > 1 ? (e.y | ((unsigned)c << 14)) : 0xFFFFFFFFu;
+            const uint2 e = reinterpret_cast<const uint2*>(s_ent)[b];
+            key[2 * c] = e.x | ((unsigned)c << 14);
+            key[2 * c + 1] = e.y | ((unsigned)c << 14);
         }
         bool two = false;  // some bucket of this texel holds two pixels
 #pragma unroll
@@ -571,35 +573,29 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
             key[3] = key[6];
             key[4] = key[5] = key[6] = key[7] = 0xFFFFFFFFu;
         }
-        // Valid keys sort first.  A batch of 4 is branch-free: every lane reads (an invalid key
-        // reads staged entry 0) and a select keeps the sum of an invalid key unchanged (acc + w*d
-        // would turn -0 into +0).  The second batch (5+ contributors) is a wave-uniform branch.
+        // Valid keys sort first.  A batch of 4 is branch-free and select-free: an invalid key
+        // (~0) reads the zero slot kGCap (weight 0, d sample 0), and adding its +-0 leaves the sum's
+        // bits unchanged -- a sum started at +0 is never -0 under round-to-nearest (x + -x and
+        // +0 + -0 both give +0), and inf / NaN stay as they are.  The second batch (5+
+        // contributors) is a wave-uniform branch.
+        const float* s_wf = reinterpret_cast<const float*>(s_w);
         auto batch = [&](int k0) {
-            float2 f[4];
+            float w[4];
             float4 d[4];
-            bool v[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                v[k] = key[k0 + k] != 0xFFFFFFFFu;
-                const int q = v[k] ? (int)(key[k0 + k] & 0x7FF) : 0;  // staged index: bits 0-10 (kGCap <= 2048)
-                f[k] = s_fr[q];
+                const bool v = key[k0 + k] != 0xFFFFFFFFu;
+                const int q = v ? (int)(key[k0 + k] & 0x7FF) : kGCap;  // staged index: bits 0-10 (kGCap <= 2048)
+                w[k] = s_wf[q * 4 + (int)((key[k0 + k] >> 14) & 3u)];  // corner bits 14-15
                 d[k] = s_ds[q];
+                hits += v ? 1u : 0u;
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float wx = f[k].x, ex = 1.0f - wx;
-                const float wy = f[k].y, sy = 1.0f - wy;
-                const unsigned c = key[k0 + k] >> 14;  // corner bits 14-15 (+ chunk bits above)
-                const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
-                const float a0 = acc[0] + w * d[k].x;
-                const float a1 = acc[1] + w * d[k].y;
-                const float a2 = acc[2] + w * d[k].z;
-                const float a3 = acc[3] + w * d[k].w;
-                acc[0] = v[k] ? a0 : acc[0];
-                acc[1] = v[k] ? a1 : acc[1];
-                acc[2] = v[k] ? a2 : acc[2];
-                acc[3] = v[k] ? a3 : acc[3];
-                hits += v[k] ? 1u : 0u;
+                acc[0] = acc[0] + w[k] * d[k].x;
+                acc[1] = acc[1] + w[k] * d[k].y;
+                acc[2] = acc[2] + w[k] * d[k].z;
+                acc[3] = acc[3] + w[k] * d[k].w;
             }
         };
         batch(0);
@@ -647,12 +643,8 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
                     const int b = __builtin_ctz(msk);
                     msk &= msk - 1;
                     const int idx = rowbase + (cur * kGridVec + (b & 7) - pixrow);
-                    const float2 f = s_fr[idx];
                     const float4 d = s_ds[idx];
-                    const float wx = f.x, ex = 1.0f - wx;
-                    const float wy = f.y, sy = 1.0f - wy;
-                    const int c = b >> 3;
-                    const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
+                    const float w = s_w[idx][b >> 3];  // corner b >> 3
                     acc[0] = acc[0] + w * d.x;
                     acc[1] = acc[1] + w * d.y;
                     acc[2] = acc[2] + w * d.z;
@@ -685,12 +677,11 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
 // (gather_texel_pass).  A texel's kGPl planes leave as one 16*kGPl-B run.
 __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
                                                          float4* __restrict__ dmpi, float margin) {
-    __shared__ int s_code[kGCap];     // local nw-tap bucket of the staged pixel, -1 = none
-    __shared__ float2 s_fr[kGCap];    // its bilinear fractions (px - floor px, py - floor py)
-    __shared__ float4 s_ds[kGCap];    // its d sample
-    __shared__ uint2 s_bent[kGNB];    // bucket lists (kGBCap entries)
-    __shared__ int s_bcnt[2][kGNB];   // bucket sizes, by pass parity (one is zeroed while the other is in use)
-    __shared__ int s_ovf[2];          // a list overflowed in this pass
+    __shared__ int s_code[kGCap];                    // local nw-tap bucket of the staged pixel, -1 = none
+    __shared__ f32x4 s_w[kGCap + 1];                 // its bilinear weights (nw, ne, sw, se); [kGCap] = 0
+    __shared__ float4 s_ds[kGCap + 1];               // its d sample; [kGCap] = 0
+    __shared__ unsigned s_ent[2][2 * kGNB];          // bucket lists (2 slots, ~0 = free), by pass parity
+    __shared__ int s_ovf[2];                         // a list overflowed in this pass
     constexpr int TB = kGTB;
     const int tiles_x = (g.W + kGTW - 1) / kGTW;
     const int ntiles = tiles_x * ((g.H + kGTH - 1) / kGTH);
@@ -701,8 +692,12 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     const int tx = tx0 + (threadIdx.x & (kWave - 1)), ty = ty0 + (threadIdx.x >> 6);
     const bool tin = tx < g.W && ty < g.H;
     const int bt = (ty - ty0 + 1) * TB + (tx - tx0 + 1);  // bucket of the texel as an nw tap
-    for (int b = threadIdx.x; b < 2 * kGNB; b += kGThreads) (&s_bcnt[0][0])[b] = 0;
+    for (int b = threadIdx.x; b < 4 * kGNB; b += kGThreads) (&s_ent[0][0])[b] = ~0u;
     if (threadIdx.x < 2) s_ovf[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        s_w[kGCap] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        s_ds[kGCap] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
     int par = 0;
     unsigned hits = 0;    // (texel, contributor) pairs found by this thread
     bool unsafe = false;  // a plane this block could not order (the view goes to the fallback)
@@ -726,13 +721,13 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
         for (int ra = by0; ra <= by1; ra += rpp) {
             const int rb = min(by1 + 1, ra + rpp);
             __syncthreads();  // the previous pass's readers are done
-            gather_stage_pass(g, ws, hp, p, proven, (int)threadIdx.x, tx0, ty0, bx0, bw, ra, rb, s_code, s_fr, s_ds,
-                              s_bent, s_bcnt[par], &s_ovf[par]);
-            for (int b = threadIdx.x; b < kGNB; b += kGThreads) s_bcnt[par ^ 1][b] = 0;  // for the next pass
+            gather_stage_pass(g, ws, hp, p, proven, (int)threadIdx.x, tx0, ty0, bx0, bw, ra, rb, s_code, s_w, s_ds,
+                              s_ent[par], &s_ovf[par]);
+            for (int b = threadIdx.x; b < 2 * kGNB; b += kGThreads) s_ent[par ^ 1][b] = ~0u;  // for the next pass
             if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
             __syncthreads();
-            gather_texel_pass(g, ws, p, margin, tx, ty, bt, tin, s_ovf[par] != 0, s_bcnt[par], s_bent, s_code, s_fr,
-                              s_ds, bx0, bx1, by0, by1, ra, rb, acc[jj], hits, unsafe);
+            gather_texel_pass(g, ws, p, margin, tx, ty, bt, tin, s_ovf[par] != 0, s_ent[par], s_code, s_w, s_ds, bx0,
+                              bx1, by0, by1, ra, rb, acc[jj], hits, unsafe);
             par ^= 1;
         }
     }
@@ -761,10 +756,9 @@ __global__ __launch_bounds__(2 * kGThreads, MPIV_GLBS) void bwd_gather_ws_kernel
                                                                           const float* __restrict__ homs, BwdWs ws,
                                                                           float4* __restrict__ dmpi, float margin) {
     __shared__ int s_code[2][kGCap];
-    __shared__ float2 s_fr[2][kGCap];
-    __shared__ float4 s_ds[2][kGCap];
-    __shared__ uint2 s_bent[2][kGNB];
-    __shared__ int s_bcnt[3][kGNB];
+    __shared__ f32x4 s_w[2][kGCap + 1];
+    __shared__ float4 s_ds[2][kGCap + 1];
+    __shared__ unsigned s_ent[3][2 * kGNB];
     __shared__ int s_ovf[3];
     constexpr int TB = kGTB;
     const int tiles_x = (g.W + kGTW - 1) / kGTW;
@@ -775,8 +769,12 @@ __global__ __launch_bounds__(2 * kGThreads, MPIV_GLBS) void bwd_gather_ws_kernel
     const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTH;
     const bool stager = threadIdx.x < kGThreads;  // wave-uniform
     const int t = (int)threadIdx.x & (kGThreads - 1);
-    for (int b = threadIdx.x; b < 3 * kGNB; b += 2 * kGThreads) (&s_bcnt[0][0])[b] = 0;
+    for (int b = threadIdx.x; b < 6 * kGNB; b += 2 * kGThreads) (&s_ent[0][0])[b] = ~0u;
     if (threadIdx.x < 3) s_ovf[threadIdx.x] = 0;
+    if (threadIdx.x < 2) {
+        s_w[threadIdx.x][kGCap] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        s_ds[threadIdx.x][kGCap] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
     // the pass sequence: (plane jj, box rows [ra, rb)); seek() finds the first pass at or after
     // (jj, ra) (ra = INT_MIN: plane jj's first), skipping planes without pixels; the texel role
     // notes planes it cannot order (bad boxes) as it passes them
@@ -816,8 +814,8 @@ __global__ __launch_bounds__(2 * kGThreads, MPIV_GLBS) void bwd_gather_ws_kernel
     if (stager) {
         if (have)
             gather_stage_pass(g, ws, homs + (int64_t)(p0 + cur.jj) * 9, p0 + cur.jj, cur.proven, t, tx0, ty0, cur.bx0,
-                              cur.bx1 - cur.bx0 + 1, cur.ra, cur.rb, s_code[0], s_fr[0], s_ds[0], s_bent[0],
-                              s_bcnt[0], &s_ovf[0]);
+                              cur.bx1 - cur.bx0 + 1, cur.ra, cur.rb, s_code[0], s_w[0], s_ds[0], s_ent[0],
+                              &s_ovf[0]);
         __syncthreads();
         for (int i = 0; have; ++i) {
             Pass nxt;
@@ -825,9 +823,8 @@ __global__ __launch_bounds__(2 * kGThreads, MPIV_GLBS) void bwd_gather_ws_kernel
             if (have)
                 gather_stage_pass(g, ws, homs + (int64_t)(p0 + nxt.jj) * 9, p0 + nxt.jj, nxt.proven, t, tx0, ty0,
                                   nxt.bx0, nxt.bx1 - nxt.bx0 + 1, nxt.ra, nxt.rb, s_code[(i + 1) & 1],
-                                  s_fr[(i + 1) & 1], s_ds[(i + 1) & 1], s_bent[(i + 1) & 1], s_bcnt[(i + 1) % 3],
-                                  &s_ovf[(i + 1) % 3]);
-            for (int b = t; b < kGNB; b += kGThreads) s_bcnt[(i + 2) % 3][b] = 0;  // for pass i + 2
+                                  s_w[(i + 1) & 1], s_ds[(i + 1) & 1], s_ent[(i + 1) % 3], &s_ovf[(i + 1) % 3]);
+            for (int b = t; b < 2 * kGNB; b += kGThreads) s_ent[(i + 2) % 3][b] = ~0u;  // for pass i + 2
             if (t == 0) s_ovf[(i + 2) % 3] = 0;
             __syncthreads();
             cur = nxt;
@@ -847,9 +844,9 @@ __global__ __launch_bounds__(2 * kGThreads, MPIV_GLBS) void bwd_gather_ws_kernel
 #pragma unroll
     for (int jj = 0; jj < kGPl; ++jj) {
         while (have && cur.jj == jj) {
-            gather_texel_pass(g, ws, p0 + jj, margin, tx, ty, bt, tin, s_ovf[i % 3] != 0, s_bcnt[i % 3], s_bent[i & 1],
-                              s_code[i & 1], s_fr[i & 1], s_ds[i & 1], cur.bx0, cur.bx1, cur.by0, cur.by1, cur.ra,
-                              cur.rb, acc[jj], hits, unsafe);
+            gather_texel_pass(g, ws, p0 + jj, margin, tx, ty, bt, tin, s_ovf[i % 3] != 0, s_ent[i % 3], s_code[i & 1],
+                              s_w[i & 1], s_ds[i & 1], cur.bx0, cur.bx1, cur.by0, cur.by1, cur.ra, cur.rb, acc[jj],
+                              hits, unsafe);
             Pass nxt;
             have = seek(cur.jj, cur.rb, nxt);
             __syncthreads();  // pass i + 1 staged; pass i's buffers free
