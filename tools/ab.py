@@ -195,6 +195,28 @@ def c3(dev, it):
     run("c3 (mpiv_plane_sweep)", [("default", {})], fn, S * H * W * 12 + S * D * H * W * 12, it)
 
 
+VSD = [("auto", {}), ("r8d4", {"render_vshare": 3}), ("r6d3", {"render_vshare": 4}), ("r9d3", {"render_vshare": 5}),
+       ("r4d4", {"render_vshare": 11})]
+
+
+def vsd(dev, it):
+    """The packed render's (rows, rows in flight) routing on config 4 (bench.py's camera-path
+    views): 125, 8 and 1 views per launch, every shipped (R, D) choice."""
+    c = configs.config4()
+    H, W, P = c["H"], c["W"], c["P"]
+    g = torch.Generator(device=dev).manual_seed(0)
+    view = torch.rand((H, W, P, 4), generator=g, device=dev)
+    packed = _lib.pack_planes(view)
+    del view
+    for V in (125, 8, 1):
+        homs = _host.render_homographies(configs.f32(c["poses"][:V]), configs.f32(c["depths"]),
+                                         configs.f32([c["K"]] * V), V).to(dev)
+        out = torch.empty((V, H, W, 3), device=dev)
+        fn = lambda: _lib._call("mpiv_render_packed", packed, H, W, P, homs, V, out, _lib._stream(dev))  # noqa: E731
+        run(f"c4 packed render, {V} views", VSD, fn, V * (P * H * W * 16 + H * W * 12), max(3, it // (1 + V // 8)))
+        del out
+
+
 DEF = [("default", {})]
 
 
