@@ -217,6 +217,19 @@ def vsd(dev, it):
         del out
 
 
+def chunkpar(dev, it):
+    """Diagnostic: the in-place render (render_chunk_kernel) with the camera-path homographies
+    against the same launch with every plane given plane 63's homography (no parallax inside a
+    chunk: each 8-lane group's taps share one 128-B line) -- the most any parallax-following lane
+    mapping could gain."""
+    mpi, homs, H, W, P = c4_mpi(dev)
+    out = torch.empty((1, H, W, 3), device=dev)
+    flat = homs.view(1, P, 9)[:, 63:64].expand(1, P, 9).contiguous()
+    for label, hh in (("camera", homs), ("no_parallax", flat)):
+        fn = lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, hh, out, _lib._stream(dev))  # noqa: E731
+        run(f"c4 in-place render, 1 view, {label}", DEF, fn, P * H * W * 16 + H * W * 12, it)
+
+
 DEF = [("default", {})]
 
 
