@@ -472,6 +472,11 @@ constexpr int kGTB = kGTW + 1;              // bucket row pitch: nw taps x in [t
 constexpr int kGNB = kGTB * (kGTH + 1);     // nw-tap buckets of a tile
 constexpr int kGBCap = 2;                   // entries per bucket list (more: the window scan)
 constexpr int kGSI = (kGCap + kGThreads - 1) / kGThreads;  // staged pixels per staging thread
+// staged bilinear weights, corner-major: s_w[c * kGWP + q] is corner c's weight of staged pixel q
+// (c = nw, ne, sw, se; q = kGCap: the zero slot).  The texel pass reads one corner per key, and
+// neighbouring texels read neighbouring staged pixels: consecutive dwords, conflict-free, where
+// a pixel-major float4 array puts a 32-lane read on 8 banks (4-way conflicts).
+constexpr int kGWP = kGCap + 1;
 
 // One staging pass of plane p over box rows [ra, rb) x columns [bx0, bx0 + bw) by the kGThreads
 // threads t of a block (or of its staging waves): each box pixel's sample position with the
@@ -483,7 +488,7 @@ constexpr int kGSI = (kGCap + kGThreads - 1) / kGThreads;  // staged pixels per 
 // latency was exposed -- 0.32 of the kernel's 1.77 ms, r03).  s_ent must be all ~0 on entry.
 __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const BwdWs& ws, const float* __restrict__ hp,
                                                   int p, bool proven, int t, int tx0, int ty0, int bx0, int bw,
-                                                  int ra, int rb, int* s_code, f32x4* s_w, float4* s_ds,
+                                                  int ra, int rb, int* s_code, float* s_w, float4* s_ds,
                                                   unsigned* s_ent, int* ovf) {
     constexpr int TB = kGTB;
     const int64_t HW = (int64_t)g.H * g.W;
@@ -523,7 +528,10 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
             // the texel pass reads the one of its corner instead of re-deriving it from fractions
             const float wx = px - fx0, ex = 1.0f - wx;
             const float wy = py - fy0, sy = 1.0f - wy;
-            s_w[q] = f32x4{sy * ex, sy * wx, wy * ex, wy * wx};
+            s_w[q] = sy * ex;
+            s_w[kGWP + q] = sy * wx;
+            s_w[2 * kGWP + q] = wy * ex;
+            s_w[3 * kGWP + q] = wy * wx;
             if (i >= MPIV_GSI)  // past the preloaded pixels (boxes over MPIV_GSI * kGThreads pixels)
                 dsv[i] = llvm_raw_buffer_load_v4f32(rds, (yy * g.W + xx) * 16, 0, 0);
             s_ds[q] = make_float4(dsv[i][0], dsv[i][1], dsv[i][2], dsv[i][3]);
@@ -546,7 +554,7 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
 // inverse map instead, one 8-pixel chunk at a time.
 __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const BwdWs& ws, int p, float margin, int tx,
                                                   int ty, int bt, bool tin, bool ovf, const unsigned* s_ent,
-                                                  const int* s_code, const f32x4* s_w, const float4* s_ds, int bx0,
+                                                  const int* s_code, const float* s_w, const float4* s_ds, int bx0,
                                                   int bx1, int by0, int by1, int ra, int rb, f32x4& acc,
                                                   unsigned& hits, bool& unsafe) {
     constexpr int TB = kGTB;
@@ -578,7 +586,6 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
         // bits unchanged -- a sum started at +0 is never -0 under round-to-nearest (x + -x and
         // +0 + -0 both give +0), and inf / NaN stay as they are.  The second batch (5+
         // contributors) is a wave-uniform branch.
-        const float* s_wf = reinterpret_cast<const float*>(s_w);
         auto batch = [&](int k0) {
             float w[4];
             float4 d[4];
@@ -586,7 +593,7 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
             for (int k = 0; k < 4; ++k) {
                 const bool v = key[k0 + k] != 0xFFFFFFFFu;
                 const int q = v ? (int)(key[k0 + k] & 0x7FF) : kGCap;  // staged index: bits 0-10 (kGCap <= 2048)
-                w[k] = s_wf[q * 4 + (int)((key[k0 + k] >> 14) & 3u)];  // corner bits 14-15
+                w[k] = s_w[(int)((key[k0 + k] >> 14) & 3u) * kGWP + q];  // corner bits 14-15
                 d[k] = s_ds[q];
                 hits += v ? 1u : 0u;
             }
@@ -644,7 +651,7 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
                     msk &= msk - 1;
                     const int idx = rowbase + (cur * kGridVec + (b & 7) - pixrow);
                     const float4 d = s_ds[idx];
-                    const float w = s_w[idx][b >> 3];  // corner b >> 3
+                    const float w = s_w[(b >> 3) * kGWP + idx];  // corner b >> 3
                     acc[0] = acc[0] + w * d.x;
                     acc[1] = acc[1] + w * d.y;
                     acc[2] = acc[2] + w * d.z;
@@ -678,7 +685,7 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
 __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
                                                          float4* __restrict__ dmpi, float margin) {
     __shared__ int s_code[kGCap];                    // local nw-tap bucket of the staged pixel, -1 = none
-    __shared__ f32x4 s_w[kGCap + 1];                 // its bilinear weights (nw, ne, sw, se); [kGCap] = 0
+    __shared__ float s_w[4 * kGWP];                  // its bilinear weights, corner-major (kGWP); [kGCap] = 0
     __shared__ float4 s_ds[kGCap + 1];               // its d sample; [kGCap] = 0
     __shared__ unsigned s_ent[2][2 * kGNB];          // bucket lists (2 slots, ~0 = free), by pass parity
     __shared__ int s_ovf[2];                         // a list overflowed in this pass
@@ -694,10 +701,8 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     const int bt = (ty - ty0 + 1) * TB + (tx - tx0 + 1);  // bucket of the texel as an nw tap
     for (int b = threadIdx.x; b < 4 * kGNB; b += kGThreads) (&s_ent[0][0])[b] = ~0u;
     if (threadIdx.x < 2) s_ovf[threadIdx.x] = 0;
-    if (threadIdx.x == 0) {
-        s_w[kGCap] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        s_ds[kGCap] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
+    if (threadIdx.x < 4) s_w[threadIdx.x * kGWP + kGCap] = 0.0f;
+    if (threadIdx.x == 0) s_ds[kGCap] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     int par = 0;
     unsigned hits = 0;    // (texel, contributor) pairs found by this thread
     bool unsafe = false;  // a plane this block could not order (the view goes to the fallback)
@@ -756,7 +761,7 @@ __global__ __launch_bounds__(2 * kGThreads, MPIV_GLBS) void bwd_gather_ws_kernel
                                                                           const float* __restrict__ homs, BwdWs ws,
                                                                           float4* __restrict__ dmpi, float margin) {
     __shared__ int s_code[2][kGCap];
-    __shared__ f32x4 s_w[2][kGCap + 1];
+    __shared__ float s_w[2][4 * kGWP];
     __shared__ float4 s_ds[2][kGCap + 1];
     __shared__ unsigned s_ent[3][2 * kGNB];
     __shared__ int s_ovf[3];
@@ -771,10 +776,8 @@ __global__ __launch_bounds__(2 * kGThreads, MPIV_GLBS) void bwd_gather_ws_kernel
     const int t = (int)threadIdx.x & (kGThreads - 1);
     for (int b = threadIdx.x; b < 6 * kGNB; b += 2 * kGThreads) (&s_ent[0][0])[b] = ~0u;
     if (threadIdx.x < 3) s_ovf[threadIdx.x] = 0;
-    if (threadIdx.x < 2) {
-        s_w[threadIdx.x][kGCap] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        s_ds[threadIdx.x][kGCap] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
+    if (threadIdx.x < 8) s_w[threadIdx.x >> 2][(threadIdx.x & 3) * kGWP + kGCap] = 0.0f;
+    if (threadIdx.x < 2) s_ds[threadIdx.x][kGCap] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     // the pass sequence: (plane jj, box rows [ra, rb)); seek() finds the first pass at or after
     // (jj, ra) (ra = INT_MIN: plane jj's first), skipping planes without pixels; the texel role
     // notes planes it cannot order (bad boxes) as it passes them
