@@ -212,9 +212,11 @@ int mpiv_assemble_mpi_backward(const float *drgba, const int64_t drgba_strides[5
  * proj:   [B][16] [[K_src,0],[0,0,0,1]] @ pose     (utils.py:431-438 / :750-757)
  * depths: [D] fp32
  * out:    [B,Ht,Wt,D*C] contiguous, channel d*C + c (torch.cat order, utils.py:470)
- * C <= 4 reads img in place: D <= 8 by plane_sweep_direct_kernel (taps gathered per sample),
- * more depths by plane_sweep_dlane_kernel (the tile's source footprint staged in LDS); C > 4 by
- * the generic one-sample-per-thread kernel.  Every route writes the same bits. */
+ * C <= 4 reads img in place: D <= 2 by plane_sweep_direct_kernel (taps gathered per sample),
+ * 3 <= D <= 8 by plane_sweep_px_kernel (pixel per lane, taps gathered per sample, the wave's
+ * samples stored as one run), more depths by plane_sweep_dlane_kernel (the tile's source
+ * footprint staged in LDS); C > 4 by the generic one-sample-per-thread kernel.  Every route
+ * writes the same bits. */
 int mpiv_plane_sweep(const float *img, const int64_t img_strides[4], int B, int Hs, int Ws, int C,
                      const float *ki, const float *proj, const float *depths, int D, int Ht, int Wt,
                      float *out, void *stream);

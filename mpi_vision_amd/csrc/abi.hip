@@ -80,7 +80,9 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
 //                      wave (0 = automatic)
 //   sweep_direct=-1|0|1  mpiv_plane_sweep[_into] without LDS staging (plane_sweep_direct_kernel):
-//                      never / automatic (D <= 8) / for any D <= 64
+//                      never / automatic (D <= 2) / for any D <= 64; 2|3: pixel per lane, the wave's
+//                      samples staged in LDS (plane_sweep_px_kernel, D * C <= 48; 64 / 32 pixels
+//                      per wave; automatic: 64 for 3 <= D <= 8)
 //   box_shrink=k       LDS-staged kernels stage boxes k texels narrower per side, which
 //                      forces their per-sample global fallback (tests)
 //   bwd_fallback=1     mpiv_render_backward skips the tile gather and runs its bucket
@@ -772,7 +774,35 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
     hipStream_t q = S(stream);
     // few depths: no LDS staging (plane_sweep_direct_kernel); sweep_direct = -1 off, 1 for any D <= 64
     const int od = opt(kOptSweepDirect);
-    if (od >= 0 && shrink == 0 && D <= (od == 1 ? kWave : kDirMaxD) && Ht <= (int)kMaxGridYZ) {
+    // automatic: D <= 2 direct, 3 <= D <= 8 pixel per lane, deeper the LDS-staged kernel
+    // (profiles/r03_sweep_few_depths_ab.txt)
+    const bool px_auto = od == 0 && D >= 3 && D <= kDirMaxD;
+    if ((px_auto || od == 2 || od == 3) && D * C <= kPxMaxDC && shrink == 0 && Ht <= (int)kMaxGridYZ) {
+        // pixel per lane, the wave's samples staged in LDS and stored as one run
+        // (plane_sweep_px_kernel; 64 pixels per wave, 32 with sweep_direct=3)
+        const int PW = od == 3 ? kWave / 2 : kWave;
+        const dim3 pgrid((unsigned)((Wt + 4 * PW - 1) / (4 * PW)), (unsigned)Ht, (unsigned)B);
+        const int CC = C < 4 ? C : 4;
+        const size_t lds = (size_t)4 * PW * D * CC * sizeof(float);
+        if (g_route) return note_route((int64_t)pgrid.x * Ht * B, 256, "plane_sweep_px_kernel<%d, %d>", CC, PW);
+        const float rDC = 1.0f / (float)(D * CC);
+#define MPIV_PX1(K, PP)                                                                                    \
+    plane_sweep_px_kernel<K, PP><<<pgrid, 256, lds, q>>>(img, is, sp, rc_hs, rc_ws, rDC, ki, proj, depths, \
+                                                         out, out_bstride, out_pstride, (int)vec)
+#define MPIV_PX(K)                     \
+    if (PW == kWave) MPIV_PX1(K, kWave); \
+    else MPIV_PX1(K, kWave / 2)
+        switch (C) {
+            case 1: MPIV_PX(1); break;
+            case 2: MPIV_PX(2); break;
+            case 3: MPIV_PX(3); break;
+            default: MPIV_PX(4); break;
+        }
+#undef MPIV_PX
+#undef MPIV_PX1
+        return launched(nm);
+    }
+    if (od >= 0 && od < 2 && shrink == 0 && D <= (od == 1 ? kWave : kDirMaxD) && Ht <= (int)kMaxGridYZ) {
         const int ppw = kWave / D;
         const int64_t gpr = (Wt + ppw - 1) / ppw;  // pixel groups per target row
         const dim3 dgrid((unsigned)((gpr + 4 * kDirG - 1) / (4 * kDirG)), (unsigned)Ht, (unsigned)B);

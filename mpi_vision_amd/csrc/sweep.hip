@@ -1110,7 +1110,8 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     }
 }
 
-// Direct depth-per-lane sweep for few depths (D <= 8; abi.hip sweep_raw_into).  The LDS box
+// Direct depth-per-lane sweep for few depths (D <= 2 automatic, 3..8 go to the pixel-per-lane
+// plane_sweep_px_kernel below; abi.hip sweep_raw_into).  The LDS box
 // of plane_sweep_dlane_kernel is sized by the depth RANGE, not the depth count, so with few
 // depths it serves few samples per staged texel and the block's two serial latencies (box
 // prologue, fill) dominate (D = 10: 0.23-0.26 ms for config 3's sources, 0.25-0.28 of HBM).
@@ -1122,8 +1123,9 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
 // row, two samples in flight per lane.  The per-sample arithmetic is the dlane kernel's
 // (bit-identical volume).
 constexpr int kDirG = 4;        // pixel groups per wave
-constexpr int kDirMaxD = 8;     // deepest volume routed here by default (measured: D = 6 0.15-0.18 ms
-                                // vs 0.19-0.23 staged; D >= 10 slower than the staged kernel)
+constexpr int kDirMaxD = 8;     // deepest volume routed past the LDS staging by default (measured:
+                                // D = 6 0.15-0.18 ms direct vs 0.19-0.23 staged, pixel per lane
+                                // 0.125; D >= 10 the staged kernel wins)
 template <int C>
 __global__ __launch_bounds__(256) void plane_sweep_direct_kernel(const float* __restrict__ img, ImgStrides is,
                                                                  SweepParams sp, float rc_hs, float rc_ws, float rD,
@@ -1203,6 +1205,108 @@ __global__ __launch_bounds__(256) void plane_sweep_direct_kernel(const float* __
                     for (int c = 0; c < C; ++c) o[c] = v[c];
                 }
             }
+        }
+    }
+}
+
+// Pixel-per-lane sweep for few depths (abi.hip sweep_raw_into; automatic for 3 <= D <= 8,
+// profiles/r03_sweep_few_depths_ab.txt): a wave takes PW consecutive
+// target pixels of one row x 64/PW depths at a time (lane = pixel lane % PW, depth offset
+// lane / PW) and walks the D depths, two such steps in flight (four measured slower: the
+// VGPRs cost occupancy).  For one depth the PW lanes
+// sample neighbouring source texels, so a tap instruction reads 64/PW runs of the source
+// instead of the depth-per-lane kernels' one run per depth, and a pixel's ray is formed once
+// for all its depths.  The samples go to a wave-private LDS slot [PW][D*C] and leave as the
+// wave's contiguous PW*D*C-float run of the volume (16-B stores where aligned); stored straight
+// from the lanes instead (each 64-lane store touching 64 pixel runs) the kernel ran 2-5x
+// slower.  No block barrier: each wave owns its slot.  The per-sample arithmetic is
+// plane_sweep_direct_kernel's (bit-identical volume).
+constexpr int kPxMaxDC = 48;  // deepest D*C staged (LDS: 4 waves x 64 x 48 floats = 48 KiB)
+template <int C, int PW>
+__global__ __launch_bounds__(256) void plane_sweep_px_kernel(const float* __restrict__ img, ImgStrides is,
+                                                             SweepParams sp, float rc_hs, float rc_ws, float rDC,
+                                                             const float* __restrict__ ki,
+                                                             const float* __restrict__ proj,
+                                                             const float* __restrict__ depths,
+                                                             float* __restrict__ out, int64_t out_bstride,
+                                                             int64_t out_pstride, int vec) {
+    static_assert(PW == 32 || PW == 64, "a wave is one or two pixel groups");
+    constexpr int DS = kWave / PW;  // depths per step
+    extern __shared__ float px_lds[];
+    const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.z, y = blockIdx.y;
+    const int x0 = (blockIdx.x * 4 + wave) * PW;
+    if (x0 >= sp.Wt) return;  // whole wave; no barrier follows
+    const int D = sp.D, DC = D * C;
+    float* slot = px_lds + wave * PW * DC;
+    const int pl = lane % PW, dsub = lane / PW;
+    const int x = min(x0 + pl, sp.Wt - 1);  // lanes past the row recompute its last pixel (not stored)
+    const float* k9 = ki + (int64_t)b * 9;
+    const float* m = proj + (int64_t)b * 16;
+    const float* imb = img + (int64_t)b * is.b;
+    float rx, ry, rz;
+    ray(k9, (float)x, (float)y, rx, ry, rz);  // pixel2cam_torch, utils.py:370
+    for (int d0 = 0; d0 < D; d0 += 2 * DS) {
+        float su[2], sv[2], dq[2];
+        int dd[2];
+        bool fast = true;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            dd[j] = d0 + j * DS + dsub;
+            dq[j] = depths[min(dd[j], D - 1)];  // past the end: the last depth again (not stored)
+            const float X = rx * dq[j], Y = ry * dq[j], Z = rz * dq[j];
+            const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+            const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+            const float den = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11] + 1e-10f;
+            fast = fast && div2_safe(pu, pv, den);
+            div2_fast(pu, pv, den, su[j], sv[j]);  // cam2pixel_torch, utils.py:388-391
+        }
+        if (__builtin_amdgcn_ballot_w64(!fast)) {  // rare: a quotient outside the fast path's range
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const float X = rx * dq[j], Y = ry * dq[j], Z = rz * dq[j];
+                const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+                const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+                const float den = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11] + 1e-10f;
+                if (!div2_safe(pu, pv, den)) {
+                    su[j] = div_rn(pu, den);
+                    sv[j] = div_rn(pv, den);
+                }
+            }
+        }
+        f32x4 s[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float cx = div_const(su[j] + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
+            const float cy = div_const(sv[j] + 0.5f, sp.fws, rc_ws);  //          y / W
+            s[j] = raw_sample<C>(imb, is, sp.Ws, sp.Hs, unnormalize(to_grid(cx), sp.half_ws),
+                                 unnormalize(to_grid(cy), sp.half_hs));
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (dd[j] < D) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) slot[pl * DC + dd[j] * C + c] = s[j][c];
+            }
+        }
+    }
+    // the wave's LDS writes before its reads of other lanes' samples
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int npx = min(PW, sp.Wt - x0);
+    const int n = npx * DC;  // floats of the wave's pixels
+    float* ob = out + (int64_t)b * out_bstride + ((int64_t)y * sp.Wt + x0) * out_pstride;
+    if (vec && out_pstride == DC && (((uintptr_t)ob) & 15) == 0) {  // one contiguous run
+        const int n4 = n >> 2;
+        for (int i = lane; i < n4; i += kWave)
+            __builtin_nontemporal_store(reinterpret_cast<const f32x4*>(slot)[i], reinterpret_cast<f32x4*>(ob) + i);
+        for (int i = (n4 << 2) + lane; i < n; i += kWave) ob[i] = slot[i];
+    } else {  // pixel runs of DC floats, out_pstride apart
+        for (int i = lane; i < n; i += kWave) {
+            int p = (int)(((float)i + 0.5f) * rDC);  // i / DC (i < 64 * kPxMaxDC: exact)
+            const int off = i - p * DC;
+            ob[(int64_t)p * out_pstride + off] = slot[i];
         }
     }
 }

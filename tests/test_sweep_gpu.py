@@ -399,6 +399,23 @@ def test_format_network_input_depth_lanes_strided(small, dev, kopts):
     assert_bits(got.numpy(), torch.cat(parts, dim=-1).numpy())
 
 
+@pytest.mark.parametrize("direct", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("D", [10, 16])
+def test_format_network_input_few_depths_routes(D, direct, small, dev, kopts):
+    """format_network_input_torch with the notebook's few depths: each source swept into its
+    channel slice of the network input (mpiv_plane_sweep_into: pixel runs D*3 floats long,
+    out_pstride = 3 + S*D*3 apart) by the automatic route, the direct depth-per-lane kernel and
+    the pixel-per-lane kernel (strided copy-out): bit-identical to the LDS-staged kernel."""
+    t = {k: torch.tensor(small[f"fni_{k}"]).to(dev) for k in ("ref", "src", "ref_pose", "src_poses", "K")}
+    planes = configs.inv_depths(1.0, 100.0, D)
+    args = (None, t["ref"], t["src"], t["ref_pose"], t["src_poses"], planes, t["K"])
+    kopts(sweep_direct="-1")
+    want = mv.format_network_input_torch(*args).cpu()
+    kopts(sweep_direct=direct)
+    got = mv.format_network_input_torch(*args).cpu()
+    assert_bits(got.numpy(), want.numpy(), f"D={D} direct={direct}")
+
+
 @pytest.mark.parametrize("shape", [(1, 1, 1, 1), (2, 3, 1, 2), (5, 4, 3, 65)])
 def test_plane_sweep_tiny_targets(shape, dev):
     """Tiny targets and depth counts through the default (depth-per-lane, in-place) sweep:
@@ -422,11 +439,14 @@ def test_plane_sweep_tiny_targets(shape, dev):
 
 @pytest.mark.parametrize("C", [1, 2, 3, 4])
 @pytest.mark.parametrize("D,direct", [(1, "0"), (6, "0"), (8, "0"), (10, "0"), (10, "1"), (16, "1"), (32, "1"), (33, "1"),
-                                      (64, "1")])
+                                      (64, "1"), (1, "2"), (5, "2"), (10, "2"), (12, "2"), (16, "2"), (1, "3"), (7, "3"), (10, "3"),
+                                      (16, "3")])
 @pytest.mark.parametrize("strided", [False, True])
 def test_plane_sweep_direct_vs_oracle(C, D, direct, strided, dev, kopts):
-    """Few depths take the direct depth-per-lane kernel (no LDS staging; automatic for D <= 8,
-    sweep_direct=1 forces it up to D = 64, -1 keeps the LDS kernel): partial pixel groups
+    """Few depths skip the LDS staging: the direct depth-per-lane kernel (automatic for D <= 2,
+    sweep_direct=1 forces it up to D = 64) and the pixel-per-lane kernel plane_sweep_px_kernel
+    (automatic for 3 <= D <= 8; sweep_direct=2 / 3 force it with 64 / 32 pixels per wave for
+    D * C <= 48, the LDS kernel above); -1 keeps the LDS kernel.  Partial pixel groups
     (64 % D idle lanes, a partial last group of a row), odd target sizes, separate source /
     target intrinsics, a strided (channel-sliced) source: bit-exact to the oracle."""
     from mpi_vision_amd import _host, _lib
@@ -448,10 +468,12 @@ def test_plane_sweep_direct_vs_oracle(C, D, direct, strided, dev, kopts):
     if direct == "0":  # mpiv_route reports production routes only
         _lib.reset_debug()
         route = _lib.route("plane_sweep", B, Hs, Ws, C, D, Ht, Wt)[0]
-        assert route.startswith("plane_sweep_direct_kernel" if D <= 8 else "plane_sweep_dlane_kernel"), route
+        want_route = ("plane_sweep_direct_kernel" if D <= 2 else "plane_sweep_px_kernel" if D <= 8
+                      else "plane_sweep_dlane_kernel")
+        assert route.startswith(want_route), route
 
 
-@pytest.mark.parametrize("direct", ["0", "-1"])
+@pytest.mark.parametrize("direct", ["0", "-1", "2", "3"])
 def test_plane_sweep_direct_off_image(direct, dev, kopts):
     """The notebook's 10 planes on landscape sources whose samples fall wholly or partly off
     the image (the swapped x / H normalisation), through the direct kernel and the LDS kernel:

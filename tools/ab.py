@@ -160,7 +160,7 @@ def bwdg(dev, it):
 def sw10(dev, it):
     """Config-3 sources into few depths (the notebook dataset's 10 planes) through
     mpiv_plane_sweep: the direct depth-per-lane kernel (no LDS staging) against the LDS-staged
-    one (sweep_direct=1 / -1; automatic: direct for D <= 32)."""
+    one and the pixel-per-lane one (sweep_direct=1 / -1 / 2; automatic: direct for D <= 8)."""
     c = configs.config3()
     S, H, W = c["S"], c["H"], c["W"]
     g = torch.Generator(device=dev).manual_seed(1)
@@ -168,13 +168,14 @@ def sw10(dev, it):
     K = configs.f32([c["K"]] * S)
     ki, proj = _host.psv_matrices(K, K, configs.f32(c["poses"]))
     ki, proj = ki.to(dev), proj.to(dev)
-    for D in (6, 10, 16, 32, 64):
+    for D in [int(v) for v in os.environ.get("SW_D", "6,10,16,32,64").split(",")]:
         d = configs.f32(configs.inv_depths(1, 100, D)).to(dev)
         out = torch.empty((S, H, W, D * 3), device=dev)
         alg = S * H * W * 12 + S * D * H * W * 12
         raw = lambda: _lib._call("mpiv_plane_sweep", img, _lib._strides(img), S, H, W, 3, ki, proj, d, D, H, W,  # noqa: E731
                                  out, _lib._stream(dev))
-        run(f"c3 sources -> {D} planes (mpiv_plane_sweep)", [("lds", {"sweep_direct": -1}), ("direct", {"sweep_direct": 1})],
+        run(f"c3 sources -> {D} planes (mpiv_plane_sweep)", [("lds", {"sweep_direct": -1}), ("direct", {"sweep_direct": 1}),
+                                                                 ("px", {"sweep_direct": 2}), ("px32", {"sweep_direct": 3})],
             raw, alg, it)
         del out
 
