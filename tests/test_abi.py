@@ -111,6 +111,24 @@ def test_ab_kernels_live_in_the_ab_library():
     assert os.path.getsize(_lib.LIB_PATH) < os.path.getsize(_lib.AB_PATH)
 
 
+@pytest.mark.parametrize("C", [1, 3, 4])
+def test_plane_sweep_routes(C):
+    """mpiv_route (dry run, no GPU): the sweep's production route by depth count -- the direct
+    depth-per-lane kernel for D <= 2, the pixel-per-lane kernel (one block per 256 pixels of a
+    row) for 3 <= D <= 8, the LDS-staged depth-per-lane kernel above; C > 4 the generic kernel."""
+    B, Hs, Ws, Ht, Wt = 5, 768, 1024, 768, 1024
+    for D in (1, 2, 3, 8, 9, 10, 64):
+        name, grid = _lib.route("plane_sweep", B, Hs, Ws, C, D, Ht, Wt)
+        if D <= 2:
+            assert name == f"plane_sweep_direct_kernel<{C}>", (D, name)
+        elif D <= 8:
+            assert name == f"plane_sweep_px_kernel<{C}, 64>", (D, name)
+            assert grid == (Wt // 256) * Ht * B * 256, (D, grid)
+        else:
+            assert name.startswith(f"plane_sweep_dlane_kernel<{C}, true, 4"), (D, name)
+    assert _lib.route("plane_sweep", B, Hs, Ws, 5, 10, Ht, Wt)[0] == "plane_sweep_kernel"
+
+
 def test_output_buffers_validated():
     """Caller-supplied outputs of the packed render / pack must be dense fp32 tensors of the
     exact shape on the same device, else a Python error (not out-of-bounds device writes)."""
