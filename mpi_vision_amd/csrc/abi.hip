@@ -820,29 +820,35 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
 #undef MPIV_DIRECT
         return launched(nm);
     }
+    // one pixel per lane and iteration for few depths (D = 10: 0.228 vs 0.243 ms), two above
+    // (D = 64: 0.640 vs 0.652; profiles/r03_sweep_few_depths_ab.txt)
+    const int pix = (SLR == 4 && D <= 16) ? 1 : kDLPix;
     if (g_route)
-        return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true, %d, %d>", C < 4 ? C : 4, SLR,
-                          SLR == 4 ? kSLCap : 4096);
-#define MPIV_DLRAW(CC, RR, CAP)                                                                              \
-    plane_sweep_dlane_kernel<CC, true, RR, CAP><<<lgrid, kDLThreads, 0, q>>>(nullptr, PadGeom{0, 0, 0, 0}, img, is, \
-                                                                            sp, rc_hs, rc_ws, ki, proj, depths, out, \
-                                                                            out_bstride, out_pstride, (int)vec, shrink)
-#define MPIV_DLRAW_C(RR, CAP)                  \
-    switch (C) {                               \
-        case 1: MPIV_DLRAW(1, RR, CAP); break; \
-        case 2: MPIV_DLRAW(2, RR, CAP); break; \
-        case 3: MPIV_DLRAW(3, RR, CAP); break; \
-        default: MPIV_DLRAW(4, RR, CAP); break; \
+        return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true, %d, %d, %d>", C < 4 ? C : 4, SLR,
+                          SLR == 4 ? kSLCap : 4096, pix);
+#define MPIV_DLRAW(CC, RR, CAP, PP)                                                                          \
+    plane_sweep_dlane_kernel<CC, true, RR, CAP, PP><<<lgrid, kDLThreads, 0, q>>>(nullptr, PadGeom{0, 0, 0, 0}, img, \
+                                                                                is, sp, rc_hs, rc_ws, ki, proj,     \
+                                                                                depths, out, out_bstride,           \
+                                                                                out_pstride, (int)vec, shrink)
+#define MPIV_DLRAW_C(RR, CAP, PP)                  \
+    switch (C) {                                   \
+        case 1: MPIV_DLRAW(1, RR, CAP, PP); break; \
+        case 2: MPIV_DLRAW(2, RR, CAP, PP); break; \
+        case 3: MPIV_DLRAW(3, RR, CAP, PP); break; \
+        default: MPIV_DLRAW(4, RR, CAP, PP); break; \
     }
 #if MPIV_AB  // taller tiles: measured within noise
     if (SLR == 8) {
-        MPIV_DLRAW_C(8, 4096)
+        MPIV_DLRAW_C(8, 4096, kDLPix)
     } else if (SLR == 6) {
-        MPIV_DLRAW_C(6, 4096)
+        MPIV_DLRAW_C(6, 4096, kDLPix)
     } else
 #endif
-    {
-        MPIV_DLRAW_C(4, kSLCap)
+    if (pix == 1) {
+        MPIV_DLRAW_C(4, kSLCap, 1)
+    } else {
+        MPIV_DLRAW_C(4, kSLCap, kDLPix)
     }
 #undef MPIV_DLRAW_C
 #undef MPIV_DLRAW

@@ -868,7 +868,8 @@ constexpr int kDLWaves = kDLThreads / kWave;
 #ifndef MPIV_DLPIX
 #define MPIV_DLPIX 2
 #endif
-constexpr int kDLPix = MPIV_DLPIX;  // pixels (samples per lane) per iteration
+constexpr int kDLPix = MPIV_DLPIX;  // pixels (samples per lane) per iteration, D > 16 (D <= 16: 1;
+                                    // profiles/r03_sweep_few_depths_ab.txt)
 static_assert(kSLCap % kDLThreads == 0, "sweep_fill_box writes every staging slot");
 
 // One source texel as a float4 (channels >= C zero), zero when !in.  Contiguous channels
@@ -946,7 +947,8 @@ __device__ __forceinline__ f32x4 raw_sample(const float* __restrict__ img, const
 // RAW: the source is the caller's strided tensor (img, is) instead of padded texels (img4, pg).
 // SLR target rows per tile, CAP staged texels: (4, 3072) by default; few depths take taller
 // tiles (more samples per staged box, abi.hip sweep_tile_rows) with a larger box.
-template <int C, bool RAW, int SLR = kSLR, int CAP = kSLCap>
+// PIX pixels (samples per lane) per iteration: 1 for few depths (D <= 16), 2 above.
+template <int C, bool RAW, int SLR = kSLR, int CAP = kSLCap, int PIX = kDLPix>
 __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     const float4* __restrict__ img4, PadGeom pg, const float* __restrict__ img, ImgStrides is, SweepParams sp,
     float rc_hs, float rc_ws, const float* __restrict__ ki, const float* __restrict__ proj,
@@ -1019,12 +1021,12 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     const bool dlive = (D <= kWave ? lane < ppw * D : dl < D);
     const float dq = depths[min(dl, D - 1)];
     float* orow = out + (int64_t)b * out_bstride + ((int64_t)(y0 + tr) * sp.Wt + x0) * out_pstride + (int64_t)dl * C;
-    for (int g0 = wave * kDLPix; g0 < ngroup; g0 += kDLWaves * kDLPix) {
-        float px[kDLPix], py[kDLPix], rxs[kDLPix], rys[kDLPix], rzs[kDLPix], dep[kDLPix];
-        float* o[kDLPix];
-        bool live[kDLPix];
+    for (int g0 = wave * PIX; g0 < ngroup; g0 += kDLWaves * PIX) {
+        float px[PIX], py[PIX], rxs[PIX], rys[PIX], rzs[PIX], dep[PIX];
+        float* o[PIX];
+        bool live[PIX];
 #pragma unroll
-        for (int j = 0; j < kDLPix; ++j) {
+        for (int j = 0; j < PIX; ++j) {
             const int pix = (g0 + j) * ppw + lp;
             live[j] = dlive && g0 + j < ngroup && pix < np;
             const int pl = min(pix, np - 1);  // idle lanes recompute the last pixel (not stored)
@@ -1032,10 +1034,10 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
             dep[j] = dq;
             o[j] = orow + (int64_t)pl * out_pstride;
         }
-        float su[kDLPix], sv[kDLPix];
+        float su[PIX], sv[PIX];
         bool fast = true;
 #pragma unroll
-        for (int j = 0; j < kDLPix; ++j) {
+        for (int j = 0; j < PIX; ++j) {
             const float X = rxs[j] * dep[j], Y = rys[j] * dep[j], Z = rzs[j] * dep[j];
             const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
             const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
@@ -1045,7 +1047,7 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
         }
         if (__builtin_amdgcn_ballot_w64(!fast)) {  // rare: a quotient outside the fast path's range
 #pragma unroll
-            for (int j = 0; j < kDLPix; ++j) {
+            for (int j = 0; j < PIX; ++j) {
                 const float X = rxs[j] * dep[j], Y = rys[j] * dep[j], Z = rzs[j] * dep[j];
                 const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
                 const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
@@ -1057,30 +1059,30 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
             }
         }
 #pragma unroll
-        for (int j = 0; j < kDLPix; ++j) {
+        for (int j = 0; j < PIX; ++j) {
             const float cx = div_const(su[j] + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
             const float cy = div_const(sv[j] + 0.5f, sp.fws, rc_ws);  //          y / W
             px[j] = unnormalize(to_grid(cx), sp.half_ws);
             py[j] = unnormalize(to_grid(cy), sp.half_hs);
         }
-        f32x4 s[kDLPix];
+        f32x4 s[PIX];
         bool staged = pitch > 0;
         if (staged) {  // 16-B tap reads (ds_read_b128: 4 LDS cycles, ds_read_b96 8)
-            TapSet ts[kDLPix];
+            TapSet ts[PIX];
 #pragma unroll
-            for (int j = 0; j < kDLPix; ++j) staged = lds_issue(s_src, lbx, px[j], py[j], ts[j]) && staged;
+            for (int j = 0; j < PIX; ++j) staged = lds_issue(s_src, lbx, px[j], py[j], ts[j]) && staged;
 #pragma unroll
-            for (int j = 0; j < kDLPix; ++j) s[j] = blend_taps(ts[j]);
+            for (int j = 0; j < PIX; ++j) s[j] = blend_taps(ts[j]);
             // the unused channels' registers stay allocated until the reads are consumed
             // (else a WAW wait serialises the reads)
 #pragma unroll
-            for (int j = 0; j < kDLPix; ++j)
+            for (int j = 0; j < PIX; ++j)
                 asm volatile("" ::"v"(ts[j].a), "v"(ts[j].b), "v"(ts[j].c), "v"(ts[j].d));
         }
         if (__builtin_amdgcn_ballot_w64(!staged)) {  // wave-uniform test, then per lane
             if (!staged) {                            // a tap origin not staged: gather from global memory
 #pragma unroll
-                for (int j = 0; j < kDLPix; ++j) {
+                for (int j = 0; j < PIX; ++j) {
                     if (RAW) {
                         s[j] = raw_sample<C>(imb, is, sp.Ws, sp.Hs, px[j], py[j]);
                     } else {
@@ -1093,7 +1095,7 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
             }
         }
 #pragma unroll
-        for (int j = 0; j < kDLPix; ++j) {
+        for (int j = 0; j < PIX; ++j) {
             if (live[j]) {
                 f32xC v;
 #pragma unroll

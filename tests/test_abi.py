@@ -115,7 +115,8 @@ def test_ab_kernels_live_in_the_ab_library():
 def test_plane_sweep_routes(C):
     """mpiv_route (dry run, no GPU): the sweep's production route by depth count -- the direct
     depth-per-lane kernel for D <= 2, the pixel-per-lane kernel (one block per 256 pixels of a
-    row) for 3 <= D <= 8, the LDS-staged depth-per-lane kernel above; C > 4 the generic kernel."""
+    row) for 3 <= D <= 8, the LDS-staged depth-per-lane kernel above (one pixel per lane and
+    iteration up to D = 16); C > 4 the generic kernel."""
     B, Hs, Ws, Ht, Wt = 5, 768, 1024, 768, 1024
     for D in (1, 2, 3, 8, 9, 10, 64):
         name, grid = _lib.route("plane_sweep", B, Hs, Ws, C, D, Ht, Wt)
@@ -124,8 +125,8 @@ def test_plane_sweep_routes(C):
         elif D <= 8:
             assert name == f"plane_sweep_px_kernel<{C}, 64>", (D, name)
             assert grid == (Wt // 256) * Ht * B * 256, (D, grid)
-        else:
-            assert name.startswith(f"plane_sweep_dlane_kernel<{C}, true, 4"), (D, name)
+        else:  # one pixel per lane and iteration up to 16 depths, two above
+            assert name == f"plane_sweep_dlane_kernel<{C}, true, 4, 3072, {1 if D <= 16 else 2}>", (D, name)
     assert _lib.route("plane_sweep", B, Hs, Ws, 5, 10, Ht, Wt)[0] == "plane_sweep_kernel"
 
 
