@@ -41,8 +41,9 @@ exactly those dispatches next to its own HIP-event time.
 Legs (--legs, default all): c4 (headline), sv (single view), c2 (config 2: 64 views
 of a 1024x576x32 MPI), c3 (config 3: PSV of 5 sources into 64 planes through
 plane_sweep_torch), nb (the notebook's 224x224x10 render + training step + PSV),
-train (config-4-size training forward + backward), c5 (config 5, plane-sharded),
-cpu (the CPU baseline, rank 0 at N = 1).
+u8 (8-bit texels: config-4-shape u8 MPI, one view and V views per launch), netout (the
+network output rendered in one kernel at config 2's size), train (config-4-size training
+forward + backward), c5 (config 5, plane-sharded), cpu (the CPU baseline, rank 0 at N = 1).
 """
 from __future__ import annotations
 
@@ -67,7 +68,7 @@ from mpi_vision_amd import _host, _lib, configs, parallel  # noqa: E402
 METRIC = "rendered Mpix/sec (node) + achieved HBM GB/s fraction, 1024²×128-plane MPI"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 kWaveBytes = 64 * 16   # one 64-lane 16-B gather instruction
-ALL_LEGS = ("c4", "sv", "c2", "c3", "nb", "train", "c5", "cpu")
+ALL_LEGS = ("c4", "sv", "c2", "c3", "nb", "u8", "netout", "train", "c5", "cpu")
 # SURVEY.md §6 / BASELINE.md: the reference utils.py on torch-CPU (MKL), 8 Xeon cores,
 # measured in the survey container (the reference cannot run on the GPU box)
 REF_CPU = {"c4_Mpix_s": 0.37, "c4_s_per_view": 2.8727, "c3_s": 5.858, "c2_proxy_Mpix_s": 1.49,
@@ -205,6 +206,10 @@ def prof_fields(kernel: str, grid: int, alg_bytes: float, ms: float):
     if e:
         res["rocprof_avg_ms"] = round(e["avg_ns"] / 1e6, 4)
         res["rocprof_calls"] = e["calls"]
+        # the summary comes from another run (tools/profile.sh): a leg whose rocprof average is
+        # more than 5 % away from this run's event time is flagged, not silently quoted
+        res["rocprof_over_event"] = round(e["avg_ns"] / 1e6 / ms, 3)
+        res["rocprof_agrees_5pct"] = abs(e["avg_ns"] / 1e6 / ms - 1.0) <= 0.05
         if e.get("hbm_bytes") is not None:
             res["traffic"] = e["hbm_bytes"]
             res["traffic_over_alg"] = round(e["hbm_bytes"] / alg_bytes, 3)
@@ -493,6 +498,81 @@ def notebook_leg(dev, stream, n=50):
     return res
 
 
+def u8_leg(dev, stream, V, homs_sv, homs_v, n=10):
+    """The 8-bit texel path (the reference's own test MPI is 8-bit, test/rgba_*.png,
+    read as u8/255, utils.py:324-331): a config-4-shape u8 MPI (counter-based synthetic bytes,
+    synth.hip, packed at 4 B per texel) rendered one view per launch (the HBM-bound case) and
+    V views per launch (the headline's camera-path views).  Self-check: the single-view frame
+    equals the float render of the same MPI as u8/255 (IEEE division on the host) bit for bit."""
+    c4 = configs.config4()
+    H, W, P = c4["H"], c4["W"], c4["P"]
+    pk = _lib.synth_mpi_packed_u8(c4["seed"], H, W, 0, P, dev)
+    one = torch.empty((1, H, W, 3), device=dev)
+    many = torch.empty((V, H, W, 3), device=dev)
+    l1 = lambda: _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs_sv, 1, one, _lib._stream(dev))  # noqa: E731
+    lv = lambda: _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs_v, V, many, _lib._stream(dev))  # noqa: E731
+    for _ in range(50):
+        l1()
+    ms1 = event_ms(l1, 20, stream)
+    lv()
+    msv = event_ms(lv, n, stream)
+    # float packed copy of u8/255 (numpy fp32 division is IEEE) for the bit-exact self-check
+    f = (pk.view(torch.uint8).cpu().numpy().reshape(P, H + 4, W + 4, 4).astype(np.float32) / np.float32(255.0))
+    fpk = torch.from_numpy(f).to(dev)
+    del f
+    ref = torch.empty((1, H, W, 3), device=dev)
+    _lib._call("mpiv_render_packed", fpk, H, W, P, homs_sv, 1, ref, _lib._stream(dev))
+    same = bool(torch.equal(ref.view(torch.int32), one.view(torch.int32)))
+    del fpk, ref
+    alg1 = P * H * W * 4 + H * W * 12
+    k1, g1 = _lib.route("render_packed_u8", H, W, P, 1)
+    kv, gv = _lib.route("render_packed_u8", H, W, P, V)
+    sv = {"kernel_ms": round(ms1, 4), "alg_bytes": alg1, "alg_def": "P*H*W*4 (u8 texels) + H*W*12",
+          "achieved_gbs": hbm(alg1, ms1)[0], "frac": hbm(alg1, ms1)[1], "bound": "hbm",
+          "frame_equals_float_render_of_u8_over_255": same}
+    sv.update(prof_fields(k1, g1, alg1, ms1))
+    algv = V * alg1
+    mv_ = {"views": V, "kernel_ms": round(msv, 4), "Mpix_per_s": round(V * H * W / 1e6 / (msv * 1e-3), 1),
+           "alg_bytes": algv, "alg_gbs": hbm(algv, msv)[0],
+           "alg_frac_note": "the views share one MPI through L2: the per-view formula can exceed 1 of HBM"}
+    mv_.update(prof_fields(kv, gv, algv, msv))
+    del pk, one, many
+    torch.cuda.empty_cache()
+    return {"workload": "config-4-shape 8-bit MPI (1024x1024x128, 4-B texels): one view and the camera-path "
+                        f"launch of {V} views", "single_view": sv, "multi_view": mv_}
+
+
+def netout_leg(dev, stream, n=20):
+    """The network output rendered in one kernel (notebook mpi_from_net_output, ipynb cell 10
+    L79-111, fused into mpi_render_view_torch: render_netout_kernel) at config 2's size
+    (1024x576, 32 planes), one view; self-check against the two-step drop-ins
+    (assemble_mpi + render), bit for bit."""
+    c = configs.config2()
+    H, W, P = c["H"], c["W"], c["P"]
+    g = torch.Generator(device=dev).manual_seed(c["seed"])
+    pred = torch.rand((1, 2 * P + 3, H, W), generator=g, device=dev) * 2 - 1
+    fg = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    homs = _host.render_homographies(configs.f32(c["poses"][5:6]), configs.f32(c["depths"]),
+                                     configs.f32([c["K"]]), 1).to(dev)
+    out = torch.empty((1, H, W, 3), device=dev)
+    launch = lambda: _lib._call("mpiv_render_net_output", pred, _lib._strides(pred), fg, _lib._strides(fg), 1,  # noqa: E731
+                                H, W, P, homs, out, _lib._stream(dev))
+    for _ in range(20):
+        launch()
+    ms = event_ms(launch, n, stream)
+    two = _lib.render(_lib.assemble_mpi(pred, fg, P), homs)
+    same = bool(torch.equal(two.view(torch.int32), out.view(torch.int32)))
+    alg = H * W * ((2 * P + 3) * 4 + 12 + 12)
+    kname, grid = _lib.route("render_net_output", 1, H, W, P)
+    res = {"workload": "network output [1, 2P+3, 576, 1024] (P = 32) + reference image -> rendered view, one kernel",
+           "kernel_ms": round(ms, 4), "alg_bytes": alg, "alg_def": "H*W*((2P+3)*4 + 12 + 12): prediction + "
+           "reference image read, frame written", "achieved_gbs": hbm(alg, ms)[0], "frac": hbm(alg, ms)[1],
+           "bound": "hbm", "equals_assemble_then_render": same}
+    res.update(prof_fields(kname, grid, alg, ms))
+    del pred, fg, out, two
+    return res
+
+
 def training_leg(dev, stream, n=10):
     """The training caller's path at config-4 size (notebook loss, ipynb cell 12 L42: a
     non-broadcast [1,H,W,P,4] MPI rendered and differentiated): the training forward
@@ -515,6 +595,7 @@ def training_leg(dev, stream, n=10):
     g2 = _lib.render_backward(mpi, homs, dout, workspace=ws)
     bwd2_ms = event_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws), n, stream)
     flag = int(ws[_lib.bwd_flag_offset(H, W, P):][:4].view(torch.int32).item())
+    aborted = _lib.render_backward_status(ws, H, W, P)
     same = bool(torch.equal(g1.view(torch.int32), g2.view(torch.int32)))
     mpi_bytes = P * H * W * 16
     f_alg = mpi_bytes + H * W * 12
@@ -528,7 +609,7 @@ def training_leg(dev, stream, n=10):
            "backward_alg_bytes": b_alg,
            "backward_alg_def": "MPI read + d MPI written + d frame read (workspace traffic not counted)",
            "backward_hbm_frac": hbm(b_alg, bwd_ms)[1],
-           "workspace_GB": round(ws.numel() / 1e9, 3), "fallback_flag": flag,
+           "workspace_GB": round(ws.numel() / 1e9, 3), "fallback_flag": flag, "fallback_aborted_views": aborted,
            "ckpt_grad_bit_identical": same, "inference": prof_fields(kname, grid, f_alg, inf_ms)}
     del mpi, ws, g1, g2, ck
     torch.cuda.empty_cache()
@@ -679,6 +760,8 @@ def main():
     torch.cuda.empty_cache()
     nb = notebook_leg(dev, stream) if "nb" in legs else None
     torch.cuda.empty_cache()
+    nout = netout_leg(dev, stream) if "netout" in legs else None
+    torch.cuda.empty_cache()
 
     run(args.warmup, 0)
     torch.cuda.synchronize()
@@ -703,12 +786,17 @@ def main():
     timed_frame_sha = one_sha = None
     peak_gbs = float("nan")
     gathers = None
+    frame_checks = []
     if extras:
         one = torch.empty((1, H, W, 3), device=dev)
-        timed_frame_sha = sha16(out[0])
-        launch(host_homs(last, 1).to(dev), 1, one)
-        torch.cuda.synchronize()
-        one_sha = sha16(one[0])
+        idx = step_indices(last)
+        for j in sorted({0, V // 2, V - 1}):
+            h1 = _host.render_homographies(poses[idx[j]:idx[j] + 1], depths, K.expand(1, 3, 3), 1).to(dev)
+            launch(h1, 1, one)
+            frame_checks.append({"view": j, "pose": idx[j], "sha16": sha16(out[j]),
+                                 "bit_exact": bool(torch.equal(out[j].view(torch.int32), one[0].view(torch.int32)))})
+        timed_frame_sha = frame_checks[0]["sha16"]
+        one_sha = timed_frame_sha if all(c["bit_exact"] for c in frame_checks) else None
         peak_gbs = gather_peak_gbs(dev, stream)
         # the texture path's real work in the timed launches: the counting build of the same
         # kernel (mpiv_render_packed_census) re-renders the timed steps and adds up the
@@ -744,6 +832,9 @@ def main():
         del view, packed
     torch.cuda.empty_cache()
 
+    u8 = None
+    if "u8" in legs:
+        u8 = u8_leg(dev, stream, V, host_homs(0, 1).to(dev), host_homs(0).to(dev))
     train = training_leg(dev, stream) if "train" in legs else None
     c5 = config5_leg(world, rank, dev, max(3, args.steps // 2), 1) if "c5" in legs else None
     ranks = {"world_size_seen": world, "backend": backend, "per_rank_kernel_ms": [round(x, 4) for x in kern_all]}
@@ -787,13 +878,16 @@ def main():
                 "rocprof": {k: v for k, v in pf.items() if k not in ("kernel", "grid_workitems")},
                 "single_view": sv,
             },
-            "timed_frame_check": {"frame": "view 0 of the last timed launch vs a 1-view launch of its pose",
+            "timed_frame_check": {"frames": "views 0, V/2 and V-1 of the last timed launch, each vs a 1-view "
+                                            "launch of its pose", "views": frame_checks,
                                   "sha16": timed_frame_sha, "bit_exact": timed_frame_sha == one_sha}
             if extras else None,
             "cpu_baseline": None,
             "config2": c2,
             "config3_psv": c3,
             "notebook": nb,
+            "u8_texels": u8,
+            "net_output_render": nout,
             "training_render_backward": train,
             "config5_plane_sharded": c5,
         }

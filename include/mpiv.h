@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 10
+#define MPIV_ABI_VERSION 11
 
 enum {
     MPIV_OK = 0,
@@ -63,6 +63,8 @@ int mpiv_debug_set(const char *name, int value);
  *   "render_packed", "render_packed_ct"  {H, W, P, V}        (mpiv_render_packed[_ct])
  *   "render"                             {B, H, W, P}        (mpiv_render, contiguous MPI)
  *   "plane_sweep"                        {B, Hs, Ws, C, D, Ht, Wt} (mpiv_plane_sweep)
+ *   "render_packed_u8"                   {H, W, P, V}        (mpiv_render_packed_u8)
+ *   "render_net_output"                  {B, H, W, P}        (mpiv_render_net_output)
  * Fails while a debug option is set (it reports production routes only). */
 int mpiv_route(const char *entry, const int64_t *args, int nargs, char *name, int name_cap, int64_t *grid_threads);
 
@@ -140,6 +142,16 @@ int mpiv_render_homographies(const float *pose, const float *depths, const float
 int mpiv_render_homographies_device(const float *pose, const float *depths, const float *K, const float *Kinv,
                                     int B, int P, float *H, void *stream);
 
+/* HOST function: proj = [[K_src, 0], [0, 0, 0, 1]] @ pose [B][4][4] for the plane sweep /
+ * inverse warp (projective_inverse_warp_torch[2], utils.py:428-438, 747-757: the torch.cat
+ * of the padded K, then torch.matmul), bit-identical to the reference's torch-CPU fp32 ops.
+ * Ks: [B][3][3] at batch stride ks_bstride floats (0: one K for every pose). */
+int mpiv_psv_proj(const float *Ks, int64_t ks_bstride, const float *pose, int B, float *proj);
+
+/* The same on the device (Ks, pose, proj in device memory), bit-identical to the host
+ * entry: the PSV drop-ins use it when the pose already lives in HBM. */
+int mpiv_psv_proj_device(const float *Ks, int64_t ks_bstride, const float *pose, int B, float *proj, void *stream);
+
 /* ---- render backward ------------------------------------------------------ */
 
 /* Workspace bytes mpiv_render_backward needs for one H x W x P MPI (reused across
@@ -161,10 +173,19 @@ size_t mpiv_render_backward_workspace_size(int H, int W, int P);
  * dmpi:    [V,H,W,P,4] contiguous, 16-byte aligned: view v's gradient is written (not
  *          accumulated);
  * workspace: >= mpiv_render_backward_workspace_size(H, W, P) bytes, 256-B aligned.
- * Deterministic (no float atomics); H*W < 2^26, P*H*W < 2^31. */
+ * Deterministic (no float atomics); H*W < 2^26, P*H*W < 2^31.
+ * A view the tile gather cannot prove complete runs the bucket fallback, whose phases are
+ * ordered by tickets (no co-residency assumption: safe beside other streams and processes).
+ * If a fallback wait ever outlasts its poll limit (not expected), that view's gradient is
+ * NaN-filled and counted; mpiv_render_backward_status reports the count. */
 int mpiv_render_backward(const float *mpi, const int64_t mpi_strides[5], int V, int H, int W, int P,
                          const float *homs, const float *dout, const float *ckpt, float *dmpi,
                          void *workspace, size_t workspace_bytes, void *stream);
+
+/* Views of the last mpiv_render_backward call on this workspace (same H, W, P) whose
+ * fallback aborted -> *aborted_views.  SYNCHRONISES the stream (the one entry point that
+ * does): a checker for tests and debug runs, not for the training loop. */
+int mpiv_render_backward_status(const void *workspace, int H, int W, int P, int *aborted_views, void *stream);
 
 /* ---- MPI assembly from the network output ------------------------------- */
 

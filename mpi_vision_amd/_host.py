@@ -72,16 +72,19 @@ def _kinv_device(intrinsics: torch.Tensor, batch: int, dev) -> torch.Tensor:
         ver = intrinsics._version
     except RuntimeError:  # inference tensors track no version: no memo
         ver = None
+    # the stream is part of the key: the copy's memory, once evicted, is reused in the order of
+    # the stream that allocated it, so each stream reads only its own copy
+    stream = torch.cuda.current_stream(dev).cuda_stream
     ent = _KINV_DEV.get(id(intrinsics))
     if (ver is not None and ent is not None and ent[0]() is intrinsics and ent[1] == ver and ent[2] == batch
-            and ent[3].device == dev):
+            and ent[3].device == dev and ent[4] == stream):
         return ent[3]
     K = _cpu32(intrinsics).expand(batch, 3, 3).contiguous()
     kinv = _inverse_cached(K).to(dev)
     if ver is not None:
         if len(_KINV_DEV) >= 64:
             _KINV_DEV.clear()
-        _KINV_DEV[id(intrinsics)] = (weakref.ref(intrinsics), ver, batch, kinv)
+        _KINV_DEV[id(intrinsics)] = (weakref.ref(intrinsics), ver, batch, kinv, stream)
     return kinv
 
 
@@ -180,4 +183,30 @@ def psv_matrices(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pos
     ki, proj = ki.reshape(B, 9).contiguous(), proj.reshape(B, 16).contiguous()
     if pin:
         ki, proj = ki.pin_memory(), proj.pin_memory()
+    return ki, proj
+
+
+def psv_matrices_device(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pose: torch.Tensor,
+                        batch: int):
+    """psv_matrices for a pose that lives on a ROCm device (the notebook's dataset call keeps
+    pose and K in HBM, ipynb cell 8 L49-75): Ki = inverse(K_tgt) memoised on the intrinsics
+    tensor object and its version (_kinv_device: one LAPACK inverse per camera, as the
+    reference), proj = K4_src @ pose by mpiv_psv_proj_device on the current stream (the host
+    entry's restatement, bit-identical).  No device-to-host copy, no page-locked staging.
+    Intrinsics [3,3] (one camera for the batch) or [batch,3,3]; pose [batch,4,4]."""
+    from . import _lib
+    dev = pose.device
+    ki = _kinv_device(tgt_intrinsics, batch, dev).reshape(batch, 9)
+    Ks = src_intrinsics.to(device=dev, dtype=_F32)
+    if Ks.dim() == 2:
+        Ks = Ks.contiguous()
+        ks_b = 0
+    else:
+        Ks = Ks.expand(batch, 3, 3)
+        if Ks.stride(1) != 3 or Ks.stride(2) != 1:
+            Ks = Ks.contiguous()
+        ks_b = Ks.stride(0)
+    pose_d = pose.to(dtype=_F32).reshape(batch, 4, 4).contiguous()
+    proj = torch.empty((batch, 16), dtype=_F32, device=dev)
+    _lib._call("mpiv_psv_proj_device", Ks, ks_b, pose_d, batch, proj, _lib._stream(dev))
     return ki, proj

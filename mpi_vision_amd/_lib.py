@@ -53,6 +53,7 @@ _SIGS = {
     "mpiv_preprocess": [_vp, _i64, _vp, _vp],
     "mpiv_deprocess_u8": [_vp, _i64, _vp, _vp],
     "mpiv_render_backward": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp],
+    "mpiv_render_backward_status": [_vp, _int, _int, _int, ctypes.POINTER(_int), _vp],
     "mpiv_render_train": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp],
     "mpiv_render_packed_census": [_vp, _int, _int, _int, _vp, _int, _vp, _vp, _vp],
     "mpiv_plane_sweep_into": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _i64, _i64,
@@ -63,6 +64,8 @@ _SIGS = {
     "mpiv_assemble_mpi_packed": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_render_homographies": [_vp, _vp, _vp, _vp, _int, _int, _vp],
     "mpiv_render_homographies_device": [_vp, _vp, _vp, _vp, _int, _int, _vp, _vp],
+    "mpiv_psv_proj": [_vp, _i64, _vp, _int, _vp],
+    "mpiv_psv_proj_device": [_vp, _i64, _vp, _int, _vp, _vp],
     "mpiv_pack_planes_u8": [_vp, _c_i64p, _int, _int, _int, _vp, _vp],
     "mpiv_render_net_output": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp],
     "mpiv_render_packed_u8": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
@@ -74,7 +77,7 @@ _SIGS = {
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
                           "mpiv_build_id", "mpiv_debug_set")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _lib = None
 _lib_ab = None
@@ -550,15 +553,30 @@ def render_train(rgba_layers: torch.Tensor, homs: torch.Tensor):
     return out, ckpt
 
 
+# MPIV_BWD_CHECK=1: every render_backward reads the fallback's abort count back (one stream
+# synchronisation per call) and raises if a view's gradient was NaN-filled (render_bwd.hip)
+BWD_CHECK = os.environ.get("MPIV_BWD_CHECK") == "1"
+
+
+def render_backward_status(workspace: torch.Tensor, H: int, W: int, P: int) -> int:
+    """Views of the last render_backward on this workspace whose bucket fallback aborted
+    (their gradients are NaN); synchronises the current stream (mpiv_render_backward_status)."""
+    n = _int(0)
+    _call("mpiv_render_backward_status", workspace, H, W, P, ctypes.byref(n), _stream(workspace.device))
+    return n.value
+
+
 def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.Tensor,
-                    workspace: torch.Tensor | None = None, ckpt: torch.Tensor | None = None) -> torch.Tensor:
+                    workspace: torch.Tensor | None = None, ckpt: torch.Tensor | None = None,
+                    check: bool | None = None) -> torch.Tensor:
     """d(mpi_render_view_torch)/d(rgba_layers): rgba_layers [B,H,W,P,4] (read in place when
     its planes are contiguous per pixel, incl. a stride-0 broadcast batch; other layouts
     are made contiguous first), homs [B,P,9] (the forward's), dout [B,H,W,3] ->
     [B,H,W,P,4] contiguous, one gradient per view (a broadcast input's views are summed
     by autograd's expand backward, as in the reference).  Bit-exact to the reference's
     CPU autograd (render_bwd.hip).  ckpt: render_train()'s checkpoints of the same views
-    (skips recomputing the forward composite)."""
+    (skips recomputing the forward composite).  check (default MPIV_BWD_CHECK): read the
+    fallback's abort count back and raise if any view aborted (costs a synchronisation)."""
     dev = _dev(rgba_layers, dout)
     B, H, W, P, _ = rgba_layers.shape
     if tuple(dout.shape) != (B, H, W, 3):
@@ -576,6 +594,11 @@ def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.T
                              or ckpt.device != dev or ckpt.dtype != torch.float32):
         raise RuntimeError(f"ckpt must be render_train()'s contiguous [{B},{(P + 7) // 8},{H},{W},4] tensor")
     _call("mpiv_render_backward", src, _strides(src), B, H, W, P, h, dout, ckpt, grad, ws, ws.numel(), _stream(dev))
+    if BWD_CHECK if check is None else check:
+        n = render_backward_status(ws, H, W, P)
+        if n:
+            raise RuntimeError(f"mpiv_render_backward: the bucket fallback aborted on {n} of {B} views "
+                               "(their gradients are NaN)")
     return grad
 
 
@@ -701,7 +724,9 @@ def _depths_on(depth_planes, dev) -> torch.Tensor:
     if isinstance(depth_planes, torch.Tensor):
         return depth_planes.detach().to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
     vals = tuple(float(x) for x in depth_planes)
-    key = (vals, str(dev))
+    # keyed on the stream too: the copy is allocated on (and its memory, once evicted, reused
+    # in the order of) the stream that made it, so each stream reads only its own copy
+    key = (vals, str(dev), torch.cuda.current_stream(dev).cuda_stream)
     d = _DEPTHS_DEV.get(key)
     if d is None:
         if len(_DEPTHS_DEV) >= 64:

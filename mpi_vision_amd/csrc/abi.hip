@@ -87,6 +87,11 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      forces their per-sample global fallback (tests)
 //   bwd_fallback=1     mpiv_render_backward skips the tile gather and runs its bucket
 //                      fallback for every view (tests)
+//   bwd_poll_limit=k   (A/B build) the backward fallback's waits give up after k polls instead of
+//                      2^24; -1: at the first wait -- tests provoke the abort path with it (NaN
+//                      gradient, counted by mpiv_render_backward_status)
+//   bwd_fb_blocks=k    (A/B build) the backward fallback launches k blocks instead of the resident
+//                      count (tests: far more blocks than fit at once still complete, by tickets)
 //   bwd_margin=k       the tile gather's pixel-window margin in 1/64 pixel (default 16);
 //                      negative values make windows miss contributors, which the pair
 //                      count must catch (tests)
@@ -95,14 +100,14 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
-                kNumOpts };
+                kOptBwdPollLimit, kOptBwdFbBlocks, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
-                                         "sweep_direct"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0};
+                                         "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks"};
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -122,6 +127,7 @@ bool ab_only(int o, int v) {
         case kOptChunkFlight: return v == 4;
         case kOptSweepRows: return v == 6 || v == 8;
         case kOptBwdGather: return v == 1 || v == 2;
+        case kOptBwdPollLimit: case kOptBwdFbBlocks: return v != 0;
         default: return false;
     }
 }
@@ -588,7 +594,7 @@ size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
     char* inv = take((size_t)P * 12 * 4);
     char* truth = take(kCtrSlots * 8);
     char* found = take(kCtrSlots * 8);
-    char* flag = take(16);
+    char* flag = take(32);
     const size_t ntiles = (size_t)((W + kGTW - 1) / kGTW) * ((H + kGTH - 1) / kGTH);
     char* box = take((size_t)P * ntiles * 16);
     char* key = take((size_t)pc * hw * 4);
@@ -663,8 +669,8 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const int force = opt(kOptBwdFallback) != 0 || !fast;
     const float margin = (float)opt(kOptBwdMargin) / 64.0f;
     hipStream_t q = S(stream);
-    // fallback grid: every block resident (its phases meet at grid barriers), at most 4 per CU; queried
-    // once per device (relaxed atomics: racing first calls store the same value)
+    // fallback grid: at most the blocks that fit at once, <= 4 per CU (more would only wait for
+    // tickets); queried once per device (relaxed atomics: racing first calls store the same value)
     static int s_fb_blocks[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(MPIV_ERR_HIP, "%s: hipGetDevice failed", nm);
@@ -681,7 +687,9 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         fbb = ncu * std::min(std::min(pc_t, pc_f), 4);
         __atomic_store_n(&s_fb_blocks[dev], fbb, __ATOMIC_RELAXED);
     }
-    const unsigned fb_blocks = (unsigned)fbb;
+    const unsigned fb_blocks = opt(kOptBwdFbBlocks) > 0 ? (unsigned)opt(kOptBwdFbBlocks) : (unsigned)fbb;
+    const int pl = opt(kOptBwdPollLimit);
+    const unsigned poll_limit = pl > 0 ? (unsigned)pl : pl < 0 ? 0u : (1u << 24);
     if (hipMemsetAsync(ws.truth, 0, 2 * kCtrSlots * 8 + 256, q) != hipSuccess)  // truth, found (adjacent)
         return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
     for (int v = 0; v < V; ++v) {
@@ -725,13 +733,30 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
             }
         }
         bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force);
-        // fallback: one launch of resident blocks, returns at once unless flagged
+        // fallback: one launch, returns at once unless flagged; its phases are ordered by tickets
+        // (render_bwd.hip), so it completes however many of its blocks are resident
         if (fast)
-            bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv);
+            bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit);
         else
-            bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv);
+            bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit);
+        // an aborted fallback (never expected) leaves a NaN gradient, never a plausible one
+        bwd_poison_kernel<<<256, 256, 0, q>>>(ws.flag, gv, (int64_t)P * HW);
     }
     return launched(nm);
+}
+
+int mpiv_render_backward_status(const void* workspace, int H, int W, int P, int* aborted_views, void* stream) {
+    const char* nm = "mpiv_render_backward_status";
+    if (!workspace || !aborted_views) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    BwdWs ws;
+    bwd_layout(H, W, P, static_cast<char*>(const_cast<void*>(workspace)), &ws);
+    hipStream_t q = S(stream);
+    if (hipMemcpyAsync(aborted_views, ws.flag + 4, sizeof(int), hipMemcpyDeviceToHost, q) != hipSuccess ||
+        hipStreamSynchronize(q) != hipSuccess)
+        return fail(MPIV_ERR_HIP, "%s: copy failed", nm);
+    g_err[0] = '\0';
+    return MPIV_OK;
 }
 
 int mpiv_combine_ct(const float* parts, int G, int64_t n, float* out, void* stream) {
@@ -1177,6 +1202,7 @@ int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* 
     const RenderGeom g = make_geom(H, W, P);
     const int64_t nb = (int64_t)blocks(W, kNTX) * blocks(H, kNTY) * B;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+    if (g_route) return note_route(nb, kNThreads, "render_netout_kernel");
     render_netout_kernel<<<(unsigned)nb, kNThreads, 0, S(stream)>>>(pred, fg, s, g, B, homs, out);
     return launched(nm);
 }
@@ -1209,6 +1235,26 @@ int mpiv_render_homographies_device(const float* pose, const float* depths, cons
     if (!pose || !depths || !K || !Kinv || !H) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
     if (B <= 0 || P <= 0 || (int64_t)B * P >= (1ll << 31)) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
     render_homographies_kernel<<<blocks((int64_t)B * P, 256), 256, 0, S(stream)>>>(pose, depths, K, Kinv, B, P, H);
+    return launched(nm);
+}
+
+// proj = [[K_src, 0], [0, 0, 0, 1]] @ pose for projective_inverse_warp_torch[2] (utils.py:428-438,
+// 747-757), torch-CPU rounding restated (geometry.hip psv_proj): on the host ...
+int mpiv_psv_proj(const float* Ks, int64_t ks_bstride, const float* pose, int B, float* proj) {
+    if (!Ks || !pose || !proj) return fail(MPIV_ERR_ARG, "mpiv_psv_proj: null pointer");
+    if (B <= 0 || ks_bstride < 0) return fail(MPIV_ERR_ARG, "mpiv_psv_proj: bad shape");
+    for (int b = 0; b < B; ++b) psv_proj(Ks + (int64_t)b * ks_bstride, pose + (int64_t)b * 16, proj + (int64_t)b * 16);
+    g_err[0] = '\0';
+    return MPIV_OK;
+}
+
+// ... and on the device, for poses / intrinsics already in HBM (the notebook's dataset call,
+// ipynb cell 8 L49-75): no device-to-host copy; bit-identical to the host entry
+int mpiv_psv_proj_device(const float* Ks, int64_t ks_bstride, const float* pose, int B, float* proj, void* stream) {
+    const char* nm = "mpiv_psv_proj_device";
+    if (!Ks || !pose || !proj) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (B <= 0 || ks_bstride < 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    psv_proj_kernel<<<blocks(B, 64), 64, 0, S(stream)>>>(Ks, ks_bstride, pose, B, proj);
     return launched(nm);
 }
 
@@ -1290,6 +1336,7 @@ static int render_u8_impl(const uint32_t* packed, int H, int W, int P, int p_beg
     const int R = rt == 0 ? (vs ? 4 : 2) : vs ? rt : rt == 8 ? 8 : 2;
     const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+    if (g_route) return note_route(nb, 256, "render_u8_kernel<%s, %d, %s>", ct ? "true" : "false", R, vs ? "true" : "false");
     const unsigned* pk = reinterpret_cast<const unsigned*>(packed);
     hipStream_t q = S(stream);
 #define MPIV_U8(CT, RR, VV)                                                                                       \
@@ -1355,6 +1402,13 @@ int mpiv_route(const char* entry, const int64_t* a, int na, char* name, int name
     } else if (strcmp(entry, "render_train") == 0 && na == 4) {
         const int64_t P = a[3], st[5] = {a[1] * a[2] * P * 4, a[2] * P * 4, P * 4, 4, 1};
         rc = mpiv_render_train(d, st, (int)a[0], (int)a[1], (int)a[2], (int)P, d, d, d, nullptr);
+    } else if (strcmp(entry, "render_packed_u8") == 0 && na == 4) {
+        rc = render_u8_impl(reinterpret_cast<const uint32_t*>(d), (int)a[0], (int)a[1], (int)a[2], 0, (int)a[2], 1, d,
+                            (int)a[3], d, false, nullptr);
+    } else if (strcmp(entry, "render_net_output") == 0 && na == 4) {
+        const int64_t B = a[0], H = a[1], W = a[2], P = a[3];
+        const int64_t ps[4] = {(2 * P + 3) * H * W, H * W, W, 1}, fs[4] = {H * W * 3, W * 3, 3, 1};
+        rc = mpiv_render_net_output(d, ps, d, fs, (int)B, (int)H, (int)W, (int)P, d, d, nullptr);
     } else if (strcmp(entry, "render") == 0 && na == 4) {
         const int64_t P = a[3], st[5] = {a[1] * a[2] * P * 4, a[2] * P * 4, P * 4, 4, 1};
         rc = mpiv_render(d, st, (int)a[0], (int)a[1], (int)a[2], (int)P, d, d, nullptr);

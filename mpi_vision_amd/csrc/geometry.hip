@@ -193,4 +193,30 @@ __global__ __launch_bounds__(256) void render_homographies_kernel(const float* _
     render_hom_chain(pose + (int64_t)b * 16, depths[p], K + (int64_t)b * 9, Kinv + (int64_t)b * 9, H + i * 9);
 }
 
+// ---------------------------------------------------------------------------
+// PSV projection (projective_inverse_warp_torch[2], utils.py:428-438, 747-757):
+//   proj = [[K_src, 0], [0, 0, 0, 1]] @ pose  (torch.cat of the padded K, then torch.matmul;
+// torch's CPU matmul of 4x4 batches rounds as plain products summed in ascending k, like the
+// render chain's: tests/test_host.py checks the host entry against torch bit for bit).
+// ---------------------------------------------------------------------------
+__host__ __device__ inline void psv_proj(const float* Ks, const float* pose, float* proj) {
+    float k4[16];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) k4[i * 4 + j] = Ks[i * 3 + j];
+        k4[i * 4 + 3] = 0.0f;
+    }
+    k4[12] = 0.0f;
+    k4[13] = 0.0f;
+    k4[14] = 0.0f;
+    k4[15] = 1.0f;
+    mm<4, 4, 4>(k4, pose, proj);
+}
+
+__global__ __launch_bounds__(64) void psv_proj_kernel(const float* __restrict__ Ks, int64_t ks_bstride,
+                                                      const float* __restrict__ pose, int B,
+                                                      float* __restrict__ proj) {
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b < B) psv_proj(Ks + (int64_t)b * ks_bstride, pose + (int64_t)b * 16, proj + (int64_t)b * 16);
+}
+
 }  // namespace mpiv

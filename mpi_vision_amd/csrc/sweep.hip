@@ -1234,7 +1234,7 @@ __global__ __launch_bounds__(256) void plane_sweep_px_kernel(const float* __rest
                                                              int64_t out_pstride, int vec) {
     static_assert(PW == 32 || PW == 64, "a wave is one or two pixel groups");
     constexpr int DS = kWave / PW;  // depths per step
-    extern __shared__ float px_lds[];
+    extern __shared__ __attribute__((aligned(16))) float px_lds[];  // read through f32x4
     const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = blockIdx.z, y = blockIdx.y;
     const int x0 = (blockIdx.x * 4 + wave) * PW;

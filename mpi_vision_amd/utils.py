@@ -235,7 +235,7 @@ def projective_inverse_warp_torch(img, depth, pose, intrinsics, ret_flows=False)
         raise RuntimeError("projective_inverse_warp_torch: ret_flows=True is not supported "
                            "(the reference raises a shape mismatch, utils.py:447-448)")
     batch, height, width, _ = img.shape
-    ki, proj = _host.psv_matrices(intrinsics, intrinsics, pose)
+    ki, proj = _warp_matrices(img, pose, intrinsics, intrinsics)
     return _lib.inverse_warp_depthmap(img, depth, ki, proj, height, width)
 
 
@@ -243,8 +243,25 @@ def plane_sweep_torch(img, depth_planes, pose, intrinsics):
     """Plane-sweep volume [B, H, W, D*C] (channel d*C+c) of img [B, H, W, C] at the
     listed depths (utils.py:452-471).  One HIP launch writes the whole volume."""
     batch, height, width, _ = img.shape
-    ki, proj = _host.psv_matrices(intrinsics, intrinsics, pose, pin=img.is_cuda)
+    return _plane_sweep(img, depth_planes, pose, intrinsics, intrinsics, height, width)
+
+
+def _plane_sweep(img, depth_planes, pose, src_intrinsics, tgt_intrinsics, height, width):
+    if img.is_cuda and pose.is_cuda:  # pose in HBM: its matrices are formed there too
+        ki, proj = _host.psv_matrices_device(src_intrinsics, tgt_intrinsics, pose, pose.shape[0])
+    else:
+        ki, proj = _host.psv_matrices(_batched(src_intrinsics), _batched(tgt_intrinsics), pose, pin=img.is_cuda)
     return _lib.plane_sweep(img, depth_planes, ki, proj, height, width)
+
+
+def _batched(k):
+    return k.unsqueeze(0) if k.dim() == 2 else k
+
+
+def _warp_matrices(img, pose, src_intrinsics, tgt_intrinsics):
+    if img.is_cuda and pose.is_cuda:
+        return _host.psv_matrices_device(src_intrinsics, tgt_intrinsics, pose, pose.shape[0])
+    return _host.psv_matrices(src_intrinsics, tgt_intrinsics, pose)
 
 
 def format_network_input_torch(self, ref_image, psv_src_images, ref_pose, psv_src_poses, planes, intrinsics):
@@ -259,9 +276,10 @@ def format_network_input_torch(self, ref_image, psv_src_images, ref_pose, psv_sr
 
 
 def plane_sweep_torch_one(img, depth_planes, pose, intrinsics):
-    """Unbatched PSV of img [H, W, C]; returns [1, H, W, D*C] (utils.py:513-533)."""
-    return plane_sweep_torch(img.unsqueeze(0), depth_planes, pose.unsqueeze(0),
-                             intrinsics.unsqueeze(0))
+    """Unbatched PSV of img [H, W, C]; returns [1, H, W, D*C] (utils.py:513-533).  The
+    caller's own intrinsics tensor (not a per-call view of it) keys the memoised inverse."""
+    return _plane_sweep(img.unsqueeze(0), depth_planes, pose.unsqueeze(0), intrinsics, intrinsics,
+                        img.shape[0], img.shape[1])
 
 
 def projective_inverse_warp_torch2(img, depth, pose, src_intrinsics, tgt_intrinsics,
@@ -271,7 +289,7 @@ def projective_inverse_warp_torch2(img, depth, pose, src_intrinsics, tgt_intrins
     if ret_flows:
         raise RuntimeError("projective_inverse_warp_torch2: ret_flows=True is not supported "
                            "(the reference raises a shape mismatch, utils.py:766-767)")
-    ki, proj = _host.psv_matrices(src_intrinsics, tgt_intrinsics, pose)
+    ki, proj = _warp_matrices(img, pose, src_intrinsics, tgt_intrinsics)
     return _lib.inverse_warp_depthmap(img, depth, ki, proj, tgt_height, tgt_width)
 
 
@@ -279,6 +297,5 @@ def plane_sweep_torch_one2(img, depth_planes, pose, src_intrinsics, tgt_intrinsi
                            tgt_height, tgt_width):
     """PSV of img [H_s, W_s, C] into a (tgt_height, tgt_width) target grid with separate
     intrinsics; returns [1, tgt_height, tgt_width, D*C] (utils.py:771-799)."""
-    ki, proj = _host.psv_matrices(src_intrinsics.unsqueeze(0), tgt_intrinsics.unsqueeze(0),
-                                  pose.unsqueeze(0), pin=img.is_cuda)
-    return _lib.plane_sweep(img.unsqueeze(0), depth_planes, ki, proj, tgt_height, tgt_width)
+    return _plane_sweep(img.unsqueeze(0), depth_planes, pose.unsqueeze(0), src_intrinsics, tgt_intrinsics,
+                        tgt_height, tgt_width)

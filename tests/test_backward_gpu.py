@@ -50,9 +50,11 @@ def _backward_flag(mpi, homs, dout, dev):
     ws = torch.zeros(L.mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
     got = _lib.render_backward(mpi, homs, dout, workspace=ws)
     off = _lib.bwd_flag_offset(H, W, P)
-    words = ws[off:off + 12].view(torch.int32).tolist()
-    # words[1]: the fallback's grid-barrier counter; words[2]: a barrier wait that timed out
-    assert words[2] == 0, "the fallback's grid barrier timed out"
+    words = ws[off:off + 20].view(torch.int32).tolist()
+    # words[1], [2]: the fallback's ticket and completion counters; [3], [4]: this view's /
+    # this call's aborted fallbacks (a wait that outlasted its poll limit)
+    assert words[3] == 0 and words[4] == 0, "the fallback aborted"
+    assert _lib.render_backward_status(ws, H, W, P) == 0
     return got, words[0]
 
 
@@ -280,3 +282,48 @@ def test_training_forward_checkpoints(cfg, rows, dev, kopts):
     a = _lib.render_backward(mpi, homs, dout)
     b = _lib.render_backward(mpi, homs, dout, ckpt=ck)
     assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+def _medium_case(V=2):
+    H, W, P = 64, 96, 12
+    mpi = configs.synthetic_mpi(V, H, W, P, 19)
+    c = configs.config4()
+    K = configs.f32([configs.intrinsics_matrix(90.0, 90.0, 48.0, 32.0)] * V)
+    homs = _host.render_homographies(configs.f32(c["poses"][40:40 + V]), configs.f32(configs.inv_depths(1, 80, P)),
+                                     K, V)
+    dout = torch.rand((V, H, W, 3), generator=torch.Generator().manual_seed(23)) * 2 - 1
+    return mpi, homs, dout
+
+
+def test_backward_fallback_more_blocks_than_resident(dev, kopts):
+    """The fallback's phases are ordered by tickets, not by a barrier over resident blocks
+    (ADVICE r3): launched with 20000 blocks -- far more than the device holds at once, which a
+    grid barrier could never release -- it completes, bit-exact to the oracle, nothing aborted."""
+    mpi, homs, dout = _medium_case()
+    want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
+    kopts(bwd_fallback=1, bwd_fb_blocks=20000)
+    got, flag = _backward_flag(mpi.to(dev), homs, dout.to(dev), dev)
+    assert flag == 1
+    assert_bits(got, want, "fallback over 20000 blocks")
+
+
+def test_backward_fallback_abort_is_loud(dev, kopts):
+    """A fallback wait that outlasts its poll limit (forced here at the first wait) never
+    returns a plausible gradient: every aborted view is NaN, the status call counts them and
+    render_backward(check=True) raises."""
+    V = 2
+    mpi, homs, dout = _medium_case(V)
+    B, H, W, P, _ = mpi.shape
+    kopts(bwd_fallback=1, bwd_poll_limit=-1)
+    L = _lib.load()
+    ws = torch.zeros(L.mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    got = _lib.render_backward(mpi.to(dev), homs, dout.to(dev), workspace=ws, check=False)
+    assert _lib.render_backward_status(ws, H, W, P) == V
+    assert torch.isnan(got).all()
+    with pytest.raises(RuntimeError, match="aborted on 2 of 2 views"):
+        _lib.render_backward(mpi.to(dev), homs, dout.to(dev), workspace=ws, check=True)
+    # the production tile path on the same workspace: nothing aborted, the count starts over
+    kopts(bwd_fallback=0, bwd_poll_limit=0)
+    want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
+    got = _lib.render_backward(mpi.to(dev), homs, dout.to(dev), workspace=ws, check=True)
+    assert_bits(got, want, "after an abort")

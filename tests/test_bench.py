@@ -24,7 +24,7 @@ def test_leg_selection(monkeypatch):
     assert _parse(monkeypatch).legs == list(bench.ALL_LEGS)
     assert _parse(monkeypatch, "--no-extras").legs == ["c4"]
     a = _parse(monkeypatch, "--no-config5", "--no-training", "--cpu-seconds", "0")
-    assert a.legs == ["c4", "sv", "c2", "c3", "nb"]
+    assert a.legs == ["c4", "sv", "c2", "c3", "nb", "u8", "netout"]
     assert _parse(monkeypatch, "--legs", "c3").legs == ["c3"]
     with pytest.raises(SystemExit):
         _parse(monkeypatch, "--legs", "c9")
@@ -88,3 +88,13 @@ def test_route_dry_run_names_the_launched_kernels():
     with _lib.debug(render_tile=-1):
         with pytest.raises(RuntimeError, match="debug options"):
             _lib.route("render_packed", 64, 64, 4, 1)
+
+
+def test_route_dry_run_u8_and_net_output():
+    """The u8 texel render and the fused net-output render report their kernels (bench legs
+    u8 / netout find their rocprof dispatches by them)."""
+    assert _lib.route("render_packed_u8", 1024, 1024, 128, 1) == ("render_u8_kernel<false, 4, true>",
+                                                                  16 * 64 * 256)
+    assert _lib.route("render_packed_u8", 1024, 1024, 128, 125)[0] == "render_u8_kernel<false, 4, true>"
+    name, grid = _lib.route("render_net_output", 1, 576, 1024, 32)
+    assert name == "render_netout_kernel" and grid > 0

@@ -9,6 +9,7 @@ from conftest import assert_bits, render_case_inputs
 pytestmark = pytest.mark.gpu
 
 import mpi_vision_amd as mv  # noqa: E402
+from mpi_vision_amd import _host, configs  # noqa: E402
 
 
 def _t(small, key, dev):
@@ -106,3 +107,29 @@ def test_device_homographies_bit_exact(dev):
         want2 = _host.render_homographies(pose, depths, K * 1.5, B).numpy()
         got2 = _host.render_homographies_device(pose.to(dev), depths.to(dev), Kd, B)
         assert_bits(got2.cpu().numpy(), want2, f"B={B} after in-place K update")
+
+
+def test_device_psv_matrices_bit_exact(dev):
+    """psv_matrices_device (Ki memoised per intrinsics tensor, proj = K4 @ pose by
+    mpiv_psv_proj_device) equals the host psv_matrices bit for bit, for one camera [3,3]
+    shared by the batch and for per-view [B,3,3] intrinsics, and again after an in-place
+    update of K (the memo follows the tensor's version)."""
+    g = torch.Generator().manual_seed(4)
+    c = configs.config4()
+    B = 40
+    pose = configs.f32(c["poses"][200:200 + B])
+    K = configs.f32([configs.intrinsics_matrix(*(torch.rand(4, generator=g) * 300 + 5).tolist()) for _ in range(B)])
+    Kd, posed = K.to(dev), pose.to(dev)
+    for _ in range(2):
+        ki, proj = _host.psv_matrices_device(Kd, Kd, posed, B)
+        wki, wproj = _host.psv_matrices(K, K, pose)
+        assert_bits(ki.cpu().numpy(), wki.numpy())
+        assert_bits(proj.cpu().numpy(), wproj.numpy())
+    K1 = Kd[7].clone()
+    for scale in (1.0, 1.5):
+        K1.mul_(scale)
+        ki, proj = _host.psv_matrices_device(K1, K1, posed, B)
+        Kh = K1.cpu()[None].expand(B, 3, 3)
+        wki, wproj = _host.psv_matrices(Kh, Kh, pose)
+        assert_bits(ki.cpu().numpy(), wki.numpy())
+        assert_bits(proj.cpu().numpy(), wproj.numpy())

@@ -143,3 +143,37 @@ def test_plane_sweep_no_depths_raises_value_error():
     K = torch.tensor([[[40.0, 0, 26], [0, 41.0, 14], [0, 0, 1]]])
     with pytest.raises(ValueError, match="non-empty list"):
         mv.plane_sweep_torch(torch.rand(1, 12, 16, 3), [], torch.eye(4)[None], K)
+
+
+def _psv_proj_host(Ks, pose):
+    from mpi_vision_amd import _lib
+    B = pose.shape[0]
+    Ks = Ks.contiguous()
+    pose = pose.contiguous()
+    out = torch.empty((B, 16), dtype=torch.float32)
+    ks_b = 0 if Ks.dim() == 2 else 9
+    rc = _lib.load().mpiv_psv_proj(Ks.data_ptr(), ks_b, pose.data_ptr(), B, out.data_ptr())
+    assert rc == 0
+    return out
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_psv_proj_restatement_equals_torch(seed):
+    """mpiv_psv_proj (geometry.hip psv_proj, the code the device entry runs too) equals
+    psv_matrices' torch-CPU proj = cat(K, 0; 0 0 0 1) @ pose bit for bit (utils.py:428-438):
+    camera-path poses, random dense 4x4 "poses" with negative zeros and signed entries, and
+    intrinsics with and without skew."""
+    g = torch.Generator().manual_seed(seed)
+    B = 64
+    c = configs.config4()
+    poses = configs.f32(c["poses"][seed * 100:seed * 100 + B // 2])
+    rnd = (torch.rand((B // 2, 4, 4), generator=g) - 0.5) * 10
+    rnd[:, 1, 2] = -0.0
+    rnd[0] = torch.tensor([[-0.0, 0.0, -1.0, 2.0], [0.0, -0.0, 0.0, -0.0], [1.0, 0.0, -0.0, 0.5], [0.0, -0.0, 0.0, 1.0]])
+    pose = torch.cat([poses, rnd])
+    K = configs.f32([configs.intrinsics_matrix(*(torch.rand(4, generator=g) * 300 + 5).tolist()) for _ in range(B)])
+    K[::3, 0, 1] = torch.rand(K[::3].shape[0], generator=g) - 0.5  # skew
+    ki, proj = _host.psv_matrices(K, K, pose)
+    assert_bits(_psv_proj_host(K, pose).numpy(), proj.numpy())
+    ki1, proj1 = _host.psv_matrices(K[:1].expand(B, 3, 3), K[:1].expand(B, 3, 3), pose)
+    assert_bits(_psv_proj_host(K[0], pose).numpy(), proj1.numpy())

@@ -400,12 +400,13 @@ def test_format_network_input_depth_lanes_strided(small, dev, kopts):
 
 
 @pytest.mark.parametrize("direct", ["0", "1", "2", "3"])
-@pytest.mark.parametrize("D", [10, 16])
+@pytest.mark.parametrize("D", [3, 6, 8, 10, 16])
 def test_format_network_input_few_depths_routes(D, direct, small, dev, kopts):
     """format_network_input_torch with the notebook's few depths: each source swept into its
     channel slice of the network input (mpiv_plane_sweep_into: pixel runs D*3 floats long,
-    out_pstride = 3 + S*D*3 apart) by the automatic route, the direct depth-per-lane kernel and
-    the pixel-per-lane kernel (strided copy-out): bit-identical to the LDS-staged kernel."""
+    out_pstride = 3 + S*D*3 apart) by the automatic route (D = 3..8: the pixel-per-lane kernel,
+    ADVICE r3), the direct depth-per-lane kernel and the pixel-per-lane kernel (strided
+    copy-out): bit-identical to the LDS-staged kernel (sweep_direct=-1)."""
     t = {k: torch.tensor(small[f"fni_{k}"]).to(dev) for k in ("ref", "src", "ref_pose", "src_poses", "K")}
     planes = configs.inv_depths(1.0, 100.0, D)
     args = (None, t["ref"], t["src"], t["ref_pose"], t["src_poses"], planes, t["K"])

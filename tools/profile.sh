@@ -9,11 +9,15 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof
+# the trace pass runs the driver's own bench command (--steps 20 --warmup 5), so every timed leg
+# has as many dispatches in the summary as in the driver's line; the counter passes only need the
+# per-dispatch shapes and stay short
+TRACE_ARGS=${PROF_TRACE_ARGS:---steps 20 --warmup 5 --cpu-seconds 0}
 ARGS=${PROF_ARGS:---steps 3 --warmup 1 --cpu-seconds 0}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
-    -- python3 -u "$ROOT/bench.py" $ARGS > "$OUT/trace.log" 2>&1 || { echo "trace pass failed"; tail -5 "$OUT/trace.log"; exit 1; }
+    -- python3 -u "$ROOT/bench.py" $TRACE_ARGS > "$OUT/trace.log" 2>&1 || { echo "trace pass failed"; tail -5 "$OUT/trace.log"; exit 1; }
 echo "trace pass ok"
 for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" \
             "TA_BUSY_avr GRBM_GUI_ACTIVE"; do
