@@ -644,7 +644,8 @@ def config5_leg(world, rank, dev, steps, warmup):
         ct = torch.empty((1, H, W, 4), device=dev)
         launch = lambda: _lib._call("mpiv_render_packed_ct", packed, H, W, p1 - p0, 0, p1 - p0,  # noqa: E731
                                     int(rank == 0), hl, 1, ct, _lib._stream(dev))
-        step = lambda: parallel.render_plane_sharded(packed, hl, H)  # noqa: E731
+        xstats = {}
+        step = lambda: parallel.render_plane_sharded(packed, hl, H, stats=xstats)  # noqa: E731
         shard_bytes = (p1 - p0) * H * W * 16 + H * W * 16
         kname, grid = _lib.route("render_packed_ct", H, W, p1 - p0, 1)
     launch()
@@ -672,6 +673,15 @@ def config5_leg(world, rank, dev, steps, warmup):
            "parallelism": "single GPU, sequential render" if world == 1 else
            f"plane-sharded x{world}: (C,T) partials + band all-to-all + ordered combine + gather",
            "frame_sha16": sha16(frame) if rank == 0 else None}
+    if world > 1:
+        # the band exchange is pipelined with the render (parallel.render_plane_sharded_pipelined):
+        # what the exchange adds over the slowest rank's render is the exposed part
+        step_ms = elapsed / steps * 1e3
+        sent = max(all_ranks(float(xstats.get("bytes_sent", 0)), world, dev))
+        res.update({"exchange": "pipelined: G-1 batched pair exchanges of row bands, each posted as soon as its "
+                                "band is rendered (mpiv_render_packed_ct_rows)",
+                    "bytes_sent_per_rank": int(sent), "exchange_exposed_ms": round(step_ms - max(kern_all), 3),
+                    "exchange_gbs_over_step": round(sent / (step_ms * 1e-3) / 1e9, 2)})
     res.update(prof_fields(kname, grid, shard_bytes, max(kern_all)))
     del packed
     torch.cuda.empty_cache()

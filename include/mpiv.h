@@ -63,6 +63,7 @@ int mpiv_debug_set(const char *name, int value);
  *   "render_packed", "render_packed_ct"  {H, W, P, V}        (mpiv_render_packed[_ct])
  *   "render"                             {B, H, W, P}        (mpiv_render, contiguous MPI)
  *   "plane_sweep"                        {B, Hs, Ws, C, D, Ht, Wt} (mpiv_plane_sweep)
+ *   "render_packed_ct_rows"              {H, W, P, V, y_begin, y_end} (mpiv_render_packed_ct_rows)
  *   "render_packed_u8"                   {H, W, P, V}        (mpiv_render_packed_u8)
  *   "render_net_output"                  {B, H, W, P}        (mpiv_render_net_output)
  * Fails while a debug option is set (it reports production routes only). */
@@ -123,6 +124,12 @@ int mpiv_render_packed_lds(const float *packed, int H, int W, int P, const float
  * reference's plane 0 (its alpha ignored, utils.py:152-153) -> T = 0. */
 int mpiv_render_packed_ct(const float *packed, int H, int W, int P, int p_begin, int p_end, int back,
                           const float *homs, int V, float *ct, void *stream);
+
+/* Rows [y_begin, y_end) of mpiv_render_packed_ct's partial (same bits; the other rows of ct
+ * [V,H,W,4] are not written): the plane-sharded render launches its row bands one at a time so
+ * each band's exchange overlaps the next band's render.  H, W >= 2. */
+int mpiv_render_packed_ct_rows(const float *packed, int H, int W, int P, int p_begin, int p_end, int back,
+                               const float *homs, int V, int y_begin, int y_end, float *ct, void *stream);
 
 /* Ordered over-operator combine: parts [G][n][4] (C,T), index 0 = back-most range
  * -> out [n][3].  (Cf,Tf) o (Cb,Tb) = (Cf + Tf*Cb, Tf*Tb). */

@@ -35,6 +35,7 @@ _SIGS = {
     "mpiv_render_packed": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_render_packed_lds": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_render_packed_ct": [_vp, _int, _int, _int, _int, _int, _int, _vp, _int, _vp, _vp],
+    "mpiv_render_packed_ct_rows": [_vp, _int, _int, _int, _int, _int, _int, _vp, _int, _int, _int, _vp, _vp],
     "mpiv_combine_ct": [_vp, _int, _i64, _vp, _vp],
     "mpiv_plane_sweep": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
     "mpiv_inverse_warp": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _c_i64p, _int, _int, _vp, _vp],
@@ -469,6 +470,21 @@ def render_packed_ct(packed: torch.Tensor, homs: torch.Tensor, back: bool, p_beg
     else:
         _check_out(out, (V, H, W, 4), dev, "render_packed_ct")
     _call("mpiv_render_packed_ct", packed, H, W, P, p_begin, p_end, int(back), h, V, out,
+          _stream(dev))
+    return out
+
+
+def render_packed_ct_rows(packed: torch.Tensor, homs: torch.Tensor, back: bool, y_begin: int, y_end: int,
+                          out: torch.Tensor, p_begin: int = 0, p_end: int | None = None) -> torch.Tensor:
+    """Rows [y_begin, y_end) of render_packed_ct's partial into out [V,H,W,4] (other rows
+    untouched): one row band of a plane shard (mpiv_render_packed_ct_rows, same bits)."""
+    dev = _dev(packed)
+    P, H, W = packed_hw(packed)
+    p_end = P if p_end is None else p_end
+    V = homs.shape[0]
+    h = _up(homs.reshape(V, P, 9), dev)
+    _check_out(out, (V, H, W, 4), dev, "render_packed_ct_rows")
+    _call("mpiv_render_packed_ct_rows", packed, H, W, P, p_begin, p_end, int(back), h, V, y_begin, y_end, out,
           _stream(dev))
     return out
 

@@ -561,6 +561,43 @@ int mpiv_render_packed_ct(const float* packed, int H, int W, int P, int p_begin,
     return render_packed_impl(packed, H, W, P, p_begin, p_end, back, homs, V, ct, true, 0, stream);
 }
 
+// Rows [y_begin, y_end) of mpiv_render_packed_ct's partial: the plane-sharded render issues its
+// G row bands one launch each, so band k can leave for rank k while the next band renders
+// (parallel.py).  Always the rows kernel with vertical tap reuse (every render route gives the
+// same bits), its (R, rows in flight) chosen as the full-frame route chooses them.
+int mpiv_render_packed_ct_rows(const float* packed, int H, int W, int P, int p_begin, int p_end, int back,
+                               const float* homs, int V, int y_begin, int y_end, float* ct, void* stream) {
+    const char* nm = "mpiv_render_packed_ct_rows";
+    if (!packed || !homs || !ct) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (V <= 0 || H < 2 || W < 2 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape (H, W >= 2)", nm);
+    if (p_begin < 0 || p_end > P || p_begin >= p_end) return fail(MPIV_ERR_ARG, "%s: bad plane range", nm);
+    if (y_begin < 0 || y_end > H || y_begin >= y_end) return fail(MPIV_ERR_ARG, "%s: bad row range", nm);
+    if (!aligned16(packed) || !aligned16(ct)) return fail(MPIV_ERR_ARG, "%s: 16-byte alignment", nm);
+    if ((int64_t)(H + 2 * kPad) * (W + 2 * kPad) * 16 >= (int64_t)kOOB || H >= (1 << 22) || W >= (1 << 22))
+        return fail(MPIV_ERR_ARG, "%s: padded plane larger than 2 GiB or a side >= 2^22", nm);
+    const float4* pk = reinterpret_cast<const float4*>(packed);
+    const int64_t ps = (int64_t)(H + 2 * kPad) * (W + 2 * kPad);
+    const RenderGeom g = make_geom(H, W, P);
+    const float sxr = (float)W / (float)(H - 1), syr = (float)H / (float)(W - 1);
+    const bool square = sxr >= 0.8f && sxr <= 1.25f && syr >= 0.8f && syr <= 1.25f;
+    const int R = V <= 2 ? 4 : V <= 8 ? 8 : square ? 6 : 9;
+    const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(y_end - y_begin, 4 * R) * V;
+    if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+    if (g_route) return note_route(nb, 256, "render_rows_kernel<true, %d, true, false, %d>", R, R <= 8 ? 4 : 3);
+    hipStream_t st = S(stream);
+#define MPIV_CTR(RR, DD)                                                                                            \
+    render_rows_kernel<true, RR, true, false, DD><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, \
+                                                                                homs, ct, nullptr, y_begin, y_end)
+    switch (R) {
+        case 4: MPIV_CTR(4, 4); break;
+        case 8: MPIV_CTR(8, 4); break;
+        case 6: MPIV_CTR(6, 3); break;
+        default: MPIV_CTR(9, 3); break;
+    }
+#undef MPIV_CTR
+    return launched(nm);
+}
+
 // ---- render backward (render_bwd.hip) ----------------------------------------------
 
 namespace {
@@ -1395,6 +1432,9 @@ int mpiv_route(const char* entry, const int64_t* a, int na, char* name, int name
         rc = render_packed_impl(d, (int)a[0], (int)a[1], (int)a[2], 0, (int)a[2], 1, d, (int)a[3], d, false, 0, nullptr);
     else if (strcmp(entry, "render_packed_ct") == 0 && na == 4)
         rc = render_packed_impl(d, (int)a[0], (int)a[1], (int)a[2], 0, (int)a[2], 1, d, (int)a[3], d, true, 0, nullptr);
+    else if (strcmp(entry, "render_packed_ct_rows") == 0 && na == 6)
+        rc = mpiv_render_packed_ct_rows(d, (int)a[0], (int)a[1], (int)a[2], 0, (int)a[2], 1, d, (int)a[3], (int)a[4],
+                                        (int)a[5], d, nullptr);
     else if (strcmp(entry, "plane_sweep") == 0 && na == 7) {
         const int64_t C = a[3], D = a[4], st[4] = {a[1] * a[2] * C, a[2] * C, C, 1};
         rc = mpiv_plane_sweep(d, st, (int)a[0], (int)a[1], (int)a[2], (int)C, d, d, d, (int)D, (int)a[5], (int)a[6], d,

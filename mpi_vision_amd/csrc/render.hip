@@ -569,17 +569,21 @@ __global__ __launch_bounds__(256) void render_rows_lds_kernel(const float4* __re
 // division proof.
 // COUNT (census build, mpiv_render_packed_census): the same kernel also adds up the gather
 // instructions its waves issue (the texture path's real work, for bench.py's roofline).
+// Rows [y_lo, y_hi) of the frame (the whole frame by default; a row band of a plane-shard
+// partial, mpiv_render_packed_ct_rows: the tiles start at y_lo, rows from y_hi on are not stored).
 template <bool CT, int R, bool VS = false, bool COUNT = false, int D = 2>
 __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restrict__ planes, int64_t plane_stride,
                                                           RenderGeom g, int V, int p_begin, int p_end, int back,
                                                           const float* __restrict__ homs, float* __restrict__ out,
-                                                          unsigned long long* __restrict__ census = nullptr) {
+                                                          unsigned long long* __restrict__ census = nullptr,
+                                                          int y_lo = 0, int y_hi = -1) {
     constexpr int TY = 4 * R;
+    if (y_hi < 0) y_hi = g.H;
     const int tiles_x = (g.W + kTileX - 1) / kTileX;
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
     const int v = lb % V;
     const int tile = lb / V;
-    const int tx0 = (tile % tiles_x) * kTileX, ty0 = (tile / tiles_x) * TY;
+    const int tx0 = (tile % tiles_x) * kTileX, ty0 = y_lo + (tile / tiles_x) * TY;
     const int x = tx0 + (int)(threadIdx.x & (kWave - 1));
     const int y0 = ty0 + (int)(threadIdx.x >> 6) * R;
     const float* hv = homs + (int64_t)v * g.P * 9;
@@ -591,7 +595,7 @@ __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restri
             ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, fy0, fy1);
     }
     const bool proven = __syncthreads_and(ok);
-    if (x >= g.W || y0 >= g.H) return;  // rows past H inside [y0, y0+R) are computed, not stored
+    if (x >= g.W || y0 >= y_hi) return;  // rows past y_hi inside [y0, y0+R) are computed, not stored
     float cr[R], cg[R], cb[R], tt[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -599,7 +603,7 @@ __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restri
     }
     if (!proven) {  // rare (w near 0 over the tile): the guarded one-pixel recipe, row by row
         int rows = 0;
-        for (int k = 0; k < R && y0 + k < g.H; ++k, ++rows) {
+        for (int k = 0; k < R && y0 + k < y_hi; ++k, ++rows) {
             const int64_t o = ((int64_t)v * g.H + y0 + k) * g.W + x;
             render_packed_pixel<CT, 1>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0 + k,
                                        CT ? out + o * 4 : out + o * 3);
@@ -620,7 +624,7 @@ __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restri
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const int y = y0 + k;
-        if (y >= g.H) break;
+        if (y >= y_hi) break;
         const int64_t o = ((int64_t)v * g.H + y) * g.W + x;
         if (CT) {
             reinterpret_cast<float4*>(out)[o] = make_float4(cr[k], cg[k], cb[k], tt[k]);

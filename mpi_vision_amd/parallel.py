@@ -120,24 +120,100 @@ def identity_partial(views: int, height: int, width: int, like: torch.Tensor) ->
 
 def render_plane_sharded(packed_local: torch.Tensor, homs_local: torch.Tensor, height: int, group=None,
                          dst: int = 0, render_ct: Optional[Callable] = None,
-                         combine: Optional[Callable[[torch.Tensor], torch.Tensor]] = None) -> Optional[torch.Tensor]:
+                         combine: Optional[Callable[[torch.Tensor], torch.Tensor]] = None,
+                         render_rows: Optional[Callable] = None, pipelined: Optional[bool] = None,
+                         stats: Optional[dict] = None) -> Optional[torch.Tensor]:
     """Plane-sharded render of V views.
 
     packed_local: this rank's planes, packed [P_local, H+4, W+4, 4] (_lib.pack_planes) (rank 0 holds the
     back-most range, which contains the reference's plane 0); homs_local
     [V, P_local, 9].  P_local may be 0 (more ranks than planes): that rank contributes the
     identity partial.  Returns the final frames [V, H, W, 3] on dst, None elsewhere.
-    render_ct / combine replace the HIP kernels (CPU tests of the exchange logic only)."""
+
+    pipelined (default on the GPU path: frames of at least 2 x 2 pixels and more than one
+    rank): the partial is rendered band by band and each band leaves for its rank as soon as it
+    is rendered, overlapping the next band's render (render_plane_sharded_pipelined); else one
+    render, one all-to-all.  render_ct / render_rows / combine replace the HIP kernels (CPU
+    tests of the exchange logic only)."""
     from . import _lib
     G, rank = _world(group)
     V = homs_local.shape[0]
     width = packed_local.shape[2] - 2 * _lib.PAD
+    if pipelined is None:
+        pipelined = G > 1 and height >= 2 and width >= 2 and (render_rows is not None or render_ct is None)
+    if pipelined:
+        return render_plane_sharded_pipelined(packed_local, homs_local, height, group, dst, render_rows, combine,
+                                              stats)
     if packed_local.shape[0] == 0:
         ct = identity_partial(V, height, width, packed_local)
     else:
         ct = (render_ct or _lib.render_packed_ct)(packed_local, homs_local, back=(rank == 0))
     parts = exchange_bands(ct, group)
     band = combine_partials(parts, combine)
+    return gather_frames(band, height, group, dst)
+
+
+def render_plane_sharded_pipelined(packed_local: torch.Tensor, homs_local: torch.Tensor, height: int, group=None,
+                                   dst: int = 0, render_rows: Optional[Callable] = None,
+                                   combine: Optional[Callable[[torch.Tensor], torch.Tensor]] = None,
+                                   stats: Optional[dict] = None) -> Optional[torch.Tensor]:
+    """render_plane_sharded with the band exchange overlapped with the render (SURVEY.md §8e
+    "pipeline bands to overlap").  G - 1 steps: at step s rank r renders row band k = r + s
+    (mod G) of its partial (mpiv_render_packed_ct_rows, one launch) and posts one batched
+    pair exchange -- band k to rank k, band r from rank r - s -- then goes on to the next band
+    while the exchange runs (RCCL's stream waits only for the work enqueued before the post).
+    Every rank walks the steps in the same order, so each step's sends and receives pair up.
+    Its own band r is rendered last and combined with the received ones in plane (source rank)
+    order (mpiv_combine_ct, as the one-shot path), then the RGB bands are gathered.
+    stats (optional): filled with the bytes this rank sent and the steps posted."""
+    from . import _lib
+    G, rank = _world(group)
+    V = homs_local.shape[0]
+    width = packed_local.shape[2] - 2 * _lib.PAD
+    bands = band_bounds(height, G)
+    b_r, e_r = bands[rank]
+    empty = packed_local.shape[0] == 0
+    ct = identity_partial(V, height, width, packed_local) if empty else \
+        packed_local.new_empty((V, height, width, 4))
+    rows = render_rows or _lib.render_packed_ct_rows
+    staged = _staged(ct, group)
+    recv = ct.new_empty((G, V, e_r - b_r, width, 4))  # band r of every rank's partial, by source rank
+    host_recv = {}
+    works, sent = [], 0
+
+    def render_band(k):
+        b, e = bands[k]
+        if e > b and not empty:
+            rows(packed_local, homs_local, rank == 0, b, e, ct)
+
+    for s in range(1, G):
+        k, j = (rank + s) % G, (rank - s) % G  # this step's destination and source
+        render_band(k)
+        ops = []
+        b, e = bands[k]
+        if e > b:
+            snd = ct[:, b:e]
+            snd = snd.contiguous() if not snd.is_contiguous() else snd
+            if staged:
+                snd = snd.cpu()
+            ops.append(dist.P2POp(dist.isend, snd, k, group))
+            sent += snd.numel() * snd.element_size()
+        if e_r > b_r:
+            rb = recv[j]
+            if staged:
+                rb = host_recv[j] = torch.empty(tuple(rb.shape), dtype=rb.dtype)
+            ops.append(dist.P2POp(dist.irecv, rb, j, group))
+        if ops:
+            works += dist.batch_isend_irecv(ops)
+    render_band(rank)
+    recv[rank] = ct[:, b_r:e_r]
+    for w in works:
+        w.wait()
+    for j, hb in host_recv.items():
+        recv[j].copy_(hb)
+    if stats is not None:
+        stats.update(bytes_sent=sent, steps=G - 1)
+    band = combine_partials(recv, combine)
     return gather_frames(band, height, group, dst)
 
 
