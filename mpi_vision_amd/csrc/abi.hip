@@ -72,9 +72,10 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      depth-per-lane (plane_sweep_dlane_kernel)
 //   sweep_rows=4|6|8   mpiv_plane_sweep[_into]'s depth-per-lane kernel with tiles of that many
 //                      target rows (staging 3072 / 4096 / 4096 texels; 0 = automatic)
-//   bwd_gather=0|1|2   render backward gather: block tiles (bwd_gather_kernel) / one texel row per
+//   bwd_gather=0|1|2|3 render backward gather: block tiles (bwd_gather_kernel) / one texel row per
 //                      wave, no block barriers (bwd_gather_wave_kernel) / staging and texel waves
-//                      (bwd_gather_ws_kernel)
+//                      (bwd_gather_ws_kernel) / block tiles with the d samples streamed into LDS
+//                      one pass ahead (bwd_gather_dma_kernel)
 //   chunk_flight=2|4   render_chunk_kernel with that many sub-steps' taps in flight per wave
 //                      (0 = automatic)
 //   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
@@ -766,6 +767,9 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                     bwd_gather_ws_kernel<<<(unsigned)gather_blocks, 2 * kGThreads, 0, q>>>(g, hv, ws, gv, margin);
                 else
 #endif
+                if (opt(kOptBwdGather) == 3)
+                    bwd_gather_dma_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
+                else
                     bwd_gather_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
             }
         }

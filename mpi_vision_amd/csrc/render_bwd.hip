@@ -487,6 +487,9 @@ constexpr int kGWP = kGCap + 1;
 // *ovf).  The pass's d samples are loaded first (MPIV_GSI per thread in flight while the
 // positions are computed: issued after each pixel's position, inside the in-tile test, their
 // latency was exposed -- 0.32 of the kernel's 1.77 ms, r03).  s_ent must be all ~0 on entry.
+// DS = false (bwd_gather_dma_kernel): the d samples arrive in LDS by DMA instead, and only the
+// fractions (wx, wy) are staged (s_w[q], s_w[kGWP + q]); the texel pass forms the corner weight.
+template <bool DS = true>
 __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const BwdWs& ws, const float* __restrict__ hp,
                                                   int p, bool proven, int t, int tx0, int ty0, int bx0, int bw,
                                                   int ra, int rb, int* s_code, float* s_w, float4* s_ds,
@@ -500,12 +503,14 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
     const float rbw = 1.0f / (float)bw;
     const __amdgpu_buffer_rsrc_t rds = make_rsrc(ws.ds + (int64_t)p * HW, (int)(HW * 16));
     f32x4 dsv[kGSI];
+    if (DS) {
 #pragma unroll
-    for (int i = 0; i < (kGSI < MPIV_GSI ? kGSI : MPIV_GSI); ++i) {
-        const int q = t + i * kGThreads;
-        const int r = (int)(((float)q + 0.5f) * rbw);  // q / bw: q, bw <= 1024, error << 0.5/bw
-        const int off = q < np ? ((ra + r) * g.W + bx0 + (q - r * bw)) * 16 : kOOB;
-        dsv[i] = llvm_raw_buffer_load_v4f32(rds, off, 0, 0);
+        for (int i = 0; i < (kGSI < MPIV_GSI ? kGSI : MPIV_GSI); ++i) {
+            const int q = t + i * kGThreads;
+            const int r = (int)(((float)q + 0.5f) * rbw);  // q / bw: q, bw <= 1024, error << 0.5/bw
+            const int off = q < np ? ((ra + r) * g.W + bx0 + (q - r * bw)) * 16 : kOOB;
+            dsv[i] = llvm_raw_buffer_load_v4f32(rds, off, 0, 0);
+        }
     }
     bool ovl = false;
 #pragma unroll
@@ -529,13 +534,18 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
             // the texel pass reads the one of its corner instead of re-deriving it from fractions
             const float wx = px - fx0, ex = 1.0f - wx;
             const float wy = py - fy0, sy = 1.0f - wy;
-            s_w[q] = sy * ex;
-            s_w[kGWP + q] = sy * wx;
-            s_w[2 * kGWP + q] = wy * ex;
-            s_w[3 * kGWP + q] = wy * wx;
-            if (i >= MPIV_GSI)  // past the preloaded pixels (boxes over MPIV_GSI * kGThreads pixels)
-                dsv[i] = llvm_raw_buffer_load_v4f32(rds, (yy * g.W + xx) * 16, 0, 0);
-            s_ds[q] = make_float4(dsv[i][0], dsv[i][1], dsv[i][2], dsv[i][3]);
+            if (DS) {
+                s_w[q] = sy * ex;
+                s_w[kGWP + q] = sy * wx;
+                s_w[2 * kGWP + q] = wy * ex;
+                s_w[3 * kGWP + q] = wy * wx;
+                if (i >= MPIV_GSI)  // past the preloaded pixels (boxes over MPIV_GSI * kGThreads pixels)
+                    dsv[i] = llvm_raw_buffer_load_v4f32(rds, (yy * g.W + xx) * 16, 0, 0);
+                s_ds[q] = make_float4(dsv[i][0], dsv[i][1], dsv[i][2], dsv[i][3]);
+            } else {
+                s_w[q] = wx;
+                s_w[kGWP + q] = wy;
+            }
             const int pix = yy * g.W + xx;
             // order key (never ~0: bits 14-15 are clear) into the first free slot of the bucket
             // (~0 = free; any order: the texel pass sorts)
@@ -553,6 +563,16 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
 // pixel%8, staged index in the low bits) go through a 4- or 8-input sorting network and are
 // added in order.  After a list overflow (magnification) the texel scans its window of the
 // inverse map instead, one 8-pixel chunk at a time.
+// corner c's bilinear weight of staged pixel q: staged products (s_w corner-major), or (FRAC)
+// formed from the staged fractions with issue_taps_padded's products (the same bits)
+template <bool FRAC>
+__device__ __forceinline__ float staged_weight(const float* s_w, int c, int q) {
+    if (!FRAC) return s_w[c * kGWP + q];
+    const float wx = s_w[q], wy = s_w[kGWP + q];
+    return ((c & 2) ? wy : 1.0f - wy) * ((c & 1) ? wx : 1.0f - wx);
+}
+
+template <bool FRAC = false>
 __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const BwdWs& ws, int p, float margin, int tx,
                                                   int ty, int bt, bool tin, bool ovf, const unsigned* s_ent,
                                                   const int* s_code, const float* s_w, const float4* s_ds, int bx0,
@@ -594,7 +614,7 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
             for (int k = 0; k < 4; ++k) {
                 const bool v = key[k0 + k] != 0xFFFFFFFFu;
                 const int q = v ? (int)(key[k0 + k] & 0x7FF) : kGCap;  // staged index: bits 0-10 (kGCap <= 2048)
-                w[k] = s_w[(int)((key[k0 + k] >> 14) & 3u) * kGWP + q];  // corner bits 14-15
+                w[k] = staged_weight<FRAC>(s_w, (int)((key[k0 + k] >> 14) & 3u), q);  // corner bits 14-15
                 d[k] = s_ds[q];
                 hits += v ? 1u : 0u;
             }
@@ -652,7 +672,7 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
                     msk &= msk - 1;
                     const int idx = rowbase + (cur * kGridVec + (b & 7) - pixrow);
                     const float4 d = s_ds[idx];
-                    const float w = s_w[(b >> 3) * kGWP + idx];  // corner b >> 3
+                    const float w = staged_weight<FRAC>(s_w, b >> 3, idx);  // corner b >> 3
                     acc[0] = acc[0] + w * d.x;
                     acc[1] = acc[1] + w * d.y;
                     acc[2] = acc[2] + w * d.z;
@@ -746,6 +766,156 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
 #pragma unroll
         for (int jj = 0; jj < kGPl; ++jj)
             if (p0 + jj < g.P) o[jj] = make_float4(acc[jj][0], acc[jj][1], acc[jj][2], acc[jj][3]);
+    }
+}
+
+// ---- 2'. gather with the d samples streamed into LDS one pass ahead (bwd_gather=3) ------
+// bwd_gather_kernel loads a pass's d samples in its staging phase and waits for them there;
+// its texel phase issues no memory traffic, so a block's loads are in flight only part of the
+// time (r03: 0.82 ms of memory phase alone, +0.8 ms with the texel phase).  Here the d samples
+// of pass i+1 go from HBM straight into LDS (buffer_load_dwordx4 ... lds, no VGPRs) while pass
+// i is staged and summed, so every block keeps one whole pass of loads in flight.  Only the
+// fractions are staged (the texel pass forms each corner's weight with the same products), so
+// a block needs 38 KiB of LDS: 4 blocks per CU.  The passes, positions, bucket lists, sums and
+// counts are bwd_gather_kernel's: the gradient is bit-identical.
+//
+// Protocol (one barrier pair per pass, as bwd_gather_kernel): every wave issues exactly kGDF
+// DMA instructions per pass (lanes past the pass's pixels get the out-of-range offset, which
+// writes +0 into the buffer's tail -- the zero slot kGCap included); at the top of pass i a
+// barrier retires pass i-1's texel phase, pass i+1's fill goes into the other buffer, pass i
+// is staged, each wave waits for its own fills of pass i (vmcnt(kGDF): the younger kGDF are
+// pass i+1's) and a barrier publishes them.  The DMA is inline asm (hipcc cannot tell which
+// LDS bytes a DMA writes and would drain vmcnt(0) before every ds_read).
+constexpr int kGDF = (kGCap + kGThreads - 1) / kGThreads;  // DMA instructions per wave and pass
+constexpr int kGDS = kGDF * kGThreads;                     // staged slots per buffer (> kGCap)
+static_assert(kGThreads == 4 * kWave && kGDS > kGCap, "the fill covers every staged slot and the zero slot");
+
+__device__ __forceinline__ void gather_dma16(__amdgpu_buffer_rsrc_t r, int voff, unsigned lds) {
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(lds)
+                 : "memory", "m0");
+}
+
+__global__ __launch_bounds__(kGThreads, 4) void bwd_gather_dma_kernel(RenderGeom g, const float* __restrict__ homs,
+                                                                      BwdWs ws, float4* __restrict__ dmpi,
+                                                                      float margin) {
+    __shared__ int s_code[kGCap];
+    __shared__ float s_w[2 * kGWP];                               // fractions wx, wy; [kGCap] = 0
+    __shared__ __attribute__((aligned(16))) float4 s_ds[2][kGDS];  // d samples by pass parity
+    __shared__ unsigned s_ent[2][2 * kGNB];
+    __shared__ int s_ovf[2];
+    const int tiles_x = (g.W + kGTW - 1) / kGTW;
+    const int ntiles = tiles_x * ((g.H + kGTH - 1) / kGTH);
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int ngroups = (g.P + kGPl - 1) / kGPl;
+    const int tile = lb / ngroups, p0 = (lb % ngroups) * kGPl;
+    const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTH;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+    const int tx = tx0 + lane, ty = ty0 + wave;
+    const bool tin = tx < g.W && ty < g.H;
+    const int bt = (ty - ty0 + 1) * kGTB + (tx - tx0 + 1);
+    const int64_t HW = (int64_t)g.H * g.W;
+    for (int b = threadIdx.x; b < 4 * kGNB; b += kGThreads) (&s_ent[0][0])[b] = ~0u;
+    if (threadIdx.x < 2) s_ovf[threadIdx.x] = 0;
+    if (threadIdx.x < 2) s_w[threadIdx.x * kGWP + kGCap] = 0.0f;
+    unsigned hits = 0;
+    bool unsafe = false;
+    // the block's planes: boxes (bwd_box_kernel); a box the block cannot gather makes the view unsafe
+    int4 bxs[kGPl];
+#pragma unroll
+    for (int jj = 0; jj < kGPl; ++jj) {
+        bxs[jj] = p0 + jj < g.P ? ws.box[(int64_t)(p0 + jj) * ntiles + tile] : make_int4(0, -1, 0, -1);
+        if (bxs[jj].x == -2) {
+            unsafe = true;
+            bxs[jj] = make_int4(0, -1, 0, -1);
+        }
+    }
+    // passes: (plane jj, first box row ra); jj == kGPl ends.  box(jj): static selects, then
+    // readfirstlane (block-uniform values: the buffer descriptor and M0 need SGPRs)
+    auto box = [&](int jj) {
+        int4 b = make_int4(0, -1, 0, -1);
+#pragma unroll
+        for (int k = 0; k < kGPl; ++k)
+            if (k == jj) b = bxs[k];
+        return make_int4(__builtin_amdgcn_readfirstlane(b.x), __builtin_amdgcn_readfirstlane(b.y),
+                         __builtin_amdgcn_readfirstlane(b.z), __builtin_amdgcn_readfirstlane(b.w));
+    };
+    auto rows_per_pass = [&](const int4& b) { return kGCap / (b.y - b.x + 1); };
+    auto first_from = [&](int jj, int& ra) {
+        for (; jj < kGPl; ++jj) {
+            const int4 b = box(jj);
+            if (b.y >= b.x && (b.w & ~kBoxProven) >= b.z) break;
+        }
+        ra = jj < kGPl ? box(jj).z : 0;
+        return jj;
+    };
+    auto fill = [&](int jj, int ra, int buf) {  // kGDF DMA instructions of this wave
+        int np = 0, bw = 1, bx0 = 0;
+        const float* base = reinterpret_cast<const float*>(ws.ds);
+        if (jj < kGPl) {
+            const int4 b = box(jj);
+            bx0 = b.x;
+            bw = b.y - bx0 + 1;
+            const int rb = min((b.w & ~kBoxProven) + 1, ra + rows_per_pass(b));
+            np = (rb - ra) * bw;
+            base += (int64_t)(p0 + jj) * HW * 4;
+        }
+        const __amdgpu_buffer_rsrc_t r = make_rsrc(base, (int)(HW * 16));
+        const float rbw = 1.0f / (float)bw;
+        const unsigned lds = (unsigned)(uintptr_t)&s_ds[buf][0] + (unsigned)wave * kWave * 16;
+#pragma unroll
+        for (int f = 0; f < kGDF; ++f) {
+            const int q = (f * 4 + wave) * kWave + lane;
+            const int rr = (int)(((float)q + 0.5f) * rbw);  // q / bw (gather_stage_pass)
+            const int voff = q < np ? ((ra + rr) * g.W + bx0 + (q - rr * bw)) * 16 : kOOB;
+            gather_dma16(r, voff, __builtin_amdgcn_readfirstlane(lds + (unsigned)(f * kGThreads * 16)));
+        }
+    };
+    f32x4 acc[kGPl];
+#pragma unroll
+    for (int jj = 0; jj < kGPl; ++jj) acc[jj] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    int ra = 0;
+    int jj = first_from(0, ra);
+    if (jj < kGPl) fill(jj, ra, 0);
+    int par = 0;
+    while (jj < kGPl) {
+        const int4 bj = box(jj);
+        const int by1 = bj.w & ~kBoxProven, rpp = rows_per_pass(bj);
+        const int rb = min(by1 + 1, ra + rpp);
+        int ra_n = rb, jj_n = jj;
+        if (ra_n > by1) jj_n = first_from(jj + 1, ra_n);
+        __syncthreads();  // the previous pass's texel phase is done with buffer par ^ 1 and the staging arrays
+        const bool more = jj_n < kGPl;
+        if (more) fill(jj_n, ra_n, par ^ 1);
+        const int p = p0 + jj;
+        const int bx0 = bj.x, bx1 = bj.y, by0 = bj.z;
+        gather_stage_pass<false>(g, ws, homs + (int64_t)p * 9, p, (bj.w & kBoxProven) != 0, (int)threadIdx.x,
+                                 tx0, ty0, bx0, bx1 - bx0 + 1, ra, rb, s_code, s_w, nullptr, s_ent[par], &s_ovf[par]);
+        for (int b = threadIdx.x; b < 2 * kGNB; b += kGThreads) s_ent[par ^ 1][b] = ~0u;  // for the next pass
+        if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
+        if (more)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGDF) : "memory");  // this pass's fills (pass i+1's are younger)
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // jj is block-uniform: the accumulator index stays static after unrolling the select
+#pragma unroll
+        for (int k = 0; k < kGPl; ++k)
+            if (k == jj)
+                gather_texel_pass<true>(g, ws, p, margin, tx, ty, bt, tin, s_ovf[par] != 0, s_ent[par], s_code, s_w,
+                                        s_ds[par], bx0, bx1, by0, by1, ra, rb, acc[k], hits, unsafe);
+        par ^= 1;
+        jj = jj_n;
+        ra = ra_n;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) hits += __shfl_xor(hits, off);
+    const unsigned long long tot = (unsigned long long)hits + (__any(unsafe) ? kUnsafe : 0ull);
+    if (lane == 0 && tot) atomicAdd(&ws.found[blockIdx.x % kCtrSlots], tot);
+    if (tin) {
+        float4* o = dmpi + ((int64_t)ty * g.W + tx) * g.P + p0;
+#pragma unroll
+        for (int k = 0; k < kGPl; ++k)
+            if (p0 + k < g.P) o[k] = make_float4(acc[k][0], acc[k][1], acc[k][2], acc[k][3]);
     }
 }
 

@@ -76,3 +76,25 @@ def test_config5_full_size_sequential_and_plane_sharded(dev):
     err = np.abs(combined.astype(np.float64) - frame_h).max()
     print(f"config 5: 8-shard combine vs sequential max |diff| = {err:.3g}")
     np.testing.assert_allclose(combined, frame_h, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("V,bands", [(1, 8), (1, 3), (3, 5), (12, 8)])
+def test_ct_row_bands_equal_whole_partial(V, bands, dev):
+    """mpiv_render_packed_ct_rows (the pipelined plane shard renders its row bands one launch
+    each): the bands stitched together are bit-identical to one mpiv_render_packed_ct of the
+    whole partial -- for a stretched frame (config 5's aspect, 1/8 size) and the back-most
+    range (plane 0 replaces) and a middle range, at 1, 3 and 12 views."""
+    from mpi_vision_amd import parallel
+    c = configs.config5()
+    H, W, P = 270, 512, 32
+    K = configs.intrinsics_matrix(c["K"][0][0] / 8, c["K"][1][1] / 8, W / 2, H / 2)
+    path = configs.config4()["poses"]
+    homs = _host.render_homographies(configs.f32(path[10:10 + V]), configs.f32(configs.inv_depths(1, 100, P)),
+                                     configs.f32([K] * V), V).to(dev)
+    packed = _lib.synth_mpi_packed(7, H, W, 0, P, dev)
+    for p0, p1, back in ((0, 12, True), (12, 32, False)):
+        whole = _lib.render_packed_ct(packed, homs, back, p0, p1)
+        banded = torch.full_like(whole, float("nan"))
+        for b, e in parallel.band_bounds(H, bands):
+            _lib.render_packed_ct_rows(packed, homs, back, b, e, banded, p0, p1)
+        assert torch.equal(whole.view(torch.int32), banded.view(torch.int32)), (p0, p1)
