@@ -127,7 +127,7 @@ bool ab_only(int o, int v) {
         case kOptChunkRows: return v == 2 || v == 4;
         case kOptChunkFlight: return v == 4;
         case kOptSweepRows: return v == 6 || v == 8;
-        case kOptBwdGather: return v == 1 || v == 2;
+        case kOptBwdGather: return v == 1 || v == 2 || v == 3;
         case kOptBwdPollLimit: case kOptBwdFbBlocks: return v != 0;
         default: return false;
     }
@@ -633,7 +633,7 @@ size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
     char* truth = take(kCtrSlots * 8);
     char* found = take(kCtrSlots * 8);
     char* flag = take(32);
-    const size_t ntiles = (size_t)((W + kGTW - 1) / kGTW) * ((H + kGTH - 1) / kGTH);
+    const size_t ntiles = (size_t)((W + kGTW - 1) / kGTW) * ((H + kGTY - 1) / kGTY);
     char* box = take((size_t)P * ntiles * 16);
     char* key = take((size_t)pc * hw * 4);
     char* count = take(nk * 4);
@@ -701,7 +701,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const bool fast = H >= 2 && W >= 2;
     const int64_t HW = (int64_t)H * W;
     const int tiles_x = (int)blocks(W, kGTW);
-    const int64_t ntiles = (int64_t)tiles_x * blocks(H, kGTH);
+    const int64_t ntiles = (int64_t)tiles_x * blocks(H, kGTY);
     const int64_t gather_blocks = ntiles * blocks(P, kGPl);
     if (gather_blocks > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const int force = opt(kOptBwdFallback) != 0 || !fast;
@@ -765,11 +765,10 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
 #if MPIV_AB
                 if (opt(kOptBwdGather) == 2)
                     bwd_gather_ws_kernel<<<(unsigned)gather_blocks, 2 * kGThreads, 0, q>>>(g, hv, ws, gv, margin);
-                else
-#endif
-                if (opt(kOptBwdGather) == 3)
+                else if (opt(kOptBwdGather) == 3)
                     bwd_gather_dma_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
                 else
+#endif
                     bwd_gather_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
             }
         }

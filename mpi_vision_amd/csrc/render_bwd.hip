@@ -45,13 +45,28 @@
 
 namespace mpiv {
 
+#ifndef MPIV_BWD_NT
+#define MPIV_BWD_NT 0  // A/B: non-temporal stores of the d samples (chain) and of d MPI (gather)
+#endif
+__device__ __forceinline__ void bwd_store(float4* p, const float4& v) {
+    if (MPIV_BWD_NT)
+        __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
+    else
+        *p = v;
+}
+
 constexpr int kGridVec = 8;        // grid_sampler_2d_backward chunk width (oracle.GRID_VEC)
 constexpr int kBwdCH = 8;          // chain: planes per chunk
 constexpr int kGTW = 64;           // gather: texel tile width (a wave = one tile row)
 #ifndef MPIV_GTH
 #define MPIV_GTH 4
 #endif
-constexpr int kGTH = MPIV_GTH;     // gather: tile rows (one wave each)
+constexpr int kGTH = MPIV_GTH;     // gather: waves per block (a texel row each)
+#ifndef MPIV_GTR
+#define MPIV_GTR 1
+#endif
+constexpr int kGTR = MPIV_GTR;     // gather: texel rows per wave (rows w, w + kGTH, ...: a tile of kGTY rows)
+constexpr int kGTY = kGTH * kGTR;  // gather: tile rows
 constexpr int kGThreads = kGTW * kGTH;
 // gather tile constants (overridable for A/B builds, tools/gpu_ab_lib.sh); measured on
 // config 4 (profiles/r02_bwd_gather_ab.txt): 4 planes x 736 staged pixels at 6 waves/SIMD
@@ -284,7 +299,7 @@ __device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, c
                         } else {
                             d = make_float4(g0[r], g1[r], g2[r], 0.0f);  // plane 0: output = rgb_0, alpha unused
                         }
-                        if (xin) ws.ds[(int64_t)p * HW + pix] = d;
+                        if (xin) bwd_store(ws.ds + (int64_t)p * HW + pix, d);
                     }
                 }
             }
@@ -400,7 +415,7 @@ __device__ __forceinline__ void pix_range(float a, float b, float e, int cl, int
 // the plane (no inverse, a corner behind the camera, a box beyond the staging limits, or an
 // 8-pixel chunk wrapping rows across two passes): the check then sends the view to the
 // fallback.  x0 > x1 or y0 > y1: no pixel samples the tile.
-constexpr int kGTHc = kGTH;
+constexpr int kGTHc = kGTY;
 constexpr int kBoxProven = 1 << 30;
 __global__ __launch_bounds__(256) void bwd_box_kernel(RenderGeom g, const float* __restrict__ homs,
                                                       const float* __restrict__ inv, int ntiles, int tiles_x,
@@ -470,7 +485,7 @@ __device__ __forceinline__ void sort8(unsigned* k) {
 }
 
 constexpr int kGTB = kGTW + 1;              // bucket row pitch: nw taps x in [tx0-1, tx0+kGTW-1]
-constexpr int kGNB = kGTB * (kGTH + 1);     // nw-tap buckets of a tile
+constexpr int kGNB = kGTB * (kGTY + 1);     // nw-tap buckets of a tile
 constexpr int kGBCap = 2;                   // entries per bucket list (more: the window scan)
 constexpr int kGSI = (kGCap + kGThreads - 1) / kGThreads;  // staged pixels per staging thread
 // staged bilinear weights, corner-major: s_w[c * kGWP + q] is corner c's weight of staged pixel q
@@ -526,7 +541,7 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
             render_pos<true>(hp, (float)xx, (float)yy, g, px, py);
         const float fx0 = floorf(px), fy0 = floorf(py);
         const float lx = fx0 - (float)(tx0 - 1), ly = fy0 - (float)(ty0 - 1);
-        const bool in = lx >= 0.0f && lx <= (float)kGTW && ly >= 0.0f && ly <= (float)kGTH;
+        const bool in = lx >= 0.0f && lx <= (float)kGTW && ly >= 0.0f && ly <= (float)kGTY;
         const int code = in ? (int)ly * TB + (int)lx : -1;
         s_code[q] = code;
         if (in) {
@@ -712,14 +727,20 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     __shared__ int s_ovf[2];                         // a list overflowed in this pass
     constexpr int TB = kGTB;
     const int tiles_x = (g.W + kGTW - 1) / kGTW;
-    const int ntiles = tiles_x * ((g.H + kGTH - 1) / kGTH);
+    const int ntiles = tiles_x * ((g.H + kGTY - 1) / kGTY);
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
     const int ngroups = (g.P + kGPl - 1) / kGPl;  // plane groups fastest: the blocks writing one texel's
     const int tile = lb / ngroups, p0 = (lb % ngroups) * kGPl;  // gradient line run together
-    const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTH;
-    const int tx = tx0 + (threadIdx.x & (kWave - 1)), ty = ty0 + (threadIdx.x >> 6);
-    const bool tin = tx < g.W && ty < g.H;
-    const int bt = (ty - ty0 + 1) * TB + (tx - tx0 + 1);  // bucket of the texel as an nw tap
+    const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTY;
+    const int tx = tx0 + (threadIdx.x & (kWave - 1));
+    int ty[kGTR], bt[kGTR];  // this thread's texel rows (kGTR independent texel sums per pass)
+    bool tin[kGTR];
+#pragma unroll
+    for (int r = 0; r < kGTR; ++r) {
+        ty[r] = ty0 + (int)(threadIdx.x >> 6) + r * kGTH;
+        tin[r] = tx < g.W && ty[r] < g.H;
+        bt[r] = (ty[r] - ty0 + 1) * TB + (tx - tx0 + 1);  // bucket of the texel as an nw tap
+    }
     for (int b = threadIdx.x; b < 4 * kGNB; b += kGThreads) (&s_ent[0][0])[b] = ~0u;
     if (threadIdx.x < 2) s_ovf[threadIdx.x] = 0;
     if (threadIdx.x < 4) s_w[threadIdx.x * kGWP + kGCap] = 0.0f;
@@ -727,10 +748,11 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     int par = 0;
     unsigned hits = 0;    // (texel, contributor) pairs found by this thread
     bool unsafe = false;  // a plane this block could not order (the view goes to the fallback)
-    f32x4 acc[kGPl];
+    f32x4 acc[kGTR][kGPl];
 #pragma unroll
     for (int jj = 0; jj < kGPl; ++jj) {
-        acc[jj] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int r = 0; r < kGTR; ++r) acc[r][jj] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         const int p = p0 + jj;
         if (p >= g.P) continue;  // block-uniform
         const int4 bx = ws.box[(int64_t)p * ntiles + tile];  // bwd_box_kernel
@@ -752,8 +774,11 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
             for (int b = threadIdx.x; b < 2 * kGNB; b += kGThreads) s_ent[par ^ 1][b] = ~0u;  // for the next pass
             if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
             __syncthreads();
-            gather_texel_pass(g, ws, p, margin, tx, ty, bt, tin, s_ovf[par] != 0, s_ent[par], s_code, s_w, s_ds, bx0,
-                              bx1, by0, by1, ra, rb, acc[jj], hits, unsafe);
+            const bool ovf = s_ovf[par] != 0;
+#pragma unroll
+            for (int r = 0; r < kGTR; ++r)
+                gather_texel_pass(g, ws, p, margin, tx, ty[r], bt[r], tin[r], ovf, s_ent[par], s_code, s_w, s_ds, bx0,
+                                  bx1, by0, by1, ra, rb, acc[r][jj], hits, unsafe);
             par ^= 1;
         }
     }
@@ -761,14 +786,19 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     for (int off = 32; off >= 1; off >>= 1) hits += __shfl_xor(hits, off);
     const unsigned long long tot = (unsigned long long)hits + (__any(unsafe) ? kUnsafe : 0ull);
     if ((threadIdx.x & (kWave - 1)) == 0 && tot) atomicAdd(&ws.found[blockIdx.x % kCtrSlots], tot);
-    if (tin) {  // the texel's kGPl planes: one 16*kGPl-B run
-        float4* o = dmpi + ((int64_t)ty * g.W + tx) * g.P + p0;
 #pragma unroll
-        for (int jj = 0; jj < kGPl; ++jj)
-            if (p0 + jj < g.P) o[jj] = make_float4(acc[jj][0], acc[jj][1], acc[jj][2], acc[jj][3]);
+    for (int r = 0; r < kGTR; ++r) {
+        if (tin[r]) {  // the texel's kGPl planes: one 16*kGPl-B run
+            float4* o = dmpi + ((int64_t)ty[r] * g.W + tx) * g.P + p0;
+#pragma unroll
+            for (int jj = 0; jj < kGPl; ++jj)
+                if (p0 + jj < g.P)
+                    bwd_store(o + jj, make_float4(acc[r][jj][0], acc[r][jj][1], acc[r][jj][2], acc[r][jj][3]));
+        }
     }
 }
 
+#if MPIV_AB  // A/B variants of the gather (libmpiv_ab.so): measured slower, DESIGN.md §8
 // ---- 2'. gather with the d samples streamed into LDS one pass ahead (bwd_gather=3) ------
 // bwd_gather_kernel loads a pass's d samples in its staging phase and waits for them there;
 // its texel phase issues no memory traffic, so a block's loads are in flight only part of the
@@ -788,7 +818,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
 // LDS bytes a DMA writes and would drain vmcnt(0) before every ds_read).
 constexpr int kGDF = (kGCap + kGThreads - 1) / kGThreads;  // DMA instructions per wave and pass
 constexpr int kGDS = kGDF * kGThreads;                     // staged slots per buffer (> kGCap)
-static_assert(kGThreads == 4 * kWave && kGDS > kGCap, "the fill covers every staged slot and the zero slot");
+static_assert(kGTR == 1 && kGThreads == 4 * kWave && kGDS > kGCap, "the fill covers every staged slot and the zero slot");
 
 __device__ __forceinline__ void gather_dma16(__amdgpu_buffer_rsrc_t r, int voff, unsigned lds) {
     asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(lds)
@@ -919,7 +949,7 @@ __global__ __launch_bounds__(kGThreads, 4) void bwd_gather_dma_kernel(RenderGeom
     }
 }
 
-#if MPIV_AB  // A/B variants of the gather (libmpiv_ab.so): measured slower, DESIGN.md §8
+
 // ---- 2a'. gather with staging and texel waves (bwd_gather=2) ---------------------------
 // bwd_gather_kernel alternates a memory phase (the staging pass: d-sample loads, positions)
 // and a compute phase (the sorted per-texel sums) behind block barriers, and the two barely
@@ -1616,7 +1646,8 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
             s_ticket = t;
         }
         __syncthreads();
-        const int t = s_ticket;
+        // block-uniform: scalar control flow through the item (its barriers are never divergent)
+        const int t = __builtin_amdgcn_readfirstlane(s_ticket);
         __syncthreads();  // s_ticket is rewritten by the next iteration
         if (t < 0) return;
         bwd_fallback_item<FAST>(g, homs, ws, dmpi, t / nblk, t % nblk, nblk, s_tmp);
