@@ -1603,8 +1603,10 @@ __device__ void bwd_fallback_item(const RenderGeom& g, const float* __restrict__
 // flag words: [0] run the fallback, [1] next ticket, [2] items done, [3] this view aborted,
 // [4] views aborted in this call (sticky; zeroed by mpiv_render_backward's first memset)
 template <bool FAST>
+// fixed != 0 (A/B diagnosis): block b takes items b, b + nblk, ... in order instead of tickets
+// (the grid-barrier schedule: needs every block resident)
 __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
-                                                           float4* __restrict__ dmpi, unsigned poll_limit) {
+                                                           float4* __restrict__ dmpi, unsigned poll_limit, int fixed) {
     __shared__ int s_tmp[kScanBlock];
     __shared__ int s_ticket;
     if (ws.flag[0] == 0) return;  // uniform over the grid: the tile gather was complete
@@ -1614,11 +1616,18 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
     unsigned* ticket = reinterpret_cast<unsigned*>(ws.flag + 1);
     unsigned* done = reinterpret_cast<unsigned*>(ws.flag + 2);
     int* abort_ = ws.flag + 3;
+    unsigned next_fixed = blockIdx.x;
     for (;;) {
         if (tid == 0) {
             int t = -1;
             if (__hip_atomic_load(abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-                const unsigned tk = atomicAdd(ticket, 1u);
+                unsigned tk;
+                if (fixed) {
+                    tk = next_fixed;
+                    next_fixed += (unsigned)nblk;
+                } else {
+                    tk = atomicAdd(ticket, 1u);
+                }
                 if (tk < total) {
                     // every item of the phases before this one done (see above)
                     const unsigned need = tk / (unsigned)nblk * (unsigned)nblk;

@@ -1,9 +1,10 @@
 #!/bin/bash
-# backward A/B across build variants (MPIV_LIB), then the fallback debug cases
+# fallback debug cases, then the backward A/B across build variants (MPIV_LIB)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
-for rep in 1 2; do
+bash tools/gpu_fbdbg.sh
+for rep in 1; do
   for v in default nt gtr2 gtr2l4 gtr2nt; do
     if [ $v = default ]; then lib=""; else lib="build/ab_$v.so"; fi
     echo "== $v rep $rep"
@@ -11,4 +12,3 @@ for rep in 1 2; do
     rc=$?; tail -2 $OUT/bwdab_${v}_$rep.jsonl; [ $rc -eq 0 ] || exit $rc
   done
 done
-bash tools/gpu_fbdbg.sh
