@@ -1353,25 +1353,25 @@ __global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force) {
 // tile sums of the sizes, their scan (one block), the exclusive scan applied, pixel ids into
 // their buckets, small buckets sorted by pixel id (large ones listed), large buckets sorted by
 // a whole block each, then per texel the four buckets merged in the reference's order; one
-// phase up front zeroes the sizes.  Each phase is a grid-stride loop over nblk virtual blocks.
+// phase up front zeroes the sizes.  Each phase is a grid-stride loop over the nblk blocks,
+// separated by grid barriers (grid_barrier: the launch is sized so every block is resident;
+// a wait that outlasts its poll limit aborts the view LOUDLY -- NaN gradient, counted in
+// flag[4] for mpiv_render_backward_status -- instead of returning a plausible wrong one).
 // (A normal launch, not hipLaunchCooperativeKernel: rocprofv3's kernel tracer crashes in its
 // teardown after a cooperative launch, and this one is issued on every backward.)
 //
-// The phases are ordered by TICKETS, not by a grid barrier over resident blocks.  A block
-// takes the next ticket t (flag[1], one device-scope atomic): virtual block t % nblk of phase
-// ph = t / nblk.  It waits until the completion counter (flag[2]) reaches ph * nblk, runs the
-// item and adds one to the counter.  The counter counts items of every phase, yet reaching
-// ph * nblk means exactly "every item of phases < ph is done": an item of phase q only runs
-// after seeing the counter at >= q * nblk, so the completions counted before it first
-// reaches ph * nblk all come from phases < ph, which hold ph * nblk items.  Tickets are taken
-// in increasing order, so every item a waiting block depends on was taken earlier by a block
-// that is running (a block that is not resident holds no ticket), and the holder of the lowest
-// unfinished ticket never waits: the pipeline completes whatever else the device runs (other
-// streams, RCCL kernels, other processes) and however few of its blocks are resident, where a
-// barrier over "all resident" blocks deadlocks.  A wait longer than poll_limit polls (never
-// expected: the argument above; tests force it with a tiny limit) sets flag[3], counts the view
-// in flag[4] (read by mpiv_render_backward_status) and every block stops; bwd_poison_kernel
-// then fills the view's gradient with NaN, so an aborted view is never a plausible gradient.
+// A/B (bwd_fb_ticket=1, libmpiv_ab.so): the same phases ordered by TICKETS instead of barriers
+// (bwd_fallback_ticket_kernel), which needs no block to be resident.  A block takes the next
+// ticket t (flag[1], one device-scope atomic): virtual block t % nblk of phase ph = t / nblk.
+// It waits until the completion counter (flag[2]) reaches ph * nblk, runs the item and adds
+// one to the counter.  The counter counts items of every phase, yet reaching ph * nblk means
+// exactly "every item of phases < ph is done": an item of phase q only runs after seeing the
+// counter at >= q * nblk, so the completions counted before it first reaches ph * nblk all come
+// from phases < ph, which hold ph * nblk items.  Tickets are taken in increasing order, so
+// every item a waiting block depends on was taken earlier by a block that is running, and the
+// holder of the lowest unfinished ticket never waits.  Round 4: this kernel hung on the box in
+// its first runs (even with 4 blocks); it stays an A/B variant until that is understood
+// (DESIGN.md §8), and the production launch keeps the barrier schedule with the loud abort.
 constexpr int kFbPhases = 8;  // per plane chunk
 
 __device__ __forceinline__ int block_exclusive_scan(int v, int* s_tmp, int& total) {
@@ -1390,10 +1390,255 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* s_tmp, int& tota
     return incl - v;
 }
 
+// Grid-wide barrier (the production fallback's phases): arrive = one device-scope atomic per
+// block after a release fence, wait = poll the counter (flag[1], zeroed by bwd_check_kernel)
+// until every block of this phase has arrived, then an acquire fence (the fences write back /
+// invalidate the XCD's L2, so the next phase sees every block's stores).  The launch is sized
+// so every block is resident (<= 4 per CU and the device's occupancy for it); should a wait
+// still outlast poll_limit polls (blocks kept from residency by other work on the device), the
+// block sets flag[3], counts the view in flag[4] and every block leaves at its next barrier:
+// bwd_poison_kernel then NaN-fills the view's gradient and mpiv_render_backward_status reports
+// it -- never a plausible wrong gradient.  poll_limit 0 (tests): abort at the first barrier.
+__device__ __forceinline__ bool grid_barrier(int* flag, unsigned target, unsigned poll_limit, int* s_abort) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* ctr = reinterpret_cast<unsigned*>(flag + 1);
+        int ab = 0;
+        __threadfence();
+        atomicAdd(ctr, 1u);
+        if (poll_limit == 0) {
+            if (atomicExch(flag + 3, 1) == 0) atomicAdd(flag + 4, 1);
+            ab = 1;
+        }
+        unsigned spins = 0;
+        while (!ab && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(flag + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                ab = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > poll_limit) {
+                if (atomicExch(flag + 3, 1) == 0) atomicAdd(flag + 4, 1);
+                ab = 1;
+            }
+        }
+        __threadfence();
+        *s_abort = ab;
+    }
+    __syncthreads();
+    return *s_abort != 0;
+}
+
 __device__ __forceinline__ unsigned order_key(int pix, int corner) {
     return ((unsigned)(pix / kGridVec) << 5) | ((unsigned)corner << 3) | (unsigned)(pix % kGridVec);
 }
 
+template <bool FAST>
+__global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
+                                                           float4* __restrict__ dmpi, unsigned poll_limit) {
+    __shared__ int s_tmp[kScanBlock];
+    __shared__ int s_abort;
+    if (ws.flag[0] == 0) return;  // uniform over the grid: the tile gather was complete
+    const int bid = blockIdx.x, nblk = gridDim.x, tid = threadIdx.x;
+    unsigned phase = 0;
+    // true: the pipeline aborted (a wait gave up here or in another block): every block stops
+    auto sync = [&]() { return grid_barrier(ws.flag, ++phase * (unsigned)nblk, poll_limit, &s_abort); };
+    const int64_t gtid = (int64_t)bid * 256 + tid, gstride = (int64_t)nblk * 256;
+    const int64_t HW = (int64_t)g.H * g.W;
+    const int K1 = g.W + 1;
+    const int64_t K = (int64_t)(g.H + 1) * K1;
+    // bucket sizes start at zero (the fill returns them to zero for the next chunk)
+    for (int64_t i = gtid; i < (int64_t)ws.pc * K; i += gstride) ws.count[i] = 0;
+    if (sync()) return;
+    for (int pc0 = 0; pc0 < g.P; pc0 += ws.pc) {
+        const int pcn = min(ws.pc, g.P - pc0);
+        const int64_t nq = pcn * HW, nk = pcn * K;
+        const int nb = (int)((nk + kScanTile - 1) / kScanTile);
+        // nw-tap bucket of every (plane of the chunk, pixel) sample; sizes counted
+        for (int64_t q = gtid; q < nq; q += gstride) {
+            const int pl = (int)(q / HW);
+            const int pix = (int)(q - pl * HW);
+            const int y = pix / g.W, x = pix - y * g.W;
+            float px, py;
+            render_pos<FAST>(homs + (int64_t)(pc0 + pl) * 9, (float)x, (float)y, g, px, py);
+            const float fx0 = floorf(px), fy0 = floorf(py);
+            // some tap lies in the image iff the nw tap is in [-1, W-1] x [-1, H-1] (NaN: none)
+            const bool in = fx0 >= -1.0f && fx0 <= (float)(g.W - 1) && fy0 >= -1.0f && fy0 <= (float)(g.H - 1);
+            const int k = in ? ((int)fy0 + 1) * K1 + (int)fx0 + 1 : -1;
+            ws.key[q] = k;
+            if (in) atomicAdd(&ws.count[pl * K + k], 1);
+        }
+        if (sync()) return;
+        // exclusive scan of the sizes: tile sums, their scan (block 0), per-tile apply
+        for (int tb = bid; tb < nb; tb += nblk) {
+            const int64_t base = (int64_t)tb * kScanTile + (int64_t)tid * kScanItems;
+            int sum = 0;
+            for (int i = 0; i < kScanItems; ++i)
+                if (base + i < nk) sum += ws.count[base + i];
+            int total;
+            block_exclusive_scan(sum, s_tmp, total);
+            if (tid == 0) ws.bsum[tb] = total;
+        }
+        if (sync()) return;
+        if (bid == 0) {
+            int carry = 0;
+            for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
+                const int i = c0 + tid;
+                const int v = i < nb ? ws.bsum[i] : 0;
+                int total;
+                const int ex = block_exclusive_scan(v, s_tmp, total);
+                if (i < nb) ws.bsum[i] = carry + ex;
+                carry += total;
+            }
+            if (tid == 0) ws.big[0] = 0;
+        }
+        if (sync()) return;
+        for (int tb = bid; tb < nb; tb += nblk) {
+            const int64_t base = (int64_t)tb * kScanTile + (int64_t)tid * kScanItems;
+            int v[kScanItems];
+            int sum = 0;
+#pragma unroll
+            for (int i = 0; i < kScanItems; ++i) {
+                v[i] = base + i < nk ? ws.count[base + i] : 0;
+                sum += v[i];
+            }
+            int total;
+            int run = ws.bsum[tb] + block_exclusive_scan(sum, s_tmp, total);
+#pragma unroll
+            for (int i = 0; i < kScanItems; ++i) {
+                if (base + i < nk) ws.offs[base + i] = run;
+                run += v[i];
+            }
+            if (tb == nb - 1 && tid == kScanBlock - 1) ws.offs[nk] = run;  // grand total
+        }
+        if (sync()) return;
+        // pixel ids into their buckets (atomic slot claim; sizes return to zero)
+        for (int64_t q = gtid; q < nq; q += gstride) {
+            const int k = ws.key[q];
+            if (k < 0) continue;
+            const int64_t pl = q / HW;
+            const int64_t pk = pl * K + k;
+            const int slot = atomicSub(&ws.count[pk], 1) - 1;
+            ws.ids[ws.offs[pk] + slot] = (int)(q - pl * HW);
+        }
+        if (sync()) return;
+        // each bucket sorted by pixel id: <= kSmallBucket ids by one thread (insertion
+        // sort), larger ones (minification, degenerate homographies) listed for a block
+        for (int64_t pk = gtid; pk < nk; pk += gstride) {
+            const int b = ws.offs[pk], e = ws.offs[pk + 1];
+            if (e - b > kSmallBucket) {
+                ws.big[1 + atomicAdd(&ws.big[0], 1)] = (int)pk;
+                continue;
+            }
+            for (int i = b + 1; i < e; ++i) {
+                const int v = ws.ids[i];
+                int jx = i - 1;
+                while (jx >= b && ws.ids[jx] > v) {
+                    ws.ids[jx + 1] = ws.ids[jx];
+                    --jx;
+                }
+                ws.ids[jx + 1] = v;
+            }
+        }
+        if (sync()) return;
+        // the large buckets: one block each, merge sort with all threads (runs of width w
+        // merged pairwise per pass, output element k of a pair found by a merge-path binary
+        // search; ids within a bucket are distinct).  Scratch: the bucket's range of `key`
+        // (dead after the fill).  O(n log^2 n / threads) per bucket.
+        const int nbig = ws.big[0];
+        for (int i = bid; i < nbig; i += nblk) {
+            const int pk = ws.big[1 + i];
+            const int b = ws.offs[pk], n = ws.offs[pk + 1] - b;
+            int* src = ws.ids + b;
+            int* dst = ws.key + b;
+            for (int w = 1; w < n; w <<= 1) {
+                for (int k0 = tid; k0 < n; k0 += 256) {
+                    const int s0 = (k0 / (2 * w)) * (2 * w);
+                    const int mm = min(s0 + w, n), e = min(s0 + 2 * w, n);
+                    const int k = k0 - s0;
+                    const int* A = src + s0;
+                    const int* Bv = src + mm;
+                    const int la = mm - s0, lb = e - mm;
+                    int lo = max(0, k - lb), hi = min(k, la);
+                    while (lo < hi) {  // number of A's elements among the pair's first k outputs
+                        const int mid = (lo + hi) >> 1;
+                        if (A[mid] < Bv[k - 1 - mid])
+                            lo = mid + 1;
+                        else
+                            hi = mid;
+                    }
+                    const int ib = k - lo;
+                    dst[k0] = (lo < la && (ib >= lb || A[lo] < Bv[ib])) ? A[lo] : Bv[ib];
+                }
+                __syncthreads();
+                int* t = src;
+                src = dst;
+                dst = t;
+            }
+            if (src != ws.ids + b)
+                for (int k0 = tid; k0 < n; k0 += 256) ws.ids[b + k0] = src[k0];
+            __syncthreads();
+        }
+        if (sync()) return;
+        // texel t of plane pc0 + pl: its four nw-tap buckets (the samples having it as nw,
+        // ne, sw, se tap) merged by the reference's order key; fractions from the position
+        for (int64_t q = gtid; q < nq; q += gstride) {
+            const int pl = (int)(q / HW);
+            const int t = (int)(q - pl * HW);
+            const int ty = t / g.W, tx = t - ty * g.W;
+            const float* h = homs + (int64_t)(pc0 + pl) * 9;
+            const int64_t base = pl * K;
+            const int64_t bk[4] = {base + (int64_t)(ty + 1) * K1 + tx + 1, base + (int64_t)(ty + 1) * K1 + tx,
+                                   base + (int64_t)ty * K1 + tx + 1, base + (int64_t)ty * K1 + tx};
+            int pos[4], end[4];
+            unsigned head[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                pos[c] = ws.offs[bk[c]];
+                end[c] = ws.offs[bk[c] + 1];
+                head[c] = pos[c] < end[c] ? order_key(ws.ids[pos[c]], c) : 0xFFFFFFFFu;
+            }
+            const float4* dsp = ws.ds + (int64_t)(pc0 + pl) * HW;
+            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+            for (;;) {
+                int c = 0;
+                unsigned m = head[0];
+#pragma unroll
+                for (int k = 1; k < 4; ++k)
+                    if (head[k] < m) {
+                        m = head[k];
+                        c = k;
+                    }
+                if (m == 0xFFFFFFFFu) break;
+                int pix = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {  // static indexing keeps pos/head in registers
+                    if (k == c) {
+                        pix = ws.ids[pos[k]];
+                        ++pos[k];
+                        head[k] = pos[k] < end[k] ? order_key(ws.ids[pos[k]], k) : 0xFFFFFFFFu;
+                    }
+                }
+                const int py_ = pix / g.W;
+                float px, py;
+                render_pos<FAST>(h, (float)(pix - py_ * g.W), (float)py_, g, px, py);
+                const float wx = px - floorf(px), ex = 1.0f - wx;
+                const float wy = py - floorf(py), sy = 1.0f - wy;
+                const float w = ((c & 2) ? wy : sy) * ((c & 1) ? wx : ex);
+                const float4 d = dsp[pix];
+                a0 = a0 + w * d.x;
+                a1 = a1 + w * d.y;
+                a2 = a2 + w * d.z;
+                a3 = a3 + w * d.w;
+            }
+            dmpi[(int64_t)t * g.P + pc0 + pl] = make_float4(a0, a1, a2, a3);
+        }
+        if (sync()) return;  // the chunk's arrays are reused by the next one
+    }
+}
+
+
+#if MPIV_AB
 // One item of the fallback pipeline: virtual block bid (of nblk) of phase ph (0: zero the
 // bucket sizes; 1 + kFbPhases * c + k: step k for plane chunk c)
 template <bool FAST>
@@ -1605,8 +1850,9 @@ __device__ void bwd_fallback_item(const RenderGeom& g, const float* __restrict__
 template <bool FAST>
 // fixed != 0 (A/B diagnosis): block b takes items b, b + nblk, ... in order instead of tickets
 // (the grid-barrier schedule: needs every block resident)
-__global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
-                                                           float4* __restrict__ dmpi, unsigned poll_limit, int fixed) {
+__global__ __launch_bounds__(256) void bwd_fallback_ticket_kernel(RenderGeom g, const float* __restrict__ homs,
+                                                                  BwdWs ws, float4* __restrict__ dmpi,
+                                                                  unsigned poll_limit, int fixed) {
     __shared__ int s_tmp[kScanBlock];
     __shared__ int s_ticket;
     if (ws.flag[0] == 0) return;  // uniform over the grid: the tile gather was complete
@@ -1667,6 +1913,8 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
         }
     }
 }
+
+#endif  // MPIV_AB
 
 // After the fallback: a view whose pipeline aborted (flag[3]) gets a NaN gradient
 __global__ __launch_bounds__(256) void bwd_poison_kernel(const int* __restrict__ flag, float4* __restrict__ dmpi,

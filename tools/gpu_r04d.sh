@@ -1,0 +1,24 @@
+#!/bin/bash
+# round-4 session: production fallback check, backward A/B (MPIV_LIB variants), GPU tests,
+# bench line, then the ticket-fallback diagnosis (last: it may hang until its time limit)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out; mkdir -p $OUT
+TAG=${TAG:-r04d}
+for c in "ga fallback" "gbig tile"; do
+  echo "== $c"; timeout -k 5 40 python3 -u tools/fb_dbg.py $c; rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+for v in default nt gtr2 gtr2l4 gtr2nt; do
+  if [ $v = default ]; then lib=""; else lib="build/ab_$v.so"; fi
+  echo "== bwd $v"
+  MPIV_LIB=$lib timeout -k 5 60 python3 -u tools/bwd_ab.py 0 > $OUT/bwdab_${v}_$TAG.jsonl 2>&1
+  rc=$?; tail -1 $OUT/bwdab_${v}_$TAG.jsonl; [ $rc -eq 0 ] || exit $rc
+done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests_$TAG.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -3 $OUT/gpu_tests_$TAG.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -u bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
+rc=$?; echo "bench rc=$rc"; tail -c 300 $OUT/bench_$TAG.err; [ $rc -eq 0 ] || exit $rc
+for c in "ga tk_one" "ga tk_fixed4" "ga tk_fixed" "ga tk"; do
+  echo "== $c"; timeout -k 5 25 python3 -u tools/fb_dbg.py $c; rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || break
+done
+echo "session done"
