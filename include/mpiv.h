@@ -249,6 +249,15 @@ int mpiv_plane_sweep(const float *img, const int64_t img_strides[4], int B, int 
                      const float *ki, const float *proj, const float *depths, int D, int Ht, int Wt,
                      float *out, void *stream);
 
+/* mpiv_plane_sweep with proj formed on the device from a pose in HBM (the notebook's dataset
+ * call): proj_scratch [B][16] receives [[K_src, 0], [0, 0, 0, 1]] @ pose (mpiv_psv_proj_device,
+ * bit-identical to the reference's torch-CPU proj), then the sweep runs from it.  Ks [B][3][3]
+ * at batch stride ks_bstride floats (0: one camera), pose [B][4][4]; ki as mpiv_plane_sweep. */
+int mpiv_plane_sweep_pose(const float *img, const int64_t img_strides[4], int B, int Hs, int Ws, int C,
+                          const float *ki, const float *Ks, int64_t ks_bstride, const float *pose,
+                          float *proj_scratch, const float *depths, int D, int Ht, int Wt, float *out,
+                          void *stream);
+
 /* The same writing into a wider tensor (C <= 4): element (b, pixel, d, c) goes to
  * out[b*out_bstride + pixel*out_pstride + d*C + c] (format_network_input_torch, utils.py:473-498,
  * writes each source's volume at its channel offset of the concatenated network input);

@@ -186,6 +186,25 @@ def psv_matrices(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pos
     return ki, proj
 
 
+def psv_ki_device(tgt_intrinsics: torch.Tensor, batch: int, dev) -> torch.Tensor:
+    """Ki = inverse(K_tgt) [batch, 9] on dev, memoised per intrinsics tensor (_kinv_device)."""
+    return _kinv_device(tgt_intrinsics, batch, dev).reshape(batch, 9)
+
+
+def device_cameras(src_intrinsics: torch.Tensor, pose: torch.Tensor, batch: int):
+    """(Ks, pose) as the device kernels take them: Ks fp32 [3,3] (one camera) or [batch,3,3]
+    with contiguous 3x3 blocks, pose fp32 [batch,4,4] contiguous, on the pose's device."""
+    dev = pose.device
+    Ks = src_intrinsics.to(device=dev, dtype=_F32)
+    if Ks.dim() == 2:
+        Ks = Ks.contiguous()
+    else:
+        Ks = Ks.expand(batch, 3, 3)
+        if Ks.stride(1) != 3 or Ks.stride(2) != 1:
+            Ks = Ks.contiguous()
+    return Ks, pose.to(dtype=_F32).reshape(batch, 4, 4).contiguous()
+
+
 def psv_matrices_device(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pose: torch.Tensor,
                         batch: int):
     """psv_matrices for a pose that lives on a ROCm device (the notebook's dataset call keeps
@@ -196,17 +215,9 @@ def psv_matrices_device(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tens
     Intrinsics [3,3] (one camera for the batch) or [batch,3,3]; pose [batch,4,4]."""
     from . import _lib
     dev = pose.device
-    ki = _kinv_device(tgt_intrinsics, batch, dev).reshape(batch, 9)
-    Ks = src_intrinsics.to(device=dev, dtype=_F32)
-    if Ks.dim() == 2:
-        Ks = Ks.contiguous()
-        ks_b = 0
-    else:
-        Ks = Ks.expand(batch, 3, 3)
-        if Ks.stride(1) != 3 or Ks.stride(2) != 1:
-            Ks = Ks.contiguous()
-        ks_b = Ks.stride(0)
-    pose_d = pose.to(dtype=_F32).reshape(batch, 4, 4).contiguous()
+    ki = psv_ki_device(tgt_intrinsics, batch, dev)
+    Ks, pose_d = device_cameras(src_intrinsics, pose, batch)
+    ks_b = 0 if Ks.dim() == 2 else Ks.stride(0)
     proj = torch.empty((batch, 16), dtype=_F32, device=dev)
     _lib._call("mpiv_psv_proj_device", Ks, ks_b, pose_d, batch, proj, _lib._stream(dev))
     return ki, proj

@@ -38,6 +38,8 @@ _SIGS = {
     "mpiv_render_packed_ct_rows": [_vp, _int, _int, _int, _int, _int, _int, _vp, _int, _int, _int, _vp, _vp],
     "mpiv_combine_ct": [_vp, _int, _i64, _vp, _vp],
     "mpiv_plane_sweep": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
+    "mpiv_plane_sweep_pose": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _i64, _vp, _vp, _vp, _int, _int, _int,
+                              _vp, _vp],
     "mpiv_inverse_warp": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _c_i64p, _int, _int, _vp, _vp],
     "mpiv_grid_sample": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _c_i64p, _int, _int, _vp, _c_i64p, _vp],
     "mpiv_over_composite": [_vp, _int, _i64, _i64, _i64, _vp, _vp],
@@ -772,6 +774,32 @@ def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.T
     out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
     kid, projd = _up(ki, dev), _up(proj, dev)
     _call("mpiv_plane_sweep", img, _strides(img), B, Hs, Ws, C, kid, projd, dd, D, tgt_h, tgt_w, out, _stream(dev))
+    return out
+
+
+_PROJ_SCRATCH: dict = {}
+
+
+def plane_sweep_pose(img: torch.Tensor, depth_planes, ki: torch.Tensor, Ks: torch.Tensor, pose: torch.Tensor,
+                     tgt_h: int, tgt_w: int) -> torch.Tensor:
+    """plane_sweep with proj = K4_src @ pose formed on the device in the same call
+    (mpiv_plane_sweep_pose): ki [B,9] on the device, Ks [3,3] (one camera) or [B,3,3] with
+    3x3 blocks contiguous, pose [B,4,4] on the device.  The [B,16] proj lands in a scratch
+    buffer kept per device and stream (reused in stream order)."""
+    _require_depths(depth_planes)
+    dev = _dev(img, Ks, pose)
+    B, Hs, Ws, C = img.shape
+    dd = _depths_on(depth_planes, dev)
+    D = dd.shape[0]
+    stream = torch.cuda.current_stream(dev)
+    key = (str(dev), stream.cuda_stream)
+    scratch = _PROJ_SCRATCH.get(key)
+    if scratch is None or scratch.numel() < B * 16:
+        scratch = _PROJ_SCRATCH[key] = torch.empty(max(B, 8) * 16, device=dev, dtype=torch.float32)
+    ks_b = 0 if Ks.dim() == 2 else Ks.stride(0)
+    out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
+    _call("mpiv_plane_sweep_pose", img, _strides(img), B, Hs, Ws, C, ki, Ks, ks_b, pose, scratch, dd, D, tgt_h, tgt_w,
+          out, ctypes.c_void_p(stream.cuda_stream))
     return out
 
 

@@ -960,6 +960,20 @@ int mpiv_plane_sweep(const float* img, const int64_t st[4], int B, int Hs, int W
     return launched("mpiv_plane_sweep");
 }
 
+// mpiv_plane_sweep for a pose already in HBM: proj = [[K_src, 0], [0, 0, 0, 1]] @ pose formed on
+// the device into proj_scratch (mpiv_psv_proj_device's kernel) and the sweep, one call.
+int mpiv_plane_sweep_pose(const float* img, const int64_t st[4], int B, int Hs, int Ws, int C, const float* ki,
+                          const float* Ks, int64_t ks_bstride, const float* pose, float* proj_scratch,
+                          const float* depths, int D, int Ht, int Wt, float* out, void* stream) {
+    const char* nm = "mpiv_plane_sweep_pose";
+    if (!Ks || !pose || !proj_scratch) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (B <= 0 || ks_bstride < 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    if (g_route) return mpiv_plane_sweep(img, st, B, Hs, Ws, C, ki, proj_scratch, depths, D, Ht, Wt, out, stream);
+    psv_proj_kernel<<<blocks(B, 64), 64, 0, S(stream)>>>(Ks, ks_bstride, pose, B, proj_scratch);
+    if (int rc = launched(nm)) return rc;
+    return mpiv_plane_sweep(img, st, B, Hs, Ws, C, ki, proj_scratch, depths, D, Ht, Wt, out, stream);
+}
+
 int mpiv_pad_texels(const float* img, const int64_t st[4], int B, int Hs, int Ws, int C, float* img4,
                     void* stream) {
     if (!img || !st || !img4) return fail(MPIV_ERR_ARG, "mpiv_pad_texels: null pointer");

@@ -247,8 +247,11 @@ def plane_sweep_torch(img, depth_planes, pose, intrinsics):
 
 
 def _plane_sweep(img, depth_planes, pose, src_intrinsics, tgt_intrinsics, height, width):
-    if img.is_cuda and pose.is_cuda:  # pose in HBM: its matrices are formed there too
-        ki, proj = _host.psv_matrices_device(src_intrinsics, tgt_intrinsics, pose, pose.shape[0])
+    if img.is_cuda and pose.is_cuda:  # pose in HBM: proj is formed there, in the sweep's own call
+        B = pose.shape[0]
+        Ks, pose_d = _host.device_cameras(src_intrinsics, pose, B)
+        return _lib.plane_sweep_pose(img, depth_planes, _host.psv_ki_device(tgt_intrinsics, B, pose.device), Ks,
+                                     pose_d, height, width)
     else:
         ki, proj = _host.psv_matrices(_batched(src_intrinsics), _batched(tgt_intrinsics), pose, pin=img.is_cuda)
     return _lib.plane_sweep(img, depth_planes, ki, proj, height, width)
