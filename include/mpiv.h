@@ -387,6 +387,12 @@ int mpiv_probe_gather(const float *window, size_t window_bytes, int iters, int b
  * x / (W-1) via a precomputed reciprocal + two residual corrections) against IEEE
  * division for all 2^32 fp32 inputs and the given integer divisor; adds the number
  * of relevant mismatches to *mismatches (device counter, caller-zeroed). */
+/* A/B diagnosis (libmpiv_ab.so only): the render backward fallback's ticket protocol with
+ * trivial items; ctr: 4 zeroed device words (tickets, completions, violations, aborted waits),
+ * marks: nphase * nvirt zeroed device ints. */
+int mpiv_selftest_tickets(int blocks, int nphase, int nvirt, unsigned poll_limit, unsigned *ctr, int *marks,
+                          void *stream);
+
 int mpiv_selftest_div_const(int divisor, unsigned long long *mismatches, void *stream);
 
 #ifdef __cplusplus

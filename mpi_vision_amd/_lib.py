@@ -49,6 +49,7 @@ _SIGS = {
     "mpiv_cam2pixel": [_vp, _vp, _int, _i64, _vp, _vp],
     "mpiv_plane_coords": [_vp, _int, _i64, _vp, _int, _int, _vp, _vp],
     "mpiv_selftest_div_const": [_int, _vp, _vp],
+    "mpiv_selftest_tickets": [_int, _int, _int, ctypes.c_uint, _vp, _vp, _vp],
     "mpiv_probe_gather": [_vp, ctypes.c_size_t, _int, _int, _vp, _vp],
     "mpiv_route": [ctypes.c_char_p, _c_i64p, _int, ctypes.c_char_p, _int, _c_i64p],
     "mpiv_pad_texels": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],

@@ -1491,6 +1491,20 @@ int mpiv_route(const char* entry, const int64_t* a, int na, char* name, int name
     return MPIV_OK;
 }
 
+// A/B diagnosis: the backward fallback's ticket protocol with trivial items (render_bwd.hip
+// ticket_selftest_kernel).  ctr: 4 zeroed device words, marks: nphase * nvirt zeroed ints.
+int mpiv_selftest_tickets(int blocks_, int nphase, int nvirt, unsigned poll_limit, unsigned* ctr, int* marks,
+                          void* stream) {
+#if MPIV_AB
+    if (!ctr || !marks || blocks_ <= 0 || nphase <= 0 || nvirt <= 0) return fail(MPIV_ERR_ARG, "mpiv_selftest_tickets: bad args");
+    ticket_selftest_kernel<<<blocks_, 256, 0, S(stream)>>>(ctr, marks, nphase, nvirt, poll_limit);
+    return launched("mpiv_selftest_tickets");
+#else
+    (void)blocks_, (void)nphase, (void)nvirt, (void)poll_limit, (void)ctr, (void)marks, (void)stream;
+    return fail(MPIV_ERR_ARG, "mpiv_selftest_tickets: an A/B diagnosis, built only into libmpiv_ab.so");
+#endif
+}
+
 int mpiv_selftest_div_const(int divisor, unsigned long long* mismatches, void* stream) {
     if (!mismatches || divisor < 1) return fail(MPIV_ERR_ARG, "mpiv_selftest_div_const: bad args");
     const float c = (float)divisor;

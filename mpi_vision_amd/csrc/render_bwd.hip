@@ -1916,6 +1916,54 @@ __global__ __launch_bounds__(256) void bwd_fallback_ticket_kernel(RenderGeom g, 
 
 #endif  // MPIV_AB
 
+#if MPIV_AB
+// Ticket-protocol self-test (diagnosis of bwd_fallback_ticket_kernel): the same ticket / wait /
+// completion code with trivial items -- item (phase q, virtual block b) checks that every item
+// of phase q-1 has left its mark, counts the ones missing in ctr[2], and marks marks[q][b].
+// ctr: [0] tickets, [1] completions, [2] violations, [3] aborted waits (zeroed by the caller).
+__global__ __launch_bounds__(256) void ticket_selftest_kernel(unsigned* __restrict__ ctr, int* __restrict__ marks,
+                                                              int nphase, int nvirt, unsigned poll_limit) {
+    __shared__ int s_ticket;
+    const int tid = threadIdx.x;
+    const unsigned total = (unsigned)nphase * (unsigned)nvirt;
+    for (;;) {
+        if (tid == 0) {
+            int t = -1;
+            const unsigned tk = atomicAdd(ctr, 1u);
+            if (tk < total) {
+                const unsigned need = tk / (unsigned)nvirt * (unsigned)nvirt;
+                unsigned spins = 0;
+                t = (int)tk;
+                while (__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > poll_limit) {
+                        atomicAdd(ctr + 3, 1u);
+                        break;
+                    }
+                }
+                __threadfence();
+            }
+            s_ticket = t;
+        }
+        __syncthreads();
+        const int t = __builtin_amdgcn_readfirstlane(s_ticket);
+        __syncthreads();
+        if (t < 0) return;
+        const int q = t / nvirt, b = t % nvirt;
+        unsigned bad = 0;
+        if (q > 0)
+            for (int i = tid; i < nvirt; i += 256) bad += marks[(q - 1) * nvirt + i] != 1;
+        if (bad) atomicAdd(ctr + 2, bad);
+        __syncthreads();
+        if (tid == 0) {
+            marks[q * nvirt + b] = 1;
+            __threadfence();
+            atomicAdd(ctr + 1, 1u);
+        }
+    }
+}
+#endif
+
 // After the fallback: a view whose pipeline aborted (flag[3]) gets a NaN gradient
 __global__ __launch_bounds__(256) void bwd_poison_kernel(const int* __restrict__ flag, float4* __restrict__ dmpi,
                                                          int64_t n) {

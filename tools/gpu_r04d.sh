@@ -18,6 +18,9 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; echo "tests rc=$rc"; tail -3 $OUT/gpu_tests_$TAG.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 -u bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
 rc=$?; echo "bench rc=$rc"; tail -c 300 $OUT/bench_$TAG.err; [ $rc -eq 0 ] || exit $rc
+for a in "1 9 4" "4 9 4" "1024 9 1024"; do
+  echo "== tickets $a"; timeout -k 5 25 python3 -u tools/ticket_selftest.py $a; rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || break
+done
 for c in "ga tk_one" "ga tk_fixed4" "ga tk_fixed" "ga tk"; do
   echo "== $c"; timeout -k 5 25 python3 -u tools/fb_dbg.py $c; rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || break
 done
