@@ -62,7 +62,7 @@ def _inverse_cached(K: torch.Tensor) -> torch.Tensor:
 _KINV_DEV: dict = {}
 
 
-def _kinv_device(intrinsics: torch.Tensor, batch: int, dev) -> torch.Tensor:
+def _kinv_device(intrinsics: torch.Tensor, batch: int, dev, sid=None) -> torch.Tensor:
     """inverse(K) [batch,3,3] on `dev` for a device-resident intrinsics tensor, memoised on
     that tensor OBJECT and its version counter (an in-place update bumps it; a new tensor
     is a new object), so a camera path that reuses one intrinsics tensor reads it back to
@@ -74,7 +74,7 @@ def _kinv_device(intrinsics: torch.Tensor, batch: int, dev) -> torch.Tensor:
         ver = None
     # the stream is part of the key: the copy's memory, once evicted, is reused in the order of
     # the stream that allocated it, so each stream reads only its own copy
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    stream = torch.cuda.current_stream(dev).cuda_stream if sid is None else sid
     ent = _KINV_DEV.get(id(intrinsics))
     if (ver is not None and ent is not None and ent[0]() is intrinsics and ent[1] == ver and ent[2] == batch
             and ent[3].device == dev and ent[4] == stream):
@@ -186,23 +186,31 @@ def psv_matrices(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pos
     return ki, proj
 
 
-def psv_ki_device(tgt_intrinsics: torch.Tensor, batch: int, dev) -> torch.Tensor:
-    """Ki = inverse(K_tgt) [batch, 9] on dev, memoised per intrinsics tensor (_kinv_device)."""
-    return _kinv_device(tgt_intrinsics, batch, dev).reshape(batch, 9)
+def psv_ki_device(tgt_intrinsics: torch.Tensor, batch: int, dev, sid=None) -> torch.Tensor:
+    """Ki = inverse(K_tgt) [batch, 3, 3] (contiguous: read as [batch, 9]) on dev, memoised per
+    intrinsics tensor (_kinv_device)."""
+    return _kinv_device(tgt_intrinsics, batch, dev, sid)
 
 
 def device_cameras(src_intrinsics: torch.Tensor, pose: torch.Tensor, batch: int):
     """(Ks, pose) as the device kernels take them: Ks fp32 [3,3] (one camera) or [batch,3,3]
     with contiguous 3x3 blocks, pose fp32 [batch,4,4] contiguous, on the pose's device."""
     dev = pose.device
-    Ks = src_intrinsics.to(device=dev, dtype=_F32)
+    Ks = src_intrinsics
+    if Ks.dtype != _F32 or Ks.device != dev:
+        Ks = Ks.to(device=dev, dtype=_F32)
     if Ks.dim() == 2:
-        Ks = Ks.contiguous()
+        if not Ks.is_contiguous():
+            Ks = Ks.contiguous()
     else:
         Ks = Ks.expand(batch, 3, 3)
         if Ks.stride(1) != 3 or Ks.stride(2) != 1:
             Ks = Ks.contiguous()
-    return Ks, pose.to(dtype=_F32).reshape(batch, 4, 4).contiguous()
+    if pose.dtype != _F32:
+        pose = pose.to(dtype=_F32)
+    if not pose.is_contiguous():
+        pose = pose.contiguous()
+    return Ks, pose  # [4,4] or [batch,4,4]: the kernel reads batch * 16 floats
 
 
 def psv_matrices_device(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pose: torch.Tensor,
@@ -215,8 +223,9 @@ def psv_matrices_device(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tens
     Intrinsics [3,3] (one camera for the batch) or [batch,3,3]; pose [batch,4,4]."""
     from . import _lib
     dev = pose.device
-    ki = psv_ki_device(tgt_intrinsics, batch, dev)
+    ki = psv_ki_device(tgt_intrinsics, batch, dev).reshape(batch, 9)
     Ks, pose_d = device_cameras(src_intrinsics, pose, batch)
+    pose_d = pose_d.reshape(batch, 4, 4)
     ks_b = 0 if Ks.dim() == 2 else Ks.stride(0)
     proj = torch.empty((batch, 16), dtype=_F32, device=dev)
     _lib._call("mpiv_psv_proj_device", Ks, ks_b, pose_d, batch, proj, _lib._stream(dev))

@@ -733,7 +733,7 @@ class AssembleFunction(torch.autograd.Function):
 _DEPTHS_DEV: dict = {}
 
 
-def _depths_on(depth_planes, dev) -> torch.Tensor:
+def _depths_on(depth_planes, dev, sid=None) -> torch.Tensor:
     """The sweep depths as a contiguous fp32 tensor on `dev`.  The reference iterates
     `for depth in depth_planes` and adds each to an fp32 zero map (utils.py:466-467), so a
     list of floats and a tensor (the notebook passes torch.Tensor(inv_depths(...)).to(device),
@@ -742,15 +742,18 @@ def _depths_on(depth_planes, dev) -> torch.Tensor:
     list and device (memoised)."""
     if isinstance(depth_planes, torch.Tensor):
         return depth_planes.detach().to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
-    vals = tuple(float(x) for x in depth_planes)
-    # keyed on the stream too: the copy is allocated on (and its memory, once evicted, reused
-    # in the order of) the stream that made it, so each stream reads only its own copy
-    key = (vals, str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    # keyed on the values (numbers hash and compare by value, so a list of Python or numpy
+    # floats finds the same entry), the device and the stream: the copy is allocated on (and
+    # its memory, once evicted, reused in the order of) the stream that made it, so each stream
+    # reads only its own copy
+    if sid is None:
+        sid = torch.cuda.current_stream(dev).cuda_stream
+    key = (tuple(depth_planes), dev.index, sid)
     d = _DEPTHS_DEV.get(key)
     if d is None:
         if len(_DEPTHS_DEV) >= 64:
             _DEPTHS_DEV.clear()
-        d = torch.tensor(vals, dtype=torch.float32).to(dev)
+        d = torch.tensor([float(x) for x in key[0]], dtype=torch.float32).to(dev)
         _DEPTHS_DEV[key] = d
     return d
 
@@ -779,28 +782,46 @@ def plane_sweep(img: torch.Tensor, depth_planes, ki: torch.Tensor, proj: torch.T
 
 
 _PROJ_SCRATCH: dict = {}
+_STRIDES4: dict = {}
 
 
 def plane_sweep_pose(img: torch.Tensor, depth_planes, ki: torch.Tensor, Ks: torch.Tensor, pose: torch.Tensor,
-                     tgt_h: int, tgt_w: int) -> torch.Tensor:
+                     tgt_h: int, tgt_w: int, stream=None) -> torch.Tensor:
     """plane_sweep with proj = K4_src @ pose formed on the device in the same call
-    (mpiv_plane_sweep_pose): ki [B,9] on the device, Ks [3,3] (one camera) or [B,3,3] with
-    3x3 blocks contiguous, pose [B,4,4] on the device.  The [B,16] proj lands in a scratch
-    buffer kept per device and stream (reused in stream order)."""
+    (mpiv_plane_sweep_pose): img [B,Hs,Ws,C] or, unbatched, [Hs,Ws,C] (plane_sweep_torch_one's
+    call: B = 1, the result still [1,...]); ki [B,9] on the device, Ks [3,3] (one camera) or
+    [B,3,3] with 3x3 blocks contiguous, pose [B,4,4] (or [4,4]) contiguous fp32 on the device.
+    The [B,16] proj lands in a scratch buffer kept per device and stream (reused in stream
+    order).  The notebook's dataset calls this once per sample at 224x224x10, where the kernel
+    is ~12 us, so the host path is kept to a handful of torch calls."""
     _require_depths(depth_planes)
     dev = _dev(img, Ks, pose)
-    B, Hs, Ws, C = img.shape
-    dd = _depths_on(depth_planes, dev)
+    if img.dim() == 3:
+        Hs, Ws, C = img.shape
+        B = 1
+        st = img.stride()
+        st = (Hs * st[0], st[0], st[1], st[2])
+    else:
+        B, Hs, Ws, C = img.shape
+        st = img.stride()
+    cst = _STRIDES4.get(st)
+    if cst is None:
+        if len(_STRIDES4) >= 256:
+            _STRIDES4.clear()
+        cst = _STRIDES4[st] = (ctypes.c_int64 * 4)(*st)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    sid = stream.cuda_stream
+    dd = _depths_on(depth_planes, dev, sid)
     D = dd.shape[0]
-    stream = torch.cuda.current_stream(dev)
-    key = (str(dev), stream.cuda_stream)
+    key = (dev.index, sid)
     scratch = _PROJ_SCRATCH.get(key)
     if scratch is None or scratch.numel() < B * 16:
         scratch = _PROJ_SCRATCH[key] = torch.empty(max(B, 8) * 16, device=dev, dtype=torch.float32)
     ks_b = 0 if Ks.dim() == 2 else Ks.stride(0)
     out = torch.empty((B, tgt_h, tgt_w, D * C), device=dev, dtype=torch.float32)
-    _call("mpiv_plane_sweep_pose", img, _strides(img), B, Hs, Ws, C, ki, Ks, ks_b, pose, scratch, dd, D, tgt_h, tgt_w,
-          out, ctypes.c_void_p(stream.cuda_stream))
+    _call("mpiv_plane_sweep_pose", img, cst, B, Hs, Ws, C, ki, Ks, ks_b, pose, scratch, dd, D, tgt_h, tgt_w,
+          out, _vp(sid))
     return out
 
 

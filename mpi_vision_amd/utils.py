@@ -246,14 +246,19 @@ def plane_sweep_torch(img, depth_planes, pose, intrinsics):
     return _plane_sweep(img, depth_planes, pose, intrinsics, intrinsics, height, width)
 
 
-def _plane_sweep(img, depth_planes, pose, src_intrinsics, tgt_intrinsics, height, width):
+def _plane_sweep(img, depth_planes, pose, src_intrinsics, tgt_intrinsics, height, width, B=None):
+    """B given (the unbatched _one calls): img [Hs,Ws,C] and pose [4,4] stand for a batch of 1."""
     if img.is_cuda and pose.is_cuda:  # pose in HBM: proj is formed there, in the sweep's own call
-        B = pose.shape[0]
+        dev = pose.device
+        if B is None:
+            B = pose.shape[0]
+        stream = torch.cuda.current_stream(dev)
         Ks, pose_d = _host.device_cameras(src_intrinsics, pose, B)
-        return _lib.plane_sweep_pose(img, depth_planes, _host.psv_ki_device(tgt_intrinsics, B, pose.device), Ks,
-                                     pose_d, height, width)
-    else:
-        ki, proj = _host.psv_matrices(_batched(src_intrinsics), _batched(tgt_intrinsics), pose, pin=img.is_cuda)
+        ki = _host.psv_ki_device(tgt_intrinsics, B, dev, stream.cuda_stream)
+        return _lib.plane_sweep_pose(img, depth_planes, ki, Ks, pose_d, height, width, stream)
+    if B is not None:
+        img, pose = img.unsqueeze(0), pose.unsqueeze(0)
+    ki, proj = _host.psv_matrices(_batched(src_intrinsics), _batched(tgt_intrinsics), pose, pin=img.is_cuda)
     return _lib.plane_sweep(img, depth_planes, ki, proj, height, width)
 
 
@@ -281,8 +286,7 @@ def format_network_input_torch(self, ref_image, psv_src_images, ref_pose, psv_sr
 def plane_sweep_torch_one(img, depth_planes, pose, intrinsics):
     """Unbatched PSV of img [H, W, C]; returns [1, H, W, D*C] (utils.py:513-533).  The
     caller's own intrinsics tensor (not a per-call view of it) keys the memoised inverse."""
-    return _plane_sweep(img.unsqueeze(0), depth_planes, pose.unsqueeze(0), intrinsics, intrinsics,
-                        img.shape[0], img.shape[1])
+    return _plane_sweep(img, depth_planes, pose, intrinsics, intrinsics, img.shape[0], img.shape[1], B=1)
 
 
 def projective_inverse_warp_torch2(img, depth, pose, src_intrinsics, tgt_intrinsics,
@@ -300,5 +304,4 @@ def plane_sweep_torch_one2(img, depth_planes, pose, src_intrinsics, tgt_intrinsi
                            tgt_height, tgt_width):
     """PSV of img [H_s, W_s, C] into a (tgt_height, tgt_width) target grid with separate
     intrinsics; returns [1, tgt_height, tgt_width, D*C] (utils.py:771-799)."""
-    return _plane_sweep(img.unsqueeze(0), depth_planes, pose.unsqueeze(0), src_intrinsics, tgt_intrinsics,
-                        tgt_height, tgt_width)
+    return _plane_sweep(img, depth_planes, pose, src_intrinsics, tgt_intrinsics, tgt_height, tgt_width, B=1)
