@@ -498,6 +498,17 @@ def notebook_leg(dev, stream, n=50):
     return res
 
 
+def guarded(fn, *args):
+    """An auxiliary leg: a Python-level failure (an entry point's error, a shape bug) is recorded
+    in the line instead of ending the run before the headline is printed."""
+    try:
+        return fn(*args)
+    except (RuntimeError, ValueError, AssertionError, TypeError) as e:
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        return {"error": f"{type(e).__name__}: {e}"[:400]}
+
+
 def u8_leg(dev, stream, V, homs_sv, homs_v, n=10):
     """The 8-bit texel path (the reference's own test MPI is 8-bit, test/rgba_*.png,
     read as u8/255, utils.py:324-331): a config-4-shape u8 MPI (counter-based synthetic bytes,
@@ -645,7 +656,9 @@ def config5_leg(world, rank, dev, steps, warmup):
         launch = lambda: _lib._call("mpiv_render_packed_ct", packed, H, W, p1 - p0, 0, p1 - p0,  # noqa: E731
                                     int(rank == 0), hl, 1, ct, _lib._stream(dev))
         xstats = {}
-        step = lambda: parallel.render_plane_sharded(packed, hl, H, stats=xstats)  # noqa: E731
+        # the band pipeline by default (MPIV_PLANE_PIPELINE=0: the one-shot all-to-all path)
+        pipe = os.environ.get("MPIV_PLANE_PIPELINE", "1") != "0"
+        step = lambda: parallel.render_plane_sharded(packed, hl, H, stats=xstats, pipelined=pipe)  # noqa: E731
         shard_bytes = (p1 - p0) * H * W * 16 + H * W * 16
         kname, grid = _lib.route("render_packed_ct", H, W, p1 - p0, 1)
     launch()
@@ -770,7 +783,7 @@ def main():
     torch.cuda.empty_cache()
     nb = notebook_leg(dev, stream) if "nb" in legs else None
     torch.cuda.empty_cache()
-    nout = netout_leg(dev, stream) if "netout" in legs else None
+    nout = guarded(netout_leg, dev, stream) if "netout" in legs else None
     torch.cuda.empty_cache()
 
     run(args.warmup, 0)
@@ -844,7 +857,7 @@ def main():
 
     u8 = None
     if "u8" in legs:
-        u8 = u8_leg(dev, stream, V, host_homs(0, 1).to(dev), host_homs(0).to(dev))
+        u8 = guarded(u8_leg, dev, stream, V, host_homs(0, 1).to(dev), host_homs(0).to(dev))
     train = training_leg(dev, stream) if "train" in legs else None
     c5 = config5_leg(world, rank, dev, max(3, args.steps // 2), 1) if "c5" in legs else None
     ranks = {"world_size_seen": world, "backend": backend, "per_rank_kernel_ms": [round(x, 4) for x in kern_all]}
