@@ -705,6 +705,9 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const int64_t ntiles = (int64_t)tiles_x * blocks(H, kGTY);
     const int64_t gather_blocks = ntiles * blocks(P, kGPl);
     if (gather_blocks > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+    if (opt(kOptBwdGather) != 0 && !(MPIV_AB && MPIV_GTR == 1))
+        return fail(MPIV_ERR_ARG, "%s: bwd_gather=%d needs an A/B build with one texel row per wave (-DMPIV_GTR=1)", nm,
+                    opt(kOptBwdGather));
     const int force = opt(kOptBwdFallback) != 0 || !fast;
     const float margin = (float)opt(kOptBwdMargin) / 64.0f;
     hipStream_t q = S(stream);
@@ -756,7 +759,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
 #undef MPIV_CHAIN
         if (!force) {
             bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
-#if MPIV_AB  // one texel row per wave / staging and texel waves: measured slower
+#if MPIV_AB && MPIV_GTR == 1  // one texel row per wave / staging and texel waves: measured slower
             if (opt(kOptBwdGather) == 1) {
                 bwd_gather_wave_kernel<<<(unsigned)gather_blocks, 256, 0, q>>>(g, hv, ws, gv, margin);
             } else
@@ -764,7 +767,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
             {
                 bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x,
                                                                                margin, ws.box);
-#if MPIV_AB
+#if MPIV_AB && MPIV_GTR == 1
                 if (opt(kOptBwdGather) == 2)
                     bwd_gather_ws_kernel<<<(unsigned)gather_blocks, 2 * kGThreads, 0, q>>>(g, hv, ws, gv, margin);
                 else if (opt(kOptBwdGather) == 3)

@@ -62,8 +62,11 @@ constexpr int kGTW = 64;           // gather: texel tile width (a wave = one til
 #define MPIV_GTH 4
 #endif
 constexpr int kGTH = MPIV_GTH;     // gather: waves per block (a texel row each)
+// two texel rows per wave (round 4, profiles/r04_bwd_gather_ab.jsonl): each thread sums two
+// independent texels per pass (64 x 8 tiles, 1.4x staged pixels per texel instead of 1.55x),
+// 112 VGPRs at 4 waves/SIMD: backward 2.68 vs 2.81 ms, bit-identical
 #ifndef MPIV_GTR
-#define MPIV_GTR 1
+#define MPIV_GTR 2
 #endif
 constexpr int kGTR = MPIV_GTR;     // gather: texel rows per wave (rows w, w + kGTH, ...: a tile of kGTY rows)
 constexpr int kGTY = kGTH * kGTR;  // gather: tile rows
@@ -80,7 +83,7 @@ constexpr int kGThreads = kGTW * kGTH;
 #define MPIV_GCAP 736
 #endif
 #ifndef MPIV_GLB
-#define MPIV_GLB 5
+#define MPIV_GLB 4
 #endif
 #ifndef MPIV_GLBS
 #define MPIV_GLBS 3  // bwd_gather_ws_kernel: 512-thread blocks per CU (50 KiB of LDS each)
@@ -798,7 +801,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     }
 }
 
-#if MPIV_AB  // A/B variants of the gather (libmpiv_ab.so): measured slower, DESIGN.md §8
+#if MPIV_AB && MPIV_GTR == 1  // A/B variants of the gather (libmpiv_ab.so, one texel row per wave): measured slower, DESIGN.md §8
 // ---- 2'. gather with the d samples streamed into LDS one pass ahead (bwd_gather=3) ------
 // bwd_gather_kernel loads a pass's d samples in its staging phase and waits for them there;
 // its texel phase issues no memory traffic, so a block's loads are in flight only part of the

@@ -129,7 +129,9 @@ def test_device_psv_matrices_bit_exact(dev):
     for scale in (1.0, 1.5):
         K1.mul_(scale)
         ki, proj = _host.psv_matrices_device(K1, K1, posed, B)
-        Kh = K1.cpu()[None].expand(B, 3, 3)
+        # one camera for the batch: the drop-in inverts it materialised per view, as the host path
+        # does for device intrinsics (its one device-to-host copy materialises them too)
+        Kh = K1.cpu()[None].expand(B, 3, 3).contiguous()
         wki, wproj = _host.psv_matrices(Kh, Kh, pose)
         assert_bits(ki.cpu().numpy(), wki.numpy())
         assert_bits(proj.cpu().numpy(), wproj.numpy())

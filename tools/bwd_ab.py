@@ -1,6 +1,7 @@
 """Render-backward A/B on the GPU (config 4, one view with checkpoints): the production
 gather against the variants selected by bwd_gather=k, bit-identical gradients required.
     python tools/bwd_ab.py [k ...]      (default: 0 3)"""
+import hashlib
 import json
 import os
 import sys
@@ -42,8 +43,10 @@ def main():
             torch.cuda.synchronize()
             ms = sorted(a.elapsed_time(b) for a, b in ev)
             _lib.reset_debug()
+            sha = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]
             print(json.dumps({"rep": rep, "bwd_gather": v, "median_ms": round(ms[len(ms) // 2], 4),
-                              "min_ms": round(ms[0], 4), "bit_identical": same, "fallback_flag": flag}), flush=True)
+                              "min_ms": round(ms[0], 4), "bit_identical_in_process": same, "grad_sha16": sha,
+                              "fallback_flag": flag}), flush=True)
 
 
 if __name__ == "__main__":
