@@ -89,7 +89,8 @@ constexpr int kGThreads = kGTW * kGTH;
 #define MPIV_GLBS 3  // bwd_gather_ws_kernel: 512-thread blocks per CU (50 KiB of LDS each)
 #endif
 #ifndef MPIV_GSI
-#define MPIV_GSI 2  // staged pixels per thread whose d samples are loaded ahead of the positions
+#define MPIV_GSI 3  // staged pixels per thread whose d samples are loaded ahead of the positions (all of
+                    // them: round 4 with two texel rows per wave, 2.51 vs 2.69 ms; r04_bwd_gather_ab.jsonl)
 #endif
 constexpr int kGPl = MPIV_GPL;     // gather: planes per block (a texel's kGPl planes are one 16*kGPl-B run)
 constexpr int kGCap = MPIV_GCAP;   // gather: output pixels staged per pass
@@ -1642,6 +1643,63 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
 
 
 #if MPIV_AB
+// The ticket schedule's two steps, written for wave 0 of a block with WAVE-UNIFORM control flow
+// (all 64 lanes run the wait loop and leave it together).  A first version ran them under
+// `if (threadIdx.x == 0)` at the top of the item loop; the compiler's structurizer then split
+// that lane's path from its wave's other lanes, which went round the barriers on their own
+// (scalar s_barrier instructions run whatever the exec mask) and read a stale ticket: every
+// box run hung, even a single block with trivial items (round 4, tools/ticket_selftest.py).
+// Returns the block's next item (ticket) or -1 (none left, or aborted).
+__device__ __forceinline__ int fallback_ticket(unsigned* ticket, unsigned* done, int* abort_, int* aborted,
+                                               unsigned total, unsigned nvirt, unsigned poll_limit,
+                                               unsigned* timeouts, unsigned* next_fixed = nullptr) {
+    const int lane = threadIdx.x & (kWave - 1);
+    if (abort_ && __builtin_amdgcn_readfirstlane(
+                      (int)__hip_atomic_load(abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
+        return -1;
+    unsigned tk = 0;
+    if (next_fixed) {
+        tk = *next_fixed;
+        *next_fixed += nvirt;
+    } else {
+        if (lane == 0) tk = atomicAdd(ticket, 1u);
+        tk = (unsigned)__builtin_amdgcn_readfirstlane((int)tk);
+    }
+    if (tk >= total) return -1;
+    const unsigned need = tk / nvirt * nvirt;  // every item of the phases before this one done
+    if (poll_limit == 0 && need > 0 && abort_) {  // tests: abort at the first wait
+        if (lane == 0 && atomicExch(abort_, 1) == 0) atomicAdd(aborted, 1);
+        return -1;
+    }
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned d = (unsigned)__builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (d >= need) break;
+        if (abort_ && __builtin_amdgcn_readfirstlane(
+                          (int)__hip_atomic_load(abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
+            return -1;
+        if (spins > poll_limit) {
+            if (lane == 0) {
+                if (abort_ && atomicExch(abort_, 1) == 0) atomicAdd(aborted, 1);
+                if (timeouts) atomicAdd(timeouts, 1u);
+            }
+            return -1;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __threadfence();  // acquire: the earlier phases' stores are visible
+    return (int)tk;
+}
+
+// after an item: every thread's stores, then one completion
+__device__ __forceinline__ void fallback_done(unsigned* done) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();  // release: this item's stores before its completion
+        atomicAdd(done, 1u);
+    }
+}
+
 // One item of the fallback pipeline: virtual block bid (of nblk) of phase ph (0: zero the
 // bucket sizes; 1 + kFbPhases * c + k: step k for plane chunk c)
 template <bool FAST>
@@ -1860,63 +1918,26 @@ __global__ __launch_bounds__(256) void bwd_fallback_ticket_kernel(RenderGeom g, 
     __shared__ int s_ticket;
     if (ws.flag[0] == 0) return;  // uniform over the grid: the tile gather was complete
     const int nblk = gridDim.x, tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: wave-uniform branches only
     const int nchunk = (g.P + ws.pc - 1) / ws.pc;
     const unsigned total = (unsigned)(1 + kFbPhases * nchunk) * (unsigned)nblk;
     unsigned* ticket = reinterpret_cast<unsigned*>(ws.flag + 1);
     unsigned* done = reinterpret_cast<unsigned*>(ws.flag + 2);
-    int* abort_ = ws.flag + 3;
     unsigned next_fixed = blockIdx.x;
     for (;;) {
-        if (tid == 0) {
-            int t = -1;
-            if (__hip_atomic_load(abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-                unsigned tk;
-                if (fixed) {
-                    tk = next_fixed;
-                    next_fixed += (unsigned)nblk;
-                } else {
-                    tk = atomicAdd(ticket, 1u);
-                }
-                if (tk < total) {
-                    // every item of the phases before this one done (see above)
-                    const unsigned need = tk / (unsigned)nblk * (unsigned)nblk;
-                    unsigned spins = 0;
-                    t = (int)tk;
-                    if (poll_limit == 0 && need > 0) {  // tests: abort at the first wait
-                        if (atomicExch(abort_, 1) == 0) atomicAdd(ws.flag + 4, 1);
-                        t = -1;
-                    }
-                    while (t >= 0 && __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-                        if (__hip_atomic_load(abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-                            t = -1;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(2);
-                        if (++spins > poll_limit) {
-                            if (atomicExch(abort_, 1) == 0) atomicAdd(ws.flag + 4, 1);
-                            t = -1;
-                            break;
-                        }
-                    }
-                    __threadfence();  // acquire: the earlier phases' stores are visible
-                }
-            }
-            s_ticket = t;
+        if (wave == 0) {
+            const int t = fallback_ticket(ticket, done, ws.flag + 3, ws.flag + 4, total, (unsigned)nblk, poll_limit,
+                                          nullptr, fixed ? &next_fixed : nullptr);
+            if (tid == 0) s_ticket = t;
         }
         __syncthreads();
-        // block-uniform: scalar control flow through the item (its barriers are never divergent)
         const int t = __builtin_amdgcn_readfirstlane(s_ticket);
         __syncthreads();  // s_ticket is rewritten by the next iteration
         if (t < 0) return;
         bwd_fallback_item<FAST>(g, homs, ws, dmpi, t / nblk, t % nblk, nblk, s_tmp);
-        __syncthreads();
-        if (tid == 0) {
-            __threadfence();  // release: this item's stores before its completion
-            atomicAdd(done, 1u);
-        }
+        fallback_done(done);
     }
 }
-
 #endif  // MPIV_AB
 
 #if MPIV_AB
@@ -1926,27 +1947,14 @@ __global__ __launch_bounds__(256) void bwd_fallback_ticket_kernel(RenderGeom g, 
 // ctr: [0] tickets, [1] completions, [2] violations, [3] aborted waits (zeroed by the caller).
 __global__ __launch_bounds__(256) void ticket_selftest_kernel(unsigned* __restrict__ ctr, int* __restrict__ marks,
                                                               int nphase, int nvirt, unsigned poll_limit) {
-    __shared__ int s_ticket;
     const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: wave-uniform branches only
     const unsigned total = (unsigned)nphase * (unsigned)nvirt;
+    __shared__ int s_ticket;
     for (;;) {
-        if (tid == 0) {
-            int t = -1;
-            const unsigned tk = atomicAdd(ctr, 1u);
-            if (tk < total) {
-                const unsigned need = tk / (unsigned)nvirt * (unsigned)nvirt;
-                unsigned spins = 0;
-                t = (int)tk;
-                while (__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > poll_limit) {
-                        atomicAdd(ctr + 3, 1u);
-                        break;
-                    }
-                }
-                __threadfence();
-            }
-            s_ticket = t;
+        if (wave == 0) {
+            const int t = fallback_ticket(ctr, ctr + 1, nullptr, nullptr, total, (unsigned)nvirt, poll_limit, ctr + 3);
+            if (tid == 0) s_ticket = t;
         }
         __syncthreads();
         const int t = __builtin_amdgcn_readfirstlane(s_ticket);
@@ -1957,12 +1965,8 @@ __global__ __launch_bounds__(256) void ticket_selftest_kernel(unsigned* __restri
         if (q > 0)
             for (int i = tid; i < nvirt; i += 256) bad += marks[(q - 1) * nvirt + i] != 1;
         if (bad) atomicAdd(ctr + 2, bad);
-        __syncthreads();
-        if (tid == 0) {
-            marks[q * nvirt + b] = 1;
-            __threadfence();
-            atomicAdd(ctr + 1, 1u);
-        }
+        if (tid == 0) marks[q * nvirt + b] = 1;
+        fallback_done(ctr + 1);
     }
 }
 #endif
