@@ -50,7 +50,8 @@ const char *mpiv_build_id(void);
  * by name ("render_mv", "render_pair", "render_native_lds", "render_chunk", "render_ring",
  * "render_tile", "render_vshare", "chunk_rows", "chunk_flight", "sweep_tile", "sweep_store",
  * "sweep_dlane", "sweep_rows", "sweep_direct", "box_shrink", "bwd_fallback", "bwd_margin",
- * "bwd_gather"; "reset" restores every default; abi.hip documents the values).  Values that
+ * "bwd_gather", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode"; "reset" restores every default;
+ * abi.hip documents the values).  Values that
  * select a kernel kept only for A/B measurement return MPIV_ERR_ARG from libmpiv.so (they are
  * compiled into libmpiv_ab.so).  Process-wide; returns MPIV_ERR_ARG for an unknown name. */
 int mpiv_debug_set(const char *name, int value);
@@ -182,9 +183,9 @@ size_t mpiv_render_backward_workspace_size(int H, int W, int P);
  * workspace: >= mpiv_render_backward_workspace_size(H, W, P) bytes, 256-B aligned.
  * Deterministic (no float atomics); H*W < 2^26, P*H*W < 2^31.
  * A view the tile gather cannot prove complete runs the bucket fallback, whose phases are
- * ordered by tickets (no co-residency assumption: safe beside other streams and processes).
- * If a fallback wait ever outlasts its poll limit (not expected), that view's gradient is
- * NaN-filled and counted; mpiv_render_backward_status reports the count. */
+ * ordered by tickets (no block needs to be resident: safe beside other streams, RCCL kernels
+ * and other processes).  If a fallback wait ever outlasts its poll limit (not expected), that
+ * view's gradient is NaN-filled and counted; mpiv_render_backward_status reports the count. */
 int mpiv_render_backward(const float *mpi, const int64_t mpi_strides[5], int V, int H, int W, int P,
                          const float *homs, const float *dout, const float *ckpt, float *dmpi,
                          void *workspace, size_t workspace_bytes, void *stream);

@@ -91,8 +91,9 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //   bwd_poll_limit=k   (A/B build) the backward fallback's waits give up after k polls instead of
 //                      2^24; -1: at the first wait -- tests provoke the abort path with it (NaN
 //                      gradient, counted by mpiv_render_backward_status)
-//   bwd_fb_ticket=1|2  (A/B build) the fallback's phases ordered by tickets (bwd_fallback_ticket_kernel);
-//                      2: the same kernel with a fixed item order (block b: b, b + nblk, ...; diagnosis)
+//   bwd_fb_mode=1|2    (A/B build) the fallback's phases at grid barriers (round 3's schedule,
+//                      bwd_fallback_barrier_kernel) / the ticket kernel with a fixed item order (block b:
+//                      b, b + nblk, ...; diagnosis)
 //   bwd_fb_blocks=k    (A/B build) the backward fallback launches k blocks instead of the resident count
 //   bwd_margin=k       the tile gather's pixel-window margin in 1/64 pixel (default 16);
 //                      negative values make windows miss contributors, which the pair
@@ -102,12 +103,12 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
-                kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbTicket, kNumOpts };
+                kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
-                                         "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_ticket"};
+                                         "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode"};
 const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
@@ -129,7 +130,7 @@ bool ab_only(int o, int v) {
         case kOptChunkFlight: return v == 4;
         case kOptSweepRows: return v == 6 || v == 8;
         case kOptBwdGather: return v == 1 || v == 2 || v == 3;
-        case kOptBwdPollLimit: case kOptBwdFbBlocks: case kOptBwdFbTicket: return v != 0;
+        case kOptBwdPollLimit: case kOptBwdFbBlocks: case kOptBwdFbMode: return v != 0;
         default: return false;
     }
 }
@@ -712,7 +713,8 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const float margin = (float)opt(kOptBwdMargin) / 64.0f;
     hipStream_t q = S(stream);
     // fallback grid: at most the blocks that fit at once, <= 4 per CU (more would only wait for
-    // tickets); queried once per device (relaxed atomics: racing first calls store the same value)
+    // tickets; fewer resident ones still complete); queried once per device (relaxed atomics:
+    // racing first calls store the same value)
     static int s_fb_blocks[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(MPIV_ERR_HIP, "%s: hipGetDevice failed", nm);
@@ -732,7 +734,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const unsigned fb_blocks = opt(kOptBwdFbBlocks) > 0 ? (unsigned)opt(kOptBwdFbBlocks) : (unsigned)fbb;
     const int pl = opt(kOptBwdPollLimit);
     const unsigned poll_limit = pl > 0 ? (unsigned)pl : pl < 0 ? 0u : (1u << 24);
-    [[maybe_unused]] const int fb_ticket = opt(kOptBwdFbTicket);
+    const int fb_mode = opt(kOptBwdFbMode);
     if (hipMemsetAsync(ws.truth, 0, 2 * kCtrSlots * 8 + 256, q) != hipSuccess)  // truth, found (adjacent)
         return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
     for (int v = 0; v < V; ++v) {
@@ -780,17 +782,17 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force);
         // fallback: one launch, returns at once unless flagged; its phases are ordered by tickets
         // (render_bwd.hip), so it completes however many of its blocks are resident
-#if MPIV_AB  // phases ordered by tickets (render_bwd.hip; under investigation)
-        if (fb_ticket && fast)
-            bwd_fallback_ticket_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, fb_ticket == 2);
-        else if (fb_ticket)
-            bwd_fallback_ticket_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, fb_ticket == 2);
+#if MPIV_AB  // round 3's grid-barrier schedule (render_bwd.hip)
+        if (fb_mode == 1 && fast)
+            bwd_fallback_barrier_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit);
+        else if (fb_mode == 1)
+            bwd_fallback_barrier_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit);
         else
 #endif
         if (fast)
-            bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit);
+            bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, fb_mode == 2);
         else
-            bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit);
+            bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, fb_mode == 2);
         // an aborted fallback (never expected) leaves a NaN gradient, never a plausible one
         bwd_poison_kernel<<<256, 256, 0, q>>>(ws.flag, gv, (int64_t)P * HW);
     }

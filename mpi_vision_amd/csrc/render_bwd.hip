@@ -1357,25 +1357,28 @@ __global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force) {
 // tile sums of the sizes, their scan (one block), the exclusive scan applied, pixel ids into
 // their buckets, small buckets sorted by pixel id (large ones listed), large buckets sorted by
 // a whole block each, then per texel the four buckets merged in the reference's order; one
-// phase up front zeroes the sizes.  Each phase is a grid-stride loop over the nblk blocks,
-// separated by grid barriers (grid_barrier: the launch is sized so every block is resident;
-// a wait that outlasts its poll limit aborts the view LOUDLY -- NaN gradient, counted in
-// flag[4] for mpiv_render_backward_status -- instead of returning a plausible wrong one).
+// phase up front zeroes the sizes.  Each phase is a grid-stride loop over nblk virtual blocks.
 // (A normal launch, not hipLaunchCooperativeKernel: rocprofv3's kernel tracer crashes in its
 // teardown after a cooperative launch, and this one is issued on every backward.)
 //
-// A/B (bwd_fb_ticket=1, libmpiv_ab.so): the same phases ordered by TICKETS instead of barriers
-// (bwd_fallback_ticket_kernel), which needs no block to be resident.  A block takes the next
-// ticket t (flag[1], one device-scope atomic): virtual block t % nblk of phase ph = t / nblk.
-// It waits until the completion counter (flag[2]) reaches ph * nblk, runs the item and adds
-// one to the counter.  The counter counts items of every phase, yet reaching ph * nblk means
-// exactly "every item of phases < ph is done": an item of phase q only runs after seeing the
-// counter at >= q * nblk, so the completions counted before it first reaches ph * nblk all come
-// from phases < ph, which hold ph * nblk items.  Tickets are taken in increasing order, so
-// every item a waiting block depends on was taken earlier by a block that is running, and the
-// holder of the lowest unfinished ticket never waits.  Round 4: this kernel hung on the box in
-// its first runs (even with 4 blocks); it stays an A/B variant until that is understood
-// (DESIGN.md §8), and the production launch keeps the barrier schedule with the loud abort.
+// The phases are ordered by TICKETS, not by grid barriers (round 3's schedule assumed every
+// block resident, "the stream runs nothing beside it" -- RCCL kernels or another process on
+// the device break that).  A block takes the next ticket t (flag[1], one
+// device-scope atomic): virtual block t % nblk of phase ph = t / nblk.  It waits until the
+// completion counter (flag[2]) reaches ph * nblk, runs the item and adds one to the counter.
+// The counter counts items of every phase, yet reaching ph * nblk means exactly "every item of
+// phases < ph is done": an item of phase q only runs after seeing the counter at >= q * nblk,
+// so the completions counted before it first reaches ph * nblk all come from phases < ph,
+// which hold ph * nblk items.  Tickets are taken in increasing order, so every item a waiting
+// block depends on was taken earlier by a block that is running (a block that is not resident
+// holds no ticket), and the holder of the lowest unfinished ticket never waits: the pipeline
+// completes whatever else the device runs and however few of its blocks are resident
+// (`test_backward_fallback_more_blocks_than_resident`: 20000 blocks).  A wait longer than its
+// poll limit (never expected: the argument above) sets flag[3], counts the view in flag[4]
+// and every block stops; bwd_poison_kernel then fills the view's gradient with NaN and
+// mpiv_render_backward_status reports it -- never a plausible wrong gradient.
+// A/B: bwd_fb_mode=1 runs round 3's barrier schedule (bwd_fallback_barrier_kernel, with the
+// same loud abort), 2 the ticket kernel with a fixed item order.
 constexpr int kFbPhases = 8;  // per plane chunk
 
 __device__ __forceinline__ int block_exclusive_scan(int v, int* s_tmp, int& total) {
@@ -1437,8 +1440,9 @@ __device__ __forceinline__ unsigned order_key(int pix, int corner) {
     return ((unsigned)(pix / kGridVec) << 5) | ((unsigned)corner << 3) | (unsigned)(pix % kGridVec);
 }
 
+#if MPIV_AB  // the round-3 schedule: phases at grid barriers over resident blocks (bwd_fb_mode=1)
 template <bool FAST>
-__global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
+__global__ __launch_bounds__(256) void bwd_fallback_barrier_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
                                                            float4* __restrict__ dmpi, unsigned poll_limit) {
     __shared__ int s_tmp[kScanBlock];
     __shared__ int s_abort;
@@ -1640,9 +1644,8 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
         if (sync()) return;  // the chunk's arrays are reused by the next one
     }
 }
+#endif
 
-
-#if MPIV_AB
 // The ticket schedule's two steps, written for wave 0 of a block with WAVE-UNIFORM control flow
 // (all 64 lanes run the wait loop and leave it together).  A first version ran them under
 // `if (threadIdx.x == 0)` at the top of the item loop; the compiler's structurizer then split
@@ -1911,7 +1914,7 @@ __device__ void bwd_fallback_item(const RenderGeom& g, const float* __restrict__
 template <bool FAST>
 // fixed != 0 (A/B diagnosis): block b takes items b, b + nblk, ... in order instead of tickets
 // (the grid-barrier schedule: needs every block resident)
-__global__ __launch_bounds__(256) void bwd_fallback_ticket_kernel(RenderGeom g, const float* __restrict__ homs,
+__global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const float* __restrict__ homs,
                                                                   BwdWs ws, float4* __restrict__ dmpi,
                                                                   unsigned poll_limit, int fixed) {
     __shared__ int s_tmp[kScanBlock];
@@ -1938,7 +1941,9 @@ __global__ __launch_bounds__(256) void bwd_fallback_ticket_kernel(RenderGeom g, 
         fallback_done(done);
     }
 }
-#endif  // MPIV_AB
+
+
+
 
 #if MPIV_AB
 // Ticket-protocol self-test (diagnosis of bwd_fallback_ticket_kernel): the same ticket / wait /

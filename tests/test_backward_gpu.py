@@ -30,9 +30,11 @@ def grad():
 # "tile": the production path (tile gather, pair count checked); "fallback": the bucket
 # pipeline for every view (bwd_fallback=1); "miss": windows 1.5 px too small
 # (bwd_margin=-96), so the tile gather misses contributors and the count must send every
-# such view to the fallback -- all bit-exact.  (The measured-and-rejected gather variants,
+# such view to the fallback; "barrier": the fallback on round 3's grid-barrier schedule
+# (bwd_fb_mode=1, A/B) -- all bit-exact.  (The measured-and-rejected gather variants,
 # bwd_gather=1|2|3, need an A/B build with one texel row per wave, -DMPIV_GTR=1.)
-BWD_MODES = {"tile": {}, "fallback": {"bwd_fallback": 1}, "miss": {"bwd_margin": -96}}
+BWD_MODES = {"tile": {}, "fallback": {"bwd_fallback": 1}, "miss": {"bwd_margin": -96},
+             "barrier": {"bwd_fallback": 1, "bwd_fb_mode": 1}}
 
 
 @pytest.fixture(params=list(BWD_MODES))
@@ -49,7 +51,7 @@ def _backward_flag(mpi, homs, dout, dev):
     got = _lib.render_backward(mpi, homs, dout, workspace=ws)
     off = _lib.bwd_flag_offset(H, W, P)
     words = ws[off:off + 20].view(torch.int32).tolist()
-    # words[1]: the fallback's barrier counter; [3], [4]: this view's /
+    # words[1], [2]: the fallback's ticket and completion counters; [3], [4]: this view's /
     # this call's aborted fallbacks (a wait that outlasted its poll limit)
     assert words[3] == 0 and words[4] == 0, "the fallback aborted"
     assert _lib.render_backward_status(ws, H, W, P) == 0
@@ -286,6 +288,39 @@ def _medium_case(V=2):
                                      K, V)
     dout = torch.rand((V, H, W, 3), generator=torch.Generator().manual_seed(23)) * 2 - 1
     return mpi, homs, dout
+
+
+def test_backward_fallback_more_blocks_than_resident(dev, kopts):
+    """The fallback's phases are ordered by tickets, not by barriers over resident blocks
+    (ADVICE r3): launched with 20000 blocks -- far more than the device holds at once, which a
+    grid barrier could never release -- it completes, bit-exact to the oracle, nothing aborted.
+    With one block (every item in turn) and a fixed item order (the barrier schedule expressed
+    with the same counters) as well."""
+    mpi, homs, dout = _medium_case()
+    want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
+    for opts in ({"bwd_fb_blocks": 20000}, {"bwd_fb_blocks": 1}, {"bwd_fb_mode": 2, "bwd_fb_blocks": 8}):
+        kopts(bwd_fallback=1, bwd_fb_mode=0, bwd_fb_blocks=0, **opts)
+        got, flag = _backward_flag(mpi.to(dev), homs, dout.to(dev), dev)
+        assert flag == 1
+        assert_bits(got, want, f"fallback {opts}")
+
+
+@pytest.mark.parametrize("blocks,nphase,nvirt", [(1, 9, 4), (4, 9, 4), (1024, 9, 1024), (20000, 9, 1024)])
+def test_ticket_protocol_selftest(blocks, nphase, nvirt, dev):
+    """The fallback's ticket schedule with trivial items (mpiv_selftest_tickets, libmpiv_ab.so):
+    every item runs once, only after all items of the phase before it (no violation), nothing
+    waits out its poll limit -- from one block to far more blocks than fit at once."""
+    import ctypes
+    L = _lib.load_ab()
+    ctr = torch.zeros(4, dtype=torch.int32, device=dev)
+    marks = torch.zeros(nphase * nvirt, dtype=torch.int32, device=dev)
+    rc = L.mpiv_selftest_tickets(blocks, nphase, nvirt, 1 << 22, ctypes.c_void_p(ctr.data_ptr()),
+                                 ctypes.c_void_p(marks.data_ptr()),
+                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0, L.mpiv_last_error()
+    c = ctr.tolist()
+    assert c[1] == nphase * nvirt and c[2] == 0 and c[3] == 0, c
+    assert int(marks.sum().item()) == nphase * nvirt
 
 
 def test_backward_fallback_abort_is_loud(dev, kopts):
