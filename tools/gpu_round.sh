@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests_$TAG.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -3 $OUT/gpu_tests_$TAG.log; [ $rc -eq 0 ] || exit $rc
