@@ -55,6 +55,9 @@ __device__ __forceinline__ void bwd_store(float4* p, const float4& v) {
         *p = v;
 }
 
+#ifndef MPIV_GPF2
+#define MPIV_GPF2 0  // A/B: the gather loads each pass's d samples during the previous texel phase
+#endif
 constexpr int kGridVec = 8;        // grid_sampler_2d_backward chunk width (oracle.GRID_VEC)
 constexpr int kBwdCH = 8;          // chain: planes per chunk
 constexpr int kGTW = 64;           // gather: texel tile width (a wave = one tile row)
@@ -508,11 +511,13 @@ constexpr int kGWP = kGCap + 1;
 // latency was exposed -- 0.32 of the kernel's 1.77 ms, r03).  s_ent must be all ~0 on entry.
 // DS = false (bwd_gather_dma_kernel): the d samples arrive in LDS by DMA instead, and only the
 // fractions (wx, wy) are staged (s_w[q], s_w[kGWP + q]); the texel pass forms the corner weight.
-template <bool DS = true>
+// PRE (MPIV_GPF2 gather): the d samples were loaded by the caller (pre[i]: staged pixel
+// t + i * kGThreads, a pass ahead) instead of here.
+template <bool DS = true, bool PRE = false>
 __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const BwdWs& ws, const float* __restrict__ hp,
                                                   int p, bool proven, int t, int tx0, int ty0, int bx0, int bw,
                                                   int ra, int rb, int* s_code, float* s_w, float4* s_ds,
-                                                  unsigned* s_ent, int* ovf) {
+                                                  unsigned* s_ent, int* ovf, const f32x4* pre = nullptr) {
     constexpr int TB = kGTB;
     const int64_t HW = (int64_t)g.H * g.W;
     const int np = (rb - ra) * bw;
@@ -522,7 +527,10 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
     const float rbw = 1.0f / (float)bw;
     const __amdgpu_buffer_rsrc_t rds = make_rsrc(ws.ds + (int64_t)p * HW, (int)(HW * 16));
     f32x4 dsv[kGSI];
-    if (DS) {
+    if (DS && PRE) {
+#pragma unroll
+        for (int i = 0; i < kGSI; ++i) dsv[i] = pre[i];
+    } else if (DS) {
 #pragma unroll
         for (int i = 0; i < (kGSI < MPIV_GSI ? kGSI : MPIV_GSI); ++i) {
             const int q = t + i * kGThreads;
@@ -558,7 +566,7 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
                 s_w[kGWP + q] = sy * wx;
                 s_w[2 * kGWP + q] = wy * ex;
                 s_w[3 * kGWP + q] = wy * wx;
-                if (i >= MPIV_GSI)  // past the preloaded pixels (boxes over MPIV_GSI * kGThreads pixels)
+                if (!PRE && i >= MPIV_GSI)  // past the preloaded pixels (boxes over MPIV_GSI * kGThreads pixels)
                     dsv[i] = llvm_raw_buffer_load_v4f32(rds, (yy * g.W + xx) * 16, 0, 0);
                 s_ds[q] = make_float4(dsv[i][0], dsv[i][1], dsv[i][2], dsv[i][3]);
             } else {
@@ -753,6 +761,87 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     unsigned hits = 0;    // (texel, contributor) pairs found by this thread
     bool unsafe = false;  // a plane this block could not order (the view goes to the fallback)
     f32x4 acc[kGTR][kGPl];
+#if MPIV_GPF2
+    // A/B: each pass's d samples are loaded into registers during the previous pass's texel phase
+    // (kGSI per thread, 12 VGPRs: the kernel stays at 4 waves/SIMD), so staging never waits on HBM
+#pragma unroll
+    for (int jj = 0; jj < kGPl; ++jj)
+#pragma unroll
+        for (int r = 0; r < kGTR; ++r) acc[r][jj] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    int4 bxs[kGPl];
+#pragma unroll
+    for (int jj = 0; jj < kGPl; ++jj) {
+        bxs[jj] = p0 + jj < g.P ? ws.box[(int64_t)(p0 + jj) * ntiles + tile] : make_int4(0, -1, 0, -1);
+        if (bxs[jj].x == -2) {  // this block cannot gather the plane: the check sends the view to the fallback
+            unsafe = true;
+            bxs[jj] = make_int4(0, -1, 0, -1);
+        }
+    }
+    auto box = [&](int jj) {  // static selects + readfirstlane: block-uniform scalars
+        int4 b = make_int4(0, -1, 0, -1);
+#pragma unroll
+        for (int k = 0; k < kGPl; ++k)
+            if (k == jj) b = bxs[k];
+        return make_int4(__builtin_amdgcn_readfirstlane(b.x), __builtin_amdgcn_readfirstlane(b.y),
+                         __builtin_amdgcn_readfirstlane(b.z), __builtin_amdgcn_readfirstlane(b.w));
+    };
+    auto first_from = [&](int jj, int& ra) {
+        for (; jj < kGPl; ++jj) {
+            const int4 b = box(jj);
+            if (b.y >= b.x && (b.w & ~kBoxProven) >= b.z) break;
+        }
+        ra = jj < kGPl ? box(jj).z : 0;
+        return jj;
+    };
+    const int64_t HWg = (int64_t)g.H * g.W;
+    f32x4 pre[kGSI];
+    auto load = [&](int jj, int ra) {
+        if (jj >= kGPl) return;
+        const int4 b = box(jj);
+        const int bw = b.y - b.x + 1;
+        const int rb = min((b.w & ~kBoxProven) + 1, ra + kGCap / bw);
+        const int np = (rb - ra) * bw;
+        const __amdgpu_buffer_rsrc_t rds = make_rsrc(ws.ds + (int64_t)(p0 + jj) * HWg, (int)(HWg * 16));
+        const float rbw = 1.0f / (float)bw;
+#pragma unroll
+        for (int i = 0; i < kGSI; ++i) {
+            const int q = (int)threadIdx.x + i * kGThreads;
+            const int r = (int)(((float)q + 0.5f) * rbw);
+            const int off = q < np ? ((ra + r) * g.W + b.x + (q - r * bw)) * 16 : kOOB;
+            pre[i] = llvm_raw_buffer_load_v4f32(rds, off, 0, 0);
+        }
+    };
+    int ra = 0;
+    int jj = first_from(0, ra);
+    load(jj, ra);
+    while (jj < kGPl) {
+        const int4 b = box(jj);
+        const int bx0 = b.x, bx1 = b.y, by0 = b.z, by1 = b.w & ~kBoxProven;
+        const int bw = bx1 - bx0 + 1;
+        const int rb = min(by1 + 1, ra + kGCap / bw);
+        int ra_n = rb, jj_n = jj;
+        if (ra_n > by1) jj_n = first_from(jj + 1, ra_n);
+        const int p = p0 + jj;
+        __syncthreads();  // the previous pass's readers are done
+        gather_stage_pass<true, true>(g, ws, homs + (int64_t)p * 9, p, (b.w & kBoxProven) != 0, (int)threadIdx.x, tx0,
+                                      ty0, bx0, bw, ra, rb, s_code, s_w, s_ds, s_ent[par], &s_ovf[par], pre);
+        for (int bb = threadIdx.x; bb < 2 * kGNB; bb += kGThreads) s_ent[par ^ 1][bb] = ~0u;  // for the next pass
+        if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
+        __syncthreads();
+        load(jj_n, ra_n);  // the next pass's d samples, in flight during this texel phase
+        const bool ovf = s_ovf[par] != 0;
+#pragma unroll
+        for (int k = 0; k < kGPl; ++k)
+            if (k == jj)
+#pragma unroll
+                for (int r = 0; r < kGTR; ++r)
+                    gather_texel_pass(g, ws, p, margin, tx, ty[r], bt[r], tin[r], ovf, s_ent[par], s_code, s_w, s_ds,
+                                      bx0, bx1, by0, by1, ra, rb, acc[r][k], hits, unsafe);
+        par ^= 1;
+        jj = jj_n;
+        ra = ra_n;
+    }
+#else
 #pragma unroll
     for (int jj = 0; jj < kGPl; ++jj) {
 #pragma unroll
@@ -786,6 +875,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
             par ^= 1;
         }
     }
+#endif
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) hits += __shfl_xor(hits, off);
     const unsigned long long tot = (unsigned long long)hits + (__any(unsafe) ? kUnsafe : 0ull);
