@@ -299,7 +299,7 @@ def test_backward_fallback_more_blocks_than_resident(dev, kopts):
     mpi, homs, dout = _medium_case()
     want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
     for opts in ({"bwd_fb_blocks": 20000}, {"bwd_fb_blocks": 1}, {"bwd_fb_mode": 2, "bwd_fb_blocks": 8}):
-        kopts(bwd_fallback=1, bwd_fb_mode=0, bwd_fb_blocks=0, **opts)
+        kopts(**{"bwd_fallback": 1, "bwd_fb_mode": 0, "bwd_fb_blocks": 0, **opts})
         got, flag = _backward_flag(mpi.to(dev), homs, dout.to(dev), dev)
         assert flag == 1
         assert_bits(got, want, f"fallback {opts}")
