@@ -80,6 +80,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (0 = automatic)
 //   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
 //                      wave (0 = automatic)
+//   chunk_strip=0|1    the in-place render at CH = 8, one row: render_chunk_kernel's 64 x 1 wave rows
+//                      (0) or render_chunk_strip_kernel's 8 x 8 strips with vertical tap reuse (1)
 //   sweep_direct=-1|0|1  mpiv_plane_sweep[_into] without LDS staging (plane_sweep_direct_kernel):
 //                      never / automatic (D <= 2) / for any D <= 64; 2|3: pixel per lane, the wave's
 //                      samples staged in LDS (plane_sweep_px_kernel, D * C <= 48; 64 / 32 pixels
@@ -103,14 +105,18 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
-                kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kNumOpts };
+                kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
-                                         "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode"};
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+                                         "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode",
+                                         "chunk_strip"};
+#ifndef MPIV_CHUNK_STRIP
+#define MPIV_CHUNK_STRIP 1  // round 4: 0.525 vs 0.64 ms in place, backward 2.33 vs 2.48 (profiles/r04j_strip_ab.jsonl)
+#endif
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -182,6 +188,13 @@ int launch_chunk(int R, const float* mpi, int64_t vstride, const RenderGeom& g, 
     const int64_t nb = (int64_t)blocks(g.W, kTileX) * blocks(g.H, kTileY * R) * B;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const int NT = (opt(kOptChunkFlight) == 4 && R == 1 && SPLIT == 1) ? 4 : 2;
+    if (CH == 8 && SPLIT == 1 && R == 1 && NT == 2 && opt(kOptChunkStrip)) {  // 8 x 8 strips, vertical tap reuse
+        const int64_t ns = (int64_t)blocks(g.W, kStripTX) * blocks(g.H, kStripTY) * B;
+        if (ns > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+        if (g_route) return note_route(ns, 256, "render_chunk_strip_kernel");
+        render_chunk_strip_kernel<<<(unsigned)ns, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
+        return launched(nm);
+    }
     if (g_route) return note_route(nb, 256, "render_chunk_kernel<%d, %d, %d, %d>", CH, SPLIT, R, NT);
 #if MPIV_AB  // R rows per wave / 4 sub-steps in flight: measured slower
     if (NT == 4)
@@ -756,6 +769,9 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         else if (!ck && R == 4) MPIV_CHAIN(false, 4);
         else if (!ck && R == 2) MPIV_CHAIN(false, 2);
 #endif
+        else if (ck && opt(kOptChunkStrip))  // 8 x 8 strips, vertical tap reuse
+            bwd_chain_strip_kernel<<<blocks(W, kStripTX) * blocks(H, kStripTY), 256, chain_lds, q>>>(mv, g, cg, hv, dv,
+                                                                                                  ck, ws, h_lds);
         else if (ck) MPIV_CHAIN(true, 1);
         else MPIV_CHAIN(false, 1);
 #undef MPIV_CHAIN

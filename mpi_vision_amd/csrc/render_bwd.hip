@@ -359,6 +359,166 @@ __global__ __launch_bounds__(256, R == 1 ? 1 : 4) void bwd_chain_kernel(const fl
         bwd_chain_wave<1, CK, R>(view, g, cg, hs, slot, tx0, y, nrows, lane, dout, ck, ws);
 }
 
+// The chain fed the forward's checkpoints, as 8 x 8 strips with vertical tap reuse
+// (render_chunk.hip render_chunk_wave_strip, round 4): row k of the strip is sub-step k of a
+// chunk, so a lane's north taps are usually the south taps it gathered one row above; the
+// composite phases run with lane = pixel (column lane % 8, row lane / 8).  Same samples,
+// same adjoint arithmetic, same pair count (every in-image tap of every sample, gathered or
+// shared): the d samples are bit-identical to bwd_chain_wave<MODE, true, 1>'s.
+template <int MODE>
+__device__ __forceinline__ void bwd_chain_wave_strip(const float* __restrict__ view, const RenderGeom& g,
+                                                     const ChunkGeom& cg, const float* __restrict__ hs,
+                                                     f32x4* __restrict__ slot, int sx0, int sy0, int lane,
+                                                     const float* __restrict__ dout, const float4* __restrict__ ck,
+                                                     const BwdWs& ws) {
+    constexpr int CH = kBwdCH;
+    const int j = lane % CH, i = lane / CH;
+    const int n = (g.P + CH - 1) / CH;
+    const int64_t HW = (int64_t)g.H * g.W;
+    const int x = sx0 + (lane & 7), y = sy0 + (lane >> 3);  // this lane's pixel in the composite phases
+    const bool in = x < g.W && y < g.H;
+    const int64_t pix = (int64_t)y * g.W + x;
+    const bool col_in = sx0 + i < g.W;
+    const float fx = (float)min(sx0 + i, g.W - 1);  // columns past the frame recompute the last (uncounted)
+    const int kstride = g.W + 8;
+    float h[9];
+    auto load_h = [&](int c, float* d) {
+        const int p = min(c * CH + j, g.P - 1);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) d[k] = hs[p * 9 + k];
+    };
+    int ntap = 0;
+    // row k of chunk c: pixel (sx0 + i, sy0 + k), plane c*CH + j (taps counted once)
+    auto issue = [&](int c, int k, const float* hh, int prev_key, bool can_share, StripTaps& t, bool cnt) {
+        const int ys = sy0 + k;
+        float px, py;
+        bwd_pos<MODE>(hh, fx, (float)min(ys, g.H - 1), g, px, py);
+        const int nt = issue_taps_strip(make_rsrc(view + (int64_t)c * CH * 4, cg.rec_bytes), g, cg, j, c * CH + j < g.P,
+                                        px, py, kstride, prev_key, can_share, t);
+        if (cnt && col_in && ys < g.H) ntap += nt;
+    };
+    StripTaps A, B;
+    f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sd = sc;
+    // chunk c into the slot; A holds its row 0 on entry and, on exit, row 0 of chunk cn
+    auto sample_chunk = [&](int c, int cn, bool cnt_next) {
+#pragma unroll
+        for (int k = 0; k < CH; k += 2) {
+            issue(c, k + 1, h, A.key, true, B, true);
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            slot[(k * CH + i) * (CH + 1) + j] = blend_strip(A, sc, sd);
+            sc = A.c;
+            sd = A.d;
+            if (k + 2 < CH) {
+                issue(c, k + 2, h, B.key, true, A, true);
+            } else {
+                load_h(cn, h);
+                issue(cn, 0, h, 0, false, A, cnt_next);
+            }
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            slot[((k + 1) * CH + i) * (CH + 1) + j] = blend_strip(B, sc, sd);
+            sc = B.c;
+            sd = B.d;
+        }
+    };
+    const f32x4* row = slot + lane * (CH + 1);
+    float g0 = 0.0f, g1 = 0.0f, g2 = 0.0f;
+    if (in) {
+        const float* d = dout + pix * 3;
+        g0 = d[0];
+        g1 = d[1];
+        g2 = d[2];
+    }
+    load_h(n - 1, h);
+    issue(n - 1, 0, h, 0, false, A, true);
+    // over_composite backward (utils.py:149-156 under autograd), chunks back to front
+    for (int c = n - 1; c >= 0; --c) {
+        float4 pre = make_float4(-0.0f, -0.0f, -0.0f, 0.0f);
+        if (c > 0 && in) pre = ck[(int64_t)c * HW + pix];
+        sample_chunk(c, c > 0 ? c - 1 : 0, c > 0);
+        float pr[CH][3];  // prefixes out_{p-1} of the chunk's planes, in the forward's order
+        pr[0][0] = pre.x;
+        pr[0][1] = pre.y;
+        pr[0][2] = pre.z;
+#pragma unroll
+        for (int k = 0; k + 1 < CH; ++k) {
+            const int p = c * CH + k;
+            float rr = pr[k][0], gr = pr[k][1], b = pr[k][2];
+            if (p < g.P) {
+                const f32x4 s = row[k];
+                const float a = p == 0 ? 1.0f : s[3];
+                const float om = 1.0f - a;
+                rr = over(s[0], a, om, rr);
+                gr = over(s[1], a, om, gr);
+                b = over(s[2], a, om, b);
+            }
+            pr[k + 1][0] = rr;
+            pr[k + 1][1] = gr;
+            pr[k + 1][2] = b;
+        }
+#pragma unroll
+        for (int k = CH - 1; k >= 0; --k) {
+            const int p = c * CH + k;
+            if (p < g.P) {
+                const f32x4 s = row[k];
+                float4 d;
+                if (p >= 1) {
+                    const float a = s[3], om = 1.0f - a;
+                    float s1 = g0 * s[0];
+                    s1 = s1 + g1 * s[1];
+                    s1 = s1 + g2 * s[2];
+                    float s2 = g0 * pr[k][0];
+                    s2 = s2 + g1 * pr[k][1];
+                    s2 = s2 + g2 * pr[k][2];
+                    d = make_float4(g0 * a, g1 * a, g2 * a, s1 + (-s2));
+                    g0 = g0 * om;
+                    g1 = g1 * om;
+                    g2 = g2 * om;
+                } else {
+                    d = make_float4(g0, g1, g2, 0.0f);  // plane 0: output = rgb_0, alpha unused
+                }
+                if (in) bwd_store(ws.ds + (int64_t)p * HW + pix, d);
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) ntap += __shfl_xor(ntap, off);
+    if (lane == 0 && ntap) atomicAdd(&ws.truth[blockIdx.x % kCtrSlots], (unsigned long long)ntap);
+}
+
+// One block = 4 waves = a 32 x 8 output tile (wave w: the 8 x 8 strip at column 8w); LDS and
+// h_lds as bwd_chain_kernel.  Fast recipe only (MODE 1 / 2 by the tile's division proof).
+__global__ __launch_bounds__(256, 1) void bwd_chain_strip_kernel(const float* __restrict__ view, RenderGeom g,
+                                                                 ChunkGeom cg, const float* __restrict__ homs,
+                                                                 const float* __restrict__ dout,
+                                                                 const float4* __restrict__ ck, BwdWs ws, int h_lds) {
+    extern __shared__ float4 bwd_lds[];
+    f32x4* slots = reinterpret_cast<f32x4*>(bwd_lds);
+    float* hl = reinterpret_cast<float*>(bwd_lds) + 4 * kWave * (kBwdCH + 1) * 4;
+    const float* hs = h_lds ? hl : homs;
+    const int tiles_x = (g.W + kStripTX - 1) / kStripTX;
+    const int tile = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int tx0 = (tile % tiles_x) * kStripTX, ty0 = (tile / tiles_x) * kStripTY;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+    if (h_lds)
+        for (int k = threadIdx.x; k < g.P * 9; k += 256) hl[k] = homs[k];
+    bool ok = true;
+    {
+        const float x0 = (float)tx0, x1 = (float)min(tx0 + kStripTX - 1, g.W - 1);
+        const float y0 = (float)ty0, y1 = (float)min(ty0 + kStripTY - 1, g.H - 1);
+        for (int p = (int)threadIdx.x; p < g.P; p += 256) ok = ok && div2_rect_safe(homs + (int64_t)p * 9, x0, x1, y0, y1);
+    }
+    const bool proven = __syncthreads_and(ok);  // also publishes hs
+    const int sx0 = tx0 + wave * 8;
+    if (sx0 >= g.W) return;  // whole wave; no barrier follows
+    f32x4* slot = slots + wave * kWave * (kBwdCH + 1);
+    if (proven)
+        bwd_chain_wave_strip<2>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws);
+    else
+        bwd_chain_wave_strip<1>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws);
+}
+
 // ---- 2. gather: per-texel sums in the reference's order ------------------------------
 
 // Per plane, the inverse of F = T S H, the map from an output pixel (x, y, 1) to its

@@ -277,6 +277,198 @@ __device__ __forceinline__ void render_chunk_wave_ring(const float* __restrict__
     }
 }
 
+// Vertical strips with tap reuse (round 4, CH = 8): a wave owns an 8 x 8 pixel strip and
+// its sub-step k is ROW k of the strip (8 columns x the chunk's 8 planes), so sub-step k+1
+// samples each lane's (column, plane) one row below sub-step k.  When a lane's tap origin
+// moved exactly one texel row down (the common case at near-unit vertical scale), its
+// north taps are the south taps it gathered for row k, already in registers; the north-tap
+// gathers are issued only when some lane of the wave needs its own (wave-uniform branch,
+// render_rows_kernel's vertical reuse).  Each tap instruction still covers 8 pixels x 8
+// consecutive planes (whole 128-B lines where the planes share a texel), so coalescing is
+// render_chunk_wave's; the composite reads the same slot rows (slot row = k*8 + column =
+// the lane of pixel (column, row k)).  Identical arithmetic: shared taps are the same
+// texels' values, so frames and checkpoints are bit-identical to render_chunk_wave's.
+struct StripTaps {
+    f32x4 a, b, c, d;  // NW, NE (own, when some lane of the wave needs them), SW, SE
+    float wx, wy;
+    int key;           // clamped tap origin iy * kstride + ix
+    bool sh;           // this lane's NW, NE = the previous row's SW, SE
+    bool own;          // wave-uniform: some lane gathered its own north taps
+};
+
+// issue_taps_chunk for a strip row: the south taps always, the north taps only where some
+// lane of the wave does not continue the previous row (t.own).  Returns the number of taps
+// inside the image (whether gathered or shared: the backward's pair count).
+__device__ __forceinline__ int issue_taps_strip(__amdgpu_buffer_rsrc_t r, const RenderGeom& g, const ChunkGeom& cg,
+                                                int jt, bool live, float px, float py, int kstride, int prev_key,
+                                                bool can_share, StripTaps& t) {
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    t.wx = px - fx0;
+    t.wy = py - fy0;
+    const int ix = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)g.W);
+    const int iy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)g.H);
+    const bool x0 = (unsigned)ix < (unsigned)g.W, x1 = (unsigned)(ix + 1) < (unsigned)g.W;
+    const bool y0 = live && (unsigned)iy < (unsigned)g.H, y1 = live && (unsigned)(iy + 1) < (unsigned)g.H;
+    const int off = (int)(((unsigned)__mul24(iy, cg.row_t) + (unsigned)__mul24(ix, cg.pix_t) + (unsigned)jt) * 16u);
+    const int pb = cg.pix_t * 16, rb = cg.row_t * 16;
+    t.key = iy * kstride + ix;
+    t.sh = can_share && t.key == prev_key + kstride;
+    t.c = llvm_raw_buffer_load_v4f32(r, (x0 && y1) ? off + rb : kOOB, 0, 0);
+    t.d = llvm_raw_buffer_load_v4f32(r, (x1 && y1) ? off + rb + pb : kOOB, 0, 0);
+    t.own = __builtin_amdgcn_ballot_w64(!t.sh) != 0;
+    if (t.own) {  // wave-uniform: some lane needs its own north taps
+        t.a = llvm_raw_buffer_load_v4f32(r, (!t.sh && x0 && y0) ? off : kOOB, 0, 0);
+        t.b = llvm_raw_buffer_load_v4f32(r, (!t.sh && x1 && y0) ? off + pb : kOOB, 0, 0);
+    }
+    return ((int)x0 + (int)x1) * ((int)y0 + (int)y1);
+}
+
+// the blended sample of a strip row; pc, pd: the previous row's south taps of this lane
+__device__ __forceinline__ f32x4 blend_strip(const StripTaps& t, const f32x4& pc, const f32x4& pd) {
+    ChunkTaps u;
+    u.a = pc;  // every lane continues (the common case): no per-lane select
+    u.b = pd;
+    u.c = t.c;
+    u.d = t.d;
+    u.wx = t.wx;
+    u.wy = t.wy;
+    if (t.own) {
+        asm volatile("");  // keeps this a real (wave-uniform) branch
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            u.a[q] = t.sh ? pc[q] : t.a[q];
+            u.b[q] = t.sh ? pd[q] : t.b[q];
+        }
+    }
+    return blend_chunk(u);
+}
+
+template <bool GUARD>
+__device__ __forceinline__ void render_chunk_wave_strip(const float* __restrict__ view, const RenderGeom& g,
+                                                        const ChunkGeom& cg, const float* __restrict__ hs,
+                                                        f32x4* __restrict__ slot, int sx0, int sy0, int lane,
+                                                        float& cr, float& cg_, float& cb, float4* __restrict__ ck,
+                                                        int64_t ck_stride) {
+    constexpr int CH = 8;
+    const int j = lane % CH, i = lane / CH;
+    const float fx = (float)min(sx0 + i, g.W - 1);  // columns past the frame recompute the last (not stored)
+    const int nchunk = (g.P + CH - 1) / CH;
+    const int kstride = g.W + 8;  // ix in [-2, W]: the key is injective
+    float h[9];
+    auto load_h = [&](int c, float* d) {
+        const int p = min(c * CH + j, g.P - 1);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) d[k] = hs[p * 9 + k];
+    };
+    // row k of chunk c: pixel (sx0 + i, sy0 + k), plane c*CH + j (issue_taps_chunk's taps)
+    auto issue = [&](int c, int k, const float* hh, int prev_key, bool can_share, StripTaps& t) {
+        float px, py;
+        chunk_pos<GUARD>(hh, fx, (float)min(sy0 + k, g.H - 1), g, px, py);
+        issue_taps_strip(make_rsrc(view + (int64_t)c * CH * 4, cg.rec_bytes), g, cg, j, c * CH + j < g.P, px, py,
+                         kstride, prev_key, can_share, t);
+    };
+    auto put = [&](int k, const StripTaps& t, const f32x4& pc, const f32x4& pd) {
+        slot[(k * CH + i) * (CH + 1) + j] = blend_strip(t, pc, pd);
+    };
+    auto over_px = [&](const f32x4& s, bool first) {
+        const float a = first ? 1.0f : s[3];
+        const float om = 1.0f - a;
+        cr = over(s[0], a, om, cr);
+        cg_ = over(s[1], a, om, cg_);
+        cb = over(s[2], a, om, cb);
+    };
+    StripTaps A, B;
+    f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sd = sc;  // the previous row's south taps
+    load_h(0, h);
+    issue(0, 0, h, 0, false, A);
+    for (int c = 0; c < nchunk; ++c) {
+        const int cn = c + 1 < nchunk ? c + 1 : c;  // past the end: re-issue (cached, unused)
+        if (ck && c > 0) ck[c * ck_stride] = make_float4(cr, cg_, cb, 0.0f);
+#pragma unroll
+        for (int k = 0; k < CH; k += 2) {  // A holds row k
+            issue(c, k + 1, h, A.key, true, B);
+            asm volatile("" ::: "memory");  // no later row's loads above this point
+            __builtin_amdgcn_sched_barrier(0);
+            put(k, A, sc, sd);
+            sc = A.c;
+            sd = A.d;
+            if (k + 2 < CH) {
+                issue(c, k + 2, h, B.key, true, A);
+            } else {
+                load_h(cn, h);  // the next chunk's homography (LDS) replaces this one's
+                issue(cn, 0, h, 0, false, A);
+            }
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            put(k + 1, B, sc, sd);
+            sc = B.c;
+            sd = B.d;
+        }
+        // composite (lane = pixel (column lane % 8, row lane / 8)): planes c*CH .. c*CH+CH-1,
+        // back to front
+        const f32x4* row = slot + lane * (CH + 1);
+        if (c * CH + CH <= g.P) {
+#pragma unroll
+            for (int j0 = 0; j0 < CH; j0 += 4) {
+                f32x4 sv[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) sv[jj] = row[j0 + jj];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) over_px(sv[jj], c == 0 && j0 + jj == 0);
+            }
+        } else {
+            for (int jj = 0; c * CH + jj < g.P; ++jj) over_px(row[jj], c * CH + jj == 0);
+        }
+    }
+}
+
+constexpr int kStripTX = 32, kStripTY = 8;  // block tile of render_chunk_strip_kernel (4 strips side by side)
+
+// One block = 4 waves = a 32 x 8 output tile of one view (wave w: the 8 x 8 strip at column
+// 8w); XCD-aware (tile, view) order, tile-level division proof.  Dynamic LDS as
+// render_chunk_kernel<8, 1, 1>.
+__global__ __launch_bounds__(256, 4) void render_chunk_strip_kernel(const float* __restrict__ mpi, int64_t view_stride,
+                                                                    RenderGeom g, ChunkGeom cg, int V,
+                                                                    const float* __restrict__ homs,
+                                                                    float* __restrict__ out,
+                                                                    float4* __restrict__ ckpt) {
+    extern __shared__ float4 chunk_lds[];
+    f32x4* slots = reinterpret_cast<f32x4*>(chunk_lds);
+    float* hs = reinterpret_cast<float*>(chunk_lds) + chunk_slot_floats<8, 1>();
+    const int tiles_x = (g.W + kStripTX - 1) / kStripTX;
+    const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int v = lb % V;
+    const int tile = lb / V;
+    const int tx0 = (tile % tiles_x) * kStripTX, ty0 = (tile / tiles_x) * kStripTY;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+    const float* hv = homs + (int64_t)v * g.P * 9;
+    for (int k = threadIdx.x; k < g.P * 9; k += 256) hs[k] = hv[k];
+    const float x0 = (float)tx0, x1 = (float)min(tx0 + kStripTX - 1, g.W - 1);
+    const float y0 = (float)ty0, y1 = (float)min(ty0 + kStripTY - 1, g.H - 1);
+    bool ok = true;
+    for (int p = (int)threadIdx.x; p < g.P; p += 256) ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, y0, y1);
+    const bool proven = __syncthreads_and(ok);  // also publishes hs
+    const int sx0 = tx0 + wave * 8;
+    if (sx0 >= g.W) return;  // whole wave; no barrier follows
+    const float* view = mpi + (int64_t)v * view_stride;
+    f32x4* slot = slots + wave * kWave * 9;
+    const int x = sx0 + (lane & 7), y = ty0 + (lane >> 3);
+    const bool in = x < g.W && y < g.H;
+    const int64_t HW = (int64_t)g.H * g.W;
+    float4* ck = (ckpt && in) ? ckpt + ((int64_t)v * ((g.P + 7) / 8)) * HW + (int64_t)y * g.W + x : nullptr;
+    float cr = -0.0f, cgr = -0.0f, cb = -0.0f;
+    if (proven)
+        render_chunk_wave_strip<false>(view, g, cg, hs, slot, sx0, ty0, lane, cr, cgr, cb, ck, HW);
+    else
+        render_chunk_wave_strip<true>(view, g, cg, hs, slot, sx0, ty0, lane, cr, cgr, cb, ck, HW);
+    if (in) {
+        float* o = out + (((int64_t)v * g.H + y) * g.W + x) * 3;
+        o[0] = cr;
+        o[1] = cgr;
+        o[2] = cb;
+    }
+}
+
 // One block = 4 waves = a 64 x 4R output tile of one view (wave w: rows w*R .. w*R+R-1 of
 // the tile); blocks in render_packed_kernel's XCD-aware (tile, view) order.  Dynamic LDS:
 // chunk_slot_floats<CH, SPLIT>() + P*9 floats.

@@ -95,7 +95,8 @@ def test_ab_kernels_live_in_the_ab_library():
         assert L.mpiv_debug_set(name.encode(), val) == -1, name
         assert b"libmpiv_ab.so" in L.mpiv_last_error()
     for name, val in (("render_tile", -1), ("render_vshare", 11), ("render_chunk", 4), ("chunk_rows", 1),
-                      ("bwd_fallback", 1), ("box_shrink", 2), ("sweep_direct", 1), ("bwd_gather", 0)):  # production kernels / test hooks
+                      ("bwd_fallback", 1), ("box_shrink", 2), ("sweep_direct", 1), ("bwd_gather", 0),
+                      ("chunk_strip", 0), ("chunk_strip", 1)):  # production kernels / test hooks
         assert L.mpiv_debug_set(name.encode(), val) == 0, name
     L.mpiv_debug_set(b"reset", 0)
     p = ctypes.c_void_p(256)

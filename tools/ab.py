@@ -102,6 +102,42 @@ def bwd(dev, it):
     run("c4 render backward with checkpoints, 1 view", ROWS, fn, 2 * P * H * W * 16 + H * W * 12, it)
 
 
+STRIP = [("rows64x1", {"chunk_strip": 0}), ("strip8x8", {"chunk_strip": 1})]
+
+
+def strip(dev, it):
+    """Round 4: render_chunk_strip_kernel (8 x 8 strips, vertical tap reuse) vs the 64 x 1
+    wave rows, in-place render and training forward; frames and checkpoints compared bit for bit."""
+    mpi, homs, H, W, P = c4_mpi(dev)
+    res = {}
+    for label, opts in STRIP:
+        with _lib.debug(**opts):
+            res[label] = _lib.render_train(mpi, homs)
+    (fa, ca), (fb, cb) = res.values()
+    print(json.dumps({"exp": "strip bit identity", "frames": bool(torch.equal(fa.view(torch.int32), fb.view(torch.int32))),
+                      "ckpts": bool(torch.equal(ca.view(torch.int32), cb.view(torch.int32)))}), flush=True)
+    del res, fa, fb, ca, cb
+    out = torch.empty((1, H, W, 3), device=dev)
+    fn = lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out, _lib._stream(dev))  # noqa: E731
+    run("c4 in-place render, 1 view", STRIP, fn, P * H * W * 16 + H * W * 12, it, passes=3)
+    fn = lambda: _lib.render_train(mpi, homs)  # noqa: E731
+    run("c4 training forward (frame + checkpoints), 1 view", STRIP, fn, P * H * W * 16 + H * W * 12, it, passes=3)
+    g = torch.Generator(device=dev).manual_seed(1)
+    dout = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    ws = torch.empty(_lib.load().mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    _, ck = _lib.render_train(mpi, homs)
+    grads = []
+    for label, opts in STRIP:
+        with _lib.debug(**opts):
+            grads.append(_lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck, check=True))
+    print(json.dumps({"exp": "strip chain bit identity", "grads": bool(torch.equal(grads[0].view(torch.int32),
+                                                                                    grads[1].view(torch.int32)))}),
+          flush=True)
+    del grads
+    fn = lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)  # noqa: E731
+    run("c4 render backward with checkpoints, 1 view", STRIP, fn, 2 * P * H * W * 16 + H * W * 12, it, passes=3)
+
+
 FLIGHT = [("flight2", {}), ("flight4", {"chunk_flight": 4})]
 
 
