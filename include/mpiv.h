@@ -50,7 +50,7 @@ const char *mpiv_build_id(void);
  * by name ("render_mv", "render_pair", "render_native_lds", "render_chunk", "render_ring",
  * "render_tile", "render_vshare", "chunk_rows", "chunk_flight", "sweep_tile", "sweep_store",
  * "sweep_dlane", "sweep_rows", "sweep_direct", "box_shrink", "bwd_fallback", "bwd_margin",
- * "bwd_gather", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode", "chunk_strip"; "reset" restores every default;
+ * "bwd_gather", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode", "chunk_strip", "u8_flight"; "reset" restores every default;
  * abi.hip documents the values).  Values that
  * select a kernel kept only for A/B measurement return MPIV_ERR_ARG from libmpiv.so (they are
  * compiled into libmpiv_ab.so).  Process-wide; returns MPIV_ERR_ARG for an unknown name. */

@@ -80,8 +80,11 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (0 = automatic)
 //   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
 //                      wave (0 = automatic)
+//   u8_flight=2|4      the u8 texel render with vertical reuse: rows in flight per work-item
+//                      (0 = automatic: 4 for launches under 2048 blocks)
 //   chunk_strip=0|1    the in-place render at CH = 8, one row: render_chunk_kernel's 64 x 1 wave rows
-//                      (0) or render_chunk_strip_kernel's 8 x 8 strips with vertical tap reuse (1)
+//                      (0) or render_chunk_strip_kernel's 8 x 16 strips with vertical tap reuse (1);
+//                      A/B: 2 = 8 x 8 strips, 3 = 8 x 8 with 3 rows in flight, 4 = 8 x 16 with 3
 //   sweep_direct=-1|0|1  mpiv_plane_sweep[_into] without LDS staging (plane_sweep_direct_kernel):
 //                      never / automatic (D <= 2) / for any D <= 64; 2|3: pixel per lane, the wave's
 //                      samples staged in LDS (plane_sweep_px_kernel, D * C <= 48; 64 / 32 pixels
@@ -105,18 +108,22 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
-                kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kNumOpts };
+                kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kOptU8Flight, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
                                          "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode",
-                                         "chunk_strip"};
+                                         "chunk_strip", "u8_flight"};
 #ifndef MPIV_CHUNK_STRIP
-#define MPIV_CHUNK_STRIP 1  // round 4: 0.525 vs 0.64 ms in place, backward 2.33 vs 2.48 (profiles/r04j_strip_ab.jsonl)
+#define MPIV_CHUNK_STRIP 1  // round 4: 0.506 vs 0.64 ms in place (profiles/r04j_strip*_ab.jsonl)
 #endif
-const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP};
+#ifndef MPIV_U8_FLIGHT
+#define MPIV_U8_FLIGHT 0
+#endif
+const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP,
+                                    MPIV_U8_FLIGHT};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP, MPIV_U8_FLIGHT};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -134,6 +141,7 @@ bool ab_only(int o, int v) {
         case kOptSweepDlane: return v == 0;
         case kOptChunkRows: return v == 2 || v == 4;
         case kOptChunkFlight: return v == 4;
+        case kOptChunkStrip: return v >= 2;
         case kOptSweepRows: return v == 6 || v == 8;
         case kOptBwdGather: return v == 1 || v == 2 || v == 3;
         case kOptBwdPollLimit: case kOptBwdFbBlocks: case kOptBwdFbMode: return v != 0;
@@ -188,11 +196,24 @@ int launch_chunk(int R, const float* mpi, int64_t vstride, const RenderGeom& g, 
     const int64_t nb = (int64_t)blocks(g.W, kTileX) * blocks(g.H, kTileY * R) * B;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     const int NT = (opt(kOptChunkFlight) == 4 && R == 1 && SPLIT == 1) ? 4 : 2;
-    if (CH == 8 && SPLIT == 1 && R == 1 && NT == 2 && opt(kOptChunkStrip)) {  // 8 x 8 strips, vertical tap reuse
-        const int64_t ns = (int64_t)blocks(g.W, kStripTX) * blocks(g.H, kStripTY) * B;
+    const int so = opt(kOptChunkStrip);
+    if (CH == 8 && SPLIT == 1 && R == 1 && NT == 2 && so > 0) {  // 8 x SR strips, vertical tap reuse
+        // 1: 8 x 16 strips, 2 rows in flight (production); A/B: 2 = 8 x 8, 3 = 8 x 8 with 3 rows in
+        // flight, 4 = 8 x 16 with 3 (profiles/r04j_strips_ab.jsonl)
+        const int SR = (so == 2 || so == 3) ? 8 : 16, SNT = so >= 3 ? 3 : 2;
+        const int64_t ns = (int64_t)blocks(g.W, kStripTX) * blocks(g.H, SR) * B;
         if (ns > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
-        if (g_route) return note_route(ns, 256, "render_chunk_strip_kernel");
-        render_chunk_strip_kernel<<<(unsigned)ns, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
+        if (g_route) return note_route(ns, 256, "render_chunk_strip_kernel<%d, %d>", SR, SNT);
+#if MPIV_AB
+        if (so == 2)
+            render_chunk_strip_kernel<8, 2><<<(unsigned)ns, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
+        else if (so == 3)
+            render_chunk_strip_kernel<8, 3><<<(unsigned)ns, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
+        else if (so == 4)
+            render_chunk_strip_kernel<16, 3><<<(unsigned)ns, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
+        else
+#endif
+            render_chunk_strip_kernel<16, 2><<<(unsigned)ns, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
         return launched(nm);
     }
     if (g_route) return note_route(nb, 256, "render_chunk_kernel<%d, %d, %d, %d>", CH, SPLIT, R, NT);
@@ -769,9 +790,14 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         else if (!ck && R == 4) MPIV_CHAIN(false, 4);
         else if (!ck && R == 2) MPIV_CHAIN(false, 2);
 #endif
+#if MPIV_AB
+        else if (ck && opt(kOptChunkStrip) == 4)  // A/B: 8 x 16 strips (2.41 vs 2.38 ms, r04j_strips_ab.jsonl)
+            bwd_chain_strip_kernel<16><<<blocks(W, kStripTX) * blocks(H, 16), 256, chain_lds, q>>>(mv, g, cg, hv, dv, ck,
+                                                                                                ws, h_lds);
+#endif
         else if (ck && opt(kOptChunkStrip))  // 8 x 8 strips, vertical tap reuse
-            bwd_chain_strip_kernel<<<blocks(W, kStripTX) * blocks(H, kStripTY), 256, chain_lds, q>>>(mv, g, cg, hv, dv,
-                                                                                                  ck, ws, h_lds);
+            bwd_chain_strip_kernel<8><<<blocks(W, kStripTX) * blocks(H, 8), 256, chain_lds, q>>>(mv, g, cg, hv, dv, ck,
+                                                                                              ws, h_lds);
         else if (ck) MPIV_CHAIN(true, 1);
         else MPIV_CHAIN(false, 1);
 #undef MPIV_CHAIN
@@ -1420,7 +1446,10 @@ static int render_u8_impl(const uint32_t* packed, int H, int W, int P, int p_beg
     const int R = rt == 0 ? (vs ? 4 : 2) : vs ? rt : rt == 8 ? 8 : 2;
     const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
-    if (g_route) return note_route(nb, 256, "render_u8_kernel<%s, %d, %s>", ct ? "true" : "false", R, vs ? "true" : "false");
+    if (g_route) {  // every template argument, as rocprof's demangled name shows it
+        const int d = (vs && R == 4 && (opt(kOptU8Flight) ? opt(kOptU8Flight) : (nb < 2048 ? 4 : 2)) == 4) ? 4 : 2;
+        return note_route(nb, 256, "render_u8_kernel<%s, %d, %s, %d>", ct ? "true" : "false", R, vs ? "true" : "false", d);
+    }
     const unsigned* pk = reinterpret_cast<const unsigned*>(packed);
     hipStream_t q = S(stream);
 #define MPIV_U8(CT, RR, VV)                                                                                       \
@@ -1435,7 +1464,15 @@ static int render_u8_impl(const uint32_t* packed, int H, int W, int P, int p_beg
         return launched(nm);
     }
 #endif
-    if (vs) {
+    // 4 rows in flight when the launch leaves the SIMDs few waves (one view: 1024 blocks = 4 waves
+    // per SIMD; 0.32 vs 0.37 ms), 2 for large launches (125 views: 30.2 vs 30.5 ms; r04j_strips_ab.jsonl)
+    const int u8f = opt(kOptU8Flight) ? opt(kOptU8Flight) : (nb < 2048 ? 4 : 2);
+    if (vs && u8f == 4) {  // 4 rows in flight
+        if (ct) render_u8_kernel<true, 4, true, 4><<<(unsigned)nb, 256, 0, q>>>(pk, npix, g, ug, V, p_begin, p_end, back,
+                                                                              homs, out);
+        else render_u8_kernel<false, 4, true, 4><<<(unsigned)nb, 256, 0, q>>>(pk, npix, g, ug, V, p_begin, p_end, 1,
+                                                                             homs, out);
+    } else if (vs) {
         if (ct) MPIV_U8(true, 4, true);
         else MPIV_U8(false, 4, true);
     } else if (ct) MPIV_U8(true, 2, false);

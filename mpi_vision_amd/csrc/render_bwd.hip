@@ -365,19 +365,20 @@ __global__ __launch_bounds__(256, R == 1 ? 1 : 4) void bwd_chain_kernel(const fl
 // composite phases run with lane = pixel (column lane % 8, row lane / 8).  Same samples,
 // same adjoint arithmetic, same pair count (every in-image tap of every sample, gathered or
 // shared): the d samples are bit-identical to bwd_chain_wave<MODE, true, 1>'s.
-template <int MODE>
+template <int MODE, int SR>
 __device__ __forceinline__ void bwd_chain_wave_strip(const float* __restrict__ view, const RenderGeom& g,
                                                      const ChunkGeom& cg, const float* __restrict__ hs,
                                                      f32x4* __restrict__ slot, int sx0, int sy0, int lane,
                                                      const float* __restrict__ dout, const float4* __restrict__ ck,
                                                      const BwdWs& ws) {
-    constexpr int CH = kBwdCH;
+    constexpr int CH = kBwdCH, NH = SR / 8;
+    static_assert(SR % 8 == 0, "strip rows");
     const int j = lane % CH, i = lane / CH;
     const int n = (g.P + CH - 1) / CH;
     const int64_t HW = (int64_t)g.H * g.W;
-    const int x = sx0 + (lane & 7), y = sy0 + (lane >> 3);  // this lane's pixel in the composite phases
-    const bool in = x < g.W && y < g.H;
+    const int x = sx0 + (lane & 7), y = sy0 + (lane >> 3);  // this lane's pixel of half 0 (half h: row y + 8h)
     const int64_t pix = (int64_t)y * g.W + x;
+    const int64_t hstep = 8 * (int64_t)g.W;
     const bool col_in = sx0 + i < g.W;
     const float fx = (float)min(sx0 + i, g.W - 1);  // columns past the frame recompute the last (uncounted)
     const int kstride = g.W + 8;
@@ -399,18 +400,22 @@ __device__ __forceinline__ void bwd_chain_wave_strip(const float* __restrict__ v
     };
     StripTaps A, B;
     f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sd = sc;
-    // chunk c into the slot; A holds its row 0 on entry and, on exit, row 0 of chunk cn
-    auto sample_chunk = [&](int c, int cn, bool cnt_next) {
+    // rows 8*hh .. 8*hh+7 of chunk c into the slot; A holds row 8*hh on entry and, on exit, the
+    // next row: 8*hh + 8 of chunk c, or row 0 of chunk cn
+    auto sample_half = [&](int c, int hh, int cn, bool cnt_next) {
 #pragma unroll
-        for (int k = 0; k < CH; k += 2) {
-            issue(c, k + 1, h, A.key, true, B, true);
+        for (int k = 0; k < 8; k += 2) {
+            const int r = 8 * hh + k;
+            issue(c, r + 1, h, A.key, true, B, true);
             asm volatile("" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             slot[(k * CH + i) * (CH + 1) + j] = blend_strip(A, sc, sd);
             sc = A.c;
             sd = A.d;
-            if (k + 2 < CH) {
-                issue(c, k + 2, h, B.key, true, A, true);
+            if (k + 2 < 8) {
+                issue(c, r + 2, h, B.key, true, A, true);
+            } else if (hh + 1 < NH) {
+                issue(c, r + 2, h, B.key, true, A, true);
             } else {
                 load_h(cn, h);
                 issue(cn, 0, h, 0, false, A, cnt_next);
@@ -423,63 +428,73 @@ __device__ __forceinline__ void bwd_chain_wave_strip(const float* __restrict__ v
         }
     };
     const f32x4* row = slot + lane * (CH + 1);
-    float g0 = 0.0f, g1 = 0.0f, g2 = 0.0f;
-    if (in) {
-        const float* d = dout + pix * 3;
-        g0 = d[0];
-        g1 = d[1];
-        g2 = d[2];
+    float g0[NH], g1[NH], g2[NH];
+    bool in[NH];
+#pragma unroll
+    for (int hh = 0; hh < NH; ++hh) {
+        in[hh] = x < g.W && y + 8 * hh < g.H;
+        g0[hh] = g1[hh] = g2[hh] = 0.0f;
+        if (in[hh]) {
+            const float* d = dout + (pix + hh * hstep) * 3;
+            g0[hh] = d[0];
+            g1[hh] = d[1];
+            g2[hh] = d[2];
+        }
     }
     load_h(n - 1, h);
     issue(n - 1, 0, h, 0, false, A, true);
     // over_composite backward (utils.py:149-156 under autograd), chunks back to front
     for (int c = n - 1; c >= 0; --c) {
-        float4 pre = make_float4(-0.0f, -0.0f, -0.0f, 0.0f);
-        if (c > 0 && in) pre = ck[(int64_t)c * HW + pix];
-        sample_chunk(c, c > 0 ? c - 1 : 0, c > 0);
-        float pr[CH][3];  // prefixes out_{p-1} of the chunk's planes, in the forward's order
-        pr[0][0] = pre.x;
-        pr[0][1] = pre.y;
-        pr[0][2] = pre.z;
 #pragma unroll
-        for (int k = 0; k + 1 < CH; ++k) {
-            const int p = c * CH + k;
-            float rr = pr[k][0], gr = pr[k][1], b = pr[k][2];
-            if (p < g.P) {
-                const f32x4 s = row[k];
-                const float a = p == 0 ? 1.0f : s[3];
-                const float om = 1.0f - a;
-                rr = over(s[0], a, om, rr);
-                gr = over(s[1], a, om, gr);
-                b = over(s[2], a, om, b);
-            }
-            pr[k + 1][0] = rr;
-            pr[k + 1][1] = gr;
-            pr[k + 1][2] = b;
-        }
+        for (int hh = 0; hh < NH; ++hh) {
+            float4 pre = make_float4(-0.0f, -0.0f, -0.0f, 0.0f);
+            if (c > 0 && in[hh]) pre = ck[(int64_t)c * HW + pix + hh * hstep];
+            sample_half(c, hh, c > 0 ? c - 1 : 0, c > 0);
+            float pr[CH][3];  // prefixes out_{p-1} of the chunk's planes, in the forward's order
+            pr[0][0] = pre.x;
+            pr[0][1] = pre.y;
+            pr[0][2] = pre.z;
 #pragma unroll
-        for (int k = CH - 1; k >= 0; --k) {
-            const int p = c * CH + k;
-            if (p < g.P) {
-                const f32x4 s = row[k];
-                float4 d;
-                if (p >= 1) {
-                    const float a = s[3], om = 1.0f - a;
-                    float s1 = g0 * s[0];
-                    s1 = s1 + g1 * s[1];
-                    s1 = s1 + g2 * s[2];
-                    float s2 = g0 * pr[k][0];
-                    s2 = s2 + g1 * pr[k][1];
-                    s2 = s2 + g2 * pr[k][2];
-                    d = make_float4(g0 * a, g1 * a, g2 * a, s1 + (-s2));
-                    g0 = g0 * om;
-                    g1 = g1 * om;
-                    g2 = g2 * om;
-                } else {
-                    d = make_float4(g0, g1, g2, 0.0f);  // plane 0: output = rgb_0, alpha unused
+            for (int k = 0; k + 1 < CH; ++k) {
+                const int p = c * CH + k;
+                float rr = pr[k][0], gr = pr[k][1], b = pr[k][2];
+                if (p < g.P) {
+                    const f32x4 s = row[k];
+                    const float a = p == 0 ? 1.0f : s[3];
+                    const float om = 1.0f - a;
+                    rr = over(s[0], a, om, rr);
+                    gr = over(s[1], a, om, gr);
+                    b = over(s[2], a, om, b);
                 }
-                if (in) bwd_store(ws.ds + (int64_t)p * HW + pix, d);
+                pr[k + 1][0] = rr;
+                pr[k + 1][1] = gr;
+                pr[k + 1][2] = b;
             }
+#pragma unroll
+            for (int k = CH - 1; k >= 0; --k) {
+                const int p = c * CH + k;
+                if (p < g.P) {
+                    const f32x4 s = row[k];
+                    float4 d;
+                    if (p >= 1) {
+                        const float a = s[3], om = 1.0f - a;
+                        float s1 = g0[hh] * s[0];
+                        s1 = s1 + g1[hh] * s[1];
+                        s1 = s1 + g2[hh] * s[2];
+                        float s2 = g0[hh] * pr[k][0];
+                        s2 = s2 + g1[hh] * pr[k][1];
+                        s2 = s2 + g2[hh] * pr[k][2];
+                        d = make_float4(g0[hh] * a, g1[hh] * a, g2[hh] * a, s1 + (-s2));
+                        g0[hh] = g0[hh] * om;
+                        g1[hh] = g1[hh] * om;
+                        g2[hh] = g2[hh] * om;
+                    } else {
+                        d = make_float4(g0[hh], g1[hh], g2[hh], 0.0f);  // plane 0: output = rgb_0, alpha unused
+                    }
+                    if (in[hh]) bwd_store(ws.ds + (int64_t)p * HW + pix + hh * hstep, d);
+                }
+            }
+            if (NH > 1) asm volatile("" : "+v"(g0[hh]), "+v"(g1[hh]), "+v"(g2[hh])::"memory");  // pinned here
         }
     }
 #pragma unroll
@@ -487,8 +502,9 @@ __device__ __forceinline__ void bwd_chain_wave_strip(const float* __restrict__ v
     if (lane == 0 && ntap) atomicAdd(&ws.truth[blockIdx.x % kCtrSlots], (unsigned long long)ntap);
 }
 
-// One block = 4 waves = a 32 x 8 output tile (wave w: the 8 x 8 strip at column 8w); LDS and
+// One block = 4 waves = a 32 x SR output tile (wave w: the 8 x SR strip at column 8w); LDS and
 // h_lds as bwd_chain_kernel.  Fast recipe only (MODE 1 / 2 by the tile's division proof).
+template <int SR>
 __global__ __launch_bounds__(256, 1) void bwd_chain_strip_kernel(const float* __restrict__ view, RenderGeom g,
                                                                  ChunkGeom cg, const float* __restrict__ homs,
                                                                  const float* __restrict__ dout,
@@ -499,14 +515,14 @@ __global__ __launch_bounds__(256, 1) void bwd_chain_strip_kernel(const float* __
     const float* hs = h_lds ? hl : homs;
     const int tiles_x = (g.W + kStripTX - 1) / kStripTX;
     const int tile = xcd_logical_block(blockIdx.x, gridDim.x);
-    const int tx0 = (tile % tiles_x) * kStripTX, ty0 = (tile / tiles_x) * kStripTY;
+    const int tx0 = (tile % tiles_x) * kStripTX, ty0 = (tile / tiles_x) * SR;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     if (h_lds)
         for (int k = threadIdx.x; k < g.P * 9; k += 256) hl[k] = homs[k];
     bool ok = true;
     {
         const float x0 = (float)tx0, x1 = (float)min(tx0 + kStripTX - 1, g.W - 1);
-        const float y0 = (float)ty0, y1 = (float)min(ty0 + kStripTY - 1, g.H - 1);
+        const float y0 = (float)ty0, y1 = (float)min(ty0 + SR - 1, g.H - 1);
         for (int p = (int)threadIdx.x; p < g.P; p += 256) ok = ok && div2_rect_safe(homs + (int64_t)p * 9, x0, x1, y0, y1);
     }
     const bool proven = __syncthreads_and(ok);  // also publishes hs
@@ -514,9 +530,9 @@ __global__ __launch_bounds__(256, 1) void bwd_chain_strip_kernel(const float* __
     if (sx0 >= g.W) return;  // whole wave; no barrier follows
     f32x4* slot = slots + wave * kWave * (kBwdCH + 1);
     if (proven)
-        bwd_chain_wave_strip<2>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws);
+        bwd_chain_wave_strip<2, SR>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws);
     else
-        bwd_chain_wave_strip<1>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws);
+        bwd_chain_wave_strip<1, SR>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws);
 }
 
 // ---- 2. gather: per-texel sums in the reference's order ------------------------------

@@ -343,18 +343,21 @@ __device__ __forceinline__ f32x4 blend_strip(const StripTaps& t, const f32x4& pc
     return blend_chunk(u);
 }
 
-template <bool GUARD>
+// SR strip rows (8 or 16: a chunk's sub-steps, one composite phase per 8 rows) and a ring of
+// NT rows in flight (row k + NT - 1 issued while row k blends, running on into the next chunk).
+template <bool GUARD, int SR, int NT>
 __device__ __forceinline__ void render_chunk_wave_strip(const float* __restrict__ view, const RenderGeom& g,
                                                         const ChunkGeom& cg, const float* __restrict__ hs,
                                                         f32x4* __restrict__ slot, int sx0, int sy0, int lane,
-                                                        float& cr, float& cg_, float& cb, float4* __restrict__ ck,
-                                                        int64_t ck_stride) {
+                                                        float (&cr)[SR / 8], float (&cg_)[SR / 8], float (&cb)[SR / 8],
+                                                        float4* __restrict__ ck, int64_t ck_stride, int64_t ck_half,
+                                                        int nhk) {
     constexpr int CH = 8;
+    static_assert(SR % 8 == 0 && NT >= 2 && NT <= SR, "strip shape");
     const int j = lane % CH, i = lane / CH;
     const float fx = (float)min(sx0 + i, g.W - 1);  // columns past the frame recompute the last (not stored)
     const int nchunk = (g.P + CH - 1) / CH;
     const int kstride = g.W + 8;  // ix in [-2, W]: the key is injective
-    float h[9];
     auto load_h = [&](int c, float* d) {
         const int p = min(c * CH + j, g.P - 1);
 #pragma unroll
@@ -367,67 +370,81 @@ __device__ __forceinline__ void render_chunk_wave_strip(const float* __restrict_
         issue_taps_strip(make_rsrc(view + (int64_t)c * CH * 4, cg.rec_bytes), g, cg, j, c * CH + j < g.P, px, py,
                          kstride, prev_key, can_share, t);
     };
-    auto put = [&](int k, const StripTaps& t, const f32x4& pc, const f32x4& pd) {
-        slot[(k * CH + i) * (CH + 1) + j] = blend_strip(t, pc, pd);
-    };
-    auto over_px = [&](const f32x4& s, bool first) {
-        const float a = first ? 1.0f : s[3];
-        const float om = 1.0f - a;
-        cr = over(s[0], a, om, cr);
-        cg_ = over(s[1], a, om, cg_);
-        cb = over(s[2], a, om, cb);
-    };
-    StripTaps A, B;
+    StripTaps T[NT];
     f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sd = sc;  // the previous row's south taps
-    load_h(0, h);
-    issue(0, 0, h, 0, false, A);
+    float hc[9];
+    load_h(0, hc);
+#pragma unroll
+    for (int k = 0; k + 1 < NT; ++k) issue(0, k, hc, k ? T[k - 1].key : 0, k > 0, T[k]);
     for (int c = 0; c < nchunk; ++c) {
         const int cn = c + 1 < nchunk ? c + 1 : c;  // past the end: re-issue (cached, unused)
-        if (ck && c > 0) ck[c * ck_stride] = make_float4(cr, cg_, cb, 0.0f);
+        if (ck && c > 0) {
 #pragma unroll
-        for (int k = 0; k < CH; k += 2) {  // A holds row k
-            issue(c, k + 1, h, A.key, true, B);
+            for (int hh = 0; hh < SR / 8; ++hh)
+                if (hh < nhk) ck[c * ck_stride + hh * ck_half] = make_float4(cr[hh], cg_[hh], cb[hh], 0.0f);
+        }
+#pragma unroll
+        for (int k = 0; k < SR; ++k) {
+            const int ka = k + NT - 1;  // the row issued now
+            if (ka < SR) {
+                issue(c, ka, hc, T[(ka - 1) % NT].key, true, T[ka % NT]);
+            } else {
+                float hn[9];
+                load_h(cn, hn);  // the next chunk's homography (LDS)
+                issue(cn, ka - SR, hn, T[(ka - 1) % NT].key, ka > SR, T[ka % NT]);
+            }
             asm volatile("" ::: "memory");  // no later row's loads above this point
             __builtin_amdgcn_sched_barrier(0);
-            put(k, A, sc, sd);
-            sc = A.c;
-            sd = A.d;
-            if (k + 2 < CH) {
-                issue(c, k + 2, h, B.key, true, A);
-            } else {
-                load_h(cn, h);  // the next chunk's homography (LDS) replaces this one's
-                issue(cn, 0, h, 0, false, A);
-            }
+            slot[((k % 8) * CH + i) * (CH + 1) + j] = blend_strip(T[k % NT], sc, sd);
+            sc = T[k % NT].c;
+            sd = T[k % NT].d;
             asm volatile("" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            put(k + 1, B, sc, sd);
-            sc = B.c;
-            sd = B.d;
-        }
-        // composite (lane = pixel (column lane % 8, row lane / 8)): planes c*CH .. c*CH+CH-1,
-        // back to front
-        const f32x4* row = slot + lane * (CH + 1);
-        if (c * CH + CH <= g.P) {
+            if (k % 8 == 7) {
+                // composite (lane = pixel (column lane % 8, row 8*hh + lane / 8)): planes
+                // c*CH .. c*CH+CH-1, back to front
+                const int hh = k / 8;
+                const f32x4* row = slot + lane * (CH + 1);
+                auto over_px = [&](const f32x4& s, bool first) {
+                    const float a = first ? 1.0f : s[3];
+                    const float om = 1.0f - a;
+                    cr[hh] = over(s[0], a, om, cr[hh]);
+                    cg_[hh] = over(s[1], a, om, cg_[hh]);
+                    cb[hh] = over(s[2], a, om, cb[hh]);
+                };
+                if (c * CH + CH <= g.P) {
 #pragma unroll
-            for (int j0 = 0; j0 < CH; j0 += 4) {
-                f32x4 sv[4];
+                    for (int j0 = 0; j0 < CH; j0 += 4) {
+                        f32x4 sv[4];
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj) sv[jj] = row[j0 + jj];
+                        for (int jj = 0; jj < 4; ++jj) sv[jj] = row[j0 + jj];
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj) over_px(sv[jj], c == 0 && j0 + jj == 0);
+                        for (int jj = 0; jj < 4; ++jj) over_px(sv[jj], c == 0 && j0 + jj == 0);
+                    }
+                } else {
+                    for (int jj = 0; c * CH + jj < g.P; ++jj) over_px(row[jj], c * CH + jj == 0);
+                }
+                if (SR > 8) asm volatile("" : "+v"(cr[hh]), "+v"(cg_[hh]), "+v"(cb[hh])::"memory");  // pinned here
             }
-        } else {
-            for (int jj = 0; c * CH + jj < g.P; ++jj) over_px(row[jj], c * CH + jj == 0);
         }
+        if constexpr (SR % NT != 0) {  // the next chunk's rows sit at ring positions SR % NT ..: rotate
+            StripTaps tmp[NT];
+#pragma unroll
+            for (int q = 0; q < NT; ++q) tmp[q] = T[(q + SR) % NT];
+#pragma unroll
+            for (int q = 0; q < NT; ++q) T[q] = tmp[q];
+        }
+        load_h(cn, hc);
     }
 }
 
-constexpr int kStripTX = 32, kStripTY = 8;  // block tile of render_chunk_strip_kernel (4 strips side by side)
+constexpr int kStripTX = 32;  // block tile width of the strip kernels (4 strips side by side)
 
-// One block = 4 waves = a 32 x 8 output tile of one view (wave w: the 8 x 8 strip at column
+// One block = 4 waves = a 32 x SR output tile of one view (wave w: the 8 x SR strip at column
 // 8w); XCD-aware (tile, view) order, tile-level division proof.  Dynamic LDS as
 // render_chunk_kernel<8, 1, 1>.
-__global__ __launch_bounds__(256, 4) void render_chunk_strip_kernel(const float* __restrict__ mpi, int64_t view_stride,
+template <int SR, int NT>
+__global__ __launch_bounds__(256, 3) void render_chunk_strip_kernel(const float* __restrict__ mpi, int64_t view_stride,
                                                                     RenderGeom g, ChunkGeom cg, int V,
                                                                     const float* __restrict__ homs,
                                                                     float* __restrict__ out,
@@ -439,12 +456,12 @@ __global__ __launch_bounds__(256, 4) void render_chunk_strip_kernel(const float*
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
     const int v = lb % V;
     const int tile = lb / V;
-    const int tx0 = (tile % tiles_x) * kStripTX, ty0 = (tile / tiles_x) * kStripTY;
+    const int tx0 = (tile % tiles_x) * kStripTX, ty0 = (tile / tiles_x) * SR;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     const float* hv = homs + (int64_t)v * g.P * 9;
     for (int k = threadIdx.x; k < g.P * 9; k += 256) hs[k] = hv[k];
     const float x0 = (float)tx0, x1 = (float)min(tx0 + kStripTX - 1, g.W - 1);
-    const float y0 = (float)ty0, y1 = (float)min(ty0 + kStripTY - 1, g.H - 1);
+    const float y0 = (float)ty0, y1 = (float)min(ty0 + SR - 1, g.H - 1);
     bool ok = true;
     for (int p = (int)threadIdx.x; p < g.P; p += 256) ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, y0, y1);
     const bool proven = __syncthreads_and(ok);  // also publishes hs
@@ -452,20 +469,29 @@ __global__ __launch_bounds__(256, 4) void render_chunk_strip_kernel(const float*
     if (sx0 >= g.W) return;  // whole wave; no barrier follows
     const float* view = mpi + (int64_t)v * view_stride;
     f32x4* slot = slots + wave * kWave * 9;
-    const int x = sx0 + (lane & 7), y = ty0 + (lane >> 3);
-    const bool in = x < g.W && y < g.H;
+    const int x = sx0 + (lane & 7), y = ty0 + (lane >> 3);  // the pixel of half 0 (half h: row y + 8h)
     const int64_t HW = (int64_t)g.H * g.W;
-    float4* ck = (ckpt && in) ? ckpt + ((int64_t)v * ((g.P + 7) / 8)) * HW + (int64_t)y * g.W + x : nullptr;
-    float cr = -0.0f, cgr = -0.0f, cb = -0.0f;
+    // checkpoints [V][nchunk][H][W]: half h of this lane at ck + h * 8W, halves past the frame skipped
+    const bool in0 = x < g.W && y < g.H;
+    float4* ck = (ckpt && in0) ? ckpt + ((int64_t)v * ((g.P + 7) / 8)) * HW + (int64_t)y * g.W + x : nullptr;
+    float cr[SR / 8], cgr[SR / 8], cb[SR / 8];
+#pragma unroll
+    for (int hh = 0; hh < SR / 8; ++hh) cr[hh] = cgr[hh] = cb[hh] = -0.0f;
+    const int nhk = min(SR / 8, (g.H - y + 7) / 8);  // halves of this lane inside the frame
     if (proven)
-        render_chunk_wave_strip<false>(view, g, cg, hs, slot, sx0, ty0, lane, cr, cgr, cb, ck, HW);
+        render_chunk_wave_strip<false, SR, NT>(view, g, cg, hs, slot, sx0, ty0, lane, cr, cgr, cb, ck, HW,
+                                               8 * (int64_t)g.W, nhk);
     else
-        render_chunk_wave_strip<true>(view, g, cg, hs, slot, sx0, ty0, lane, cr, cgr, cb, ck, HW);
-    if (in) {
-        float* o = out + (((int64_t)v * g.H + y) * g.W + x) * 3;
-        o[0] = cr;
-        o[1] = cgr;
-        o[2] = cb;
+        render_chunk_wave_strip<true, SR, NT>(view, g, cg, hs, slot, sx0, ty0, lane, cr, cgr, cb, ck, HW,
+                                              8 * (int64_t)g.W, nhk);
+#pragma unroll
+    for (int hh = 0; hh < SR / 8; ++hh) {
+        if (x < g.W && y + 8 * hh < g.H) {
+            float* o = out + (((int64_t)v * g.H + y + 8 * hh) * g.W + x) * 3;
+            o[0] = cr[hh];
+            o[1] = cgr[hh];
+            o[2] = cb[hh];
+        }
     }
 }
 

@@ -121,7 +121,10 @@ __device__ __forceinline__ void render_u8_pixels(const unsigned* __restrict__ pl
 // words) -- and so are their CONVERTED values, so a continuing row converts 2 taps instead of
 // 4 (the u8 -> RN(u8/255) conversion is most of this kernel's VALU).  North taps are gathered
 // only when some lane of the wave does not continue (wave-uniform branch).
-template <bool CT, bool GUARD, int R>
+// D > 2: a ring of D rows in flight (row k + D - 1 issued while row k blends, running on into the
+// next plane; R % D == 0 keeps ring positions static across planes).  At one view the launch has
+// 4 waves per SIMD (R = 4), so the loads each wave keeps in flight are what hides HBM latency.
+template <bool CT, bool GUARD, int R, int D = 2>
 __device__ __forceinline__ void render_u8_vs_pixels(const unsigned* __restrict__ planes, int64_t plane_stride,
                                                     const RenderGeom& g, const U8Geom& ug, int p_begin, int p_end,
                                                     int back, const float* __restrict__ hv, int x, int y0, float* cr,
@@ -196,9 +199,38 @@ __device__ __forceinline__ void render_u8_vs_pixels(const unsigned* __restrict__
         asm volatile("" : "+v"(cr[k]), "+v"(cg[k]), "+v"(cb[k]));  // pinned here (render.hip)
         if (CT) asm volatile("" : "+v"(tt[k]));
     };
-    RowU8 A, B;
     f32x4 pc = {0.f, 0.f, 0.f, 0.f}, pd = pc;
     Hom9 h = hom(p_begin), hn = hom(p_begin + 1);
+    if constexpr (D != 2) {
+        static_assert(R % D == 0 && D > 2, "ring depth must divide R");
+        RowU8 T[D];
+        issue(p_begin, 0, h, 0, false, T[0]);
+#pragma unroll
+        for (int k = 1; k < D - 1; ++k) issue(p_begin, k, h, T[k - 1].off, true, T[k]);
+        for (int p = p_begin; p < p_end; ++p) {
+            const bool first = replace_first && p == p_begin;
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const int kk = k + D - 1;  // the row issued now
+                if (kk < R)
+                    issue(p, kk, h, T[(kk - 1) % D].off, true, T[kk % D]);
+                else if (kk == R)
+                    issue(p + 1, 0, hn, 0, false, T[kk % D]);  // past the end: the last plane again (unused)
+                else
+                    issue(p + 1, kk - R, hn, T[(kk - 1) % D].off, true, T[kk % D]);
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                f32x4 sc, sd;
+                consume(T[k % D], pc, pd, k, first, sc, sd);
+                pc = sc;
+                pd = sd;
+            }
+            h = hn;
+            hn = hom(p + 2);
+        }
+        return;
+    }
+    RowU8 A, B;
     issue(p_begin, 0, h, 0, false, A);
     for (int p = p_begin; p < p_end; ++p) {
         const bool first = replace_first && p == p_begin;
@@ -229,7 +261,7 @@ __device__ __forceinline__ void render_u8_vs_pixels(const unsigned* __restrict__
 // render_rows_kernel's contract on the packed u8 layout (FAST recipe: H, W >= 2): a
 // 256-thread block = 64 x 4R tile, XCD-aware (tile, view) order, tile-level division
 // proof; a tile where the proof fails runs the per-sample guarded recipe (GUARD).
-template <bool CT, int R, bool VS = false>
+template <bool CT, int R, bool VS = false, int D = 2>
 __global__ __launch_bounds__(256) void render_u8_kernel(const unsigned* __restrict__ planes, int64_t plane_stride,
                                                         RenderGeom g, U8Geom ug, int V, int p_begin, int p_end,
                                                         int back, const float* __restrict__ homs,
@@ -259,8 +291,8 @@ __global__ __launch_bounds__(256) void render_u8_kernel(const unsigned* __restri
     }
     if (proven) {
         if constexpr (VS)
-            render_u8_vs_pixels<CT, false, R>(planes, plane_stride, g, ug, p_begin, p_end, back, hv, x, y0, cr, cg, cb,
-                                              tt);
+            render_u8_vs_pixels<CT, false, R, D>(planes, plane_stride, g, ug, p_begin, p_end, back, hv, x, y0, cr, cg,
+                                                 cb, tt);
         else
             render_u8_pixels<CT, false, R>(planes, plane_stride, g, ug, p_begin, p_end, back, hv, x, y0, cr, cg, cb,
                                            tt);

@@ -91,12 +91,12 @@ def test_ab_kernels_live_in_the_ab_library():
     for name, val in (("render_mv", 1), ("render_ring", 4), ("render_pair", 1), ("render_tile", 8),
                       ("render_vshare", 1), ("sweep_tile", 1), ("sweep_store", 2), ("render_chunk", 108),
                       ("sweep_dlane", 0), ("chunk_rows", 2), ("chunk_flight", 4), ("sweep_rows", 8),
-                      ("bwd_gather", 1), ("bwd_gather", 2)):
+                      ("bwd_gather", 1), ("bwd_gather", 2), ("chunk_strip", 2)):
         assert L.mpiv_debug_set(name.encode(), val) == -1, name
         assert b"libmpiv_ab.so" in L.mpiv_last_error()
     for name, val in (("render_tile", -1), ("render_vshare", 11), ("render_chunk", 4), ("chunk_rows", 1),
                       ("bwd_fallback", 1), ("box_shrink", 2), ("sweep_direct", 1), ("bwd_gather", 0),
-                      ("chunk_strip", 0), ("chunk_strip", 1)):  # production kernels / test hooks
+                      ("chunk_strip", 0), ("chunk_strip", 1), ("u8_flight", 2), ("u8_flight", 4)):  # production kernels / test hooks
         assert L.mpiv_debug_set(name.encode(), val) == 0, name
     L.mpiv_debug_set(b"reset", 0)
     p = ctypes.c_void_p(256)

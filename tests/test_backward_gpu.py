@@ -253,16 +253,17 @@ def test_backward_full_size_tile_equals_fallback(cfg, dev, kopts):
     assert torch.equal(fast.view(torch.int32), slow.view(torch.int32))
 
 
-@pytest.mark.parametrize("rows", [1, 2, 4, "f4", "strip"])
+@pytest.mark.parametrize("rows", [1, 2, 4, "f4", "strip", "strip8", "strip_n3", "strip16_n3"])
 @pytest.mark.parametrize("cfg", ["config2", "config4"])
 def test_training_forward_checkpoints(cfg, rows, dev, kopts):
     """mpiv_render_train: frames bit-identical to the inference render; the backward fed its
     checkpoints (one pass) is bit-identical to the backward that recomputes them (two
     passes); two views in one launch (non-broadcast [2,H,W,P,4]); the forward at 1, 2 and 4
-    rows per wave (chunk_rows), 4 sub-steps in flight and 8 x 8 strips with vertical tap reuse
+    rows per wave (chunk_rows), 4 sub-steps in flight and 8 x 16 / 8 x 8 strips with vertical tap reuse
     writes the same frames and checkpoints."""
     kopts(**{1: dict(chunk_strip=0), 2: dict(chunk_rows=2), 4: dict(chunk_rows=4), "f4": dict(chunk_flight=4),
-             "strip": dict(chunk_strip=1)}[rows])
+             "strip": dict(chunk_strip=1), "strip8": dict(chunk_strip=2), "strip_n3": dict(chunk_strip=3),
+             "strip16_n3": dict(chunk_strip=4)}[rows])
     c = getattr(configs, cfg)()
     H, W, P = c["H"], c["W"], c["P"]
     if cfg == "config4":

@@ -81,8 +81,8 @@ def test_route_dry_run_names_the_launched_kernels():
     assert _lib.route("render_packed", 576, 1024, 32, 1)[0] == "render_packed_kernel<false, true>"
     assert _lib.route("plane_sweep", 5, 768, 1024, 3, 64, 768, 1024) == ("plane_sweep_dlane_kernel<3, true, 4, 3072, 2>",
                                                                          16 * 192 * 5 * 512)
-    assert _lib.route("render", 1, 1024, 1024, 128) == ("render_chunk_strip_kernel", 32 * 128 * 256)
-    assert _lib.route("render_train", 1, 1024, 1024, 128)[0] == "render_chunk_strip_kernel"
+    assert _lib.route("render", 1, 1024, 1024, 128) == ("render_chunk_strip_kernel<16, 2>", 32 * 64 * 256)
+    assert _lib.route("render_train", 1, 1024, 1024, 128)[0] == "render_chunk_strip_kernel<16, 2>"
     with pytest.raises(RuntimeError, match="unknown entry"):
         _lib.route("nope", 1)
     with _lib.debug(render_tile=-1):
@@ -93,8 +93,9 @@ def test_route_dry_run_names_the_launched_kernels():
 def test_route_dry_run_u8_and_net_output():
     """The u8 texel render and the fused net-output render report their kernels (bench legs
     u8 / netout find their rocprof dispatches by them)."""
-    assert _lib.route("render_packed_u8", 1024, 1024, 128, 1) == ("render_u8_kernel<false, 4, true>",
+    # one view leaves the SIMDs 4 waves each: 4 rows in flight; the 125-view launch: 2
+    assert _lib.route("render_packed_u8", 1024, 1024, 128, 1) == ("render_u8_kernel<false, 4, true, 4>",
                                                                   16 * 64 * 256)
-    assert _lib.route("render_packed_u8", 1024, 1024, 128, 125)[0] == "render_u8_kernel<false, 4, true>"
+    assert _lib.route("render_packed_u8", 1024, 1024, 128, 125)[0] == "render_u8_kernel<false, 4, true, 2>"
     name, grid = _lib.route("render_net_output", 1, 576, 1024, 32)
     assert name == "render_netout_kernel" and grid > 0

@@ -32,7 +32,7 @@ def test_render_matches_reference(name, small, meta, dev):
 
 # in-place ([B,H,W,P,4]) kernels behind mpiv_render, selected by libmpiv's debug options
 NATIVE_KERNELS = {"chunk8": dict(render_chunk=8, chunk_strip=0), "chunk4": dict(render_chunk=4),
-                  "chunk8strip": dict(render_chunk=8, chunk_strip=1),
+                  "chunk8strip": dict(render_chunk=8, chunk_strip=1), "chunk8strip8": dict(render_chunk=8, chunk_strip=2),
                   "chunk8r2": dict(render_chunk=8, chunk_rows=2), "chunk8r4": dict(render_chunk=8, chunk_rows=4),
                   "chunk4r4": dict(render_chunk=4, chunk_rows=4),
                   "chunk8f4": dict(render_chunk=8, chunk_flight=4), "chunk4f4": dict(render_chunk=4, chunk_flight=4),
@@ -343,17 +343,18 @@ def _chunk_case(H, W, P, V, seed):
 
 
 CHUNK_ROWS = {1: dict(chunk_strip=0), 2: dict(chunk_rows=2), 4: dict(chunk_rows=4), "f4": dict(chunk_flight=4),
-              "strip": dict(chunk_strip=1)}
+              "strip": dict(chunk_strip=1), "strip8": dict(chunk_strip=2), "strip_n3": dict(chunk_strip=3),
+              "strip16_n3": dict(chunk_strip=4)}
 
 
-@pytest.mark.parametrize("rows", [1, 2, 4, "f4", "strip"])
+@pytest.mark.parametrize("rows", list(CHUNK_ROWS))
 @pytest.mark.parametrize("ch", [4, 8])
 @pytest.mark.parametrize("shape", [(37, 203, 13), (70, 150, 9), (33, 64, 8), (21, 70, 3), (5, 130, 21)])
 def test_chunk_kernel_odd_shapes_extreme_poses(ch, rows, shape, dev, kopts):
     """render_chunk_kernel: plane counts that leave a partial last chunk, partial tiles in
     x and y (and a wave's row group past the frame), non-broadcast batches and extreme views,
-    at 1, 2 and 4 rows per wave, with 4 sub-steps in flight ("f4") and as 8 x 8 strips with
-    vertical tap reuse ("strip", CH = 8 only): bit-exact vs the oracle."""
+    at 1, 2 and 4 rows per wave, with 4 sub-steps in flight ("f4") and as 8 x 16 / 8 x 8 strips with
+    vertical tap reuse ("strip*", CH = 8 only): bit-exact vs the oracle."""
     kopts(render_chunk=ch, **CHUNK_ROWS[rows])
     H, W, P = shape
     mpi, homs = _chunk_case(H, W, P, 5, seed=H + W + P)

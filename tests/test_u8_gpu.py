@@ -30,14 +30,16 @@ def _u8_to_float(u8: np.ndarray) -> np.ndarray:
 
 
 def _rows_opts(kopts, rows):
-    """rows: 2 / 8 rows per lane, or "4vs" / "8vs": that many with vertical tap reuse (A/B)."""
+    """rows: 2 / 8 rows per lane, or "4vs" / "8vs": that many with vertical tap reuse (A/B);
+    "4vsf2" / "4vsf4": 4 rows with reuse and 2 / 4 rows in flight (u8_flight); 0: automatic."""
     if isinstance(rows, str):
-        kopts(render_tile=int(rows[:-2]), render_vshare=1)
+        n, _, f = rows.partition("vs")
+        kopts(render_tile=int(n), render_vshare=1, **({"u8_flight": int(f[1:])} if f else {}))
     else:
         kopts(render_tile=rows)
 
 
-@pytest.mark.parametrize("rows", [0, 2, 8, "4vs", "8vs"])
+@pytest.mark.parametrize("rows", [0, 2, 8, "4vs", "8vs", "4vsf2", "4vsf4"])
 def test_u8_render_reference_test_mpi(rows, large, meta, dev, kopts):
     """Config 1: the reference's 10-plane uint8 test MPI, two poses, against the goldens
     the reference produced from u8 / 255 (tools/gen_goldens.py)."""
@@ -68,7 +70,7 @@ def _extreme_case(V, H, W, P, seed):
     return u8, homs
 
 
-@pytest.mark.parametrize("rows", [2, 8, "4vs", "8vs"])
+@pytest.mark.parametrize("rows", [2, 8, "4vs", "8vs", "4vsf2", "4vsf4"])
 @pytest.mark.parametrize("shape", [(70, 150, 9), (37, 203, 7), (64, 66, 16)])
 def test_u8_render_random_vs_oracle(rows, shape, dev, kopts):
     """Random bytes (every value 0..255 occurs), odd sizes, partial tiles, planes partly
@@ -85,7 +87,7 @@ def test_u8_render_random_vs_oracle(rows, shape, dev, kopts):
     assert_bits(_lib.render_packed(_lib.pack_planes(fl[0].to(dev)), homs).cpu().numpy(), want, "float path")
 
 
-@pytest.mark.parametrize("rows", [2, 8, "4vs", "8vs"])
+@pytest.mark.parametrize("rows", [2, 8, "4vs", "8vs", "4vsf2", "4vsf4"])
 def test_u8_ct_partials(rows, dev, kopts):
     """Plane-range (C, T) partials of a u8 MPI equal the oracle's; their ordered combine
     equals the sequential render within 1e-5 (north_star)."""

@@ -102,7 +102,44 @@ def bwd(dev, it):
     run("c4 render backward with checkpoints, 1 view", ROWS, fn, 2 * P * H * W * 16 + H * W * 12, it)
 
 
-STRIP = [("rows64x1", {"chunk_strip": 0}), ("strip8x8", {"chunk_strip": 1})]
+STRIP = [("rows64x1", {"chunk_strip": 0}), ("strip8x16", {"chunk_strip": 1})]
+STRIPS = [("strip8x16", {"chunk_strip": 1}), ("strip8x8", {"chunk_strip": 2}), ("strip8x8_nt3", {"chunk_strip": 3}),
+          ("strip8x16_nt3", {"chunk_strip": 4})]
+
+
+def strips(dev, it):
+    """Round 4: strip shapes of render_chunk_strip_kernel (in-place render, training forward)."""
+    mpi, homs, H, W, P = c4_mpi(dev)
+    ref = None
+    for label, opts in STRIPS:
+        with _lib.debug(**opts):
+            f, ck = _lib.render_train(mpi, homs)
+        if ref is None:
+            ref = (f, ck)
+        print(json.dumps({"exp": "strips bit identity", "variant": label,
+                          "frames": bool(torch.equal(f.view(torch.int32), ref[0].view(torch.int32))),
+                          "ckpts": bool(torch.equal(ck.view(torch.int32), ref[1].view(torch.int32)))}), flush=True)
+    del ref, f, ck
+    out = torch.empty((1, H, W, 3), device=dev)
+    fn = lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out, _lib._stream(dev))  # noqa: E731
+    run("c4 in-place render, 1 view", STRIPS, fn, P * H * W * 16 + H * W * 12, it, passes=2)
+    fn = lambda: _lib.render_train(mpi, homs)  # noqa: E731
+    run("c4 training forward (frame + checkpoints), 1 view", STRIPS, fn, P * H * W * 16 + H * W * 12, it, passes=2)
+    g = torch.Generator(device=dev).manual_seed(1)
+    dout = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    ws = torch.empty(_lib.load().mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    _, ck = _lib.render_train(mpi, homs)
+    chains = [("chain64x1", {"chunk_strip": 0}), ("chain8x16", {"chunk_strip": 1}), ("chain8x8", {"chunk_strip": 2})]
+    grads = []
+    for label, opts in chains:
+        with _lib.debug(**opts):
+            grads.append(_lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck, check=True))
+    print(json.dumps({"exp": "chain strips bit identity", "grads": [bool(torch.equal(x.view(torch.int32),
+                                                                                      grads[0].view(torch.int32)))
+                                                                     for x in grads]}), flush=True)
+    del grads
+    fn = lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)  # noqa: E731
+    run("c4 render backward with checkpoints, 1 view", chains, fn, 2 * P * H * W * 16 + H * W * 12, it, passes=2)
 
 
 def strip(dev, it):
@@ -136,6 +173,32 @@ def strip(dev, it):
     del grads
     fn = lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)  # noqa: E731
     run("c4 render backward with checkpoints, 1 view", STRIP, fn, 2 * P * H * W * 16 + H * W * 12, it, passes=3)
+
+
+U8F = [("u8_flight2", {"u8_flight": 2}), ("u8_flight4", {"u8_flight": 4})]
+
+
+def u8f(dev, it):
+    """Round 4: the u8 render (vertical reuse, 4 rows) with 2 vs 4 rows in flight, 1 and 125 views."""
+    c = configs.config4()
+    H, W, P = c["H"], c["W"], c["P"]
+    pk = _lib.synth_mpi_packed_u8(c["seed"], H, W, 0, P, dev)
+    for V, pose0, iters in ((1, 100, it), (125, 0, 3)):
+        homs = _host.render_homographies(configs.f32(c["poses"][pose0:pose0 + V]), configs.f32(c["depths"]),
+                                         configs.f32([c["K"]] * V), V).to(dev)
+        out = torch.empty((V, H, W, 3), device=dev)
+        outs = []
+        for label, opts in U8F:
+            with _lib.debug(**opts):
+                _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs, V, out, _lib._stream(dev))
+            outs.append(out.clone())
+        print(json.dumps({"exp": f"u8 flight bit identity, {V} views",
+                          "same": bool(torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)))}), flush=True)
+        del outs
+        fn = lambda: _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs, V, out, _lib._stream(dev))  # noqa: E731
+        run(f"u8 render, {V} views", U8F, fn, V * (P * H * W * 4 + H * W * 12), iters, passes=2)
+        del out
+        torch.cuda.empty_cache()
 
 
 FLIGHT = [("flight2", {}), ("flight4", {"chunk_flight": 4})]
