@@ -55,6 +55,9 @@ __device__ __forceinline__ void bwd_store(float4* p, const float4& v) {
         *p = v;
 }
 
+#ifndef MPIV_GFRAC
+#define MPIV_GFRAC 0  // A/B: the gather stages fractions (2 floats) instead of the 4 corner weights
+#endif
 #ifndef MPIV_GPF2
 #define MPIV_GPF2 0  // A/B: the gather loads each pass's d samples during the previous texel phase
 #endif
@@ -689,7 +692,7 @@ constexpr int kGWP = kGCap + 1;
 // fractions (wx, wy) are staged (s_w[q], s_w[kGWP + q]); the texel pass forms the corner weight.
 // PRE (MPIV_GPF2 gather): the d samples were loaded by the caller (pre[i]: staged pixel
 // t + i * kGThreads, a pass ahead) instead of here.
-template <bool DS = true, bool PRE = false>
+template <bool DS = true, bool PRE = false, bool FR = false>
 __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const BwdWs& ws, const float* __restrict__ hp,
                                                   int p, bool proven, int t, int tx0, int ty0, int bx0, int bw,
                                                   int ra, int rb, int* s_code, float* s_w, float4* s_ds,
@@ -738,10 +741,15 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
             const float wx = px - fx0, ex = 1.0f - wx;
             const float wy = py - fy0, sy = 1.0f - wy;
             if (DS) {
-                s_w[q] = sy * ex;
-                s_w[kGWP + q] = sy * wx;
-                s_w[2 * kGWP + q] = wy * ex;
-                s_w[3 * kGWP + q] = wy * wx;
+                if (FR) {  // fractions only (MPIV_GFRAC): the texel pass forms the corner weight
+                    s_w[q] = wx;
+                    s_w[kGWP + q] = wy;
+                } else {
+                    s_w[q] = sy * ex;
+                    s_w[kGWP + q] = sy * wx;
+                    s_w[2 * kGWP + q] = wy * ex;
+                    s_w[3 * kGWP + q] = wy * wx;
+                }
                 if (!PRE && i >= MPIV_GSI)  // past the preloaded pixels (boxes over MPIV_GSI * kGThreads pixels)
                     dsv[i] = llvm_raw_buffer_load_v4f32(rds, (yy * g.W + xx) * 16, 0, 0);
                 s_ds[q] = make_float4(dsv[i][0], dsv[i][1], dsv[i][2], dsv[i][3]);
@@ -909,7 +917,8 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
 __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
                                                          float4* __restrict__ dmpi, float margin) {
     __shared__ int s_code[kGCap];                    // local nw-tap bucket of the staged pixel, -1 = none
-    __shared__ float s_w[4 * kGWP];                  // its bilinear weights, corner-major (kGWP); [kGCap] = 0
+    __shared__ float s_w[(MPIV_GFRAC ? 2 : 4) * kGWP];  // its bilinear weights, corner-major (kGWP), or
+                                                        // (MPIV_GFRAC) its fractions; [kGCap] = 0
     __shared__ float4 s_ds[kGCap + 1];               // its d sample; [kGCap] = 0
     __shared__ unsigned s_ent[2][2 * kGNB];          // bucket lists (2 slots, ~0 = free), by pass parity
     __shared__ int s_ovf[2];                         // a list overflowed in this pass
@@ -931,7 +940,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     }
     for (int b = threadIdx.x; b < 4 * kGNB; b += kGThreads) (&s_ent[0][0])[b] = ~0u;
     if (threadIdx.x < 2) s_ovf[threadIdx.x] = 0;
-    if (threadIdx.x < 4) s_w[threadIdx.x * kGWP + kGCap] = 0.0f;
+    if (threadIdx.x < (MPIV_GFRAC ? 2 : 4)) s_w[threadIdx.x * kGWP + kGCap] = 0.0f;  // FRAC: weight 1 x d sample 0
     if (threadIdx.x == 0) s_ds[kGCap] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     int par = 0;
     unsigned hits = 0;    // (texel, contributor) pairs found by this thread
@@ -999,7 +1008,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
         if (ra_n > by1) jj_n = first_from(jj + 1, ra_n);
         const int p = p0 + jj;
         __syncthreads();  // the previous pass's readers are done
-        gather_stage_pass<true, true>(g, ws, homs + (int64_t)p * 9, p, (b.w & kBoxProven) != 0, (int)threadIdx.x, tx0,
+        gather_stage_pass<true, true, MPIV_GFRAC>(g, ws, homs + (int64_t)p * 9, p, (b.w & kBoxProven) != 0, (int)threadIdx.x, tx0,
                                       ty0, bx0, bw, ra, rb, s_code, s_w, s_ds, s_ent[par], &s_ovf[par], pre);
         for (int bb = threadIdx.x; bb < 2 * kGNB; bb += kGThreads) s_ent[par ^ 1][bb] = ~0u;  // for the next pass
         if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
@@ -1011,8 +1020,8 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
             if (k == jj)
 #pragma unroll
                 for (int r = 0; r < kGTR; ++r)
-                    gather_texel_pass(g, ws, p, margin, tx, ty[r], bt[r], tin[r], ovf, s_ent[par], s_code, s_w, s_ds,
-                                      bx0, bx1, by0, by1, ra, rb, acc[r][k], hits, unsafe);
+                    gather_texel_pass<MPIV_GFRAC>(g, ws, p, margin, tx, ty[r], bt[r], tin[r], ovf, s_ent[par], s_code,
+                                                  s_w, s_ds, bx0, bx1, by0, by1, ra, rb, acc[r][k], hits, unsafe);
         par ^= 1;
         jj = jj_n;
         ra = ra_n;
@@ -1038,16 +1047,16 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
         for (int ra = by0; ra <= by1; ra += rpp) {
             const int rb = min(by1 + 1, ra + rpp);
             __syncthreads();  // the previous pass's readers are done
-            gather_stage_pass(g, ws, hp, p, proven, (int)threadIdx.x, tx0, ty0, bx0, bw, ra, rb, s_code, s_w, s_ds,
-                              s_ent[par], &s_ovf[par]);
+            gather_stage_pass<true, false, MPIV_GFRAC>(g, ws, hp, p, proven, (int)threadIdx.x, tx0, ty0, bx0, bw, ra,
+                                                       rb, s_code, s_w, s_ds, s_ent[par], &s_ovf[par]);
             for (int b = threadIdx.x; b < 2 * kGNB; b += kGThreads) s_ent[par ^ 1][b] = ~0u;  // for the next pass
             if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
             __syncthreads();
             const bool ovf = s_ovf[par] != 0;
 #pragma unroll
             for (int r = 0; r < kGTR; ++r)
-                gather_texel_pass(g, ws, p, margin, tx, ty[r], bt[r], tin[r], ovf, s_ent[par], s_code, s_w, s_ds, bx0,
-                                  bx1, by0, by1, ra, rb, acc[r][jj], hits, unsafe);
+                gather_texel_pass<MPIV_GFRAC>(g, ws, p, margin, tx, ty[r], bt[r], tin[r], ovf, s_ent[par], s_code, s_w,
+                                              s_ds, bx0, bx1, by0, by1, ra, rb, acc[r][jj], hits, unsafe);
             par ^= 1;
         }
     }
