@@ -80,7 +80,7 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (0 = automatic)
 //   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
 //                      wave (0 = automatic)
-//   u8_flight=2|4      the u8 texel render with vertical reuse: rows in flight per work-item
+//   u8_flight=2|4|8    the u8 texel render with vertical reuse: rows in flight per work-item
 //                      (0 = automatic: 4 for launches under 2048 blocks)
 //   chunk_strip=0|1    the in-place render at CH = 8, one row: render_chunk_kernel's 64 x 1 wave rows
 //                      (0) or render_chunk_strip_kernel's 8 x 16 strips with vertical tap reuse (1);
@@ -1447,7 +1447,8 @@ static int render_u8_impl(const uint32_t* packed, int H, int W, int P, int p_beg
     const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     if (g_route) {  // every template argument, as rocprof's demangled name shows it
-        const int d = (vs && R == 4 && (opt(kOptU8Flight) ? opt(kOptU8Flight) : (nb < 2048 ? 4 : 2)) == 4) ? 4 : 2;
+        const int f = opt(kOptU8Flight) ? opt(kOptU8Flight) : (nb < 2048 ? 4 : 2);
+        const int d = (vs && R == 4 && (f == 4 || f == 8)) ? f : 2;
         return note_route(nb, 256, "render_u8_kernel<%s, %d, %s, %d>", ct ? "true" : "false", R, vs ? "true" : "false", d);
     }
     const unsigned* pk = reinterpret_cast<const unsigned*>(packed);
@@ -1467,7 +1468,12 @@ static int render_u8_impl(const uint32_t* packed, int H, int W, int P, int p_beg
     // 4 rows in flight when the launch leaves the SIMDs few waves (one view: 1024 blocks = 4 waves
     // per SIMD; 0.32 vs 0.37 ms), 2 for large launches (125 views: 30.2 vs 30.5 ms; r04j_strips_ab.jsonl)
     const int u8f = opt(kOptU8Flight) ? opt(kOptU8Flight) : (nb < 2048 ? 4 : 2);
-    if (vs && u8f == 4) {  // 4 rows in flight
+    if (vs && u8f == 8) {  // 8 rows in flight (two planes' rows)
+        if (ct) render_u8_kernel<true, 4, true, 8><<<(unsigned)nb, 256, 0, q>>>(pk, npix, g, ug, V, p_begin, p_end, back,
+                                                                              homs, out);
+        else render_u8_kernel<false, 4, true, 8><<<(unsigned)nb, 256, 0, q>>>(pk, npix, g, ug, V, p_begin, p_end, 1,
+                                                                             homs, out);
+    } else if (vs && u8f == 4) {  // 4 rows in flight
         if (ct) render_u8_kernel<true, 4, true, 4><<<(unsigned)nb, 256, 0, q>>>(pk, npix, g, ug, V, p_begin, p_end, back,
                                                                               homs, out);
         else render_u8_kernel<false, 4, true, 4><<<(unsigned)nb, 256, 0, q>>>(pk, npix, g, ug, V, p_begin, p_end, 1,

@@ -121,8 +121,11 @@ __device__ __forceinline__ void render_u8_pixels(const unsigned* __restrict__ pl
 // words) -- and so are their CONVERTED values, so a continuing row converts 2 taps instead of
 // 4 (the u8 -> RN(u8/255) conversion is most of this kernel's VALU).  North taps are gathered
 // only when some lane of the wave does not continue (wave-uniform branch).
+#ifndef MPIV_U8PAIR
+#define MPIV_U8PAIR 0  // A/B: the ring's rows consumed two per step (their blends interleaved)
+#endif
 // D > 2: a ring of D rows in flight (row k + D - 1 issued while row k blends, running on into the
-// next plane; R % D == 0 keeps ring positions static across planes).  At one view the launch has
+// next planes; the plane loop is unrolled by D / R when D > R so ring positions stay static).  At one view the launch has
 // 4 waves per SIMD (R = 4), so the loads each wave keeps in flight are what hides HBM latency.
 template <bool CT, bool GUARD, int R, int D = 2>
 __device__ __forceinline__ void render_u8_vs_pixels(const unsigned* __restrict__ planes, int64_t plane_stride,
@@ -196,37 +199,62 @@ __device__ __forceinline__ void render_u8_vs_pixels(const unsigned* __restrict__
         cg[k] = over(s[1], a, om, cg[k]);
         cb[k] = over(s[2], a, om, cb[k]);
         if (CT) tt[k] = tt[k] * om;
-        asm volatile("" : "+v"(cr[k]), "+v"(cg[k]), "+v"(cb[k]));  // pinned here (render.hip)
-        if (CT) asm volatile("" : "+v"(tt[k]));
+        if (!MPIV_U8PAIR || D == 2) {
+            asm volatile("" : "+v"(cr[k]), "+v"(cg[k]), "+v"(cb[k]));  // pinned here (render.hip)
+            if (CT) asm volatile("" : "+v"(tt[k]));
+        }
     };
     f32x4 pc = {0.f, 0.f, 0.f, 0.f}, pd = pc;
     Hom9 h = hom(p_begin), hn = hom(p_begin + 1);
     if constexpr (D != 2) {
-        static_assert(R % D == 0 && D > 2, "ring depth must divide R");
+        static_assert((R % D == 0 || D % R == 0) && D > 2, "ring positions must repeat every plane group");
+        constexpr int U = D > R ? D / R : 1;       // planes per unrolled group (static ring positions)
+        constexpr int NH = (R + D - 2) / R + 1;    // homographies live at once: planes p .. p+NH-1
         RowU8 T[D];
-        issue(p_begin, 0, h, 0, false, T[0]);
+        Hom9 hq[NH];
 #pragma unroll
-        for (int k = 1; k < D - 1; ++k) issue(p_begin, k, h, T[k - 1].off, true, T[k]);
-        for (int p = p_begin; p < p_end; ++p) {
-            const bool first = replace_first && p == p_begin;
+        for (int j = 0; j < NH; ++j) hq[j] = hom(p_begin + j);
+        constexpr int KS = MPIV_U8PAIR ? 2 : 1;  // rows consumed per step (A/B: two interleaved blends)
+        constexpr int AHEAD = D - KS;             // rows issued ahead of the one consumed
 #pragma unroll
-            for (int k = 0; k < R; ++k) {
-                const int kk = k + D - 1;  // the row issued now
-                if (kk < R)
-                    issue(p, kk, h, T[(kk - 1) % D].off, true, T[kk % D]);
-                else if (kk == R)
-                    issue(p + 1, 0, hn, 0, false, T[kk % D]);  // past the end: the last plane again (unused)
-                else
-                    issue(p + 1, kk - R, hn, T[(kk - 1) % D].off, true, T[kk % D]);
-                asm volatile("" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                f32x4 sc, sd;
-                consume(T[k % D], pc, pd, k, first, sc, sd);
-                pc = sc;
-                pd = sd;
+        for (int it = 0; it < AHEAD; ++it)
+            issue(p_begin + it / R, it % R, hq[it / R], it % R ? T[(it + D - 1) % D].off : 0, it % R != 0, T[it % D]);
+        for (int p = p_begin; p < p_end; p += U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int pu = p + u;
+                if (U > 1 && pu >= p_end) break;  // wave-uniform: an odd tail plane
+                const bool first = replace_first && pu == p_begin;
+#pragma unroll
+                for (int k0 = 0; k0 < R; k0 += KS) {
+#pragma unroll
+                    for (int k = k0; k < k0 + KS; ++k) {
+                        const int it = u * R + k;  // the row consumed now (item of the group)
+                        const int ia = it + AHEAD;  // the row issued now: plane pu + dp (past the end: the last plane again)
+                        const int dp = ia / R - u, row = ia % R;
+                        issue(pu + dp, row, hq[dp], T[(ia + D - 1) % D].off, row != 0, T[ia % D]);
+                    }
+                    asm volatile("" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int k = k0; k < k0 + KS; ++k) {
+                        f32x4 sc, sd;
+                        consume(T[(u * R + k) % D], pc, pd, k, first, sc, sd);
+                        pc = sc;
+                        pd = sd;
+                    }
+                    if (MPIV_U8PAIR) {
+#pragma unroll
+                        for (int k = k0; k < k0 + KS; ++k) {
+                            asm volatile("" : "+v"(cr[k]), "+v"(cg[k]), "+v"(cb[k]));
+                            if (CT) asm volatile("" : "+v"(tt[k]));
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j + 1 < NH; ++j) hq[j] = hq[j + 1];
+                hq[NH - 1] = hom(pu + NH);
             }
-            h = hn;
-            hn = hom(p + 2);
         }
         return;
     }

@@ -39,7 +39,7 @@ def _rows_opts(kopts, rows):
         kopts(render_tile=rows)
 
 
-@pytest.mark.parametrize("rows", [0, 2, 8, "4vs", "8vs", "4vsf2", "4vsf4"])
+@pytest.mark.parametrize("rows", [0, 2, 8, "4vs", "8vs", "4vsf2", "4vsf4", "4vsf8"])
 def test_u8_render_reference_test_mpi(rows, large, meta, dev, kopts):
     """Config 1: the reference's 10-plane uint8 test MPI, two poses, against the goldens
     the reference produced from u8 / 255 (tools/gen_goldens.py)."""
@@ -70,7 +70,7 @@ def _extreme_case(V, H, W, P, seed):
     return u8, homs
 
 
-@pytest.mark.parametrize("rows", [2, 8, "4vs", "8vs", "4vsf2", "4vsf4"])
+@pytest.mark.parametrize("rows", [2, 8, "4vs", "8vs", "4vsf2", "4vsf4", "4vsf8"])
 @pytest.mark.parametrize("shape", [(70, 150, 9), (37, 203, 7), (64, 66, 16)])
 def test_u8_render_random_vs_oracle(rows, shape, dev, kopts):
     """Random bytes (every value 0..255 occurs), odd sizes, partial tiles, planes partly
@@ -87,7 +87,7 @@ def test_u8_render_random_vs_oracle(rows, shape, dev, kopts):
     assert_bits(_lib.render_packed(_lib.pack_planes(fl[0].to(dev)), homs).cpu().numpy(), want, "float path")
 
 
-@pytest.mark.parametrize("rows", [2, 8, "4vs", "8vs", "4vsf2", "4vsf4"])
+@pytest.mark.parametrize("rows", [2, 8, "4vs", "8vs", "4vsf2", "4vsf4", "4vsf8"])
 def test_u8_ct_partials(rows, dev, kopts):
     """Plane-range (C, T) partials of a u8 MPI equal the oracle's; their ordered combine
     equals the sequential render within 1e-5 (north_star)."""

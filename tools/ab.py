@@ -175,7 +175,7 @@ def strip(dev, it):
     run("c4 render backward with checkpoints, 1 view", STRIP, fn, 2 * P * H * W * 16 + H * W * 12, it, passes=3)
 
 
-U8F = [("u8_flight2", {"u8_flight": 2}), ("u8_flight4", {"u8_flight": 4})]
+U8F = [("u8_flight2", {"u8_flight": 2}), ("u8_flight4", {"u8_flight": 4}), ("u8_flight8", {"u8_flight": 8})]
 
 
 def u8f(dev, it):
@@ -193,7 +193,8 @@ def u8f(dev, it):
                 _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs, V, out, _lib._stream(dev))
             outs.append(out.clone())
         print(json.dumps({"exp": f"u8 flight bit identity, {V} views",
-                          "same": bool(torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)))}), flush=True)
+                          "same": [bool(torch.equal(o.view(torch.int32), outs[0].view(torch.int32))) for o in outs]}),
+              flush=True)
         del outs
         fn = lambda: _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs, V, out, _lib._stream(dev))  # noqa: E731
         run(f"u8 render, {V} views", U8F, fn, V * (P * H * W * 4 + H * W * 12), iters, passes=2)
