@@ -616,6 +616,13 @@ def training_leg(dev, stream, n=10):
     bwd_ms = span_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck), n, stream)
     g2 = _lib.render_backward(mpi, homs, dout, workspace=ws)
     bwd2_ms = span_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws), n, stream)
+    # the smallest workspace (plane groups, round 4): same gradient, d samples of one group resident
+    ws_min = torch.empty(_lib.load().mpiv_render_backward_workspace_size_min(H, W, P), dtype=torch.uint8, device=dev)
+    g3 = _lib.render_backward(mpi, homs, dout, workspace=ws_min, ckpt=ck)
+    bwd3_ms = span_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws_min, ckpt=ck), n, stream)
+    same_min = bool(torch.equal(g1.view(torch.int32), g3.view(torch.int32)))
+    ws_min_gb = round(ws_min.numel() / 1e9, 3)
+    del g3, ws_min
     flag = int(ws[_lib.bwd_flag_offset(H, W, P):][:4].view(torch.int32).item())
     aborted = _lib.render_backward_status(ws, H, W, P)
     same = bool(torch.equal(g1.view(torch.int32), g2.view(torch.int32)))
@@ -636,6 +643,9 @@ def training_leg(dev, stream, n=10):
            "backward_alg_def": "MPI read + d MPI written + d frame read (workspace traffic not counted)",
            "backward_hbm_frac": hbm(b_alg, bwd_ms)[1],
            "workspace_GB": round(ws.numel() / 1e9, 3), "fallback_flag": flag, "fallback_aborted_views": aborted,
+           "backward_min_workspace_ms": round(bwd3_ms, 4), "workspace_min_GB": ws_min_gb,
+           "min_workspace_grad_bit_identical": same_min,
+           "min_workspace_def": "mpiv_render_backward_workspace_size_min: plane groups of 32, one group's d samples resident",
            "ckpt_grad_bit_identical": same, "inference": prof_fields(kname, grid, f_alg, inf_ms)}
     del mpi, ws, g1, g2, ck
     torch.cuda.empty_cache()

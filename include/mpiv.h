@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 11
+#define MPIV_ABI_VERSION 12
 
 enum {
     MPIV_OK = 0,
@@ -50,7 +50,7 @@ const char *mpiv_build_id(void);
  * by name ("render_mv", "render_pair", "render_native_lds", "render_chunk", "render_ring",
  * "render_tile", "render_vshare", "chunk_rows", "chunk_flight", "sweep_tile", "sweep_store",
  * "sweep_dlane", "sweep_rows", "sweep_direct", "box_shrink", "bwd_fallback", "bwd_margin",
- * "bwd_gather", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode", "chunk_strip", "u8_flight"; "reset" restores every default;
+ * "bwd_gather", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode", "chunk_strip", "u8_flight", "bwd_group"; "reset" restores every default;
  * abi.hip documents the values).  Values that
  * select a kernel kept only for A/B measurement return MPIV_ERR_ARG from libmpiv.so (they are
  * compiled into libmpiv_ab.so).  Process-wide; returns MPIV_ERR_ARG for an unknown name. */
@@ -162,11 +162,16 @@ int mpiv_psv_proj_device(const float *Ks, int64_t ks_bstride, const float *pose,
 
 /* ---- render backward ------------------------------------------------------ */
 
-/* Workspace bytes mpiv_render_backward needs for one H x W x P MPI (reused across
- * views): 16 B per plane-pixel of d samples + 2 B per plane-pixel of colour
- * checkpoints + the fallback's bucket arrays (<= 16 B per plane-pixel of one plane
- * chunk, chunks sized to at most 2^25 plane-pixels). */
+/* Workspace bytes for the fastest schedule of mpiv_render_backward on one H x W x P MPI
+ * (reused across views): 16 B per plane-pixel of d samples for every plane + 2 B per
+ * plane-pixel of colour checkpoints + the fallback's bucket arrays (<= 16 B per plane-pixel
+ * of one plane group, groups sized to at most 2^25 plane-pixels).  Config 4: 3.0 GB. */
 size_t mpiv_render_backward_workspace_size(int H, int W, int P);
+
+/* The smallest workspace (round 4): given less than the size above, mpiv_render_backward runs
+ * a view in plane groups of <= 2^25 plane-pixels, back to front, holding one group's d samples
+ * at a time (bit-identical gradients, a few percent slower).  Config 4: 1.3 GB. */
+size_t mpiv_render_backward_workspace_size_min(int H, int W, int P);
 
 /* d(mpi_render_view_torch)/d(rgba_layers) (utils.py:267-294 under autograd), bit-exact
  * to the reference's CPU autograd: the over-composite adjoint followed by

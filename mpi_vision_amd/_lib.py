@@ -80,8 +80,8 @@ _SIGS = {
                                    _vp],
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
-                          "mpiv_build_id", "mpiv_debug_set")
-ABI_VERSION = 11
+                          "mpiv_render_backward_workspace_size_min", "mpiv_build_id", "mpiv_debug_set")
+ABI_VERSION = 12
 
 _lib = None
 _lib_ab = None
@@ -147,6 +147,8 @@ def _open(path: str, check_id: bool):
     L.mpiv_last_error.restype = ctypes.c_char_p
     L.mpiv_render_backward_workspace_size.argtypes = [_int, _int, _int]
     L.mpiv_render_backward_workspace_size.restype = ctypes.c_size_t
+    L.mpiv_render_backward_workspace_size_min.argtypes = [_int, _int, _int]
+    L.mpiv_render_backward_workspace_size_min.restype = ctypes.c_size_t
     if L.mpiv_abi_version() != ABI_VERSION:
         raise RuntimeError(f"mpi_vision_amd: {path} ABI version mismatch")
     return L
@@ -550,8 +552,7 @@ def bwd_layout_ok(rgba_layers: torch.Tensor) -> bool:
 def bwd_flag_offset(H: int, W: int, P: int) -> int:
     """Byte offset of the fallback flag in mpiv_render_backward's workspace (abi.hip
     bwd_layout): 1 after a call whose last view went through the bucket fallback."""
-    a = lambda n: (n + 255) // 256 * 256  # noqa: E731
-    return a(P * H * W * 16) + a((P + 7) // 8 * H * W * 16) + a(P * 48) + 2 * a(64 * 8)
+    return 2 * 64 * 8  # the two pair counters (64 slots of 8 B each) precede it (round 4 layout)
 
 
 def render_train(rgba_layers: torch.Tensor, homs: torch.Tensor):
@@ -571,6 +572,10 @@ def render_train(rgba_layers: torch.Tensor, homs: torch.Tensor):
     _call("mpiv_render_train", rgba_layers, _strides(rgba_layers), B, H, W, P, h, out, ckpt, _stream(dev))
     return out, ckpt
 
+
+# MPIV_BWD_MIN_WS=1: render_backward allocates the smallest workspace (plane groups: config 4
+# 1.3 GB instead of 3.0, bit-identical gradients, a few percent slower)
+BWD_MIN_WS = os.environ.get("MPIV_BWD_MIN_WS") == "1"
 
 # MPIV_BWD_CHECK=1: every render_backward reads the fallback's abort count back (one stream
 # synchronisation per call) and raises if a view's gradient was NaN-filled (render_bwd.hip)
@@ -602,8 +607,11 @@ def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.T
         raise RuntimeError(f"grad_output must be [{B},{H},{W},3], got {tuple(dout.shape)}")
     src = rgba_layers if bwd_layout_ok(rgba_layers) else rgba_layers.contiguous()
     L = load()
-    need = L.mpiv_render_backward_workspace_size(H, W, P)
-    ws = workspace if workspace is not None else torch.empty(need, dtype=torch.uint8, device=dev)
+    # a caller's workspace of at least the minimum (plane groups, render_bwd.hip); our own: the
+    # one-group size (the fastest schedule) unless MPIV_BWD_MIN_WS=1
+    need = L.mpiv_render_backward_workspace_size_min(H, W, P)
+    ws = workspace if workspace is not None else torch.empty(
+        need if BWD_MIN_WS else L.mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
     if ws.dtype != torch.uint8 or not ws.is_contiguous() or ws.numel() < need or ws.device != dev:
         raise RuntimeError(f"workspace must be a contiguous uint8 tensor of >= {need} bytes on {dev}")
     grad = torch.empty((B, H, W, P, 4), device=dev, dtype=torch.float32)

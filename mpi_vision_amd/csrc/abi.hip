@@ -80,6 +80,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (0 = automatic)
 //   chunk_rows=1|2|4   render_chunk_kernel (mpiv_render / mpiv_render_train) with that many rows per
 //                      wave (0 = automatic)
+//   bwd_group=k        test hook: the render backward's plane groups of k planes (rounded up to whole
+//                      8-plane chunks; the workspace size follows), 0 = automatic (bwd_group_planes)
 //   u8_flight=2|4|8    the u8 texel render with vertical reuse: rows in flight per work-item
 //                      (0 = automatic: 4 for launches under 2048 blocks)
 //   chunk_strip=0|1    the in-place render at CH = 8, one row: render_chunk_kernel's 64 x 1 wave rows
@@ -108,13 +110,14 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOptSweepStore, kOptBoxShrink,
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
-                kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kOptU8Flight, kNumOpts };
+                kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kOptU8Flight, kOptBwdGroup,
+                kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
                                          "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode",
-                                         "chunk_strip", "u8_flight"};
+                                         "chunk_strip", "u8_flight", "bwd_group"};
 #ifndef MPIV_CHUNK_STRIP
 #define MPIV_CHUNK_STRIP 1  // round 4: 0.506 vs 0.64 ms in place (profiles/r04j_strip*_ab.jsonl)
 #endif
@@ -122,8 +125,8 @@ const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_nat
 #define MPIV_U8_FLIGHT 0
 #endif
 const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP,
-                                    MPIV_U8_FLIGHT};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP, MPIV_U8_FLIGHT};
+                                    MPIV_U8_FLIGHT, 0};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP, MPIV_U8_FLIGHT, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -641,19 +644,30 @@ namespace {
 
 inline size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
 
-// Planes per fallback chunk: all of them up to 2^25 plane-pixels, else the fewest equal
-// chunks below that (the bucket arrays are then <= 1/4 of the d-sample array).
-int bwd_fallback_planes(int H, int W, int P) {
+// Planes per group (round 4): all of them up to 2^25 plane-pixels, else the fewest equal groups
+// below that, rounded up to whole 8-plane chunks.  A view's backward runs group by group, back
+// to front (chain -> gather -> check -> fallback per group, the running g handed down in
+// gbuf), so the workspace holds the d samples of one group (config 4: 32 of 128 planes, 0.54 GB
+// instead of 2.15) and the fallback's bucket arrays are sized for one group too.
+int bwd_group_planes(int H, int W, int P) {
     const int64_t n = (int64_t)P * H * W, cap = (int64_t)1 << 25;
+    if (H < 2 || W < 2) return P;  // degenerate frames take the generic recipe, one group
+    if (opt(kOptBwdGroup) > 0) return std::min(P, (opt(kOptBwdGroup) + kBwdCH - 1) / kBwdCH * kBwdCH);
     if (n <= cap) return P;
-    const int64_t chunks = (n + cap - 1) / cap;
-    return (int)(((int64_t)P + chunks - 1) / chunks);
+    const int64_t groups = (n + cap - 1) / cap;
+    const int gp = (int)(((int64_t)P + groups - 1) / groups);
+    return std::min(P, (gp + kBwdCH - 1) / kBwdCH * kBwdCH);
 }
 
 // workspace carve-up for one view; returns the total size in bytes
-size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
+// (the counters and flags first: _lib.bwd_flag_offset mirrors their offsets; gbuf: the running
+// over-composite adjoint g handed from one plane group to the next, also the frame scratch of the
+// forward that fills ckpt when the caller has no checkpoints and the view has several groups)
+// dsp: planes whose d samples are resident (P: one group; bwd_group_planes: the smallest); the
+// fallback's bucket arrays always take one group of bwd_group_planes (its plane chunk)
+size_t bwd_layout(int H, int W, int P, int dsp, char* base, BwdWs* ws, float4** gbuf = nullptr) {
     const size_t hw = (size_t)H * W;
-    const int pc = bwd_fallback_planes(H, W, P);
+    const int pc = bwd_group_planes(H, W, P);
     const size_t nk = (size_t)pc * (H + 1) * (W + 1);
     const size_t nb = (nk + kScanTile - 1) / kScanTile;
     const size_t nchunk = (size_t)(P + kBwdCH - 1) / kBwdCH;
@@ -663,12 +677,14 @@ size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
         off += align256(bytes);
         return p;
     };
-    char* ds = take((size_t)P * hw * 16);
-    char* ckpt = take(nchunk * hw * 16);
-    char* inv = take((size_t)P * 12 * 4);
     char* truth = take(kCtrSlots * 8);
     char* found = take(kCtrSlots * 8);
     char* flag = take(32);
+    char* ds = take((size_t)dsp * hw * 16);
+    char* ckpt = take(nchunk * hw * 16);
+    char* inv = take((size_t)P * 12 * 4);
+    char* gb = take(dsp < P ? hw * 16 : 0);
+    if (gbuf) *gbuf = reinterpret_cast<float4*>(gb);
     const size_t ntiles = (size_t)((W + kGTW - 1) / kGTW) * ((H + kGTY - 1) / kGTY);
     char* box = take((size_t)P * ntiles * 16);
     char* key = take((size_t)pc * hw * 4);
@@ -699,9 +715,17 @@ size_t bwd_layout(int H, int W, int P, char* base, BwdWs* ws) {
 
 }  // namespace
 
+// one plane group (every plane's d samples resident: the fastest schedule), unless the
+// bwd_group test hook asks for groups
 size_t mpiv_render_backward_workspace_size(int H, int W, int P) {
     if (H <= 0 || W <= 0 || P <= 0) return 0;
-    return bwd_layout(H, W, P, nullptr, nullptr);
+    return bwd_layout(H, W, P, opt(kOptBwdGroup) > 0 ? bwd_group_planes(H, W, P) : P, nullptr, nullptr);
+}
+
+// the smallest workspace: plane groups of bwd_group_planes (config 4: 1.3 GB instead of 3.0)
+size_t mpiv_render_backward_workspace_size_min(int H, int W, int P) {
+    if (H <= 0 || W <= 0 || P <= 0) return 0;
+    return bwd_layout(H, W, P, bwd_group_planes(H, W, P), nullptr, nullptr);
 }
 
 int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, int W, int P, const float* homs,
@@ -729,8 +753,14 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     // pixel ids, bucket ids and order keys are 32-bit
     if ((int64_t)H * W >= ((int64_t)1 << 26) || (int64_t)P * H * W >= ((int64_t)1 << 31))
         return fail(MPIV_ERR_ARG, "%s: MPI too large for one backward launch", nm);
+    // plane groups: one (every plane's d samples resident) when the workspace holds it, else
+    // groups of bwd_group_planes (mpiv_render_backward_workspace_size / _size_min)
+    const int GP = (opt(kOptBwdGroup) > 0 || ws_bytes < bwd_layout(H, W, P, P, nullptr, nullptr))
+                       ? bwd_group_planes(H, W, P) : P;
+    const int G = (P + GP - 1) / GP;
     BwdWs ws;
-    const size_t need = bwd_layout(H, W, P, static_cast<char*>(workspace), &ws);
+    float4* gbuf = nullptr;
+    const size_t need = bwd_layout(H, W, P, GP, static_cast<char*>(workspace), &ws, &gbuf);
     if (ws_bytes < need) return fail(MPIV_ERR_ARG, "%s: workspace too small (%zu < %zu bytes)", nm, ws_bytes, need);
     const RenderGeom g = make_geom(H, W, P);
     const ChunkGeom cg{(int)(st[1] / 4), (int)(st[2] / 4), (int)rec};
@@ -778,6 +808,39 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         float4* gv = reinterpret_cast<float4*>(dmpi) + (int64_t)v * HW * P;
         const float4* ck = ckpt ? reinterpret_cast<const float4*>(ckpt) + (int64_t)v * ((P + kBwdCH - 1) / kBwdCH) * HW
                                 : nullptr;
+        if (G > 1) {  // several plane groups, back to front (fast recipe: H, W >= 2 here, P * H * W > 2^25)
+            const float4* ckv = ck;
+            if (!ckv) {  // the checkpoints from a forward pass into the workspace (frame into gbuf, unused)
+                const unsigned fb = blocks(W, kStripTX) * blocks(H, 16);
+                const size_t flds = (size_t)chunk_slot_floats<8, 1>() * 4 + (h_lds ? (size_t)P * 36 : 0);
+                render_chunk_strip_kernel<16, 2><<<fb, 256, flds, q>>>(mv, 0, g, cg, 1, hv, reinterpret_cast<float*>(gbuf),
+                                                                      ws.ckpt, h_lds);
+                ckv = ws.ckpt;
+            }
+            if (!force) {
+                bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
+                bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x,
+                                                                               margin, ws.box);
+            }
+            for (int grp = G - 1; grp >= 0; --grp) {
+                const int p_lo = grp * GP, p_hi = std::min(P, p_lo + GP);
+                BwdWs wg = ws;
+                wg.ds = ws.ds - (int64_t)p_lo * HW;  // the group's d samples: planes p_lo .. p_hi-1 of the window
+                bwd_chain_strip_kernel<8><<<blocks(W, kStripTX) * blocks(H, 8), 256, chain_lds, q>>>(
+                    mv, g, cg, hv, dv, ckv, wg, h_lds, p_lo / kBwdCH, (p_hi + kBwdCH - 1) / kBwdCH, gbuf);
+                if (!force)
+                    bwd_gather_kernel<<<(unsigned)(ntiles * blocks(p_hi - p_lo, kGPl)), kGThreads, 0, q>>>(
+                        g, hv, wg, gv, margin, p_lo, p_hi - p_lo);
+                bwd_check_kernel<<<1, kWave, 0, q>>>(wg, force, grp != G - 1);
+                if (fast)
+                    bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, wg, gv, poll_limit, fb_mode == 2, p_lo, p_hi);
+                else
+                    bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, wg, gv, poll_limit, fb_mode == 2, p_lo,
+                                                                         p_hi);
+            }
+            bwd_poison_kernel<<<256, 256, 0, q>>>(ws.flag, gv, (int64_t)P * HW);
+            continue;
+        }
         const int R = fast ? chunk_rows() : 1;
         const unsigned cb = blocks(W, kTileX) * blocks(H, kTileY * R);
 #define MPIV_CHAIN(CKB, RR)                                                                                  \
@@ -793,11 +856,13 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
 #if MPIV_AB
         else if (ck && opt(kOptChunkStrip) == 4)  // A/B: 8 x 16 strips (2.41 vs 2.38 ms, r04j_strips_ab.jsonl)
             bwd_chain_strip_kernel<16><<<blocks(W, kStripTX) * blocks(H, 16), 256, chain_lds, q>>>(mv, g, cg, hv, dv, ck,
-                                                                                                ws, h_lds);
+                                                                                                ws, h_lds, 0, (P + 7) / 8,
+                                                                                                gbuf);
 #endif
         else if (ck && opt(kOptChunkStrip))  // 8 x 8 strips, vertical tap reuse
             bwd_chain_strip_kernel<8><<<blocks(W, kStripTX) * blocks(H, 8), 256, chain_lds, q>>>(mv, g, cg, hv, dv, ck,
-                                                                                              ws, h_lds);
+                                                                                              ws, h_lds, 0, (P + 7) / 8,
+                                                                                              gbuf);
         else if (ck) MPIV_CHAIN(true, 1);
         else MPIV_CHAIN(false, 1);
 #undef MPIV_CHAIN
@@ -818,10 +883,10 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                     bwd_gather_dma_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
                 else
 #endif
-                    bwd_gather_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
+                    bwd_gather_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin, 0, P);
             }
         }
-        bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force);
+        bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force, 0);
         // fallback: one launch, returns at once unless flagged; its phases are ordered by tickets
         // (render_bwd.hip), so it completes however many of its blocks are resident
 #if MPIV_AB  // round 3's grid-barrier schedule (render_bwd.hip)
@@ -832,9 +897,9 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         else
 #endif
         if (fast)
-            bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, fb_mode == 2);
+            bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, fb_mode == 2, 0, P);
         else
-            bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, fb_mode == 2);
+            bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, fb_mode == 2, 0, P);
         // an aborted fallback (never expected) leaves a NaN gradient, never a plausible one
         bwd_poison_kernel<<<256, 256, 0, q>>>(ws.flag, gv, (int64_t)P * HW);
     }
@@ -845,8 +910,8 @@ int mpiv_render_backward_status(const void* workspace, int H, int W, int P, int*
     const char* nm = "mpiv_render_backward_status";
     if (!workspace || !aborted_views) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
     if (H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
-    BwdWs ws;
-    bwd_layout(H, W, P, static_cast<char*>(const_cast<void*>(workspace)), &ws);
+    BwdWs ws;  // (the flag words sit at the same offset for every group size)
+    bwd_layout(H, W, P, P, static_cast<char*>(const_cast<void*>(workspace)), &ws);
     hipStream_t q = S(stream);
     if (hipMemcpyAsync(aborted_views, ws.flag + 4, sizeof(int), hipMemcpyDeviceToHost, q) != hipSuccess ||
         hipStreamSynchronize(q) != hipSuccess)

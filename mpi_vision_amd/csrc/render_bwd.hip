@@ -368,12 +368,15 @@ __global__ __launch_bounds__(256, R == 1 ? 1 : 4) void bwd_chain_kernel(const fl
 // composite phases run with lane = pixel (column lane % 8, row lane / 8).  Same samples,
 // same adjoint arithmetic, same pair count (every in-image tap of every sample, gathered or
 // shared): the d samples are bit-identical to bwd_chain_wave<MODE, true, 1>'s.
+// Chunks [c_lo, c_hi) only (a plane group, mpiv_render_backward: groups back to front so the
+// d samples of one group at a time fit the workspace): g starts from dout for the top group
+// (c_hi == n) and from gbuf otherwise, and leaves in gbuf for the group below (c_lo > 0).
 template <int MODE, int SR>
 __device__ __forceinline__ void bwd_chain_wave_strip(const float* __restrict__ view, const RenderGeom& g,
                                                      const ChunkGeom& cg, const float* __restrict__ hs,
                                                      f32x4* __restrict__ slot, int sx0, int sy0, int lane,
                                                      const float* __restrict__ dout, const float4* __restrict__ ck,
-                                                     const BwdWs& ws) {
+                                                     const BwdWs& ws, int c_lo, int c_hi, float4* __restrict__ gbuf) {
     constexpr int CH = kBwdCH, NH = SR / 8;
     static_assert(SR % 8 == 0, "strip rows");
     const int j = lane % CH, i = lane / CH;
@@ -437,22 +440,28 @@ __device__ __forceinline__ void bwd_chain_wave_strip(const float* __restrict__ v
     for (int hh = 0; hh < NH; ++hh) {
         in[hh] = x < g.W && y + 8 * hh < g.H;
         g0[hh] = g1[hh] = g2[hh] = 0.0f;
-        if (in[hh]) {
+        if (in[hh] && c_hi == n) {
             const float* d = dout + (pix + hh * hstep) * 3;
             g0[hh] = d[0];
             g1[hh] = d[1];
             g2[hh] = d[2];
+        } else if (in[hh]) {  // the group above left g here
+            const float4 gv = gbuf[pix + hh * hstep];
+            g0[hh] = gv.x;
+            g1[hh] = gv.y;
+            g2[hh] = gv.z;
         }
     }
-    load_h(n - 1, h);
-    issue(n - 1, 0, h, 0, false, A, true);
+    load_h(c_hi - 1, h);
+    issue(c_hi - 1, 0, h, 0, false, A, true);
     // over_composite backward (utils.py:149-156 under autograd), chunks back to front
-    for (int c = n - 1; c >= 0; --c) {
+    for (int c = c_hi - 1; c >= c_lo; --c) {
 #pragma unroll
         for (int hh = 0; hh < NH; ++hh) {
             float4 pre = make_float4(-0.0f, -0.0f, -0.0f, 0.0f);
             if (c > 0 && in[hh]) pre = ck[(int64_t)c * HW + pix + hh * hstep];
-            sample_half(c, hh, c > 0 ? c - 1 : 0, c > 0);
+            // the row issued ahead for chunk c-1 belongs to this group (counted) only above c_lo
+            sample_half(c, hh, c > c_lo ? c - 1 : c_lo, c > c_lo);
             float pr[CH][3];  // prefixes out_{p-1} of the chunk's planes, in the forward's order
             pr[0][0] = pre.x;
             pr[0][1] = pre.y;
@@ -500,6 +509,11 @@ __device__ __forceinline__ void bwd_chain_wave_strip(const float* __restrict__ v
             if (NH > 1) asm volatile("" : "+v"(g0[hh]), "+v"(g1[hh]), "+v"(g2[hh])::"memory");  // pinned here
         }
     }
+    if (c_lo > 0) {
+#pragma unroll
+        for (int hh = 0; hh < NH; ++hh)
+            if (in[hh]) gbuf[pix + hh * hstep] = make_float4(g0[hh], g1[hh], g2[hh], 0.0f);
+    }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) ntap += __shfl_xor(ntap, off);
     if (lane == 0 && ntap) atomicAdd(&ws.truth[blockIdx.x % kCtrSlots], (unsigned long long)ntap);
@@ -511,7 +525,8 @@ template <int SR>
 __global__ __launch_bounds__(256, 1) void bwd_chain_strip_kernel(const float* __restrict__ view, RenderGeom g,
                                                                  ChunkGeom cg, const float* __restrict__ homs,
                                                                  const float* __restrict__ dout,
-                                                                 const float4* __restrict__ ck, BwdWs ws, int h_lds) {
+                                                                 const float4* __restrict__ ck, BwdWs ws, int h_lds,
+                                                                 int c_lo, int c_hi, float4* __restrict__ gbuf) {
     extern __shared__ float4 bwd_lds[];
     f32x4* slots = reinterpret_cast<f32x4*>(bwd_lds);
     float* hl = reinterpret_cast<float*>(bwd_lds) + 4 * kWave * (kBwdCH + 1) * 4;
@@ -526,16 +541,18 @@ __global__ __launch_bounds__(256, 1) void bwd_chain_strip_kernel(const float* __
     {
         const float x0 = (float)tx0, x1 = (float)min(tx0 + kStripTX - 1, g.W - 1);
         const float y0 = (float)ty0, y1 = (float)min(ty0 + SR - 1, g.H - 1);
-        for (int p = (int)threadIdx.x; p < g.P; p += 256) ok = ok && div2_rect_safe(homs + (int64_t)p * 9, x0, x1, y0, y1);
+        const int p_end = min(g.P, c_hi * kBwdCH);  // the group's planes (the rows issued past it are unused)
+        for (int p = c_lo * kBwdCH + (int)threadIdx.x; p < p_end; p += 256)
+            ok = ok && div2_rect_safe(homs + (int64_t)p * 9, x0, x1, y0, y1);
     }
     const bool proven = __syncthreads_and(ok);  // also publishes hs
     const int sx0 = tx0 + wave * 8;
     if (sx0 >= g.W) return;  // whole wave; no barrier follows
     f32x4* slot = slots + wave * kWave * (kBwdCH + 1);
     if (proven)
-        bwd_chain_wave_strip<2, SR>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws);
+        bwd_chain_wave_strip<2, SR>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws, c_lo, c_hi, gbuf);
     else
-        bwd_chain_wave_strip<1, SR>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws);
+        bwd_chain_wave_strip<1, SR>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws, c_lo, c_hi, gbuf);
 }
 
 // ---- 2. gather: per-texel sums in the reference's order ------------------------------
@@ -914,8 +931,9 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
 // of pixel q to texel t: weight(corner) * d s_q, added in key order from +0.  Per plane and
 // pass: one staging pass (gather_stage_pass) by all 4 waves, a barrier, one texel pass
 // (gather_texel_pass).  A texel's kGPl planes leave as one 16*kGPl-B run.
+// Planes [p_lo, p_lo + np) (a plane group of mpiv_render_backward; p_lo a multiple of kGPl).
 __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
-                                                         float4* __restrict__ dmpi, float margin) {
+                                                         float4* __restrict__ dmpi, float margin, int p_lo, int np) {
     __shared__ int s_code[kGCap];                    // local nw-tap bucket of the staged pixel, -1 = none
     __shared__ float s_w[(MPIV_GFRAC ? 2 : 4) * kGWP];  // its bilinear weights, corner-major (kGWP), or
                                                         // (MPIV_GFRAC) its fractions; [kGCap] = 0
@@ -926,8 +944,8 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     const int tiles_x = (g.W + kGTW - 1) / kGTW;
     const int ntiles = tiles_x * ((g.H + kGTY - 1) / kGTY);
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
-    const int ngroups = (g.P + kGPl - 1) / kGPl;  // plane groups fastest: the blocks writing one texel's
-    const int tile = lb / ngroups, p0 = (lb % ngroups) * kGPl;  // gradient line run together
+    const int ngroups = (np + kGPl - 1) / kGPl;  // plane groups fastest: the blocks writing one texel's
+    const int tile = lb / ngroups, p0 = p_lo + (lb % ngroups) * kGPl;  // gradient line run together
     const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTY;
     const int tx = tx0 + (threadIdx.x & (kWave - 1));
     int ty[kGTR], bt[kGTR];  // this thread's texel rows (kGTR independent texel sums per pass)
@@ -1608,7 +1626,8 @@ __global__ __launch_bounds__(256, MPIV_GLBW) void bwd_gather_wave_kernel(RenderG
 #endif  // MPIV_AB
 
 // ---- 3. check: found == truth, else the fallback runs; counters reset for the next view
-__global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force) {
+// keep_abort: a later plane group of the same view (flag[3] stays set once any group aborted)
+__global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force, int keep_abort) {
     const int l = threadIdx.x;
     unsigned long long t = ws.truth[l], f = ws.found[l];
 #pragma unroll
@@ -1622,7 +1641,7 @@ __global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force) {
         ws.flag[0] = (force || t != f) ? 1 : 0;
         ws.flag[1] = 0;  // the fallback's ticket and completion counters, abort flag
         ws.flag[2] = 0;
-        ws.flag[3] = 0;
+        if (!keep_abort) ws.flag[3] = 0;
     }
 }
 
@@ -1982,7 +2001,8 @@ __device__ __forceinline__ void fallback_done(unsigned* done) {
 // bucket sizes; 1 + kFbPhases * c + k: step k for plane chunk c)
 template <bool FAST>
 __device__ void bwd_fallback_item(const RenderGeom& g, const float* __restrict__ homs, const BwdWs& ws,
-                                  float4* __restrict__ dmpi, int ph, int bid, int nblk, int* s_tmp) {
+                                  float4* __restrict__ dmpi, int ph, int bid, int nblk, int* s_tmp, int p_lo,
+                                  int p_hi) {
     const int tid = threadIdx.x;
     const int64_t gtid = (int64_t)bid * 256 + tid, gstride = (int64_t)nblk * 256;
     const int64_t HW = (int64_t)g.H * g.W;
@@ -1992,9 +2012,9 @@ __device__ void bwd_fallback_item(const RenderGeom& g, const float* __restrict__
         for (int64_t i = gtid; i < (int64_t)ws.pc * K; i += gstride) ws.count[i] = 0;
         return;
     }
-    const int pc0 = (ph - 1) / kFbPhases * ws.pc;
+    const int pc0 = p_lo + (ph - 1) / kFbPhases * ws.pc;
     const int step = (ph - 1) % kFbPhases;
-    const int pcn = min(ws.pc, g.P - pc0);
+    const int pcn = min(ws.pc, p_hi - pc0);
     const int64_t nq = pcn * HW, nk = pcn * K;
     const int nb = (int)((nk + kScanTile - 1) / kScanTile);
     switch (step) {
@@ -2189,15 +2209,16 @@ __device__ void bwd_fallback_item(const RenderGeom& g, const float* __restrict__
 template <bool FAST>
 // fixed != 0 (A/B diagnosis): block b takes items b, b + nblk, ... in order instead of tickets
 // (the grid-barrier schedule: needs every block resident)
+// planes [p_lo, p_hi) (a plane group of mpiv_render_backward, or all of them)
 __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const float* __restrict__ homs,
                                                                   BwdWs ws, float4* __restrict__ dmpi,
-                                                                  unsigned poll_limit, int fixed) {
+                                                                  unsigned poll_limit, int fixed, int p_lo, int p_hi) {
     __shared__ int s_tmp[kScanBlock];
     __shared__ int s_ticket;
     if (ws.flag[0] == 0) return;  // uniform over the grid: the tile gather was complete
     const int nblk = gridDim.x, tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: wave-uniform branches only
-    const int nchunk = (g.P + ws.pc - 1) / ws.pc;
+    const int nchunk = (p_hi - p_lo + ws.pc - 1) / ws.pc;
     const unsigned total = (unsigned)(1 + kFbPhases * nchunk) * (unsigned)nblk;
     unsigned* ticket = reinterpret_cast<unsigned*>(ws.flag + 1);
     unsigned* done = reinterpret_cast<unsigned*>(ws.flag + 2);
@@ -2212,7 +2233,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
         const int t = __builtin_amdgcn_readfirstlane(s_ticket);
         __syncthreads();  // s_ticket is rewritten by the next iteration
         if (t < 0) return;
-        bwd_fallback_item<FAST>(g, homs, ws, dmpi, t / nblk, t % nblk, nblk, s_tmp);
+        bwd_fallback_item<FAST>(g, homs, ws, dmpi, t / nblk, t % nblk, nblk, s_tmp, p_lo, p_hi);
         fallback_done(done);
     }
 }

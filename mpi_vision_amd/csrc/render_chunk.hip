@@ -448,10 +448,12 @@ __global__ __launch_bounds__(256, 3) void render_chunk_strip_kernel(const float*
                                                                     RenderGeom g, ChunkGeom cg, int V,
                                                                     const float* __restrict__ homs,
                                                                     float* __restrict__ out,
-                                                                    float4* __restrict__ ckpt) {
+                                                                    float4* __restrict__ ckpt, int h_lds = 1) {
     extern __shared__ float4 chunk_lds[];
     f32x4* slots = reinterpret_cast<f32x4*>(chunk_lds);
-    float* hs = reinterpret_cast<float*>(chunk_lds) + chunk_slot_floats<8, 1>();
+    // the view's homographies in LDS beside the slots, or (h_lds == 0: more planes than fit, the
+    // backward's checkpoint pass) read from global memory through the caches
+    float* hl = reinterpret_cast<float*>(chunk_lds) + chunk_slot_floats<8, 1>();
     const int tiles_x = (g.W + kStripTX - 1) / kStripTX;
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
     const int v = lb % V;
@@ -459,7 +461,9 @@ __global__ __launch_bounds__(256, 3) void render_chunk_strip_kernel(const float*
     const int tx0 = (tile % tiles_x) * kStripTX, ty0 = (tile / tiles_x) * SR;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     const float* hv = homs + (int64_t)v * g.P * 9;
-    for (int k = threadIdx.x; k < g.P * 9; k += 256) hs[k] = hv[k];
+    if (h_lds)
+        for (int k = threadIdx.x; k < g.P * 9; k += 256) hl[k] = hv[k];
+    const float* hs = h_lds ? hl : hv;
     const float x0 = (float)tx0, x1 = (float)min(tx0 + kStripTX - 1, g.W - 1);
     const float y0 = (float)ty0, y1 = (float)min(ty0 + SR - 1, g.H - 1);
     bool ok = true;

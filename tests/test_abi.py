@@ -96,7 +96,8 @@ def test_ab_kernels_live_in_the_ab_library():
         assert b"libmpiv_ab.so" in L.mpiv_last_error()
     for name, val in (("render_tile", -1), ("render_vshare", 11), ("render_chunk", 4), ("chunk_rows", 1),
                       ("bwd_fallback", 1), ("box_shrink", 2), ("sweep_direct", 1), ("bwd_gather", 0),
-                      ("chunk_strip", 0), ("chunk_strip", 1), ("u8_flight", 2), ("u8_flight", 4)):  # production kernels / test hooks
+                      ("chunk_strip", 0), ("chunk_strip", 1), ("u8_flight", 2), ("u8_flight", 4),
+                      ("bwd_group", 8)):  # production kernels / test hooks
         assert L.mpiv_debug_set(name.encode(), val) == 0, name
     L.mpiv_debug_set(b"reset", 0)
     p = ctypes.c_void_p(256)
@@ -159,3 +160,22 @@ def test_host_asan_builds():
                        text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "abi_check: 0 failure(s)" in r.stdout and "oracle_check: ok" in r.stdout
+
+
+def test_backward_workspace_plane_groups():
+    """mpiv_render_backward's smallest workspace holds one plane group's d samples (round 4):
+    config 4 (1024x1024x128, 4 groups of 32 planes) fits in 1.5 GB, the one-group (fastest)
+    size holds every plane's; a view under 2^25 plane-pixels is one group either way; the
+    bwd_group test hook shrinks the groups (and the workspace) on demand."""
+    L = _lib.load_main()
+    full = L.mpiv_render_backward_workspace_size(1024, 1024, 128)
+    small = L.mpiv_render_backward_workspace_size_min(1024, 1024, 128)
+    assert 1.0e9 < small <= 1.5e9 < 1024 * 1024 * 128 * 16 < full, (small, full)
+    one = L.mpiv_render_backward_workspace_size(64, 96, 12)
+    assert one == L.mpiv_render_backward_workspace_size_min(64, 96, 12) > 64 * 96 * 12 * 16
+    assert L.mpiv_debug_set(b"bwd_group", 8) == 0
+    try:
+        grouped = L.mpiv_render_backward_workspace_size(64, 96, 12)
+    finally:
+        L.mpiv_debug_set(b"reset", 0)
+    assert grouped < one
