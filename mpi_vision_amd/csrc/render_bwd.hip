@@ -55,6 +55,9 @@ __device__ __forceinline__ void bwd_store(float4* p, const float4& v) {
         *p = v;
 }
 
+#ifndef MPIV_BWD_NTOUT
+#define MPIV_BWD_NTOUT 0  // A/B: non-temporal stores of the gather's d MPI only
+#endif
 #ifndef MPIV_GFRAC
 #define MPIV_GFRAC 0  // A/B: the gather stages fractions (2 floats) instead of the 4 corner weights
 #endif
@@ -1090,7 +1093,11 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
 #pragma unroll
             for (int jj = 0; jj < kGPl; ++jj)
                 if (p0 + jj < g.P)
-                    bwd_store(o + jj, make_float4(acc[r][jj][0], acc[r][jj][1], acc[r][jj][2], acc[r][jj][3]));
+                    if (MPIV_BWD_NTOUT)  // A/B: d MPI past the caches (written once, never re-read here)
+                        __builtin_nontemporal_store(f32x4{acc[r][jj][0], acc[r][jj][1], acc[r][jj][2], acc[r][jj][3]},
+                                                    reinterpret_cast<f32x4*>(o + jj));
+                    else
+                        bwd_store(o + jj, make_float4(acc[r][jj][0], acc[r][jj][1], acc[r][jj][2], acc[r][jj][3]));
         }
     }
 }

@@ -42,10 +42,20 @@ def main():
                 b.record()
             torch.cuda.synchronize()
             ms = sorted(a.elapsed_time(b) for a, b in ev)
+            ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+            for a, b in ev2:  # without checkpoints (the backward recomputes them)
+                a.record()
+                _lib.render_backward(mpi, homs, dout, workspace=ws)
+                b.record()
+            torch.cuda.synchronize()
+            ms2 = sorted(a.elapsed_time(b) for a, b in ev2)
+            nock_same = bool(torch.equal(_lib.render_backward(mpi, homs, dout, workspace=ws).view(torch.int32),
+                                         out.view(torch.int32)))
             _lib.reset_debug()
             sha = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]
             print(json.dumps({"rep": rep, "bwd_gather": v, "median_ms": round(ms[len(ms) // 2], 4),
                               "min_ms": round(ms[0], 4), "bit_identical_in_process": same, "grad_sha16": sha,
+                              "no_ckpt_median_ms": round(ms2[len(ms2) // 2], 4), "no_ckpt_bit_identical": nock_same,
                               "fallback_flag": flag}), flush=True)
 
 
