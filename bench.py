@@ -883,8 +883,9 @@ def main():
     u8 = None
     if "u8" in legs:
         u8 = guarded(u8_leg, dev, stream, V, host_homs(0, 1).to(dev), host_homs(0).to(dev))
-    train = training_leg(dev, stream) if "train" in legs else None
-    c5 = config5_leg(world, rank, dev, max(3, args.steps // 2), 1) if "c5" in legs else None
+    train = guarded(training_leg, dev, stream) if "train" in legs else None
+    # (a Python-level failure is the same on every rank, so every rank records it and goes on)
+    c5 = guarded(config5_leg, world, rank, dev, max(3, args.steps // 2), 1) if "c5" in legs else None
     ranks = {"world_size_seen": world, "backend": backend, "per_rank_kernel_ms": [round(x, 4) for x in kern_all]}
     if world > 1:
         import torch.distributed as dist
