@@ -45,11 +45,14 @@ _KINV_CACHE: dict = {}
 
 
 def _inverse_cached(K: torch.Tensor) -> torch.Tensor:
-    """torch.inverse(K) for contiguous fp32 CPU K [B,3,3], memoised on K's exact bits
-    (intrinsics rarely change along a camera path; LAPACK is ~10 us of the host path).
-    Every batch element is inverted on its own, so the result equals the reference's
-    inverse of its [P,B,3,3] repeat element for element (tests/test_host.py)."""
-    key = K.numpy().tobytes()
+    """torch.inverse(K) for fp32 CPU K [B,3,3] AS LAID OUT (contiguous [B,3,3] result),
+    memoised on K's exact bits and its size / strides (intrinsics rarely change along a camera
+    path; LAPACK is ~10 us of the host path).  The layout is part of the key because torch's
+    CPU inverse returns different bits for the same values in a different layout (a stride-0
+    batch, F-ordered or sliced blocks: tests/test_kstride.py).  A contiguous batch is inverted
+    element by element, so the result equals the reference's inverse of its [P,B,3,3] repeat
+    element for element (tests/test_host.py)."""
+    key = (tuple(K.shape), tuple(K.stride()), K.contiguous().numpy().tobytes())
     kinv = _KINV_CACHE.get(key)
     if kinv is None:
         if len(_KINV_CACHE) >= 256:
@@ -59,15 +62,52 @@ def _inverse_cached(K: torch.Tensor) -> torch.Tensor:
     return kinv
 
 
+def cpu32_like(x: torch.Tensor) -> torch.Tensor:
+    """fp32 CPU tensor with x's values AND x's size and strides (stride-0 broadcasts, F-ordered
+    or sliced blocks kept).  `.cpu()` materialises a non-dense tensor, which would change what
+    torch.inverse returns; here the storage span x covers is copied once and re-viewed with x's
+    strides."""
+    x = x.detach()
+    if x.device.type == "cpu" and x.dtype == _F32:
+        return x
+    if x.numel() == 0:
+        return torch.empty(x.shape, dtype=_F32)
+    span = 1 + sum((n - 1) * st for n, st in zip(x.shape, x.stride()))
+    flat = torch.as_strided(x, (span,), (1,), x.storage_offset()).to(device=_CPU, dtype=_F32)
+    return torch.as_strided(flat, x.shape, x.stride())
+
+
+def psv_inverse(K: torch.Tensor, batch: int) -> torch.Tensor:
+    """Ki = inverse(K_tgt) [batch, 3, 3] (contiguous) as pixel2cam_torch computes it:
+    `torch.inverse(intrinsics)` on the CALLER's tensor (utils.py:370, from :428 / :747), so on
+    a CPU copy with the caller's strides (cpu32_like), not a materialised one -- a shared camera
+    passed as K[None].expand(B,3,3) inverts to other bits than its .contiguous() copy, and the
+    PSV moves by up to ~6e-5 with it (tests/golden/kstride.npz, tools/gen_goldens_kstride.py).
+    The unbatched _one / _one2 calls pass intrinsics.unsqueeze(0) (utils.py:530, :795), which this
+    receives as [1,3,3].  A single camera for a larger batch ([3,3] or [1,3,3], which the
+    reference's torch.cat rejects, utils.py:433) is inverted once as given and broadcast."""
+    Kc = cpu32_like(K)
+    if Kc.dim() == 2:
+        Kc = Kc.unsqueeze(0)
+    kinv = _inverse_cached(Kc)
+    if kinv.shape[0] != batch:
+        kinv = kinv.expand(batch, 3, 3).contiguous()
+    return kinv
+
+
 _KINV_DEV: dict = {}
 
 
-def _kinv_device(intrinsics: torch.Tensor, batch: int, dev, sid=None) -> torch.Tensor:
+def _kinv_device(intrinsics: torch.Tensor, batch: int, dev, sid=None, psv: bool = False) -> torch.Tensor:
     """inverse(K) [batch,3,3] on `dev` for a device-resident intrinsics tensor, memoised on
     that tensor OBJECT and its version counter (an in-place update bumps it; a new tensor
     is a new object), so a camera path that reuses one intrinsics tensor reads it back to
     the host once.  On a miss: one device-to-host copy of K and LAPACK (torch.inverse, as
-    the reference), then the upload."""
+    the reference), then the upload.
+
+    psv=False (render): the reference inverts its materialised [P,B,3,3] repeat of K
+    (utils.py:225-228 -> :60), so K is inverted contiguous.  psv=True: the caller's own layout
+    (psv_inverse, utils.py:370)."""
     try:
         ver = intrinsics._version
     except RuntimeError:  # inference tensors track no version: no memo
@@ -75,16 +115,19 @@ def _kinv_device(intrinsics: torch.Tensor, batch: int, dev, sid=None) -> torch.T
     # the stream is part of the key: the copy's memory, once evicted, is reused in the order of
     # the stream that allocated it, so each stream reads only its own copy
     stream = torch.cuda.current_stream(dev).cuda_stream if sid is None else sid
-    ent = _KINV_DEV.get(id(intrinsics))
+    ent = _KINV_DEV.get((id(intrinsics), psv))
     if (ver is not None and ent is not None and ent[0]() is intrinsics and ent[1] == ver and ent[2] == batch
             and ent[3].device == dev and ent[4] == stream):
         return ent[3]
-    K = _cpu32(intrinsics).expand(batch, 3, 3).contiguous()
-    kinv = _inverse_cached(K).to(dev)
+    if psv:
+        kinv = psv_inverse(intrinsics, batch).to(dev)
+    else:
+        K = _cpu32(intrinsics).expand(batch, 3, 3).contiguous()
+        kinv = _inverse_cached(K).to(dev)
     if ver is not None:
         if len(_KINV_DEV) >= 64:
             _KINV_DEV.clear()
-        _KINV_DEV[id(intrinsics)] = (weakref.ref(intrinsics), ver, batch, kinv, stream)
+        _KINV_DEV[(id(intrinsics), psv)] = (weakref.ref(intrinsics), ver, batch, kinv, stream)
     return kinv
 
 
@@ -174,9 +217,10 @@ def psv_matrices(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pos
         proj = [[K_src, 0], [0, 0, 0, 1]] @ pose    [B, 16]
     computed on CPU in fp32 with the reference's ops (page-locked with pin=True, ready for
     an asynchronous upload)."""
-    Ks, Kt, pose = _cpu32_together(src_intrinsics, tgt_intrinsics, pose)
+    Ks, pose = _cpu32_together(src_intrinsics, pose)
     B = pose.shape[0]
-    ki = torch.inverse(Kt)
+    ki = psv_inverse(tgt_intrinsics, B)  # the caller's layout (utils.py:370)
+    Ks = Ks.expand(B, 3, 3)
     k4 = torch.cat([Ks, torch.zeros(B, 3, 1)], dim=2)
     k4 = torch.cat([k4, torch.tensor([[[0.0, 0.0, 0.0, 1.0]]]).repeat(B, 1, 1)], dim=1)
     proj = torch.matmul(k4, pose)
@@ -188,8 +232,8 @@ def psv_matrices(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pos
 
 def psv_ki_device(tgt_intrinsics: torch.Tensor, batch: int, dev, sid=None) -> torch.Tensor:
     """Ki = inverse(K_tgt) [batch, 3, 3] (contiguous: read as [batch, 9]) on dev, memoised per
-    intrinsics tensor (_kinv_device)."""
-    return _kinv_device(tgt_intrinsics, batch, dev, sid)
+    intrinsics tensor (_kinv_device), inverted in the caller's layout (psv_inverse)."""
+    return _kinv_device(tgt_intrinsics, batch, dev, sid, psv=True)
 
 
 def device_cameras(src_intrinsics: torch.Tensor, pose: torch.Tensor, batch: int):

@@ -6,6 +6,7 @@ without the built library these functions raise.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import ctypes
 import hashlib
@@ -590,6 +591,51 @@ def render_backward_status(workspace: torch.Tensor, H: int, W: int, P: int) -> i
     return n.value
 
 
+class _AbortMonitor:
+    """The default (check=None) render_backward's abort count, surfaced without a synchronisation
+    (ADVICE r4): after each call the workspace's abort word is copied, stream-ordered, into a small
+    page-locked buffer and an event is recorded; the next render_backward (or
+    render_backward_raise_pending) reads every copy whose event has completed and raises if a view
+    was NaN-filled.  So an aborted fallback (never expected: render_bwd.hip) fails the training
+    loop at the latest one step later instead of silently feeding NaN gradients to the optimiser."""
+
+    def __init__(self):
+        self.pending = collections.deque()
+        self.free = []
+
+    def raise_completed(self, wait: bool = False):
+        while self.pending and (wait or self.pending[0][0].query()):
+            ev, buf, nviews = self.pending.popleft()
+            ev.synchronize()
+            n = int(buf[0])
+            self.free.append(buf)
+            if n:
+                self.pending.clear()
+                raise RuntimeError(f"mpiv_render_backward: the bucket fallback aborted on {n} of {nviews} views of an "
+                                   "earlier backward (their gradients were NaN)")
+
+    def post(self, ws: torch.Tensor, H: int, W: int, P: int, nviews: int, dev):
+        off = bwd_flag_offset(H, W, P) + 16  # flag[4]: views aborted in the call
+        buf = self.free.pop() if self.free else torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        buf.copy_(ws[off:off + 4].view(torch.int32), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        self.pending.append((ev, buf, nviews))
+        if len(self.pending) > 64:  # a caller that never lets the stream drain: bound the ring
+            self.raise_completed(wait=True)
+
+
+_ABORTS: dict = {}
+
+
+def render_backward_raise_pending(dev=None) -> None:
+    """Wait for every earlier default render_backward on `dev` (all devices if None) and raise if
+    any of them NaN-filled a view (the check the next call would make)."""
+    for d, mon in list(_ABORTS.items()):
+        if dev is None or d == torch.device(dev):
+            mon.raise_completed(wait=True)
+
+
 def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.Tensor,
                     workspace: torch.Tensor | None = None, ckpt: torch.Tensor | None = None,
                     check: bool | None = None) -> torch.Tensor:
@@ -600,7 +646,9 @@ def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.T
     by autograd's expand backward, as in the reference).  Bit-exact to the reference's
     CPU autograd (render_bwd.hip).  ckpt: render_train()'s checkpoints of the same views
     (skips recomputing the forward composite).  check (default MPIV_BWD_CHECK): read the
-    fallback's abort count back and raise if any view aborted (costs a synchronisation)."""
+    fallback's abort count back and raise if any view aborted (costs a synchronisation); left at
+    None without MPIV_BWD_CHECK, the count is read back asynchronously and a later call raises
+    (_AbortMonitor); False: not watched at all."""
     dev = _dev(rgba_layers, dout)
     B, H, W, P, _ = rgba_layers.shape
     if tuple(dout.shape) != (B, H, W, 3):
@@ -620,12 +668,19 @@ def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.T
     if ckpt is not None and (tuple(ckpt.shape) != (B, (P + 7) // 8, H, W, 4) or not ckpt.is_contiguous()
                              or ckpt.device != dev or ckpt.dtype != torch.float32):
         raise RuntimeError(f"ckpt must be render_train()'s contiguous [{B},{(P + 7) // 8},{H},{W},4] tensor")
+    mon = _ABORTS.get(dev) if check is None else None
+    if check is None and mon is None:
+        mon = _ABORTS.setdefault(dev, _AbortMonitor())
+    if mon is not None:
+        mon.raise_completed()  # an earlier call's abort, read without waiting
     _call("mpiv_render_backward", src, _strides(src), B, H, W, P, h, dout, ckpt, grad, ws, ws.numel(), _stream(dev))
     if BWD_CHECK if check is None else check:
         n = render_backward_status(ws, H, W, P)
         if n:
             raise RuntimeError(f"mpiv_render_backward: the bucket fallback aborted on {n} of {B} views "
                                "(their gradients are NaN)")
+    elif mon is not None:
+        mon.post(ws, H, W, P, B, dev)
     return grad
 
 

@@ -95,8 +95,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      forces their per-sample global fallback (tests)
 //   bwd_fallback=1     mpiv_render_backward skips the tile gather and runs its bucket
 //                      fallback for every view (tests)
-//   bwd_poll_limit=k   (A/B build) the backward fallback's waits give up after k polls instead of
-//                      2^24; -1: at the first wait -- tests provoke the abort path with it (NaN
+//   bwd_poll_limit=k   (A/B build) the backward fallback's waits also give up after k polls (the
+//                      production limit is 60 s of wall clock per wait); -1: at the first wait -- tests provoke the abort path with it (NaN
 //                      gradient, counted by mpiv_render_backward_status)
 //   bwd_fb_mode=1|2    (A/B build) the fallback's phases at grid barriers (round 3's schedule,
 //                      bwd_fallback_barrier_kernel) / the ticket kernel with a fixed item order (block b:
@@ -780,6 +780,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     // tickets; fewer resident ones still complete); queried once per device (relaxed atomics:
     // racing first calls store the same value)
     static int s_fb_blocks[64] = {};
+    static long long s_clock_khz[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(MPIV_ERR_HIP, "%s: hipGetDevice failed", nm);
     int fbb = __atomic_load_n(&s_fb_blocks[dev], __ATOMIC_RELAXED);
@@ -793,11 +794,19 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
             ncu <= 0 || pc_t <= 0 || pc_f <= 0)
             return fail(MPIV_ERR_HIP, "%s: device query failed", nm);
         fbb = ncu * std::min(std::min(pc_t, pc_f), 4);
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+            khz = 100000;  // gfx9's constant 100 MHz wall clock
+        __atomic_store_n(&s_clock_khz[dev], (long long)khz, __ATOMIC_RELAXED);
         __atomic_store_n(&s_fb_blocks[dev], fbb, __ATOMIC_RELAXED);
     }
     const unsigned fb_blocks = opt(kOptBwdFbBlocks) > 0 ? (unsigned)opt(kOptBwdFbBlocks) : (unsigned)fbb;
     const int pl = opt(kOptBwdPollLimit);
-    const unsigned poll_limit = pl > 0 ? (unsigned)pl : pl < 0 ? 0u : (1u << 24);
+    // production: no poll-count limit, a 60 s wall-clock limit per wait (a poll budget
+    // could expire on a slow but correct fallback); bwd_poll_limit=k (A/B, tests) adds a count limit
+    const unsigned poll_limit = pl > 0 ? (unsigned)pl : pl < 0 ? 0u : ~0u;
+    const unsigned long long tick_limit =
+        60000ull * (unsigned long long)__atomic_load_n(&s_clock_khz[dev], __ATOMIC_RELAXED);
     const int fb_mode = opt(kOptBwdFbMode);
     if (hipMemsetAsync(ws.truth, 0, 2 * kCtrSlots * 8 + 256, q) != hipSuccess)  // truth, found (adjacent)
         return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
@@ -825,7 +834,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
             for (int grp = G - 1; grp >= 0; --grp) {
                 const int p_lo = grp * GP, p_hi = std::min(P, p_lo + GP);
                 BwdWs wg = ws;
-                wg.ds = ws.ds - (int64_t)p_lo * HW;  // the group's d samples: planes p_lo .. p_hi-1 of the window
+                wg.ds_p0 = p_lo;  // the window holds the group's d samples: planes p_lo .. p_hi-1
                 bwd_chain_strip_kernel<8><<<blocks(W, kStripTX) * blocks(H, 8), 256, chain_lds, q>>>(
                     mv, g, cg, hv, dv, ckv, wg, h_lds, p_lo / kBwdCH, (p_hi + kBwdCH - 1) / kBwdCH, gbuf);
                 if (!force)
@@ -833,9 +842,10 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                         g, hv, wg, gv, margin, p_lo, p_hi - p_lo);
                 bwd_check_kernel<<<1, kWave, 0, q>>>(wg, force, grp != G - 1);
                 if (fast)
-                    bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, wg, gv, poll_limit, fb_mode == 2, p_lo, p_hi);
+                    bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, wg, gv, poll_limit, tick_limit, fb_mode == 2, p_lo,
+                                                                        p_hi);
                 else
-                    bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, wg, gv, poll_limit, fb_mode == 2, p_lo,
+                    bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, wg, gv, poll_limit, tick_limit, fb_mode == 2, p_lo,
                                                                          p_hi);
             }
             bwd_poison_kernel<<<256, 256, 0, q>>>(ws.flag, gv, (int64_t)P * HW);
@@ -899,17 +909,19 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force, 0);
         // fallback: one launch, returns at once unless flagged; its phases are ordered by tickets
         // (render_bwd.hip), so it completes however many of its blocks are resident
-#if MPIV_AB  // round 3's grid-barrier schedule (render_bwd.hip)
+#if MPIV_AB  // round 3's grid-barrier schedule (render_bwd.hip; it needs every block resident, so it
+            // keeps its poll-count limit)
+        const unsigned bar_polls = poll_limit == ~0u ? (1u << 24) : poll_limit;
         if (fb_mode == 1 && fast)
-            bwd_fallback_barrier_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit);
+            bwd_fallback_barrier_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, bar_polls);
         else if (fb_mode == 1)
-            bwd_fallback_barrier_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit);
+            bwd_fallback_barrier_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, bar_polls);
         else
 #endif
         if (fast)
-            bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, fb_mode == 2, 0, P);
+            bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, tick_limit, fb_mode == 2, 0, P);
         else
-            bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, fb_mode == 2, 0, P);
+            bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, tick_limit, fb_mode == 2, 0, P);
         // an aborted fallback (never expected) leaves a NaN gradient, never a plausible one
         bwd_poison_kernel<<<256, 256, 0, q>>>(ws.flag, gv, (int64_t)P * HW);
     }

@@ -102,6 +102,7 @@ constexpr int kGThreads = kGTW * kGTH;
                     // them: round 4 with two texel rows per wave, 2.51 vs 2.69 ms; r04_bwd_gather_ab.jsonl)
 #endif
 constexpr int kGPl = MPIV_GPL;     // gather: planes per block (a texel's kGPl planes are one 16*kGPl-B run)
+static_assert(kBwdCH % kGPl == 0, "plane groups start at multiples of kBwdCH: a gather block never straddles two");
 constexpr int kGCap = MPIV_GCAP;   // gather: output pixels staged per pass
 constexpr int kGMaxBox = 64 * kGCap;  // gather: larger boxes (extreme magnification) -> fallback
 constexpr int kCtrSlots = 64;      // the two pair counters are spread over 64 words each
@@ -113,7 +114,9 @@ constexpr int kScanTile = kScanItems * kScanBlock;
 constexpr int kSmallBucket = 32;   // fallback: larger buckets are sorted by a whole block
 
 struct BwdWs {
-    float4* ds;    // [P][HW]  d sample (d rgb, d a) per plane-pixel
+    float4* ds;    // [P][HW]  d sample (d rgb, d a) per plane-pixel; in plane groups only the group's
+                   //          planes ds_p0 .. ds_p0 + GP - 1 (index through ds_plane)
+    int ds_p0 = 0;
     float4* ckpt;  // [nchunk][HW] composited colour before chunk c (c >= 1)
     float* inv;    // [P][12]  texel -> output pixel inverse map (9 floats), [9] = valid
     int4* box;     // [P][tiles] gather pixel box (x0, x1, y0, y1); x0 = -2: the block cannot gather
@@ -132,6 +135,11 @@ struct BwdWs {
     int* bsum;     // scan block sums
     int* big;      // [0] = number of large buckets, [1..] their indices
 };
+
+// the d samples of plane p (an absolute plane number) in the workspace's window
+__device__ __forceinline__ float4* ds_plane(const BwdWs& ws, int p, int64_t HW) {
+    return ws.ds + (int64_t)(p - ws.ds_p0) * HW;
+}
 
 // ---- 1. chain: forward recompute + over-chain adjoint, in place ----------------------
 
@@ -312,7 +320,7 @@ __device__ __forceinline__ void bwd_chain_wave(const float* __restrict__ view, c
                         } else {
                             d = make_float4(g0[r], g1[r], g2[r], 0.0f);  // plane 0: output = rgb_0, alpha unused
                         }
-                        if (xin) bwd_store(ws.ds + (int64_t)p * HW + pix, d);
+                        if (xin) bwd_store(ds_plane(ws, p, HW) + pix, d);
                     }
                 }
             }
@@ -506,7 +514,7 @@ __device__ __forceinline__ void bwd_chain_wave_strip(const float* __restrict__ v
                     } else {
                         d = make_float4(g0[hh], g1[hh], g2[hh], 0.0f);  // plane 0: output = rgb_0, alpha unused
                     }
-                    if (in[hh]) bwd_store(ws.ds + (int64_t)p * HW + pix + hh * hstep, d);
+                    if (in[hh]) bwd_store(ds_plane(ws, p, HW) + pix + hh * hstep, d);
                 }
             }
             if (NH > 1) asm volatile("" : "+v"(g0[hh]), "+v"(g1[hh]), "+v"(g2[hh])::"memory");  // pinned here
@@ -724,7 +732,7 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
     // order keys hold (chunk - gbase) in 16 bits
     if (t == 0 && (int64_t)(rb - ra + 1) * g.W >= ((int64_t)1 << 19)) *ovf = 1;
     const float rbw = 1.0f / (float)bw;
-    const __amdgpu_buffer_rsrc_t rds = make_rsrc(ws.ds + (int64_t)p * HW, (int)(HW * 16));
+    const __amdgpu_buffer_rsrc_t rds = make_rsrc(ds_plane(ws, p, HW), (int)(HW * 16));
     f32x4 dsv[kGSI];
     if (DS && PRE) {
 #pragma unroll
@@ -949,6 +957,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
     const int ngroups = (np + kGPl - 1) / kGPl;  // plane groups fastest: the blocks writing one texel's
     const int tile = lb / ngroups, p0 = p_lo + (lb % ngroups) * kGPl;  // gradient line run together
+    const int p_end = p_lo + np;  // never past the group, whatever kGPl
     const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTY;
     const int tx = tx0 + (threadIdx.x & (kWave - 1));
     int ty[kGTR], bt[kGTR];  // this thread's texel rows (kGTR independent texel sums per pass)
@@ -977,7 +986,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
     int4 bxs[kGPl];
 #pragma unroll
     for (int jj = 0; jj < kGPl; ++jj) {
-        bxs[jj] = p0 + jj < g.P ? ws.box[(int64_t)(p0 + jj) * ntiles + tile] : make_int4(0, -1, 0, -1);
+        bxs[jj] = p0 + jj < p_end ? ws.box[(int64_t)(p0 + jj) * ntiles + tile] : make_int4(0, -1, 0, -1);
         if (bxs[jj].x == -2) {  // this block cannot gather the plane: the check sends the view to the fallback
             unsafe = true;
             bxs[jj] = make_int4(0, -1, 0, -1);
@@ -1007,7 +1016,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
         const int bw = b.y - b.x + 1;
         const int rb = min((b.w & ~kBoxProven) + 1, ra + kGCap / bw);
         const int np = (rb - ra) * bw;
-        const __amdgpu_buffer_rsrc_t rds = make_rsrc(ws.ds + (int64_t)(p0 + jj) * HWg, (int)(HWg * 16));
+        const __amdgpu_buffer_rsrc_t rds = make_rsrc(ds_plane(ws, p0 + jj, HWg), (int)(HWg * 16));
         const float rbw = 1.0f / (float)bw;
 #pragma unroll
         for (int i = 0; i < kGSI; ++i) {
@@ -1053,7 +1062,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
 #pragma unroll
         for (int r = 0; r < kGTR; ++r) acc[r][jj] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         const int p = p0 + jj;
-        if (p >= g.P) continue;  // block-uniform
+        if (p >= p_end) continue;  // block-uniform
         const int4 bx = ws.box[(int64_t)p * ntiles + tile];  // bwd_box_kernel
         const int bx0 = bx.x, bx1 = bx.y, by0 = bx.z, by1 = bx.w & ~kBoxProven;
         const bool proven = (bx.w & kBoxProven) != 0;
@@ -1092,12 +1101,13 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
             float4* o = dmpi + ((int64_t)ty[r] * g.W + tx) * g.P + p0;
 #pragma unroll
             for (int jj = 0; jj < kGPl; ++jj)
-                if (p0 + jj < g.P)
+                if (p0 + jj < p_end) {
                     if (MPIV_BWD_NTOUT)  // A/B: d MPI past the caches (written once, never re-read here)
                         __builtin_nontemporal_store(f32x4{acc[r][jj][0], acc[r][jj][1], acc[r][jj][2], acc[r][jj][3]},
                                                     reinterpret_cast<f32x4*>(o + jj));
                     else
                         bwd_store(o + jj, make_float4(acc[r][jj][0], acc[r][jj][1], acc[r][jj][2], acc[r][jj][3]));
+                }
         }
     }
 }
@@ -1184,14 +1194,14 @@ __global__ __launch_bounds__(kGThreads, 4) void bwd_gather_dma_kernel(RenderGeom
     };
     auto fill = [&](int jj, int ra, int buf) {  // kGDF DMA instructions of this wave
         int np = 0, bw = 1, bx0 = 0;
-        const float* base = reinterpret_cast<const float*>(ws.ds);
+        const float* base = reinterpret_cast<const float*>(ds_plane(ws, 0, 0));
         if (jj < kGPl) {
             const int4 b = box(jj);
             bx0 = b.x;
             bw = b.y - bx0 + 1;
             const int rb = min((b.w & ~kBoxProven) + 1, ra + rows_per_pass(b));
             np = (rb - ra) * bw;
-            base += (int64_t)(p0 + jj) * HW * 4;
+            base = reinterpret_cast<const float*>(ds_plane(ws, p0 + jj, HW));
         }
         const __amdgpu_buffer_rsrc_t r = make_rsrc(base, (int)(HW * 16));
         const float rbw = 1.0f / (float)bw;
@@ -1462,7 +1472,7 @@ __global__ __launch_bounds__(256, MPIV_GLBW) void bwd_gather_wave_kernel(RenderG
         const float* hp = homs + (int64_t)p * 9;
         const bool proven = div2_rect_safe(hp, (float)bx0, (float)bx1, (float)by0, (float)by1);
         const int rpp = kWCap / bw;
-        const float4* dsp = ws.ds + (int64_t)p * HW;
+        const float4* dsp = ds_plane(ws, p, HW);
         for (int ra = by0; ra <= by1; ra += rpp) {
             const int rb = min(by1 + 1, ra + rpp);
             const int np = (rb - ra) * bw;
@@ -1907,7 +1917,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_barrier_kernel(RenderGeom g,
                 end[c] = ws.offs[bk[c] + 1];
                 head[c] = pos[c] < end[c] ? order_key(ws.ids[pos[c]], c) : 0xFFFFFFFFu;
             }
-            const float4* dsp = ws.ds + (int64_t)(pc0 + pl) * HW;
+            const float4* dsp = ds_plane(ws, pc0 + pl, HW);
             float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
             for (;;) {
                 int c = 0;
@@ -1954,9 +1964,14 @@ __global__ __launch_bounds__(256) void bwd_fallback_barrier_kernel(RenderGeom g,
 // (scalar s_barrier instructions run whatever the exec mask) and read a stale ticket: every
 // box run hung, even a single block with trivial items (round 4, tools/ticket_selftest.py).
 // Returns the block's next item (ticket) or -1 (none left, or aborted).
+// A wait gives up after poll_limit polls (an A/B / test knob; ~0u in production) or after
+// tick_limit wall-clock ticks (production: 60 s at the device's constant wall-clock rate; 0 = no
+// time limit).  Giving up is never expected (the ticket argument above); a slow but correct wait --
+// one block merge-sorting a huge bucket of a strongly minifying view -- takes seconds, not a minute.
 __device__ __forceinline__ int fallback_ticket(unsigned* ticket, unsigned* done, int* abort_, int* aborted,
                                                unsigned total, unsigned nvirt, unsigned poll_limit,
-                                               unsigned* timeouts, unsigned* next_fixed = nullptr) {
+                                               unsigned long long tick_limit, unsigned* timeouts,
+                                               unsigned* next_fixed = nullptr) {
     const int lane = threadIdx.x & (kWave - 1);
     if (abort_ && __builtin_amdgcn_readfirstlane(
                       (int)__hip_atomic_load(abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
@@ -1975,6 +1990,7 @@ __device__ __forceinline__ int fallback_ticket(unsigned* ticket, unsigned* done,
         if (lane == 0 && atomicExch(abort_, 1) == 0) atomicAdd(aborted, 1);
         return -1;
     }
+    const long long t0 = tick_limit ? wall_clock64() : 0;
     for (unsigned spins = 0;; ++spins) {
         const unsigned d = (unsigned)__builtin_amdgcn_readfirstlane(
             (int)__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1982,7 +1998,10 @@ __device__ __forceinline__ int fallback_ticket(unsigned* ticket, unsigned* done,
         if (abort_ && __builtin_amdgcn_readfirstlane(
                           (int)__hip_atomic_load(abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
             return -1;
-        if (spins > poll_limit) {
+        int give_up = spins > poll_limit;
+        if (tick_limit && (spins & 63) == 63)
+            give_up |= (unsigned long long)(wall_clock64() - t0) > tick_limit;
+        if (__builtin_amdgcn_readfirstlane(give_up)) {
             if (lane == 0) {
                 if (abort_ && atomicExch(abort_, 1) == 0) atomicAdd(aborted, 1);
                 if (timeouts) atomicAdd(timeouts, 1u);
@@ -2172,7 +2191,7 @@ __device__ void bwd_fallback_item(const RenderGeom& g, const float* __restrict__
                     end[c] = ws.offs[bk[c] + 1];
                     head[c] = pos[c] < end[c] ? order_key(ws.ids[pos[c]], c) : 0xFFFFFFFFu;
                 }
-                const float4* dsp = ws.ds + (int64_t)(pc0 + pl) * HW;
+                const float4* dsp = ds_plane(ws, pc0 + pl, HW);
                 float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
                 for (;;) {
                     int c = 0;
@@ -2219,7 +2238,8 @@ template <bool FAST>
 // planes [p_lo, p_hi) (a plane group of mpiv_render_backward, or all of them)
 __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const float* __restrict__ homs,
                                                                   BwdWs ws, float4* __restrict__ dmpi,
-                                                                  unsigned poll_limit, int fixed, int p_lo, int p_hi) {
+                                                                  unsigned poll_limit, unsigned long long tick_limit,
+                                                                  int fixed, int p_lo, int p_hi) {
     __shared__ int s_tmp[kScanBlock];
     __shared__ int s_ticket;
     if (ws.flag[0] == 0) return;  // uniform over the grid: the tile gather was complete
@@ -2233,7 +2253,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
     for (;;) {
         if (wave == 0) {
             const int t = fallback_ticket(ticket, done, ws.flag + 3, ws.flag + 4, total, (unsigned)nblk, poll_limit,
-                                          nullptr, fixed ? &next_fixed : nullptr);
+                                          tick_limit, nullptr, fixed ? &next_fixed : nullptr);
             if (tid == 0) s_ticket = t;
         }
         __syncthreads();
@@ -2261,7 +2281,8 @@ __global__ __launch_bounds__(256) void ticket_selftest_kernel(unsigned* __restri
     __shared__ int s_ticket;
     for (;;) {
         if (wave == 0) {
-            const int t = fallback_ticket(ctr, ctr + 1, nullptr, nullptr, total, (unsigned)nvirt, poll_limit, ctr + 3);
+            const int t = fallback_ticket(ctr, ctr + 1, nullptr, nullptr, total, (unsigned)nvirt, poll_limit, 0ull,
+                                          ctr + 3);
             if (tid == 0) s_ticket = t;
         }
         __syncthreads();

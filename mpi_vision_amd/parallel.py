@@ -118,6 +118,14 @@ def identity_partial(views: int, height: int, width: int, like: torch.Tensor) ->
     return ct
 
 
+def pipeline_by_default(world: int, height: int, width: int) -> bool:
+    """The band pipeline is the default when there is more than one rank and every row band is
+    non-empty (height >= world), so every rank posts a P2P batch at every step (with
+    RCCL, a rank that skips a group's first P2P batch while the others post is undefined).
+    Shorter frames take the one-shot all-to-all (gloo tests still drive the pipeline on them)."""
+    return world > 1 and height >= world and width >= 2
+
+
 def render_plane_sharded(packed_local: torch.Tensor, homs_local: torch.Tensor, height: int, group=None,
                          dst: int = 0, render_ct: Optional[Callable] = None,
                          combine: Optional[Callable[[torch.Tensor], torch.Tensor]] = None,
@@ -130,8 +138,7 @@ def render_plane_sharded(packed_local: torch.Tensor, homs_local: torch.Tensor, h
     [V, P_local, 9].  P_local may be 0 (more ranks than planes): that rank contributes the
     identity partial.  Returns the final frames [V, H, W, 3] on dst, None elsewhere.
 
-    pipelined (default on the GPU path: frames of at least 2 x 2 pixels and more than one
-    rank): the partial is rendered band by band and each band leaves for its rank as soon as it
+    pipelined (default on the GPU path: pipeline_by_default): the partial is rendered band by band and each band leaves for its rank as soon as it
     is rendered, overlapping the next band's render (render_plane_sharded_pipelined); else one
     render, one all-to-all.  render_ct / render_rows / combine replace the HIP kernels (CPU
     tests of the exchange logic only)."""
@@ -140,7 +147,7 @@ def render_plane_sharded(packed_local: torch.Tensor, homs_local: torch.Tensor, h
     V = homs_local.shape[0]
     width = packed_local.shape[2] - 2 * _lib.PAD
     if pipelined is None:
-        pipelined = G > 1 and height >= 2 and width >= 2 and (render_rows is not None or render_ct is None)
+        pipelined = pipeline_by_default(G, height, width) and (render_rows is not None or render_ct is None)
     if pipelined:
         return render_plane_sharded_pipelined(packed_local, homs_local, height, group, dst, render_rows, combine,
                                               stats)
@@ -156,7 +163,8 @@ def render_plane_sharded(packed_local: torch.Tensor, homs_local: torch.Tensor, h
 def render_plane_sharded_pipelined(packed_local: torch.Tensor, homs_local: torch.Tensor, height: int, group=None,
                                    dst: int = 0, render_rows: Optional[Callable] = None,
                                    combine: Optional[Callable[[torch.Tensor], torch.Tensor]] = None,
-                                   stats: Optional[dict] = None) -> Optional[torch.Tensor]:
+                                   stats: Optional[dict] = None, world: Optional[tuple[int, int]] = None,
+                                   peer: Optional[Callable[[int], int]] = None) -> Optional[torch.Tensor]:
     """render_plane_sharded with the band exchange overlapped with the render (SURVEY.md §8e
     "pipeline bands to overlap").  G - 1 steps: at step s rank r renders row band k = r + s
     (mod G) of its partial (mpiv_render_packed_ct_rows, one launch) and posts one batched
@@ -165,9 +173,18 @@ def render_plane_sharded_pipelined(packed_local: torch.Tensor, homs_local: torch
     Every rank walks the steps in the same order, so each step's sends and receives pair up.
     Its own band r is rendered last and combined with the received ones in plane (source rank)
     order (mpiv_combine_ct, as the one-shot path), then the RGB bands are gathered.
-    stats (optional): filled with the bytes this rank sent and the steps posted."""
+    stats (optional): filled with the bytes this rank sent and the steps posted.
+    world / peer (tests only): the (G, rank) the band schedule uses and the process-group rank a
+    band rank's P2P ops go to -- a world-1 RCCL test plays G band ranks against itself (self
+    send / receive) to run this function's posting on the device; the frames are then not a
+    render of the MPI, and gather_frames is skipped (the band is returned).
+
+    The send tensors (a view of ct, or its contiguous copy when V > 1) are kept referenced until
+    every exchange has completed (wait()), so the caching allocator cannot hand their memory to
+    the next band's render while RCCL still reads it."""
     from . import _lib
-    G, rank = _world(group)
+    G, rank = _world(group) if world is None else world
+    to = peer or (lambda r: r)
     V = homs_local.shape[0]
     width = packed_local.shape[2] - 2 * _lib.PAD
     bands = band_bounds(height, G)
@@ -179,7 +196,7 @@ def render_plane_sharded_pipelined(packed_local: torch.Tensor, homs_local: torch
     staged = _staged(ct, group)
     recv = ct.new_empty((G, V, e_r - b_r, width, 4))  # band r of every rank's partial, by source rank
     host_recv = {}
-    works, sent = [], 0
+    works, keep, sent = [], [], 0
 
     def render_band(k):
         b, e = bands[k]
@@ -196,25 +213,27 @@ def render_plane_sharded_pipelined(packed_local: torch.Tensor, homs_local: torch
             snd = snd.contiguous() if not snd.is_contiguous() else snd
             if staged:
                 snd = snd.cpu()
-            ops.append(dist.P2POp(dist.isend, snd, k, group))
+            keep.append(snd)
+            ops.append(dist.P2POp(dist.isend, snd, to(k), group))
             sent += snd.numel() * snd.element_size()
         if e_r > b_r:
             rb = recv[j]
             if staged:
                 rb = host_recv[j] = torch.empty(tuple(rb.shape), dtype=rb.dtype)
-            ops.append(dist.P2POp(dist.irecv, rb, j, group))
+            ops.append(dist.P2POp(dist.irecv, rb, to(j), group))
         if ops:
             works += dist.batch_isend_irecv(ops)
     render_band(rank)
     recv[rank] = ct[:, b_r:e_r]
     for w in works:
         w.wait()
+    keep.clear()  # the exchanges are complete (on RCCL: the current stream now waits for them)
     for j, hb in host_recv.items():
         recv[j].copy_(hb)
     if stats is not None:
         stats.update(bytes_sent=sent, steps=G - 1)
     band = combine_partials(recv, combine)
-    return gather_frames(band, height, group, dst)
+    return band if world is not None else gather_frames(band, height, group, dst)
 
 
 def view_shard(n_views: int, rank: int, world: int) -> slice:

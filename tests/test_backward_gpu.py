@@ -349,6 +349,30 @@ def test_backward_fallback_abort_is_loud(dev, kopts):
     assert_bits(got, want, "after an abort")
 
 
+def test_backward_abort_surfaces_on_next_default_call(dev, kopts):
+    """the default render_backward (check=None, the autograd path) reads the abort
+    count back asynchronously -- no synchronisation -- and the next call raises; so a training
+    loop cannot keep stepping on NaN gradients.  render_backward_raise_pending waits and raises."""
+    mpi, homs, dout = _medium_case(2)
+    kopts(bwd_fallback=1, bwd_poll_limit=-1)
+    leaf = mpi.to(dev).requires_grad_(True)
+    out = _lib.RenderFunction.apply(leaf, homs.to(dev))
+    out.backward(dout.to(dev))  # aborted (forced): NaN gradient, nothing raised yet
+    assert torch.isnan(leaf.grad).all()
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="aborted on 2 of 2 views of an earlier backward"):
+        _lib.render_backward(mpi.to(dev), homs, dout.to(dev))
+    # the explicit wait-and-raise form
+    _lib.render_backward(mpi.to(dev), homs, dout.to(dev))
+    with pytest.raises(RuntimeError, match="earlier backward"):
+        _lib.render_backward_raise_pending(dev)
+    # production settings: no aborts, nothing raised, pending copies drain
+    kopts(bwd_fallback=0, bwd_poll_limit=0)
+    for _ in range(3):
+        _lib.render_backward(mpi.to(dev), homs, dout.to(dev))
+    _lib.render_backward_raise_pending(dev)
+
+
 @pytest.mark.parametrize("group", [8, 16])
 def test_backward_plane_groups_vs_oracle(group, dev, bwd_mode, kopts):
     """Plane groups (round 4: a view's backward runs group by group, back to front, the running

@@ -128,10 +128,18 @@ def test_device_psv_matrices_bit_exact(dev):
     K1 = Kd[7].clone()
     for scale in (1.0, 1.5):
         K1.mul_(scale)
-        ki, proj = _host.psv_matrices_device(K1, K1, posed, B)
-        # one camera for the batch: the drop-in inverts it materialised per view, as the host path
-        # does for device intrinsics (its one device-to-host copy materialises them too)
-        Kh = K1.cpu()[None].expand(B, 3, 3).contiguous()
+        # one camera for the batch, passed the way the reference's caller would: expanded
+        # (stride 0).  The reference inverts that tensor as laid out (utils.py:370), and so must
+        # both drop-in paths (tests/test_kstride.py holds the reference goldens for it)
+        Ke = K1[None].expand(B, 3, 3)
+        ki, proj = _host.psv_matrices_device(Ke, Ke, posed, B)
+        Kh = K1.cpu()[None].expand(B, 3, 3)
         wki, wproj = _host.psv_matrices(Kh, Kh, pose)
+        assert_bits(ki.cpu().numpy(), wki.numpy())
+        assert_bits(ki.cpu().numpy(), torch.inverse(Kh).reshape(B, 9).numpy())
+        assert_bits(proj.cpu().numpy(), wproj.numpy())
+        # an unbatched [3,3] camera: inverted once as given, broadcast over the batch
+        ki, proj = _host.psv_matrices_device(K1, K1, posed, B)
+        wki, wproj = _host.psv_matrices(K1.cpu(), K1.cpu(), pose)
         assert_bits(ki.cpu().numpy(), wki.numpy())
         assert_bits(proj.cpu().numpy(), wproj.numpy())

@@ -137,7 +137,8 @@ def _pipelined_worker(rank, world, port, H, W, P, out_path):
     comb = lambda x: torch.from_numpy(oracle.combine_ct(x.numpy()))  # noqa: E731
     hl = torch.from_numpy(np.ascontiguousarray(homs[:, p0:p1]))
     stats = {}
-    got = parallel.render_plane_sharded(packed, hl, H, render_rows=rows, combine=comb, stats=stats)
+    # forced on: short frames (H < world, empty bands) take the one-shot path by default
+    got = parallel.render_plane_sharded(packed, hl, H, render_rows=rows, combine=comb, stats=stats, pipelined=True)
     one = parallel.render_plane_sharded(packed, hl, H, render_ct=lambda pk, h, back: full, combine=comb,
                                         pipelined=False) if p1 > p0 else \
         parallel.render_plane_sharded(packed, hl, H, combine=comb, pipelined=False)
@@ -166,6 +167,16 @@ def test_plane_sharded_pipelined_equals_one_shot(world, H, W, P, tmp_path):
     assert np.array_equal(got.view(np.uint32), one.view(np.uint32))
     mpi, homs = _case(H, W, P)
     np.testing.assert_allclose(got, oracle.render(mpi, homs), rtol=0, atol=1e-5)
+
+
+def test_pipeline_default_needs_every_band_non_empty():
+    sys.path.insert(0, REPO)
+    from mpi_vision_amd import parallel
+    assert parallel.pipeline_by_default(8, 2160, 4096)
+    assert parallel.pipeline_by_default(2, 2, 2)
+    assert not parallel.pipeline_by_default(1, 2160, 4096)
+    assert not parallel.pipeline_by_default(4, 3, 6)   # one rank's band would be empty
+    assert not parallel.pipeline_by_default(3, 37, 1)
 
 
 def test_shard_ranges_cover_exactly():
@@ -320,6 +331,23 @@ def _rccl_worker(rank, world, port, out_path):
         np.save(out_path, frames.cpu().numpy())
         np.save(out_path + ".plane.npy", frame.cpu().numpy())
         np.save(out_path + ".seq.npy", _lib.render_packed(packed, homs).cpu().numpy())
+    # the pipelined band exchange's own RCCL calls: this rank plays 4 band
+    # ranks against itself (every P2P op goes to rank 0: a self send / receive pair per step), so
+    # render_plane_sharded_pipelined posts its batch_isend_irecv between the per-band row renders
+    # exactly as at world 4; 2 views make every send a .contiguous() temporary.  Received band j
+    # at step s is this rank's band s, so the combine sees bands 0, 3, 2, 1 in that order.
+    G, H2 = 4, 36
+    packed2 = _lib.pack_planes(configs.synthetic_mpi(1, H2, W, P, 6)[0].to(dev))
+    homs2 = homs[:2].contiguous()
+    stats = {}
+    got = parallel.render_plane_sharded_pipelined(packed2, homs2, H2, world=(G, 0), peer=lambda r: 0, stats=stats)
+    ct = _lib.render_packed_ct(packed2, homs2, back=True)
+    bh = H2 // G
+    parts = torch.stack([ct[:, k * bh:(k + 1) * bh] for k in (0, 3, 2, 1)])
+    if rank == 0:
+        np.save(out_path + ".pipe.npy", got.cpu().numpy())
+        np.save(out_path + ".pipe_want.npy", _lib.combine_ct(parts.contiguous()).cpu().numpy())
+        np.save(out_path + ".pipe_sent.npy", np.array([stats["bytes_sent"], stats["steps"]]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -333,3 +361,5 @@ def test_sharded_paths_over_rccl_world1(tmp_path):
     seq = np.load(out + ".seq.npy")
     np.testing.assert_array_equal(np.load(out), seq)
     np.testing.assert_array_equal(np.load(out + ".plane.npy"), seq[:1])
+    np.testing.assert_array_equal(np.load(out + ".pipe.npy"), np.load(out + ".pipe_want.npy"))
+    assert list(np.load(out + ".pipe_sent.npy")) == [3 * 2 * 9 * 53 * 4 * 4, 3]
