@@ -186,24 +186,54 @@ def prof_summary():
     return _PROF or None
 
 
-def prof_for(kernel: str, grid: int):
-    """The summary's entry for the dispatches of `kernel` with `grid` work-items."""
+def prof_for(kernel: str, grid: int, tag: str | None = None):
+    """The summary's entry for the dispatches of `kernel` with `grid` work-items inside the timed
+    region marked `tag` (mpiv_mark phase tags), or over the whole run (tag None or no tagged entry)."""
     d = prof_summary()
     if not d:
         return None
+    whole = None
     for e in d.get("launches", []):
         if e["kernel"] == kernel and e["grid"] == grid:
-            return e
-    return None
+            if tag is not None and e.get("tag") == tag:
+                return e
+            if "tag" not in e:
+                whole = e
+    return whole
 
 
-def prof_fields(kernel: str, grid: int, alg_bytes: float, ms: float):
+def prof_tag_kernels(tag: str, calls_per_region: int):
+    """Every libmpiv kernel the summary saw inside the region marked `tag`, by total time: per
+    kernel the rocprof average, dispatches per call of the region's operation and the PMC HBM
+    traffic per dispatch (the backward's chain, gather, ... separately)."""
+    d = prof_summary()
+    if not d:
+        return None
+    out = []
+    for e in d.get("launches", []):
+        if e.get("tag") == tag and e.get("calls"):
+            out.append({"kernel": e["kernel"], "grid_workitems": e["grid"], "rocprof_avg_ms": round(e["avg_ns"] / 1e6, 4),
+                        "dispatches_per_call": round(e["calls"] / calls_per_region, 2),
+                        "ms_per_call": round(e["avg_ns"] / 1e6 * e["calls"] / calls_per_region, 4),
+                        "traffic": e.get("hbm_bytes"), "valu_issue_frac": e.get("valu_issue_frac"),
+                        "ta_busy_frac": e.get("ta_busy_frac")})
+    return sorted(out, key=lambda x: -x["ms_per_call"])
+
+
+def mark(name: str, dev):
+    """Phase marker (mpiv_mark) for the rocprof summary: the dispatches after it belong to `name`."""
+    _lib._call("mpiv_mark", configs.PROF_TAGS[name], _lib._stream(dev))
+
+
+def prof_fields(kernel: str, grid: int, alg_bytes: float, ms: float, tag: str | None = None):
     """rocprof average and PMC traffic of this leg's launch, with the ratios the verdict
-    recomputes: rocprof ms vs the bench's own HIP-event ms, HBM traffic vs algorithmic bytes."""
-    e = prof_for(kernel, grid)
+    recomputes: rocprof ms vs the bench's own HIP-event ms, HBM traffic vs algorithmic bytes.
+    tag: the leg's timed region (its dispatches only, when the summary has them)."""
+    e = prof_for(kernel, grid, tag)
     res = {"kernel": kernel, "grid_workitems": grid,
            "prof_source": "profiles/prof_summary.json (same build id)" if e else "no rocprof summary of this build"}
     if e:
+        res["prof_region"] = e.get("tag", "all dispatches of this kernel and grid")
         res["rocprof_avg_ms"] = round(e["avg_ns"] / 1e6, 4)
         res["rocprof_calls"] = e["calls"]
         # the summary comes from another run (tools/profile.sh): a leg whose rocprof average is
@@ -224,15 +254,16 @@ def prof_fields(kernel: str, grid: int, alg_bytes: float, ms: float):
 # timing helpers
 # ---------------------------------------------------------------------------
 
-def event_ms(fn, n, stream):
-    """Average device time of fn() over n calls, HIP events on the launch stream."""
+def event_ms(fn, n, stream, each=False):
+    """Average device time of fn() over n calls, HIP events on the launch stream (each: the list)."""
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
     for a, b in ev:
         a.record(stream)
         fn()
         b.record(stream)
     torch.cuda.synchronize()
-    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    t = [a.elapsed_time(b) for a, b in ev]
+    return t if each else float(np.mean(t))
 
 
 def span_ms(fn, n, stream):
@@ -335,13 +366,15 @@ def single_view_leg(packed, H, W, P, h_sv, dev, stream):
     launch = lambda: _lib._call("mpiv_render_packed", packed, H, W, P, h_sv, 1, one, _lib._stream(dev))  # noqa: E731
     for _ in range(50):  # ~20 ms of untimed launches: the clocks leave their idle state first
         launch()
+    mark("sv", dev)
     ms = event_ms(launch, 20, stream)
+    mark("untimed", dev)
     alg = P * H * W * 16 + H * W * 12
     gbs, frac = hbm(alg, ms)
     kname, grid = _lib.route("render_packed", H, W, P, 1)
     res = {"workload": "config 4 MPI, one view per launch", "kernel_ms": round(ms, 4), "alg_bytes": alg,
            "alg_def": "P*H*W*16 + H*W*12", "achieved_gbs": gbs, "peak": HBM_PEAK_GBS, "frac": frac, "bound": "hbm"}
-    res.update(prof_fields(kname, grid, alg, ms))
+    res.update(prof_fields(kname, grid, alg, ms, "sv"))
     return res
 
 
@@ -358,7 +391,9 @@ def config2_leg(dev, stream, n=20):
     launch = lambda: _lib._call("mpiv_render_packed", packed, H, W, P, homs, V, out, _lib._stream(dev))  # noqa: E731
     for _ in range(3):
         launch()
+    mark("c2", dev)
     ms = event_ms(launch, n, stream)
+    mark("untimed", dev)
     alg = V * (P * H * W * 16 + H * W * 12)
     gbs, frac = hbm(alg, ms)
     kname, grid = _lib.route("render_packed", H, W, P, V)
@@ -367,7 +402,7 @@ def config2_leg(dev, stream, n=20):
            "baseline_bar_Mpix_s": 9160, "alg_bytes": alg, "alg_def": "V*(P*H*W*16 + H*W*12) (SURVEY §8d)",
            "alg_gbs": gbs, "alg_frac": frac,
            "alg_frac_note": "the 64 views share one MPI through L2, so the per-view formula can exceed 1 of HBM"}
-    res.update(prof_fields(kname, grid, alg, ms))
+    res.update(prof_fields(kname, grid, alg, ms, "c2"))
     del packed, out
     return res
 
@@ -387,7 +422,9 @@ def config3_leg(dev, stream, n=20):
     vol = mv.plane_sweep_torch(img, depths, pose, K)
     for _ in range(3):
         mv.plane_sweep_torch(img, depths, pose, K)
+    mark("c3_dropin", dev)
     dropin_ms = span_ms(lambda: mv.plane_sweep_torch(img, depths, pose, K), n, stream)
+    mark("untimed", dev)
     ki, proj = _host.psv_matrices(K.cpu(), K.cpu(), pose.cpu())
     ki, proj = ki.to(dev), proj.to(dev)
     dd = configs.f32(depths).to(dev)
@@ -396,12 +433,15 @@ def config3_leg(dev, stream, n=20):
                                 out, _lib._stream(dev))
     launch()
     same = bool(torch.equal(out.view(torch.int32), vol.view(torch.int32)))
-    # steady state: the first few dozen launches of a run are 15-20 % slower (measured 0.73-0.76 ms
-    # against 0.61-0.63 ms from the third dozen on, profiles/r03_sweep_few_depths_ab.txt), so ~25 ms
-    # of untimed launches come first
-    for _ in range(40):
+    # every timed launch counts: 3 untimed launches, then the mean of 3n back-to-back launches --
+    # the rate this write-heavy kernel sustains, including its slowdown under sustained load
+    # (round 4 quoted the best steady state after 40 untimed launches)
+    for _ in range(3):
         launch()
-    ms = event_ms(launch, n, stream)
+    mark("c3", dev)
+    ms_each = event_ms(launch, 3 * n, stream, each=True)
+    mark("untimed", dev)
+    ms = float(np.mean(ms_each))
     alg = S * H * W * 12 + S * D * H * W * 12
     gbs, frac = hbm(alg, ms)
     kname, grid = _lib.route("plane_sweep", S, H, W, 3, D, H, W)
@@ -413,25 +453,29 @@ def config3_leg(dev, stream, n=20):
     img10 = img[:S10]
     launch10 = lambda: _lib._call("mpiv_plane_sweep", img10, _lib._strides(img10), S10, H, W, 3, ki, proj, d10,  # noqa: E731
                                   D10, H, W, out10, _lib._stream(dev))
-    for _ in range(20):
+    for _ in range(3):
         launch10()
+    mark("c3_ten", dev)
     ms10 = event_ms(launch10, n, stream)
+    mark("untimed", dev)
     alg10 = S10 * H * W * 12 + S10 * D10 * H * W * 12
     k10, g10 = _lib.route("plane_sweep", S10, H, W, 3, D10, H, W)
     ten = {"workload": "4 of config 3's sources into 10 depth planes (the notebook dataset's depth count)",
            "kernel_ms": round(ms10, 4), "alg_bytes": alg10, "achieved_gbs": hbm(alg10, ms10)[0],
            "frac": hbm(alg10, ms10)[1], "bound": "hbm"}
-    ten.update(prof_fields(k10, g10, alg10, ms10))
+    ten.update(prof_fields(k10, g10, alg10, ms10, "c3_ten"))
     del out10
     res = {"workload": "BASELINE config 3: PSV of 5 source 1024x768x3 images into 64 depth planes "
                        "(plane_sweep_torch, utils.py:452-471)",
-           "kernel_ms": round(ms, 4), "dropin_ms": round(dropin_ms, 4),
+           "kernel_ms": round(ms, 4), "kernel_ms_def": f"mean of {3 * n} back-to-back launches after 3 untimed",
+           "kernel_ms_first_last_third": [round(float(np.mean(ms_each[:n])), 4), round(float(np.mean(ms_each[-n:])), 4)],
+           "dropin_ms": round(dropin_ms, 4),
            "Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1),
            "alg_bytes": alg, "alg_def": "S*Hs*Ws*C*4 + S*D*Ht*Wt*C*4 (SURVEY §8d)", "achieved_gbs": gbs,
            "peak": HBM_PEAK_GBS, "frac": frac, "bound": "hbm", "baseline_bar_ms": 0.64,
            "dropin_equals_kernel": same,
            "reference_cpu": {"s": REF_CPU["c3_s"], "cores": REF_CPU["cores"], "source": REF_CPU["source"]}}
-    res.update(prof_fields(kname, grid, alg, ms))
+    res.update(prof_fields(kname, grid, alg, ms, "c3"))
     res["ten_planes"] = ten
     del img, out, vol
     return res
@@ -464,7 +508,9 @@ def notebook_leg(dev, stream, n=50):
     launch = lambda: _lib._call("mpiv_plane_sweep", img4, _lib._strides(img4), 1, S, N, 3, ki, proj, dd, P, S, N,  # noqa: E731
                                 out, _lib._stream(dev))
     launch()
+    mark("nb", dev)
     psv_kernel_ms = event_ms(launch, n, stream)
+    mark("untimed", dev)
     psv_alg = S * N * 12 + P * S * N * 12
     mpi = configs.synthetic_mpi(1, S, N, P, 9).to(dev)
     planes = configs.f32(depths).to(dev)
@@ -493,7 +539,7 @@ def notebook_leg(dev, stream, n=50):
            "train_step_ms": round(train_ms, 4),
            "train_step_def": "mpi_render_view_torch forward (autograd, checkpoints) + backward through the drop-in",
            "note": "8 MB of texels: launch-latency-bound at this size", "psv": prof_fields(kname, grid, psv_alg,
-                                                                                             psv_kernel_ms)}
+                                                                                             psv_kernel_ms, "nb")}
     del mpi, leaf, out
     return res
 
@@ -521,12 +567,35 @@ def u8_leg(dev, stream, V, homs_sv, homs_v, n=10):
     one = torch.empty((1, H, W, 3), device=dev)
     many = torch.empty((V, H, W, 3), device=dev)
     l1 = lambda: _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs_sv, 1, one, _lib._stream(dev))  # noqa: E731
-    lv = lambda: _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs_v, V, many, _lib._stream(dev))  # noqa: E731
+    lv_u8 = lambda: _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs_v, V, many, _lib._stream(dev))  # noqa: E731
     for _ in range(50):
         l1()
+    mark("u8_sv", dev)
     ms1 = event_ms(l1, 20, stream)
+    mark("untimed", dev)
+    # V views per launch: the route render_packed_u8 takes there (>= U8_FLOAT_MIN_VIEWS): the float
+    # kernel on the MPI's exact float copy, converted once per MPI (timed separately, outside)
+    route_float = V >= _lib.U8_FLOAT_MIN_VIEWS
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    fcopy = _lib.u8_float_copy(pk) if route_float else None
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    convert_ms = ev0.elapsed_time(ev1) if route_float else None
+    lv = (lambda: _lib._call("mpiv_render_packed", fcopy, H, W, P, homs_v, V, many, _lib._stream(dev))) \
+        if route_float else lv_u8  # noqa: E731
     lv()
+    mark("u8_mv", dev)
     msv = event_ms(lv, n, stream)
+    mark("untimed", dev)
+    want = many.clone()
+    lv_u8()
+    mark("u8_kernel", dev)
+    msv_u8 = event_ms(lv_u8, n, stream)
+    mark("untimed", dev)
+    same_v = bool(torch.equal(want.view(torch.int32), many.view(torch.int32)))
+    del fcopy, want
+    _lib._U8_FLOAT.clear()
     # float packed copy of u8/255 (numpy fp32 division is IEEE) for the bit-exact self-check
     f = (pk.view(torch.uint8).cpu().numpy().reshape(P, H + 4, W + 4, 4).astype(np.float32) / np.float32(255.0))
     fpk = torch.from_numpy(f).to(dev)
@@ -537,16 +606,23 @@ def u8_leg(dev, stream, V, homs_sv, homs_v, n=10):
     del fpk, ref
     alg1 = P * H * W * 4 + H * W * 12
     k1, g1 = _lib.route("render_packed_u8", H, W, P, 1)
-    kv, gv = _lib.route("render_packed_u8", H, W, P, V)
+    kv, gv = _lib.route("render_packed" if route_float else "render_packed_u8", H, W, P, V)
+    ku, gu = _lib.route("render_packed_u8", H, W, P, V)
     sv = {"kernel_ms": round(ms1, 4), "alg_bytes": alg1, "alg_def": "P*H*W*4 (u8 texels) + H*W*12",
           "achieved_gbs": hbm(alg1, ms1)[0], "frac": hbm(alg1, ms1)[1], "bound": "hbm",
           "frame_equals_float_render_of_u8_over_255": same}
-    sv.update(prof_fields(k1, g1, alg1, ms1))
+    sv.update(prof_fields(k1, g1, alg1, ms1, "u8_sv"))
     algv = V * alg1
     mv_ = {"views": V, "kernel_ms": round(msv, 4), "Mpix_per_s": round(V * H * W / 1e6 / (msv * 1e-3), 1),
+           "route": ("float kernel on the MPI's exact float copy (render_packed_u8 at >= "
+                     f"{_lib.U8_FLOAT_MIN_VIEWS} views per launch)") if route_float else "u8 kernel",
+           "u8_to_float_copy_ms_once": round(convert_ms, 4) if convert_ms is not None else None,
+           "frames_equal_u8_kernel": same_v,
            "alg_bytes": algv, "alg_gbs": hbm(algv, msv)[0],
            "alg_frac_note": "the views share one MPI through L2: the per-view formula can exceed 1 of HBM"}
-    mv_.update(prof_fields(kv, gv, algv, msv))
+    mv_.update(prof_fields(kv, gv, algv, msv, "u8_mv"))
+    mv_["u8_kernel"] = {"kernel_ms": round(msv_u8, 4)}
+    mv_["u8_kernel"].update(prof_fields(ku, gu, algv, msv_u8, "u8_kernel"))
     del pk, one, many
     torch.cuda.empty_cache()
     return {"workload": "config-4-shape 8-bit MPI (1024x1024x128, 4-B texels): one view and the camera-path "
@@ -570,7 +646,9 @@ def netout_leg(dev, stream, n=20):
                                 H, W, P, homs, out, _lib._stream(dev))
     for _ in range(20):
         launch()
+    mark("netout", dev)
     ms = event_ms(launch, n, stream)
+    mark("untimed", dev)
     two = _lib.render(_lib.assemble_mpi(pred, fg, P), homs)
     same = bool(torch.equal(two.view(torch.int32), out.view(torch.int32)))
     alg = H * W * ((2 * P + 3) * 4 + 12 + 12)
@@ -579,7 +657,7 @@ def netout_leg(dev, stream, n=20):
            "kernel_ms": round(ms, 4), "alg_bytes": alg, "alg_def": "H*W*((2P+3)*4 + 12 + 12): prediction + "
            "reference image read, frame written", "achieved_gbs": hbm(alg, ms)[0], "frac": hbm(alg, ms)[1],
            "bound": "hbm", "equals_assemble_then_render": same}
-    res.update(prof_fields(kname, grid, alg, ms))
+    res.update(prof_fields(kname, grid, alg, ms, "netout"))
     del pred, fg, out, two
     return res
 
@@ -605,21 +683,32 @@ def training_leg(dev, stream, n=10):
     f_out = torch.empty((1, H, W, 3), device=dev)
     f_ck = torch.empty_like(ck)
     st = _lib._strides(mpi)
+    mark("train_fwd", dev)
     fwd_ms = span_ms(lambda: _lib._call("mpiv_render_train", mpi, st, 1, H, W, P, homs, f_out, f_ck,  # noqa: E731
                                         _lib._stream(dev)), n, stream)
+    mark("train_inf", dev)
     inf_ms = span_ms(lambda: _lib._call("mpiv_render", mpi, st, 1, H, W, P, homs, f_out, _lib._stream(dev)),  # noqa: E731
                      n, stream)
+    mark("train_inf_dropin", dev)
     inf_dropin_ms = event_ms(lambda: _lib.render(mpi, homs), n, stream)
+    mark("untimed", dev)
     same_ck = bool(torch.equal(f_ck.view(torch.int32), ck.view(torch.int32)))
     del f_ck
     g1 = _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)
+    mark("train_bwd", dev)
     bwd_ms = span_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck), n, stream)
+    mark("untimed", dev)
     g2 = _lib.render_backward(mpi, homs, dout, workspace=ws)
+    mark("train_bwd_nockpt", dev)
     bwd2_ms = span_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws), n, stream)
+    mark("untimed", dev)
     # the smallest workspace (plane groups, round 4): same gradient, d samples of one group resident
     ws_min = torch.empty(_lib.load().mpiv_render_backward_workspace_size_min(H, W, P), dtype=torch.uint8, device=dev)
     g3 = _lib.render_backward(mpi, homs, dout, workspace=ws_min, ckpt=ck)
-    bwd3_ms = span_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws_min, ckpt=ck), n, stream)
+    mark("train_bwd_minws", dev)
+    bwd3_ms = span_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws_min, ckpt=ck), n,
+                      stream)
+    mark("untimed", dev)
     same_min = bool(torch.equal(g1.view(torch.int32), g3.view(torch.int32)))
     ws_min_gb = round(ws_min.numel() / 1e9, 3)
     del g3, ws_min
@@ -646,7 +735,14 @@ def training_leg(dev, stream, n=10):
            "backward_min_workspace_ms": round(bwd3_ms, 4), "workspace_min_GB": ws_min_gb,
            "min_workspace_grad_bit_identical": same_min,
            "min_workspace_def": "mpiv_render_backward_workspace_size_min: plane groups of 32, one group's d samples resident",
-           "ckpt_grad_bit_identical": same, "inference": prof_fields(kname, grid, f_alg, inf_ms)}
+           "ckpt_grad_bit_identical": same, "inference": prof_fields(kname, grid, f_alg, inf_ms, "train_inf"),
+           # per-kernel rocprof attribution of each timed sub-leg (phase-tagged dispatches,
+           # tools/parse_prof.py): chain, gather, ... with dispatches and ms per call
+           "rocprof_kernels": {t: prof_tag_kernels(t, n) for t in
+                               ("train_fwd", "train_bwd", "train_bwd_nockpt", "train_bwd_minws")}}
+    fk = prof_for(_lib.route("render_train", 1, H, W, P)[0], _lib.route("render_train", 1, H, W, P)[1], "train_fwd")
+    if fk:
+        res["forward_rocprof_ms"] = round(fk["avg_ns"] / 1e6, 4)
     del mpi, ws, g1, g2, ck
     torch.cuda.empty_cache()
     return res
@@ -687,7 +783,9 @@ def config5_leg(world, rank, dev, steps, warmup):
         shard_bytes = (p1 - p0) * H * W * 16 + H * W * 16
         kname, grid = _lib.route("render_packed_ct", H, W, p1 - p0, 1)
     launch()
+    mark("c5_kernel", dev)
     kern_ms = event_ms(launch, 3, stream)
+    mark("untimed", dev)
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -720,7 +818,7 @@ def config5_leg(world, rank, dev, steps, warmup):
                                 "band is rendered (mpiv_render_packed_ct_rows)",
                     "bytes_sent_per_rank": int(sent), "exchange_exposed_ms": round(step_ms - max(kern_all), 3),
                     "exchange_gbs_over_step": round(sent / (step_ms * 1e-3) / 1e9, 2)})
-    res.update(prof_fields(kname, grid, shard_bytes, max(kern_all)))
+    res.update(prof_fields(kname, grid, shard_bytes, max(kern_all), "c5_kernel"))
     del packed
     torch.cuda.empty_cache()
     return res
@@ -817,10 +915,12 @@ def main():
     torch.cuda.synchronize()
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
+    mark("c4", dev)  # an empty marker kernel (phase tag of the rocprof summary), before the clock starts
     t0 = time.perf_counter()
     run(args.steps, args.warmup, events)
     torch.cuda.synchronize()
     barrier(world)
+    mark("untimed", dev)
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, world, dev)
     kern_ms_local = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -865,7 +965,7 @@ def main():
     hbm_alg_bytes = V * (P * H * W * 16 + H * W * 12)  # every view reading its MPI once (§8d)
     gather_bytes = gathers * kWaveBytes if gathers else tap_bytes
     achieved = gather_bytes / (kern_ms * 1e-3) / 1e9
-    pf = prof_fields(kernel_name, grid, hbm_alg_bytes, kern_ms)
+    pf = prof_fields(kernel_name, grid, hbm_alg_bytes, kern_ms, "c4")
     traffic = pf.get("traffic")
 
     cpu_frames, cpu_view = None, None

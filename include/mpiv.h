@@ -376,11 +376,21 @@ int mpiv_render_packed_u8(const uint32_t *packed, int H, int W, int P, const flo
 int mpiv_render_packed_u8_ct(const uint32_t *packed, int H, int W, int P, int p_begin, int p_end, int back,
                              const float *homs, int V, float *ct, void *stream);
 
+/* Packed u8 planes [P][H+4][W+4] -> packed float planes out [P][H+4][W+4] float4 (mpiv_pack_planes'
+ * layout, 16-B aligned), every channel RN(u8 / 255) exactly: the float MPI the reference's
+ * u8.float() / 255 gives (its test MPI, utils.py:324-331).  The render of many views per launch
+ * converts an 8-bit MPI once with it and runs the float kernel (bit-identical frames). */
+int mpiv_unpack_planes_u8(const uint32_t *packed, int H, int W, int P, float *out, void *stream);
+
 /* Counter-based synthetic u8 MPI (mpiv_synth_mpi_packed's hash, one byte per channel =
  * the top 8 bits of its hash, plane 0 alpha 255) into the packed u8 layout. */
 int mpiv_synth_mpi_packed_u8(uint32_t seed, int H, int W, int p_begin, int p_end, uint32_t *packed, void *stream);
 
 /* ---- diagnostics ------------------------------------------------------------ */
+
+/* Phase marker for profiles: launches an empty kernel of `tag` x 64 work-items (tag in 1..4096) on
+ * the stream; tools/parse_prof.py files later dispatches under the last marker's tag. */
+int mpiv_mark(int tag, void *stream);
 
 /* Gather-rate probe (bench.py's texture-path roofline): `blocks` x 256 work-items each
  * issue iters x 8 16-B buffer loads (1 KiB per wave instruction, the render's tap shape)

@@ -11,6 +11,7 @@ import contextlib
 import ctypes
 import hashlib
 import os
+import weakref
 
 import torch
 from torch.autograd.function import once_differentiable
@@ -52,6 +53,7 @@ _SIGS = {
     "mpiv_selftest_div_const": [_int, _vp, _vp],
     "mpiv_selftest_tickets": [_int, _int, _int, ctypes.c_uint, _vp, _vp, _vp],
     "mpiv_probe_gather": [_vp, ctypes.c_size_t, _int, _int, _vp, _vp],
+    "mpiv_mark": [_int, _vp],
     "mpiv_route": [ctypes.c_char_p, _c_i64p, _int, ctypes.c_char_p, _int, _c_i64p],
     "mpiv_pad_texels": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_plane_sweep_padded": [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _int, _int, _int, _vp, _vp],
@@ -76,6 +78,7 @@ _SIGS = {
     "mpiv_render_packed_u8": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_render_packed_u8_ct": [_vp, _int, _int, _int, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_synth_mpi_packed_u8": [ctypes.c_uint32, _int, _int, _int, _int, _vp, _vp],
+    "mpiv_unpack_planes_u8": [_vp, _int, _int, _int, _vp, _vp],
     "mpiv_synth_mpi_packed": [ctypes.c_uint32, _int, _int, _int, _int, _vp, _vp],
     "mpiv_assemble_mpi_backward": [_vp, _c_i64p, _vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp,
                                    _vp],
@@ -408,10 +411,47 @@ def _u8_hw(packed: torch.Tensor):
     return packed.shape[0], packed.shape[1] - 2 * PAD, packed.shape[2] - 2 * PAD
 
 
-def render_packed_u8(packed: torch.Tensor, homs: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """packed u8 [P,H+4,W+4] + homs [V,P,9] -> [V,H,W,3] fp32, bit-identical to rendering the
-    float MPI u8.float() / 255 (render_u8.hip)."""
+def unpack_planes_u8(packed: torch.Tensor) -> torch.Tensor:
+    """packed u8 [P,H+4,W+4] -> the packed float MPI [P,H+4,W+4,4] of u8.float() / 255 (exact)."""
     P, H, W = _u8_hw(packed)
+    out = torch.empty(packed_shape(H, W, P), device=packed.device, dtype=torch.float32)
+    _call("mpiv_unpack_planes_u8", packed, H, W, P, out, _stream(packed.device))
+    return out
+
+
+# Views per launch from which render_packed_u8 renders an 8-bit MPI through its float copy (the
+# float rows kernel at 125 views: 26.6 ms vs 29.8 for the u8 kernel, VALU-bound on the exact
+# per-tap conversion; at one view the u8 kernel reads 4x fewer bytes and wins, 0.31 vs 0.38 ms).
+U8_FLOAT_MIN_VIEWS = int(os.environ.get("MPIV_U8_FLOAT_MIN_VIEWS", "32"))
+_U8_FLOAT: dict = {}
+
+
+def u8_float_copy(packed: torch.Tensor) -> torch.Tensor:
+    """The packed float copy of a packed u8 MPI, memoised per device on the tensor object, its
+    storage and version counter (a camera path converts its MPI once; an in-place edit or a new
+    MPI converts again).  One entry per device: the copy is 4x the u8 MPI (2.2 GB at config 4)."""
+    dev = packed.device
+    key = (id(packed), packed.data_ptr(), packed._version, tuple(packed.shape))
+    ent = _U8_FLOAT.get(dev)
+    if ent is not None and ent[0] == key and ent[1]() is packed:
+        return ent[2]
+    _U8_FLOAT.pop(dev, None)  # free the old copy first
+    f = unpack_planes_u8(packed)
+    _U8_FLOAT[dev] = (key, weakref.ref(packed), f)
+    return f
+
+
+def render_packed_u8(packed: torch.Tensor, homs: torch.Tensor, out: torch.Tensor | None = None,
+                     route_float: bool | None = None) -> torch.Tensor:
+    """packed u8 [P,H+4,W+4] + homs [V,P,9] -> [V,H,W,3] fp32, bit-identical to rendering the
+    float MPI u8.float() / 255 (render_u8.hip).  Launches of >= U8_FLOAT_MIN_VIEWS views
+    (route_float None) render the MPI's exact float copy (u8_float_copy, converted once per MPI)
+    with the float kernel instead: the same bits, faster where the texture path binds."""
+    P, H, W = _u8_hw(packed)
+    if route_float is None:
+        route_float = homs.shape[0] >= U8_FLOAT_MIN_VIEWS
+    if route_float:
+        return render_packed(u8_float_copy(packed), homs, out=out)
     dev = packed.device
     V = homs.shape[0]
     h = _up(homs.reshape(V, P, 9), dev)

@@ -114,3 +114,12 @@ def config5():
     return dict(H=H, W=W, P=P, K=intrinsics_matrix(f, f, W / 2.0, H / 2.0),
                 poses=[pose_from(rot_y(1.0), (0.05, -0.02, 0.03))],
                 depths=inv_depths(1, 100, P), seed=0)
+
+
+# Phase tags of bench.py's timed regions (mpiv_mark: an empty marker kernel of tag x 64 work-items
+# launched before each region; tools/parse_prof.py files every later dispatch under the last
+# marker's tag, so the rocprof summary separates legs that launch the same kernel and grid).
+PROF_TAGS = {"untimed": 1, "c4": 2, "sv": 3, "c2": 4, "c3_dropin": 5, "c3": 6, "c3_ten": 7, "nb": 8,
+             "netout": 9, "u8_sv": 10, "u8_mv": 11, "u8_kernel": 12, "train_fwd": 13, "train_inf": 14,
+             "train_inf_dropin": 15, "train_bwd": 16, "train_bwd_nockpt": 17, "train_bwd_minws": 18, "c5": 19,
+             "c5_kernel": 20}

@@ -102,6 +102,10 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      bwd_fallback_barrier_kernel) / the ticket kernel with a fixed item order (block b:
 //                      b, b + nblk, ...; diagnosis)
 //   bwd_fb_blocks=k    (A/B build) the backward fallback launches k blocks instead of the resident count
+//   netout_geo=WRD     render_netout_kernel<W, R, D>: W waves per block, R rows per work-item
+//                      (64 x W*R tiles), D planes' w / a loads in flight (e.g. 821; 0 = automatic)
+//   netout_buf=0|1     render_netout_kernel's staged loads through pointers (0) or buffer resources
+//                      with 32-bit offsets (1, default where the spans fit)
 //   bwd_margin=k       the tile gather's pixel-window margin in 1/64 pixel (default 16);
 //                      negative values make windows miss contributors, which the pair
 //                      count must catch (tests)
@@ -111,13 +115,13 @@ enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOpt
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
                 kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kOptU8Flight, kOptBwdGroup,
-                kNumOpts };
+                kOptNetoutGeo, kOptNetoutBuf, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
                                          "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode",
-                                         "chunk_strip", "u8_flight", "bwd_group"};
+                                         "chunk_strip", "u8_flight", "bwd_group", "netout_geo", "netout_buf"};
 #ifndef MPIV_CHUNK_STRIP
 #define MPIV_CHUNK_STRIP 1  // round 4: 0.506 vs 0.64 ms in place (profiles/r04j_strip*_ab.jsonl)
 #endif
@@ -125,8 +129,9 @@ const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_nat
 #define MPIV_U8_FLIGHT 0
 #endif
 const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP,
-                                    MPIV_U8_FLIGHT, 0};
-int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP, MPIV_U8_FLIGHT, 0};
+                                    MPIV_U8_FLIGHT, 0, 0, 1};
+int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP, MPIV_U8_FLIGHT, 0,
+                        0, 1};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -1387,6 +1392,15 @@ int mpiv_assemble_mpi_backward(const float* drgba, const int64_t gs[5], const fl
     return launched("mpiv_assemble_mpi_backward");
 }
 
+// render_netout_kernel's geometry (netout_geo = 100 * waves + 10 * rows + depth; automatic: 821)
+static int netout_geo() {
+    const int o = opt(kOptNetoutGeo);
+    switch (o) {
+        case 811: case 821: case 822: case 422: return o;
+        default: return 821;
+    }
+}
+
 // The assembly fused into the render (assemble.hip render_netout_kernel): pred/fg -> frames.
 int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* fg, const int64_t fs[4], int B, int H,
                            int W, int P, const float* homs, float* out, void* stream) {
@@ -1397,10 +1411,31 @@ int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* 
         return fail(MPIV_ERR_ARG, "%s: needs 2 <= H, W < 32764 and P <= %d", nm, kNMaxP);
     const NetStrides s{ps[0], ps[1], ps[2], ps[3], fs[0], fs[1], fs[2], fs[3]};
     const RenderGeom g = make_geom(H, W, P);
-    const int64_t nb = (int64_t)blocks(W, kNTX) * blocks(H, kNTY) * B;
+    const int geo = netout_geo();
+    const int NW = geo / 100, R = geo / 10 % 10;
+    const int64_t nb = (int64_t)blocks(W, kNTX) * blocks(H, NW * R) * B;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
-    if (g_route) return note_route(nb, kNThreads, "render_netout_kernel");
-    render_netout_kernel<<<(unsigned)nb, kNThreads, 0, S(stream)>>>(pred, fg, s, g, B, homs, out);
+    // buffer addressing when one batch element's pred / fg spans fit a 32-bit byte offset
+    NetStrides sb = s;
+    const int64_t pspan = ((int64_t)(2 * P + 2) * ps[1] + (int64_t)(H - 1) * ps[2] + (int64_t)(W - 1) * ps[3] + 1) * 4;
+    const int64_t fspan = ((int64_t)(H - 1) * fs[1] + (int64_t)(W - 1) * fs[2] + 2 * fs[3] + 1) * 4;
+    const bool buf = opt(kOptNetoutBuf) != 0 && pspan < (int64_t)kOOB && fspan < (int64_t)kOOB;
+    if (buf) {
+        sb.pred_bytes = (int)pspan;
+        sb.fg_bytes = (int)fspan;
+    }
+    if (g_route) return note_route(nb, 64 * NW, "render_netout_kernel<%d, %d, %d, %s>", NW, R, geo % 10, buf ? "true" : "false");
+    const unsigned nbu = (unsigned)nb;
+    hipStream_t q = S(stream);
+    switch (geo * 2 + (buf ? 1 : 0)) {
+#define MPIV_NETOUT(A, B_, C, D)                                                                           \
+    case (A * 100 + B_ * 10 + C) * 2 + D:                                                                  \
+        render_netout_kernel<A, B_, C, D><<<nbu, 64 * A, 0, q>>>(pred, fg, sb, g, B, homs, out);           \
+        break;
+        MPIV_NETOUT(8, 1, 1, 0) MPIV_NETOUT(8, 2, 1, 0) MPIV_NETOUT(8, 2, 2, 0) MPIV_NETOUT(4, 2, 2, 0)
+        MPIV_NETOUT(8, 1, 1, 1) MPIV_NETOUT(8, 2, 1, 1) MPIV_NETOUT(8, 2, 2, 1) MPIV_NETOUT(4, 2, 2, 1)
+#undef MPIV_NETOUT
+    }
     return launched(nm);
 }
 
@@ -1483,6 +1518,18 @@ int mpiv_pack_planes_u8(const uint8_t* mpi, const int64_t st[4], int H, int W, i
     const NativeStrides s{0, st[0], st[1], st[2], st[3]};
     pack_planes_u8_kernel<<<dim3(blocks(npix, kPackPix), blocks(P, kPackPl)), 256, 0, S(stream)>>>(
         mpi, s, H, W, P, make_fastdiv((unsigned)(W + 2 * kPad)), packed, npix);
+    return launched(nm);
+}
+
+int mpiv_unpack_planes_u8(const uint32_t* packed, int H, int W, int P, float* out, void* stream) {
+    const char* nm = "mpiv_unpack_planes_u8";
+    if (!packed || !out) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
+    if ((reinterpret_cast<uintptr_t>(packed) & 3) || !aligned16(out))
+        return fail(MPIV_ERR_ARG, "%s: alignment (packed 4 B, out 16 B)", nm);
+    const int64_t n = (int64_t)P * (H + 2 * kPad) * (W + 2 * kPad);
+    const int64_t nb = std::min<int64_t>(blocks(n, 256), 1 << 20);
+    unpack_u8_planes_kernel<<<(unsigned)nb, 256, 0, S(stream)>>>(packed, reinterpret_cast<float4*>(out), n);
     return launched(nm);
 }
 
@@ -1582,6 +1629,12 @@ int mpiv_render_packed_u8(const uint32_t* packed, int H, int W, int P, const flo
 int mpiv_render_packed_u8_ct(const uint32_t* packed, int H, int W, int P, int p_begin, int p_end, int back,
                              const float* homs, int V, float* ct, void* stream) {
     return render_u8_impl(packed, H, W, P, p_begin, p_end, back, homs, V, ct, true, stream);
+}
+
+int mpiv_mark(int tag, void* stream) {
+    if (tag < 1 || tag > 4096) return fail(MPIV_ERR_ARG, "mpiv_mark: tag must be in 1..4096");
+    mark_kernel<<<tag, 64, 0, S(stream)>>>();
+    return launched("mpiv_mark");
 }
 
 int mpiv_probe_gather(const float* window, size_t window_bytes, int iters, int blocks_, float* sink, void* stream) {

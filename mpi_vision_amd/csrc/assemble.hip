@@ -25,6 +25,7 @@ namespace mpiv {
 struct NetStrides {   // element strides
     int64_t pb, pc, py, px;   // pred [B, 2P+3, H, W]
     int64_t fb, fy, fx, fc;   // fg   [B, H, W, 3]
+    int pred_bytes = 0, fg_bytes = 0;  // one batch element's byte span (0: not buffer-addressable)
 };
 
 // one MPI texel of plane p at pixel (y, x) of batch element b
@@ -226,9 +227,8 @@ __global__ __launch_bounds__(kAbPix) void assemble_backward_dense_kernel(const f
 // frame is bit-identical to assemble + render.
 constexpr int kNTX = 64, kNTY = 8;
 constexpr int kNThreads = kNTX * kNTY;
-constexpr int kNCap = 1024;   // texels per staged box (16 KiB)
+constexpr int kNCap = 1024;   // texels per staged box of a 64x8 tile (16 KiB)
 constexpr int kNMaxP = 512;   // planes in the box table
-constexpr int kNFill = kNCap / kNThreads;
 
 // one texel of plane p at image texel (tx, ty), zero outside the image (grid_sample's
 // zero padding of the packed border)
@@ -276,29 +276,113 @@ __device__ __forceinline__ float4 net_assemble(const NetRaw& r) {
     return t;
 }
 
-__global__ __launch_bounds__(kNThreads) void render_netout_kernel(const float* __restrict__ pred,
-                                                                  const float* __restrict__ fg, NetStrides ns,
-                                                                  RenderGeom g, int V, const float* __restrict__ homs,
-                                                                  float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float4 s_tex[kNCap];
+// the same inputs split by lifetime: the plane's blend weight and alpha (w, a: from HBM, loaded
+// DEPTH planes ahead) and the plane-independent background / reference colour (mostly cache hits:
+// the neighbouring planes' boxes overlap, loaded one plane ahead)
+struct NetWA {
+    float w, a;
+};
+struct NetBF {
+    float b0, b1, b2, f0, f1, f2;
+    bool in;
+};
+
+__device__ __forceinline__ NetWA net_load_wa(const float* __restrict__ pred, const NetStrides& s, int H, int W, int P,
+                                             int b, int p, int tx, int ty) {
+    const int cx = min(max(tx, 0), W - 1), cy = min(max(ty, 0), H - 1);  // always valid memory
+    const float* pp = pred + (int64_t)b * s.pb + (int64_t)cy * s.py + (int64_t)cx * s.px;
+    return NetWA{pp[(int64_t)p * s.pc], pp[(int64_t)(P + p) * s.pc]};
+}
+
+__device__ __forceinline__ NetBF net_load_bf(const float* __restrict__ pred, const float* __restrict__ fg,
+                                             const NetStrides& s, int H, int W, int P, int b, int tx, int ty) {
+    NetBF r;
+    r.in = (unsigned)tx < (unsigned)W && (unsigned)ty < (unsigned)H;
+    const int cx = min(max(tx, 0), W - 1), cy = min(max(ty, 0), H - 1);
+    const float* pp = pred + (int64_t)b * s.pb + (int64_t)cy * s.py + (int64_t)cx * s.px;
+    const float* fp = fg + (int64_t)b * s.fb + (int64_t)cy * s.fy + (int64_t)cx * s.fx;
+    r.b0 = pp[(int64_t)(2 * P + 0) * s.pc];
+    r.b1 = pp[(int64_t)(2 * P + 1) * s.pc];
+    r.b2 = pp[(int64_t)(2 * P + 2) * s.pc];
+    r.f0 = fp[0];
+    r.f1 = fp[s.fc];
+    r.f2 = fp[2 * s.fc];
+    return r;
+}
+
+// The same loads through buffer resources with 32-bit offsets (one batch element's spans < 2 GiB,
+// render_netout_kernel<.., BUF = true>): a texel's address is one 32-bit offset shared by its
+// loads, each channel plane / colour a scalar offset -- the 64-bit address arithmetic of the
+// pointer loads was ~25 VALU per staged texel.
+struct NetRsrc {
+    __amdgpu_buffer_rsrc_t pred, fg;
+    int pc4, fc4;  // channel strides in bytes
+};
+
+__device__ __forceinline__ NetWA net_load_wa_buf(const NetRsrc& r, const NetStrides& s, int H, int W, int P, int p,
+                                                 int tx, int ty) {
+    const int cx = min(max(tx, 0), W - 1), cy = min(max(ty, 0), H - 1);
+    const int off = (cy * (int)s.py + cx * (int)s.px) * 4;
+    return NetWA{llvm_raw_buffer_load_f32(r.pred, off, p * r.pc4, 0), llvm_raw_buffer_load_f32(r.pred, off, (P + p) * r.pc4, 0)};
+}
+
+__device__ __forceinline__ NetBF net_load_bf_buf(const NetRsrc& r, const NetStrides& s, int H, int W, int P, int tx,
+                                                 int ty) {
+    NetBF q;
+    q.in = (unsigned)tx < (unsigned)W && (unsigned)ty < (unsigned)H;
+    const int cx = min(max(tx, 0), W - 1), cy = min(max(ty, 0), H - 1);
+    const int off = (cy * (int)s.py + cx * (int)s.px) * 4;
+    const int offf = (cy * (int)s.fy + cx * (int)s.fx) * 4;
+    q.b0 = llvm_raw_buffer_load_f32(r.pred, off, (2 * P) * r.pc4, 0);
+    q.b1 = llvm_raw_buffer_load_f32(r.pred, off, (2 * P + 1) * r.pc4, 0);
+    q.b2 = llvm_raw_buffer_load_f32(r.pred, off, (2 * P + 2) * r.pc4, 0);
+    q.f0 = llvm_raw_buffer_load_f32(r.fg, offf, 0, 0);
+    q.f1 = llvm_raw_buffer_load_f32(r.fg, offf, r.fc4, 0);
+    q.f2 = llvm_raw_buffer_load_f32(r.fg, offf, 2 * r.fc4, 0);
+    return q;
+}
+
+__device__ __forceinline__ float4 net_assemble2(const NetWA& q, const NetBF& r) {
+    return net_assemble(NetRaw{q.w, q.a, r.b0, r.b1, r.b2, r.f0, r.f1, r.f2, r.in});
+}
+
+
+
+// RPT rows per work-item: the block's tile is 64 x 8*RPT pixels (work-item (lane, wave) renders
+// rows wave, wave + 8, ...), its staged box holds kNCap * RPT texels.  Taller tiles mean fewer
+// blocks: at RPT = 2 a 1024x576 view is 576 blocks, all resident at once (3 per CU), where the
+// 1152 blocks of RPT = 1 ran in two rounds of a latency-bound per-plane loop (round 4: 0.14 ms).
+// NW waves per block (tile 64 x NW*RPT); the planes' w / a loads run DEPTH planes ahead (1: plane
+// p+1's while plane p is sampled), bg / fg one plane ahead.
+template <int NW, int RPT, int DEPTH, bool BUF>
+__global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __restrict__ pred,
+                                                                const float* __restrict__ fg, NetStrides ns,
+                                                                RenderGeom g, int V, const float* __restrict__ homs,
+                                                                float* __restrict__ out) {
+    constexpr int kThreads = 64 * NW;
+    constexpr int kTY = NW * RPT;
+    constexpr int kCap = 128 * kTY;  // texels per staged box: a 64 x 8 tile 1024 (its box at the swapped
+                                     // normalisation's x stretch 1.78: ~940; 64 x 16: up to ~1550)
+    constexpr int kFill = kCap / kThreads;
+    static_assert(DEPTH >= 1 && DEPTH <= 3, "planes in flight");
+    __shared__ __attribute__((aligned(16))) float4 s_tex[kCap];
     __shared__ int2 s_box[kNMaxP];  // per plane: (x_lo, y_lo), (rows, direct) as 16-bit pairs
     __shared__ int s_pitch;
     const int tiles_x = (g.W + kNTX - 1) / kNTX;
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
     const int v = lb % V;
     const int tile = lb / V;
-    const int tx0 = (tile % tiles_x) * kNTX, ty0 = (tile / tiles_x) * kNTY;
+    const int tx0 = (tile % tiles_x) * kNTX, ty0 = (tile / tiles_x) * kTY;
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
-    const int x = tx0 + lane, y = ty0 + wave;
-    const bool active = x < g.W && y < g.H;
+    const int x = tx0 + lane;
     const float* hv = homs + (int64_t)v * g.P * 9;
     const int P = g.P;
     if (threadIdx.x == 0) s_pitch = 0;
     __syncthreads();
     // ---- footprint boxes (thread q -> plane q/4, corner q%4) + the tile's division proof
-    const int cx1 = min(tx0 + kNTX - 1, g.W - 1), cy1 = min(ty0 + kNTY - 1, g.H - 1);
+    const int cx1 = min(tx0 + kNTX - 1, g.W - 1), cy1 = min(ty0 + kTY - 1, g.H - 1);
     bool ok_div = true;
-    for (int q0 = 0; q0 < 4 * P; q0 += kNThreads) {
+    for (int q0 = 0; q0 < 4 * P; q0 += kThreads) {
         const int q = q0 + (int)threadIdx.x;
         const bool live = q < 4 * P;
         const int pl = live ? (q >> 2) : 0;
@@ -328,7 +412,7 @@ __global__ __launch_bounds__(kNThreads) void render_netout_kernel(const float* _
             const int xl = ok ? max((int)xmin - 1, -2) : 0, xh = ok ? min((int)xmax + 2, g.W + 1) : 0;
             const int yl = ok ? max((int)ymin - 1, -2) : 0, yh = ok ? min((int)ymax + 2, g.H + 1) : 0;
             const int width = xh - xl + 1, rows = yh - yl + 1;
-            const int direct = (!ok || width < 2 || rows < 2 || width > 256 || width * rows > kNCap) ? 1 : 0;
+            const int direct = (!ok || width < 2 || rows < 2 || width > 256 || width * rows > kCap) ? 1 : 0;
             s_box[q >> 2] = make_int2((xl & 0xFFFF) | (yl << 16), rows | (direct << 16));
             if (!direct) atomicMax(&s_pitch, width);
         }
@@ -339,86 +423,136 @@ __global__ __launch_bounds__(kNThreads) void render_netout_kernel(const float* _
         const int2 bb = s_box[i];
         return make_int4((int)(short)(bb.x & 0xFFFF), bb.x >> 16, bb.y & 0xFFFF, bb.y >> 16);
     };
-    auto staged = [&](const int4& bx) { return bx.w == 0 && bx.z * pitch <= kNCap; };
+    auto staged = [&](const int4& bx) { return bx.w == 0 && bx.z * pitch <= kCap; };
     // this thread's box texels: idx = tid + 512*j -> (row, col) with the common pitch
-    int row_j[kNFill], col_j[kNFill];
+    int row_j[kFill], col_j[kFill];
 #pragma unroll
-    for (int j = 0; j < kNFill; ++j) {
-        const int idx = (int)threadIdx.x + kNThreads * j;
+    for (int j = 0; j < kFill; ++j) {
+        const int idx = (int)threadIdx.x + kThreads * j;
         row_j[j] = pitch > 0 ? idx / pitch : 0;
         col_j[j] = idx - row_j[j] * pitch;
     }
-    NetRaw stg[kNFill];
-    auto fetch = [&](int p, const int4& bx) {
+    NetWA wa[DEPTH][kFill];
+    NetBF bf[kFill];
+    NetRsrc rs;
+    if (BUF) {
+        rs.pred = make_rsrc(pred + (int64_t)v * ns.pb, ns.pred_bytes);
+        rs.fg = make_rsrc(fg + (int64_t)v * ns.fb, ns.fg_bytes);
+        rs.pc4 = (int)ns.pc * 4;
+        rs.fc4 = (int)ns.fc * 4;
+    }
+    auto fetch_wa = [&](NetWA (&st)[kFill], int p, const int4& bx) {
         const int nfp = bx.z * pitch;
 #pragma unroll
-        for (int j = 0; j < kNFill; ++j)
-            if (kNThreads * j < nfp)  // block-uniform
-                stg[j] = net_load(pred, fg, ns, g.H, g.W, P, v, p, bx.x + col_j[j], bx.y + row_j[j]);
+        for (int j = 0; j < kFill; ++j)
+            if (kThreads * j < nfp)  // block-uniform
+                st[j] = BUF ? net_load_wa_buf(rs, ns, g.H, g.W, P, p, bx.x + col_j[j], bx.y + row_j[j])
+                            : net_load_wa(pred, ns, g.H, g.W, P, v, p, bx.x + col_j[j], bx.y + row_j[j]);
     };
-    auto commit = [&](const int4& bx) {
+    auto fetch_bf = [&](const int4& bx) {
         const int nfp = bx.z * pitch;
 #pragma unroll
-        for (int j = 0; j < kNFill; ++j)
-            if ((int)threadIdx.x + kNThreads * j < nfp) s_tex[threadIdx.x + kNThreads * j] = net_assemble(stg[j]);
+        for (int j = 0; j < kFill; ++j)
+            if (kThreads * j < nfp)
+                bf[j] = BUF ? net_load_bf_buf(rs, ns, g.H, g.W, P, bx.x + col_j[j], bx.y + row_j[j])
+                            : net_load_bf(pred, fg, ns, g.H, g.W, P, v, bx.x + col_j[j], bx.y + row_j[j]);
     };
-    const float fx = (float)x, fy = (float)y;
-    float cr = -0.0f, cg = -0.0f, cb = -0.0f;  // plane 0 replaces it exactly (render.hip)
-    int4 bx_next = box_of(0);
-    if (staged(bx_next)) fetch(0, bx_next);
-    for (int p = 0; p < P; ++p) {
-        const int4 bx = bx_next;
-        if (staged(bx)) commit(bx);
+    auto commit = [&](const NetWA (&st)[kFill], const int4& bx) {
+        const int nfp = bx.z * pitch;
+#pragma unroll
+        for (int j = 0; j < kFill; ++j)
+            if ((int)threadIdx.x + kThreads * j < nfp) s_tex[threadIdx.x + kThreads * j] = net_assemble2(st[j], bf[j]);
+    };
+    const float fx = (float)x;
+    float cr[RPT], cg[RPT], cb[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) cr[r] = cg[r] = cb[r] = -0.0f;  // plane 0 replaces it exactly (render.hip)
+    auto sample = [&](int p, const int4& bx) {
+        const float* hp = hv + (int64_t)p * 9;
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            const int y = ty0 + wave + NW * r;
+            if (x < g.W && y < g.H) {
+                const float fy = (float)y;
+                float px, py;
+                if (proven)
+                    render_pos_fast<false>(hp, fx, fy, g, px, py);
+                else
+                    render_pos<true>(hp, fx, fy, g, px, py);
+                TapSet ts;
+                bool hit = false;
+                if (staged(bx)) {
+                    const LdsBox box = make_lds_box(bx.x, bx.y, bx.z, pitch, g.W, g.H);
+                    hit = lds_issue(s_tex, box, px, py, ts);
+                }
+                if (!hit) {  // assemble the four taps directly (rare)
+                    const float fx0 = floorf(px), fy0 = floorf(py);
+                    const float wx = px - fx0, ex = 1.0f - wx;
+                    const float wy = py - fy0, sy = 1.0f - wy;
+                    ts.nw = sy * ex;
+                    ts.ne = sy * wx;
+                    ts.sw = wy * ex;
+                    ts.se = wy * wx;
+                    const int ix = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)g.W);
+                    const int iy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)g.H);
+                    const float4 t0 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix, iy);
+                    const float4 t1 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix + 1, iy);
+                    const float4 t2 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix, iy + 1);
+                    const float4 t3 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix + 1, iy + 1);
+                    ts.a = {t0.x, t0.y, t0.z, t0.w};
+                    ts.b = {t1.x, t1.y, t1.z, t1.w};
+                    ts.c = {t2.x, t2.y, t2.z, t2.w};
+                    ts.d = {t3.x, t3.y, t3.z, t3.w};
+                }
+                const f32x4 sm = blend_taps(ts);
+                const float a = p == 0 ? 1.0f : sm[3];
+                const float om = 1.0f - a;
+                cr[r] = over(sm[0], a, om, cr[r]);
+                cg[r] = over(sm[1], a, om, cg[r]);
+                cb[r] = over(sm[2], a, om, cb[r]);
+            }
+        }
+    };
+    // plane p: its w / a (fetched DEPTH planes earlier into ring slot p % DEPTH) and bg / fg (fetched
+    // one plane earlier) are assembled into LDS; then the slot takes plane p + DEPTH's w / a and bf
+    // plane p + 1's bg / fg, in flight while plane p is sampled
+    auto step = [&](int p, NetWA (&st)[kFill]) {
+        const int4 bx = box_of(p);
+        if (staged(bx)) commit(st, bx);
         __syncthreads();  // plane p's box is in LDS
         if (p + 1 < P) {
-            bx_next = box_of(p + 1);
-            if (staged(bx_next)) fetch(p + 1, bx_next);  // in flight while plane p is sampled
+            const int4 bn = box_of(p + 1);
+            if (staged(bn)) fetch_bf(bn);
         }
-        if (active) {
-            float px, py;
-            if (proven)
-                render_pos_fast<false>(hv + (int64_t)p * 9, fx, fy, g, px, py);
-            else
-                render_pos<true>(hv + (int64_t)p * 9, fx, fy, g, px, py);
-            TapSet ts;
-            bool hit = false;
-            if (staged(bx)) {
-                const LdsBox box = make_lds_box(bx.x, bx.y, bx.z, pitch, g.W, g.H);
-                hit = lds_issue(s_tex, box, px, py, ts);
-            }
-            if (!hit) {  // assemble the four taps directly (rare)
-                const float fx0 = floorf(px), fy0 = floorf(py);
-                const float wx = px - fx0, ex = 1.0f - wx;
-                const float wy = py - fy0, sy = 1.0f - wy;
-                ts.nw = sy * ex;
-                ts.ne = sy * wx;
-                ts.sw = wy * ex;
-                ts.se = wy * wx;
-                const int ix = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)g.W);
-                const int iy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)g.H);
-                const float4 t0 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix, iy);
-                const float4 t1 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix + 1, iy);
-                const float4 t2 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix, iy + 1);
-                const float4 t3 = net_texel(pred, fg, ns, g.H, g.W, P, v, p, ix + 1, iy + 1);
-                ts.a = {t0.x, t0.y, t0.z, t0.w};
-                ts.b = {t1.x, t1.y, t1.z, t1.w};
-                ts.c = {t2.x, t2.y, t2.z, t2.w};
-                ts.d = {t3.x, t3.y, t3.z, t3.w};
-            }
-            const f32x4 sm = blend_taps(ts);
-            const float a = p == 0 ? 1.0f : sm[3];
-            const float om = 1.0f - a;
-            cr = over(sm[0], a, om, cr);
-            cg = over(sm[1], a, om, cg);
-            cb = over(sm[2], a, om, cb);
+        if (p + DEPTH < P) {
+            const int4 bn = box_of(p + DEPTH);
+            if (staged(bn)) fetch_wa(st, p + DEPTH, bn);
         }
+        sample(p, bx);
         __syncthreads();  // every sample of plane p has read the box
+    };
+    if (staged(box_of(0))) fetch_bf(box_of(0));
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+        if (d < P && staged(box_of(d))) fetch_wa(wa[d], d, box_of(d));
+    int p = 0;
+    for (; p + DEPTH <= P; p += DEPTH) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) step(p + d, wa[d]);  // static ring slots
     }
-    if (!active) return;
-    const int64_t o = (((int64_t)v * g.H + y) * g.W + x) * 3;
-    out[o + 0] = cr;
-    out[o + 1] = cg;
-    out[o + 2] = cb;
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+        if (p + d < P) step(p + d, wa[d]);
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+        const int y = ty0 + wave + NW * r;
+        if (x < g.W && y < g.H) {
+            const int64_t o = (((int64_t)v * g.H + y) * g.W + x) * 3;
+            out[o + 0] = cr[r];
+            out[o + 1] = cg[r];
+            out[o + 2] = cb[r];
+        }
+    }
 }
 
 }  // namespace mpiv

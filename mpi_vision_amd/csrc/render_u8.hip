@@ -383,6 +383,20 @@ __global__ __launch_bounds__(256) void pack_planes_u8_kernel(const uint8_t* __re
     }
 }
 
+// Packed u8 planes -> packed float planes (the same padded [P][H+4][W+4] layout as
+// mpiv_pack_planes), every channel RN(u8/255) exactly (u8_unit): the texels of the float MPI
+// u8.float() / 255 the reference renders.  The many-view route of the u8 render: at 125 views per
+// launch the float rows kernel (texture path and VALU co-limited) beats the u8 kernel (VALU-bound
+// on the per-tap conversion), so a camera path converts its 8-bit MPI once.
+// One texel per work-item: a 4-B read, a 16-B write.
+__global__ __launch_bounds__(256) void unpack_u8_planes_kernel(const unsigned* __restrict__ src,
+                                                               float4* __restrict__ dst, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const unsigned t = src[i];
+        dst[i] = make_float4(u8_unit(t & 255u), u8_unit((t >> 8) & 255u), u8_unit((t >> 16) & 255u), u8_unit(t >> 24));
+    }
+}
+
 // Counter-based synthetic u8 MPI (synth.hip's hash; bytes = top 8 bits of each channel's
 // hash, plane 0 alpha 255), straight into the packed u8 layout: a config-5 shard per GPU.
 __global__ __launch_bounds__(256) void synth_packed_u8_kernel(uint32_t seed, int H, int W, int p_begin,

@@ -130,8 +130,9 @@ def test_fused_net_output_render(dev):
     assert_bits(got.cpu().numpy(), want.cpu().numpy(), "fused assemble + render")
 
 
+@pytest.mark.parametrize("geo", [0, 811, 821, 822, 422, -811, -821])
 @pytest.mark.parametrize("case", ["odd", "extreme", "strided", "big"])
-def test_fused_net_output_render_cases(case, dev):
+def test_fused_net_output_render_cases(case, geo, dev, kopts):
     """The one-kernel assembly + render (render_netout_kernel) against the two-step drop-ins
     (bit-exact, themselves pinned to the notebook / reference goldens): partial tiles, views
     with planes behind the camera (taps assembled directly, boxes that do not fit), a
@@ -157,6 +158,8 @@ def test_fused_net_output_render_cases(case, dev):
     planes = configs.f32(mv.inv_depths(0.5 if case == "extreme" else 1, 100, P)).to(dev)
     dep = {"mpi_planes": torch.zeros((B, P), device=dev), "ref_img": ref}
     want = mv.mpi_render_view_torch(mv.mpi_from_net_output(pred, dep), poses, planes, K)
+    # 0: automatic; 100 * waves + 10 * rows per work-item + planes in flight; negative: pointer loads
+    kopts(netout_geo=abs(geo), netout_buf=0 if geo < 0 else 1)
     got = mv.mpi_render_net_output_torch(pred, ref, poses, planes, K)
     torch.cuda.synchronize()
-    assert_bits(got.cpu().numpy(), want.cpu().numpy(), f"fused assemble + render ({case})")
+    assert_bits(got.cpu().numpy(), want.cpu().numpy(), f"fused assemble + render ({case}, geo {geo})")

@@ -142,3 +142,43 @@ def test_u8_render_rejects_unknown_row_variants(dev, kopts):
         kopts(render_tile=rows)
         with pytest.raises(RuntimeError, match="not a u8 render variant"):
             _lib.render_packed_u8(packed, homs)
+
+
+def test_u8_unpack_is_exact_float_of_every_byte(dev):
+    """mpiv_unpack_planes_u8: every channel becomes RN(u8/255) (all 256 values, border zeros)."""
+    H, W, P = 6, 16, 5
+    g = torch.Generator().manual_seed(3)
+    u8 = torch.randint(0, 256, (H, W, P, 4), generator=g, dtype=torch.uint8)
+    u8.view(-1)[:256] = torch.arange(256, dtype=torch.int32).to(torch.uint8)
+    pk = _lib.pack_planes_u8(u8.to(dev))
+    f = _lib.unpack_planes_u8(pk)
+    want = _lib.pack_planes((u8.float() / 255).to(dev))  # the float MPI's packed layout, same border
+    assert_bits(f.cpu().numpy(), want.cpu().numpy(), "unpack")
+
+
+def test_u8_many_views_route_through_float_copy(large, dev):
+    """Launches of >= U8_FLOAT_MIN_VIEWS views render the MPI's exact float copy with the float
+    kernel: the reference's config-1 goldens at 40 views (the two golden poses, 20 times each),
+    and the same frames as the u8 kernel; the copy is made once per MPI (memo) and again after an
+    in-place edit."""
+    u8 = _test_mpi_u8().to(dev)
+    V = 40
+    assert V >= _lib.U8_FLOAT_MIN_VIEWS
+    pose = torch.tensor(large["c1_pose"]).to(dev)[torch.arange(V) % 2]
+    K = torch.tensor(large["c1_K"]).to(dev)[torch.arange(V) % 2]
+    depths = torch.tensor(large["c1_depths"]).to(dev)
+    out = mvu.mpi_render_view_u8(u8.expand(V, *u8.shape[1:]), pose, depths, K)
+    assert_bits(out.cpu().numpy(), large["c1_out"][np.arange(V) % 2], "40 views of the golden poses")
+    homs = _host.render_homographies(pose.cpu(), depths.cpu(), K.cpu(), V)
+    pk = _lib.pack_planes_u8(u8[0])
+    a = _lib.render_packed_u8(pk, homs, route_float=True)
+    f1 = _lib.u8_float_copy(pk)
+    assert _lib.u8_float_copy(pk) is f1  # memoised
+    b = _lib.render_packed_u8(pk, homs, route_float=False)
+    assert_bits(a.cpu().numpy(), b.cpu().numpy(), "float route vs u8 kernel")
+    pk.view(torch.uint8)[..., 0] ^= 1  # in place: a new copy, new frames
+    assert _lib.u8_float_copy(pk) is not f1
+    c = _lib.render_packed_u8(pk, homs, route_float=True)
+    d = _lib.render_packed_u8(pk, homs, route_float=False)
+    assert_bits(c.cpu().numpy(), d.cpu().numpy(), "after an in-place edit")
+    assert not torch.equal(a, c)

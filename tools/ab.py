@@ -335,6 +335,32 @@ def chunkpar(dev, it):
 DEF = [("default", {})]
 
 
+def netout(dev, it):
+    """render_netout_kernel (network output -> view, bench.py netout_leg's case) with 1 / 2 / 4 rows
+    per work-item; every variant's frame is checked against the two-step assemble + render."""
+    c = configs.config2()
+    H, W, P = c["H"], c["W"], c["P"]
+    g = torch.Generator(device=dev).manual_seed(c["seed"])
+    pred = torch.rand((1, 2 * P + 3, H, W), generator=g, device=dev) * 2 - 1
+    fg = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    for k in (5, 20):
+        homs = _host.render_homographies(configs.f32(c["poses"][k:k + 1]), configs.f32(c["depths"]),
+                                         configs.f32([c["K"]]), 1).to(dev)
+        out = torch.empty((1, H, W, 3), device=dev)
+        fn = lambda: _lib._call("mpiv_render_net_output", pred, _lib._strides(pred), fg, _lib._strides(fg), 1,  # noqa: E731
+                                H, W, P, homs, out, _lib._stream(dev))
+        two = _lib.render(_lib.assemble_mpi(pred, fg, P), homs)
+        variants = [(f"geo{gg}b{bb}", {"netout_geo": gg, "netout_buf": bb}) for gg in (811, 821, 822, 422) for bb in (0, 1)]
+        for label, opts in variants:
+            with _lib.debug(**opts):
+                out.zero_()
+                fn()
+                torch.cuda.synchronize()
+                print(json.dumps({"exp": "netout bit-exact", "pose": k, "variant": label,
+                                  "same": bool(torch.equal(out.view(torch.int32), two.view(torch.int32)))}), flush=True)
+        run(f"netout 1024x576x32, pose {k}", variants, fn, H * W * ((2 * P + 3) * 4 + 24), it)
+
+
 def dflt(dev, it):
     """The default routes of the training path (in-place render, training forward, backward with
     checkpoints) -- for A/B across library builds (MPIV_LIB, tools/gpu_ab_any.sh)."""

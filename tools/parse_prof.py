@@ -4,8 +4,12 @@
     python tools/parse_prof.py gpurun_out/prof <tag>
 
 Every libmpiv dispatch of the profiled bench.py run is grouped by its kernel name
-(template arguments included, as mpiv_route reports it) and its grid size in work-items,
-which separates the bench's legs even when two legs launch the same kernel.  Per group:
+(template arguments included, as mpiv_route reports it) and its grid size in work-items, and
+again per bench phase tag: bench.py launches a marker kernel (mpiv_mark) before each timed region,
+and every later dispatch belongs to the last marker's tag (configs.PROF_TAGS), which separates
+sub-legs that launch the same kernel and grid (the backward with and without checkpoints, in plane
+groups; config 3's drop-in and its timed launches).  Entries without "tag" aggregate every dispatch
+of that kernel and grid.  Per group:
 rocprof's call count and average / min / max duration (kernel-trace pass) and, from the
 separate --pmc passes, per-dispatch averages of
 
@@ -57,26 +61,53 @@ def rows(path_glob):
     return out
 
 
-def trace_groups(trace_rows):
-    g = {}
-    for r in trace_rows:
-        if "mpiv::" not in r.get("Kernel_Name", ""):
+def _tagged(rows, grid_of):
+    """(row, tag) for every libmpiv dispatch in submission order (Dispatch_Id): the tag is the name
+    of the last mark_kernel dispatched before it (bench.py phase markers, grid = tag x 64), None
+    before the first marker."""
+    from mpi_vision_amd.configs import PROF_TAGS
+    names = {v: k for k, v in PROF_TAGS.items()}
+    tag = None
+    for r in sorted(rows, key=lambda r: int(r["Dispatch_Id"])):
+        name = r.get("Kernel_Name", "")
+        if "mpiv::" not in name:
             continue
-        grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
-        key = (short_name(r["Kernel_Name"]), grid)
-        g.setdefault(key, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        if "mark_kernel" in name:
+            tag = names.get(grid_of(r) // 64)
+            continue
+        yield r, tag
+
+
+def trace_groups(trace_rows):
+    """{(kernel, grid, tag): [duration ns]} plus the untagged aggregate {(kernel, grid, None): ...}."""
+    g = {}
+    grid_of = lambda r: int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])  # noqa: E731
+    for r, tag in _tagged(trace_rows, grid_of):
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        k = (short_name(r["Kernel_Name"]), grid_of(r))
+        g.setdefault(k + (None,), []).append(d)
+        if tag is not None:
+            g.setdefault(k + (tag,), []).append(d)
     return g
 
 
 def counter_groups(counter_rows):
-    """{(kernel, grid): {counter: [per-dispatch value]}}"""
+    """{(kernel, grid, tag): {counter: [per-dispatch value]}} (tag None: every dispatch)"""
     per = {}
+    # one row per (dispatch, counter): the marker logic needs one row per dispatch, so tag the
+    # dispatch ids first
+    first = {}
     for r in counter_rows:
-        if "mpiv::" not in r.get("Kernel_Name", ""):
+        first.setdefault(r["Dispatch_Id"], r)
+    tags = {r["Dispatch_Id"]: t for r, t in _tagged(list(first.values()), lambda r: int(r["Grid_Size"]))}
+    for r in counter_rows:
+        if "mpiv::" not in r.get("Kernel_Name", "") or "mark_kernel" in r["Kernel_Name"]:
             continue
-        key = (short_name(r["Kernel_Name"]), int(r["Grid_Size"]))
-        d = per.setdefault(key, {}).setdefault(r["Counter_Name"], {})
-        d[r["Dispatch_Id"]] = d.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+        k = (short_name(r["Kernel_Name"]), int(r["Grid_Size"]))
+        tag = tags.get(r["Dispatch_Id"])
+        for key in [k + (None,)] + ([k + (tag,)] if tag is not None else []):
+            d = per.setdefault(key, {}).setdefault(r["Counter_Name"], {})
+            d[r["Dispatch_Id"]] = d.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return {k: {c: list(v.values()) for c, v in cs.items()} for k, cs in per.items()}
 
 
@@ -98,9 +129,11 @@ def main():
         for k, cs in counter_groups(rows(os.path.join(out_dir, p, "**", "*counter_collection.csv"))).items():
             cg.setdefault(k, {}).update(cs)
     launches = []
-    for key in sorted(set(tg) | set(cg)):
-        kern, grid = key
+    for key in sorted(set(tg) | set(cg), key=lambda k: (k[0], k[1], k[2] or "")):
+        kern, grid, tag = key
         e = {"kernel": kern, "grid": grid}
+        if tag is not None:
+            e["tag"] = tag
         d = tg.get(key)
         if d:
             e.update(calls=len(d), avg_ns=mean(d), min_ns=min(d), max_ns=max(d))
