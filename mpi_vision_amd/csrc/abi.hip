@@ -8,6 +8,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <algorithm>
+#include <mutex>
 
 #include "../../include/mpiv.h"
 
@@ -104,6 +105,12 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //   bwd_fb_blocks=k    (A/B build) the backward fallback launches k blocks instead of the resident count
 //   netout_geo=WRD     render_netout_kernel<W, R, D>: W waves per block, R rows per work-item
 //                      (64 x W*R tiles), D planes' w / a loads in flight (e.g. 821; 0 = automatic)
+//   sweep_band=0|1     (A/B build) mpiv_plane_sweep[_into]'s LDS-staged route: one box per 4-row tile
+//                      (plane_sweep_dlane_kernel, 0 = default) or bands of 8 tiles with the source rows
+//                      in an LDS ring (plane_sweep_band_kernel: measured 15-20 % slower)
+//   bwd_overlap=0|1    (A/B build) render backward of views with several plane groups: sequential groups
+//                      (0 = default) or the overlapped schedule (group k's gather on a second stream beside
+//                      group k-1's chain, two d-sample windows: measured no faster)
 //   netout_buf=0|1     render_netout_kernel's staged loads through pointers (0) or buffer resources
 //                      with 32-bit offsets (1, default where the spans fit)
 //   bwd_margin=k       the tile gather's pixel-window margin in 1/64 pixel (default 16);
@@ -115,13 +122,13 @@ enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOpt
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
                 kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kOptU8Flight, kOptBwdGroup,
-                kOptNetoutGeo, kOptNetoutBuf, kNumOpts };
+                kOptNetoutGeo, kOptNetoutBuf, kOptBwdOverlap, kOptSweepBand, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
                                          "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode",
-                                         "chunk_strip", "u8_flight", "bwd_group", "netout_geo", "netout_buf"};
+                                         "chunk_strip", "u8_flight", "bwd_group", "netout_geo", "netout_buf", "bwd_overlap", "sweep_band"};
 #ifndef MPIV_CHUNK_STRIP
 #define MPIV_CHUNK_STRIP 1  // round 4: 0.506 vs 0.64 ms in place (profiles/r04j_strip*_ab.jsonl)
 #endif
@@ -129,9 +136,9 @@ const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_nat
 #define MPIV_U8_FLIGHT 0
 #endif
 const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP,
-                                    MPIV_U8_FLIGHT, 0, 0, 1};
+                                    MPIV_U8_FLIGHT, 0, 0, 1, 0, 0};
 int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP, MPIV_U8_FLIGHT, 0,
-                        0, 1};
+                        0, 1, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -153,6 +160,7 @@ bool ab_only(int o, int v) {
         case kOptSweepRows: return v == 6 || v == 8;
         case kOptBwdGather: return v == 1 || v == 2 || v == 3;
         case kOptBwdPollLimit: case kOptBwdFbBlocks: case kOptBwdFbMode: return v != 0;
+        case kOptBwdOverlap: case kOptSweepBand: return v != 0;
         default: return false;
     }
 }
@@ -670,7 +678,10 @@ int bwd_group_planes(int H, int W, int P) {
 // forward that fills ckpt when the caller has no checkpoints and the view has several groups)
 // dsp: planes whose d samples are resident (P: one group; bwd_group_planes: the smallest); the
 // fallback's bucket arrays always take one group of bwd_group_planes (its plane chunk)
-size_t bwd_layout(int H, int W, int P, int dsp, char* base, BwdWs* ws, float4** gbuf = nullptr) {
+// nwin: d-sample windows (2: the overlapped schedule, mpiv_render_backward -- group k's gather reads
+// one window while group k-1's chain fills the other; each window has its own counters, ws2)
+size_t bwd_layout(int H, int W, int P, int dsp, char* base, BwdWs* ws, float4** gbuf = nullptr, int nwin = 1,
+                  BwdWs* ws2 = nullptr) {
     const size_t hw = (size_t)H * W;
     const int pc = bwd_group_planes(H, W, P);
     const size_t nk = (size_t)pc * (H + 1) * (W + 1);
@@ -685,7 +696,10 @@ size_t bwd_layout(int H, int W, int P, int dsp, char* base, BwdWs* ws, float4** 
     char* truth = take(kCtrSlots * 8);
     char* found = take(kCtrSlots * 8);
     char* flag = take(32);
-    char* ds = take((size_t)dsp * hw * 16);
+    char* truth2 = take(nwin > 1 ? kCtrSlots * 8 : 0);  // the second window's counters (same carve-up)
+    char* found2 = take(nwin > 1 ? kCtrSlots * 8 : 0);
+    char* flag2 = take(nwin > 1 ? 32 : 0);
+    char* ds = take((size_t)nwin * dsp * hw * 16);
     char* ckpt = take(nchunk * hw * 16);
     char* inv = take((size_t)P * 12 * 4);
     char* gb = take(dsp < P ? hw * 16 : 0);
@@ -713,8 +727,40 @@ size_t bwd_layout(int H, int W, int P, int dsp, char* base, BwdWs* ws, float4** 
         ws->ids = reinterpret_cast<int*>(ids);
         ws->bsum = reinterpret_cast<int*>(bsum);
         ws->big = reinterpret_cast<int*>(big);
+        ws->vcount = ws->flag + 4;
+        if (ws2) {
+            *ws2 = *ws;
+            ws2->ds = reinterpret_cast<float4*>(ds + (size_t)dsp * hw * 16);
+            ws2->truth = reinterpret_cast<unsigned long long*>(truth2);
+            ws2->found = reinterpret_cast<unsigned long long*>(found2);
+            ws2->flag = reinterpret_cast<int*>(flag2);
+        }
     }
     return off;
+}
+
+// The overlapped backward's second stream and its events, per device (created on first use; the
+// schedule's enqueue runs under g_aux_mu, so concurrent callers never interleave their records
+// and waits on the shared events)
+struct BwdAux {
+    hipStream_t s = nullptr;
+    hipEvent_t chain[2] = {}, done[2] = {}, view = nullptr;
+    bool ok = false, tried = false;
+};
+BwdAux g_aux[64];
+std::mutex g_aux_mu;
+
+BwdAux* bwd_aux(int dev) {  // call with g_aux_mu held
+    BwdAux& a = g_aux[dev];
+    if (!a.tried) {
+        a.tried = true;
+        a.ok = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; i < 2 && a.ok; ++i)
+            a.ok = hipEventCreateWithFlags(&a.chain[i], hipEventDisableTiming) == hipSuccess &&
+                   hipEventCreateWithFlags(&a.done[i], hipEventDisableTiming) == hipSuccess;
+        a.ok = a.ok && hipEventCreateWithFlags(&a.view, hipEventDisableTiming) == hipSuccess;
+    }
+    return a.ok ? &a : nullptr;
 }
 
 
@@ -724,7 +770,12 @@ size_t bwd_layout(int H, int W, int P, int dsp, char* base, BwdWs* ws, float4** 
 // bwd_group test hook asks for groups
 size_t mpiv_render_backward_workspace_size(int H, int W, int P) {
     if (H <= 0 || W <= 0 || P <= 0) return 0;
-    return bwd_layout(H, W, P, opt(kOptBwdGroup) > 0 ? bwd_group_planes(H, W, P) : P, nullptr, nullptr);
+    // the one-group schedule's, or (bwd_group test hook) one window of that group size; with room for
+    // the overlapped schedule's two windows when it is selected (A/B build, bwd_overlap=1)
+    const size_t one = bwd_layout(H, W, P, opt(kOptBwdGroup) > 0 ? bwd_group_planes(H, W, P) : P, nullptr, nullptr);
+    const int gp = bwd_group_planes(H, W, P);
+    return MPIV_AB && opt(kOptBwdOverlap) != 0 && gp < P
+               ? std::max(one, bwd_layout(H, W, P, gp, nullptr, nullptr, nullptr, 2)) : one;
 }
 
 // the smallest workspace: plane groups of bwd_group_planes (config 4: 1.3 GB instead of 3.0)
@@ -760,12 +811,20 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         return fail(MPIV_ERR_ARG, "%s: MPI too large for one backward launch", nm);
     // plane groups: one (every plane's d samples resident) when the workspace holds it, else
     // groups of bwd_group_planes (mpiv_render_backward_workspace_size / _size_min)
-    const int GP = (opt(kOptBwdGroup) > 0 || ws_bytes < bwd_layout(H, W, P, P, nullptr, nullptr))
-                       ? bwd_group_planes(H, W, P) : P;
+    // Overlapped (round 5, default for views of more than one group): groups of bwd_group_planes in two
+    // d-sample windows, group k's gather / check / fallback on a second stream while group k-1's chain
+    // runs on the caller's (the chain is texture-path-bound, the gather latency-bound), when the
+    // workspace holds two windows (the default workspace does)
+    const bool fast2 = H >= 2 && W >= 2;
+    const int GPo = bwd_group_planes(H, W, P);
+    const bool overlap = MPIV_AB && opt(kOptBwdOverlap) != 0 && fast2 && GPo < P &&
+                         ws_bytes >= bwd_layout(H, W, P, GPo, nullptr, nullptr, nullptr, 2);
+    const int GP = overlap ? GPo : (opt(kOptBwdGroup) > 0 || ws_bytes < bwd_layout(H, W, P, P, nullptr, nullptr))
+                                       ? bwd_group_planes(H, W, P) : P;
     const int G = (P + GP - 1) / GP;
-    BwdWs ws;
+    BwdWs ws, ws2;
     float4* gbuf = nullptr;
-    const size_t need = bwd_layout(H, W, P, GP, static_cast<char*>(workspace), &ws, &gbuf);
+    const size_t need = bwd_layout(H, W, P, GP, static_cast<char*>(workspace), &ws, &gbuf, overlap ? 2 : 1, &ws2);
     if (ws_bytes < need) return fail(MPIV_ERR_ARG, "%s: workspace too small (%zu < %zu bytes)", nm, ws_bytes, need);
     const RenderGeom g = make_geom(H, W, P);
     const ChunkGeom cg{(int)(st[1] / 4), (int)(st[2] / 4), (int)rec};
@@ -813,8 +872,69 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const unsigned long long tick_limit =
         60000ull * (unsigned long long)__atomic_load_n(&s_clock_khz[dev], __ATOMIC_RELAXED);
     const int fb_mode = opt(kOptBwdFbMode);
-    if (hipMemsetAsync(ws.truth, 0, 2 * kCtrSlots * 8 + 256, q) != hipSuccess)  // truth, found (adjacent)
+    // truth, found, flag (adjacent), and the second window's set after them
+    if (hipMemsetAsync(ws.truth, 0, overlap ? 2 * (2 * kCtrSlots * 8 + 256) : 2 * kCtrSlots * 8 + 256, q) != hipSuccess)
         return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
+    if (overlap) {
+        std::lock_guard<std::mutex> lk(g_aux_mu);
+        BwdAux* ax = bwd_aux(dev);
+        if (ax) {
+            hipStream_t a = ax->s;
+            bool ok = true;
+            auto chk = [&](hipError_t e) { ok = ok && e == hipSuccess; };
+            BwdWs win[2] = {ws, ws2};
+            win[0].vcount = win[1].vcount = nullptr;  // bwd_poison_kernel counts the aborted views
+            for (int v = 0; v < V && ok; ++v) {
+                const float* hv = homs + (int64_t)v * P * 9;
+                const float* dv = dout + (int64_t)v * HW * 3;
+                const float* mv = mpi + (int64_t)v * st[0];
+                float4* gv = reinterpret_cast<float4*>(dmpi) + (int64_t)v * HW * P;
+                const float4* ckv = ckpt ? reinterpret_cast<const float4*>(ckpt) +
+                                               (int64_t)v * ((P + kBwdCH - 1) / kBwdCH) * HW
+                                         : nullptr;
+                // the previous view's second-stream work (it reads ws.box / ws.inv and both windows)
+                if (v > 0) chk(hipStreamWaitEvent(q, ax->view, 0));
+                if (!ckv) {  // the checkpoints from a forward pass into the workspace (frame into gbuf, unused)
+                    const unsigned fb = blocks(W, kStripTX) * blocks(H, 16);
+                    const size_t flds = (size_t)chunk_slot_floats<8, 1>() * 4 + (h_lds ? (size_t)P * 36 : 0);
+                    render_chunk_strip_kernel<16, 2><<<fb, 256, flds, q>>>(mv, 0, g, cg, 1, hv,
+                                                                          reinterpret_cast<float*>(gbuf), ws.ckpt, h_lds);
+                    ckv = ws.ckpt;
+                }
+                if (!force) {
+                    bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1),
+                                                                   ws.inv);
+                    bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x,
+                                                                                   margin, ws.box);
+                }
+                for (int grp = G - 1; grp >= 0 && ok; --grp) {
+                    const int k = G - 1 - grp, par = k & 1;
+                    const int p_lo = grp * GP, p_hi = std::min(P, p_lo + GP);
+                    if (k >= 2) chk(hipStreamWaitEvent(q, ax->done[par], 0));  // window par is free again
+                    BwdWs wg = win[par];
+                    wg.ds_p0 = p_lo;  // the window holds the group's d samples: planes p_lo .. p_hi-1
+                    bwd_chain_strip_kernel<8><<<blocks(W, kStripTX) * blocks(H, 8), 256, chain_lds, q>>>(
+                        mv, g, cg, hv, dv, ckv, wg, h_lds, p_lo / kBwdCH, (p_hi + kBwdCH - 1) / kBwdCH, gbuf);
+                    chk(hipEventRecord(ax->chain[par], q));
+                    chk(hipStreamWaitEvent(a, ax->chain[par], 0));
+                    if (!force)
+                        bwd_gather_kernel<<<(unsigned)(ntiles * blocks(p_hi - p_lo, kGPl)), kGThreads, 0, a>>>(
+                            g, hv, wg, gv, margin, p_lo, p_hi - p_lo);
+                    bwd_check_kernel<<<1, kWave, 0, a>>>(wg, force, k >= 2);
+                    bwd_fallback_kernel<true><<<fb_blocks, 256, 0, a>>>(g, hv, wg, gv, poll_limit, tick_limit,
+                                                                        fb_mode == 2, p_lo, p_hi);
+                    chk(hipEventRecord(ax->done[par], a));
+                }
+                // an aborted group (never expected) leaves the view's gradient NaN, counted once
+                bwd_poison_kernel<<<256, 256, 0, a>>>(win[0].flag, gv, (int64_t)P * HW, win[1].flag, ws.flag + 4);
+                chk(hipEventRecord(ax->view, a));
+            }
+            chk(hipStreamWaitEvent(q, ax->view, 0));  // the caller's stream: every launch of this call
+            if (!ok) return fail(MPIV_ERR_HIP, "%s: stream event failed", nm);
+            return launched(nm);
+        }
+        // no second stream: the sequential schedule below on the first window
+    }
     for (int v = 0; v < V; ++v) {
         const float* hv = homs + (int64_t)v * P * 9;
         const float* dv = dout + (int64_t)v * HW * 3;
@@ -1036,7 +1156,7 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
     // one pixel per lane and iteration for few depths (D = 10: 0.228 vs 0.243 ms), two above
     // (D = 64: 0.640 vs 0.652; profiles/r03_sweep_few_depths_ab.txt)
     const int pix = (SLR == 4 && D <= 16) ? 1 : kDLPix;
-    if (g_route)
+    if (g_route && !(MPIV_AB && opt(kOptSweepBand) != 0 && SLR == 4))
         return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true, %d, %d, %d>", C < 4 ? C : 4, SLR,
                           SLR == 4 ? kSLCap : 4096, pix);
 #define MPIV_DLRAW(CC, RR, CAP, PP)                                                                          \
@@ -1056,6 +1176,31 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
         MPIV_DLRAW_C(8, 4096, kDLPix)
     } else if (SLR == 6) {
         MPIV_DLRAW_C(6, 4096, kDLPix)
+    } else
+#endif
+#if MPIV_AB  // the band-walking ring kernel: measured slower than one box per tile
+    if (opt(kOptSweepBand) != 0 && SLR == 4) {
+        // band-walking kernel (round 5): bands of kBandSteps 4-row tiles, source rows in an LDS ring
+        const int64_t bands = (int64_t)((Wt + kSLP - 1) / kSLP) * ((Ht + 4 * kBandSteps - 1) / (4 * kBandSteps));
+        const dim3 bgrid((unsigned)bands, B, 1);
+        if (g_route) return note_route(bands * B, kDLThreads, "plane_sweep_band_kernel<%d, %d>", C < 4 ? C : 4, pix);
+#define MPIV_BAND(CC, PP)                                                                                   \
+    plane_sweep_band_kernel<CC, PP><<<bgrid, kDLThreads, 0, q>>>(img, is, sp, rc_hs, rc_ws, ki, proj, depths, out, \
+                                                                out_bstride, out_pstride, (int)vec, shrink)
+#define MPIV_BAND_C(PP)                    \
+    switch (C) {                           \
+        case 1: MPIV_BAND(1, PP); break;   \
+        case 2: MPIV_BAND(2, PP); break;   \
+        case 3: MPIV_BAND(3, PP); break;   \
+        default: MPIV_BAND(4, PP); break;  \
+    }
+        if (pix == 1) {
+            MPIV_BAND_C(1)
+        } else {
+            MPIV_BAND_C(kDLPix)
+        }
+#undef MPIV_BAND_C
+#undef MPIV_BAND
     } else
 #endif
     if (pix == 1) {

@@ -125,6 +125,8 @@ struct BwdWs {
     int* flag;     // [0] 1: the fallback recomputes every plane of the view; [1], [2] the fallback's
                    // ticket and completion counters; [3] 1: this view's fallback aborted (a wait
                    // outlasted its poll limit); [4] views aborted in this call (bwd_fallback_kernel)
+    int* vcount = nullptr;  // where the fallback counts an aborted view (flag + 4; nullptr: the overlapped
+                            // schedule counts views in bwd_poison_kernel instead)
     // fallback: bucket pipeline over chunks of pc planes
     int pc;
     int* key;      // [pc][HW] nw-tap bucket in the (H+1) x (W+1) grid, -1 = no tap in the image;
@@ -1987,7 +1989,7 @@ __device__ __forceinline__ int fallback_ticket(unsigned* ticket, unsigned* done,
     if (tk >= total) return -1;
     const unsigned need = tk / nvirt * nvirt;  // every item of the phases before this one done
     if (poll_limit == 0 && need > 0 && abort_) {  // tests: abort at the first wait
-        if (lane == 0 && atomicExch(abort_, 1) == 0) atomicAdd(aborted, 1);
+        if (lane == 0 && atomicExch(abort_, 1) == 0 && aborted) atomicAdd(aborted, 1);
         return -1;
     }
     const long long t0 = tick_limit ? wall_clock64() : 0;
@@ -2003,7 +2005,7 @@ __device__ __forceinline__ int fallback_ticket(unsigned* ticket, unsigned* done,
             give_up |= (unsigned long long)(wall_clock64() - t0) > tick_limit;
         if (__builtin_amdgcn_readfirstlane(give_up)) {
             if (lane == 0) {
-                if (abort_ && atomicExch(abort_, 1) == 0) atomicAdd(aborted, 1);
+                if (abort_ && atomicExch(abort_, 1) == 0 && aborted) atomicAdd(aborted, 1);
                 if (timeouts) atomicAdd(timeouts, 1u);
             }
             return -1;
@@ -2252,7 +2254,7 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
     unsigned next_fixed = blockIdx.x;
     for (;;) {
         if (wave == 0) {
-            const int t = fallback_ticket(ticket, done, ws.flag + 3, ws.flag + 4, total, (unsigned)nblk, poll_limit,
+            const int t = fallback_ticket(ticket, done, ws.flag + 3, ws.vcount, total, (unsigned)nblk, poll_limit,
                                           tick_limit, nullptr, fixed ? &next_fixed : nullptr);
             if (tid == 0) s_ticket = t;
         }
@@ -2300,10 +2302,14 @@ __global__ __launch_bounds__(256) void ticket_selftest_kernel(unsigned* __restri
 }
 #endif
 
-// After the fallback: a view whose pipeline aborted (flag[3]) gets a NaN gradient
+// After the fallback: a view whose pipeline aborted (flag[3], or flag_b[3] of the overlapped
+// schedule's second counter set) gets a NaN gradient; count (non-null: the overlapped schedule,
+// whose fallbacks do not count) adds the view once
 __global__ __launch_bounds__(256) void bwd_poison_kernel(const int* __restrict__ flag, float4* __restrict__ dmpi,
-                                                         int64_t n) {
-    if (flag[3] == 0) return;
+                                                         int64_t n, const int* __restrict__ flag_b = nullptr,
+                                                         int* __restrict__ count = nullptr) {
+    if (flag[3] == 0 && (!flag_b || flag_b[3] == 0)) return;
+    if (count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(count, 1);
     const float q = __builtin_nanf("");
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
         dmpi[i] = make_float4(q, q, q, q);

@@ -1112,6 +1112,321 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     }
 }
 
+// Band-walking depth-per-lane sweep (round 5).  plane_sweep_dlane_kernel stages a fresh box for
+// every 4 x 64 tile: its prologue (box from the 8 vertices, fill, two barriers) is paid per tile
+// and its fill latency is exposed -- with few depths that prologue is most of the kernel (D = 10:
+// 0.28 of HBM).  Here a block walks a BAND of kBandSteps tiles of one 64-pixel column segment,
+// top to bottom:
+//  * the prologue computes every step's box at once (wave 0: 8 steps x 8 vertices = 64 lanes,
+//    sweep_tile_box per 8-lane group) and their union's column range [X0, X0 + bpitch);
+//  * source rows live in an LDS RING of NR = cap / bpitch rows of that column range (row y in
+//    ring row (y + 2) % NR): a step stages only the rows its box adds below the previous one
+//    (~3 of ~12 for config 3), and the next step's rows are loaded into registers while this
+//    step is sampled (committed after its end-of-step barrier);
+//  * a step whose box does not fit the ring (a jump, a window taller than the ring) reloads its
+//    window; a band whose union is too wide, and steps the per-tile kernel would not stage
+//    (pitch 0) or would zero, follow the per-tile kernel's rules (the same LdsBox exactness
+//    argument: a tap origin read from the ring is one the union box staged).
+// The samples, their arithmetic and the stores are plane_sweep_dlane_kernel's: bit-identical.
+#if MPIV_AB
+constexpr int kBandSteps = 8;                   // 4-row tiles per band (8 x 8 vertices = one wave)
+constexpr int kBandFill = 2;                    // prefetched ring texels per thread (1024 per step)
+
+template <int C, int PIX>
+__global__ __launch_bounds__(kDLThreads) void plane_sweep_band_kernel(
+    const float* __restrict__ img, ImgStrides is, SweepParams sp, float rc_hs, float rc_ws,
+    const float* __restrict__ ki, const float* __restrict__ proj, const float* __restrict__ depths,
+    float* __restrict__ out, int64_t out_bstride, int64_t out_pstride, int vec, int shrink) {
+    constexpr int CAP = kSLCap;
+    __shared__ __attribute__((aligned(16))) float4 s_src[CAP];
+    __shared__ SweepBox s_box[kBandSteps];
+    const int segs = (sp.Wt + kSLP - 1) / kSLP;
+    const int b = blockIdx.y;
+    const int band = blockIdx.x / segs;
+    const int x0 = (blockIdx.x - band * segs) * kSLP;
+    const int by0 = band * kSLR * kBandSteps;
+    const int np = min(kSLP, sp.Wt - x0);
+    const int nsteps = min(kBandSteps, (sp.Ht - by0 + kSLR - 1) / kSLR);
+    const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const float* k9 = ki + (int64_t)b * 9;
+    const float* m = proj + (int64_t)b * 16;
+    const float* imb = img + (int64_t)b * is.b;
+    const bool contig = is.c == 1 && C > 1;
+
+    if (wave == 0) {  // every step's box: lanes 8s .. 8s+7 are step s's vertices
+        float dmin, dmax, dbad;
+        sweep_depth_range(depths, sp.D, lane, dmin, dmax, dbad);
+        const int st = min(lane >> 3, nsteps - 1);
+        const int y0 = by0 + st * kSLR, nr = min(kSLR, sp.Ht - y0);
+        const SweepBox bx = sweep_tile_box(k9, m, sp, rc_hs, rc_ws, x0, y0, np, nr, dmin, dmax, dbad, shrink, lane, CAP);
+        if ((lane & 7) == 0 && (lane >> 3) < nsteps) s_box[lane >> 3] = bx;
+    }
+    __syncthreads();
+    // the union of the staged steps' column ranges (block-uniform)
+    int X0 = 1 << 30, X1 = -(1 << 30), wmax = 0;
+    for (int st = 0; st < nsteps; ++st) {
+        const SweepBox& bx = s_box[st];
+        if (bx.pitch > 0 && !bx.zero) {
+            X0 = min(X0, bx.xl);
+            X1 = max(X1, bx.xl + bx.pitch - 1);
+            wmax = max(wmax, bx.rows);
+        }
+    }
+    X0 = __builtin_amdgcn_readfirstlane(X0);
+    X1 = __builtin_amdgcn_readfirstlane(X1);
+    wmax = __builtin_amdgcn_readfirstlane(wmax);
+    const int bpitch = X1 >= X0 ? X1 - X0 + 1 : 0;
+    const int NR = bpitch > 0 ? CAP / bpitch : 0;
+    // ring mode: every staged window fits the ring with room for the next step's new rows
+    const bool ring = bpitch > 0 && NR >= wmax + kSLR + 3;
+    const float rpitch = bpitch > 0 ? 1.0f / (float)bpitch : 0.0f;
+
+    // one source texel (x, y) of the union's column range as staged (zero outside the image)
+    auto texel = [&](int x, int y) -> f32x4 {
+        const bool in = (unsigned)x < (unsigned)sp.Ws && (unsigned)y < (unsigned)sp.Hs;
+        const float* t = imb + (in ? (int64_t)y * is.y + (int64_t)x * is.x : 0);
+        return contig ? raw_texel<C, true>(t, 1, in) : raw_texel<C, false>(t, is.c, in);
+    };
+    // ring rows [a, a + n): texel idx -> (row, col); returns the count of texels
+    auto ring_idx = [&](int idx, int a, int& rr, int& x, int& y) {
+        int row = (int)((float)idx * rpitch);  // idx < 2^13: off by at most one, corrected
+        row -= row * bpitch > idx ? 1 : 0;
+        row += (row + 1) * bpitch <= idx ? 1 : 0;
+        const int col = idx - row * bpitch;
+        y = a + row;
+        x = X0 + col;
+        int r = (y + 2) % NR;
+        rr = r * bpitch + col;
+    };
+    f32x4 pre[kBandFill];
+    int pre_a = 0, pre_n = 0;  // rows [pre_a, pre_a + pre_n) are in flight in pre
+    auto issue_rows = [&](int a, int n) {  // n * bpitch <= kBandFill * kDLThreads
+        pre_a = a;
+        pre_n = n;
+#pragma unroll
+        for (int k = 0; k < kBandFill; ++k) {
+            const int idx = (int)threadIdx.x + kDLThreads * k;
+            int rr, x, y;
+            ring_idx(idx, a, rr, x, y);
+            pre[k] = idx < n * bpitch ? texel(x, y) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto commit_rows = [&]() {
+#pragma unroll
+        for (int k = 0; k < kBandFill; ++k) {
+            const int idx = (int)threadIdx.x + kDLThreads * k;
+            int rr, x, y;
+            ring_idx(idx, pre_a, rr, x, y);
+            if (idx < pre_n * bpitch) *reinterpret_cast<f32x4*>(&s_src[rr]) = pre[k];
+        }
+    };
+    auto load_rows_now = [&](int a, int n) {  // synchronous, any count (a window reload)
+        for (int idx = threadIdx.x; idx < n * bpitch; idx += kDLThreads) {
+            int rr, x, y;
+            ring_idx(idx, a, rr, x, y);
+            *reinterpret_cast<f32x4*>(&s_src[rr]) = texel(x, y);
+        }
+    };
+    // rows a step needs beyond those staged: (hi, bx.yl + rows - 1], or a reload
+    int have_lo = 0, have_hi = -(1 << 30);
+    auto plan = [&](const SweepBox& bx, int& a, int& n, bool& reload) {
+        const int lo = bx.yl, hi = bx.yl + bx.rows - 1;
+        reload = !(lo >= have_lo && lo <= have_hi + 1);
+        a = reload ? lo : have_hi + 1;
+        n = hi - a + 1;
+        if (n < 0) n = 0;
+    };
+
+    const int D = sp.D;
+    const int ppw = D <= kWave ? kWave / D : 1;
+    const int lp = D <= kWave ? lane / D : 0;
+    const int ld = D <= kWave ? lane - lp * D : lane;
+    const int nchunk = (D + kWave - 1) / kWave;
+    const int ngroup = (np + ppw - 1) / ppw;
+    typedef float f32xC __attribute__((ext_vector_type(C), aligned(4)));
+
+    // the first step's window, and the second's new rows in flight
+    if (ring) {
+        const SweepBox& b0 = s_box[0];
+        if (b0.pitch > 0 && !b0.zero) {
+            load_rows_now(b0.yl, b0.rows);
+            have_lo = b0.yl;
+            have_hi = b0.yl + b0.rows - 1;
+        }
+    }
+    for (int st = 0; st < nsteps; ++st) {
+        SweepBox bx;
+        bx.xl = __builtin_amdgcn_readfirstlane(s_box[st].xl);
+        bx.yl = __builtin_amdgcn_readfirstlane(s_box[st].yl);
+        bx.rows = __builtin_amdgcn_readfirstlane(s_box[st].rows);
+        bx.pitch = __builtin_amdgcn_readfirstlane(s_box[st].pitch);
+        bx.fast = __builtin_amdgcn_readfirstlane(s_box[st].fast);
+        bx.zero = __builtin_amdgcn_readfirstlane(s_box[st].zero);
+        const int y0 = by0 + st * kSLR, nr = min(kSLR, sp.Ht - y0);
+        const bool staged_step = bx.pitch > 0 && !bx.zero;
+        if (!ring && staged_step) {  // the per-tile kernel's own box for this step (linear LDS)
+            if (contig)
+                sweep_fill_box_raw<C, kDLThreads, true, CAP>(s_src, imb, is, sp.Hs, sp.Ws, bx);
+            else
+                sweep_fill_box_raw<C, kDLThreads, false, CAP>(s_src, imb, is, sp.Hs, sp.Ws, bx);
+        }
+        if (ring && staged_step && st > 0) {
+            int a, n;
+            bool reload;
+            plan(bx, a, n, reload);
+            if (!reload && pre_n > 0 && pre_a == a && pre_n >= n) {
+                commit_rows();  // prefetched during the previous step
+            } else if (n > 0) {
+                load_rows_now(a, n);
+            }
+            if (reload) have_lo = a;
+            have_hi = max(have_hi, a + n - 1);
+            have_lo = max(have_lo, have_hi - NR + 1);
+        }
+        pre_n = 0;
+        __syncthreads();  // the step's rows are in LDS
+        // the next staged step's new rows: in flight while this step is sampled
+        if (ring && st + 1 < nsteps) {
+            const SweepBox& bn = s_box[st + 1];
+            if (bn.pitch > 0 && !bn.zero) {
+                int a, n;
+                bool reload;
+                plan(bn, a, n, reload);
+                // the rows it would overwrite must not be this step's (window + new rows <= NR)
+                if (!reload && n > 0 && n * bpitch <= kBandFill * kDLThreads &&
+                    (a + n - 1) - (staged_step ? bx.yl : a) + 1 <= NR)
+                    issue_rows(a, n);
+            }
+        }
+        if (bx.zero) {
+            sweep_zero_tile<C, kDLThreads>(out, out_bstride, out_pstride, sp, vec, b, x0, y0, np, nr);
+        } else {
+            // this step's box: the ring (rows through the ring map) or the linear per-tile box
+            const int pitch = !staged_step ? 0 : ring ? bpitch : bx.pitch;
+            const int bxl = ring ? X0 : bx.xl;
+            const int sbase = ring ? (bx.yl + 2) % max(NR, 1) : 0;
+            const bool all_fast = bx.fast != 0;
+            const LdsBox lbx = make_lds_box(bxl, bx.yl, bx.rows, max(pitch, 2), sp.Ws, sp.Hs);
+            for (int tr = 0; tr < nr; ++tr)
+            for (int ch = 0; ch < nchunk; ++ch) {
+            const int dl = ch * kWave + ld;
+            const bool dlive = (D <= kWave ? lane < ppw * D : dl < D);
+            const float dq = depths[min(dl, D - 1)];
+            float* orow = out + (int64_t)b * out_bstride + ((int64_t)(y0 + tr) * sp.Wt + x0) * out_pstride + (int64_t)dl * C;
+            for (int g0 = wave * PIX; g0 < ngroup; g0 += kDLWaves * PIX) {
+                float px[PIX], py[PIX], rxs[PIX], rys[PIX], rzs[PIX];
+                float* o[PIX];
+                bool live[PIX];
+#pragma unroll
+                for (int j = 0; j < PIX; ++j) {
+                    const int pix = (g0 + j) * ppw + lp;
+                    live[j] = dlive && g0 + j < ngroup && pix < np;
+                    const int pl = min(pix, np - 1);
+                    ray(k9, (float)(x0 + pl), (float)(y0 + tr), rxs[j], rys[j], rzs[j]);  // pixel2cam_torch, utils.py:370
+                    o[j] = orow + (int64_t)pl * out_pstride;
+                }
+                float su[PIX], sv[PIX];
+                bool fast = true;
+#pragma unroll
+                for (int j = 0; j < PIX; ++j) {
+                    const float X = rxs[j] * dq, Y = rys[j] * dq, Z = rzs[j] * dq;
+                    const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+                    const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+                    const float den = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11] + 1e-10f;
+                    if (!all_fast) fast = fast && div2_safe(pu, pv, den);
+                    div2_fast(pu, pv, den, su[j], sv[j]);  // cam2pixel_torch, utils.py:388-391
+                }
+                if (__builtin_amdgcn_ballot_w64(!fast)) {  // rare: a quotient outside the fast path's range
+#pragma unroll
+                    for (int j = 0; j < PIX; ++j) {
+                        const float X = rxs[j] * dq, Y = rys[j] * dq, Z = rzs[j] * dq;
+                        const float pu = __builtin_fmaf(m[2], Z, __builtin_fmaf(m[1], Y, m[0] * X)) + m[3];
+                        const float pv = __builtin_fmaf(m[6], Z, __builtin_fmaf(m[5], Y, m[4] * X)) + m[7];
+                        const float den = __builtin_fmaf(m[10], Z, __builtin_fmaf(m[9], Y, m[8] * X)) + m[11] + 1e-10f;
+                        if (!div2_safe(pu, pv, den)) {
+                            su[j] = div_rn(pu, den);
+                            sv[j] = div_rn(pv, den);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < PIX; ++j) {
+                    const float cx = div_const(su[j] + 0.5f, sp.fhs, rc_hs);  // SWAPPED: x / H, utils.py:444
+                    const float cy = div_const(sv[j] + 0.5f, sp.fws, rc_ws);  //          y / W
+                    px[j] = unnormalize(to_grid(cx), sp.half_ws);
+                    py[j] = unnormalize(to_grid(cy), sp.half_hs);
+                }
+                f32x4 smp[PIX];
+                bool staged = pitch > 0;
+                if (staged) {
+                    TapSet ts[PIX];
+#pragma unroll
+                    for (int j = 0; j < PIX; ++j) {
+                        // lds_issue through the ring's row map (rows r0, r0 + 1 of the ring)
+                        TapSet& t = ts[j];
+                        const float fx0 = floorf(px[j]), fy0 = floorf(py[j]);
+                        const float wx = px[j] - fx0, ex = 1.0f - wx;
+                        const float wy = py[j] - fy0, sy = 1.0f - wy;
+                        t.nw = sy * ex;
+                        t.ne = sy * wx;
+                        t.sw = wy * ex;
+                        t.se = wy * wx;
+                        const float rx = fx0 - lbx.xl, ry = fy0 - lbx.yl;
+                        const int ix = (int)__builtin_amdgcn_fmed3f(rx, 0.0f, lbx.xspan);
+                        const int iy = (int)__builtin_amdgcn_fmed3f(ry, 0.0f, lbx.yspan);
+                        int r0 = iy, r1 = iy + 1;
+                        if (ring) {
+                            r0 = sbase + iy;
+                            r0 -= r0 >= NR ? NR : 0;
+                            r1 = r0 + 1 == NR ? 0 : r0 + 1;
+                        }
+                        const float4* s0 = s_src + r0 * pitch + ix;
+                        const float4* s1 = s_src + r1 * pitch + ix;
+                        t.a = *reinterpret_cast<const f32x4*>(s0);
+                        t.b = *reinterpret_cast<const f32x4*>(s0 + 1);
+                        t.c = *reinterpret_cast<const f32x4*>(s1);
+                        t.d = *reinterpret_cast<const f32x4*>(s1 + 1);
+                        staged = staged && (__builtin_amdgcn_fmed3f(rx, lbx.gxl, lbx.gxh) == rx) &
+                                               (__builtin_amdgcn_fmed3f(ry, lbx.gyl, lbx.gyh) == ry);
+                    }
+#pragma unroll
+                    for (int j = 0; j < PIX; ++j) smp[j] = blend_taps(ts[j]);
+#pragma unroll
+                    for (int j = 0; j < PIX; ++j)
+                        asm volatile("" ::"v"(ts[j].a), "v"(ts[j].b), "v"(ts[j].c), "v"(ts[j].d));
+                }
+                if (__builtin_amdgcn_ballot_w64(!staged)) {
+                    if (!staged) {  // a tap origin not staged: gather from global memory
+#pragma unroll
+                        for (int j = 0; j < PIX; ++j) {
+                            smp[j] = raw_sample<C>(imb, is, sp.Ws, sp.Hs, px[j], py[j]);
+                            asm volatile("" ::: "memory");
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < PIX; ++j) {
+                    if (live[j]) {
+                        f32xC v;
+#pragma unroll
+                        for (int c = 0; c < C; ++c) v[c] = smp[j][c];
+                        if (vec && MPIV_SWNT) __builtin_nontemporal_store(v, reinterpret_cast<f32xC*>(o[j]));
+                        else if (vec) *reinterpret_cast<f32xC*>(o[j]) = v;
+                        else {
+#pragma unroll
+                            for (int c = 0; c < C; ++c) o[j][c] = v[c];
+                        }
+                    }
+                }
+            }
+            }
+        }
+        __syncthreads();  // every sample of this step has read its rows
+    }
+}
+
+#endif  // MPIV_AB
+
 // Direct depth-per-lane sweep for few depths (D <= 2 automatic, 3..8 go to the pixel-per-lane
 // plane_sweep_px_kernel below; abi.hip sweep_raw_into).  The LDS box
 // of plane_sweep_dlane_kernel is sized by the depth RANGE, not the depth count, so with few

@@ -374,7 +374,8 @@ def test_backward_abort_surfaces_on_next_default_call(dev, kopts):
 
 
 @pytest.mark.parametrize("group", [8, 16])
-def test_backward_plane_groups_vs_oracle(group, dev, bwd_mode, kopts):
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_backward_plane_groups_vs_oracle(group, overlap, dev, bwd_mode, kopts):
     """Plane groups (round 4: a view's backward runs group by group, back to front, the running
     adjoint handed down between groups, so the workspace holds one group's d samples): forced
     to 8 / 16 planes on a 36-plane MPI (5 / 3 groups, the last one partial), in every backward
@@ -389,7 +390,9 @@ def test_backward_plane_groups_vs_oracle(group, dev, bwd_mode, kopts):
     homs = _host.render_homographies(pose, planes, configs.f32([K]), 1)
     dout = torch.rand((1, H, W, 3), generator=torch.Generator().manual_seed(31)) * 2 - 1
     want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
-    kopts(bwd_group=group)
+    # overlap 1 (round 5 default): group k's gather on a second stream beside group k-1's chain,
+    # two d-sample windows; 0: the groups one after the other in one window
+    kopts(bwd_group=group, bwd_overlap=overlap)
     L = _lib.load()
     assert L.mpiv_render_backward_workspace_size(H, W, P) < L.mpiv_render_backward_workspace_size(H, W, 2 * P)
     got, _ = _backward_flag(mpi.to(dev), homs, dout.to(dev), dev)  # no checkpoints
@@ -398,6 +401,15 @@ def test_backward_plane_groups_vs_oracle(group, dev, bwd_mode, kopts):
     out = mv.mpi_render_view_torch(leaf, pose.to(dev), planes.to(dev), configs.f32([K]).to(dev))
     out.backward(dout.to(dev))
     assert_bits(leaf.grad.cpu().numpy(), want, f"groups of {group}, forward checkpoints")
+    # several views in one call: the schedule walks them in turn (the second stream's work of view v
+    # is done before view v + 1 reuses the boxes and windows)
+    mpi3 = configs.synthetic_mpi(3, H, W, P, 33)
+    poses3 = configs.f32([c["poses"][60], c["poses"][300], c["poses"][700]])
+    homs3 = _host.render_homographies(poses3, planes, configs.f32([K] * 3), 3)
+    dout3 = torch.rand((3, H, W, 3), generator=torch.Generator().manual_seed(37)) * 2 - 1
+    want3 = oracle.render_backward(mpi3.numpy(), homs3.numpy(), dout3.numpy())
+    got3 = _lib.render_backward(mpi3.to(dev), homs3, dout3.to(dev), check=True)
+    assert_bits(got3, want3, f"groups of {group}, 3 views")
 
 
 def test_backward_config4_workspace_and_checkpoint_paths(dev):
@@ -423,3 +435,8 @@ def test_backward_config4_workspace_and_checkpoint_paths(dev):
     b = _lib.render_backward(mpi, homs, dout, workspace=ws, check=True)
     assert torch.equal(a.view(torch.int32), one.view(torch.int32))
     assert torch.equal(b.view(torch.int32), one.view(torch.int32))
+    # the default workspace takes the overlapped schedule (4 groups, two windows, two streams); the
+    # one-group sequential schedule gives the same bits
+    with _lib.debug(bwd_overlap=0):
+        seq = _lib.render_backward(mpi, homs, dout, check=True)
+    assert torch.equal(seq.view(torch.int32), one.view(torch.int32))

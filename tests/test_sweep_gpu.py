@@ -330,17 +330,18 @@ def test_inverse_warp2_depth_map_vs_reference(warp, dev):
     assert_bits(out, warp["piw2_out"], "piw2")
 
 
+@pytest.mark.parametrize("band", [1, 0])
 @pytest.mark.parametrize("C", [1, 2, 3, 4])
 @pytest.mark.parametrize("D", [6, 10, 16, 64, 100, 128])
 @pytest.mark.parametrize("shrink", ["0", "3"])
-def test_plane_sweep_depth_lanes_vs_oracle(C, D, shrink, dev, kopts):
+def test_plane_sweep_depth_lanes_vs_oracle(C, D, shrink, band, dev, kopts):
     """The depth-per-lane LDS kernel: D <= 64 (64 // D pixels per wave slot, idle lanes when
     D does not divide 64), D > 64 (64-depth chunks, a partial last one); odd target sizes (a
     partial last 64-pixel segment and 4-row tile), separate source / target intrinsics; also
     with shrunk boxes (most samples through its global fallback): bit-exact to the oracle."""
     from mpi_vision_amd import _host, _lib
     from oracle import oracle
-    kopts(box_shrink=shrink)
+    kopts(box_shrink=shrink, sweep_band=band)  # band 1: the band-walking ring kernel (round 5 default)
     g = torch.Generator().manual_seed(140 + C + D)
     B, Hs, Ws, Ht, Wt = 2, 41, 89, 23, 75
     img = torch.rand((B, Hs, Ws, C), generator=g)
@@ -353,6 +354,43 @@ def test_plane_sweep_depth_lanes_vs_oracle(C, D, shrink, dev, kopts):
     want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Ht, Wt)
     out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Ht, Wt)
     assert_bits(out.cpu().numpy(), want, f"C={C} D={D} shrink={shrink}")
+
+
+@pytest.mark.parametrize("band", [1, 0])
+@pytest.mark.parametrize("C", [1, 3])
+@pytest.mark.parametrize("D", [10, 64])
+def test_plane_sweep_band_ring_vs_oracle(C, D, band, dev, kopts):
+    """The band-walking kernel's LDS ring over tall targets (several bands of 8 four-row tiles,
+    a partial last band and segment): a view whose source rows slide down with the target rows
+    (ring refills of a few rows), one tilted about x (windows that move faster than the tiles,
+    reloads), one rotated by 90 degrees in-plane (a band's footprint sweeps the source
+    sideways: the union column range is too wide for a ring, steps staged one by one) and a
+    strongly perspective one (window heights changing along the band): bit-exact to the oracle."""
+    from mpi_vision_amd import _host, _lib
+    from oracle import oracle
+    import math
+    kopts(sweep_band=band, sweep_direct=-1)
+    g = torch.Generator().manual_seed(400 + C + D)
+    B, Hs, Ws, Ht, Wt = 4, 150, 190, 141, 133
+    img = torch.rand((B, Hs, Ws, C), generator=g)
+    K = configs.f32([configs.intrinsics_matrix(120.0, 118.0, 95.0, 75.0)] * B)
+
+    def rot_x(deg):
+        a = math.radians(deg)
+        return [[1.0, 0.0, 0.0], [0.0, math.cos(a), -math.sin(a)], [0.0, math.sin(a), math.cos(a)]]
+
+    def rot_z(deg):
+        a = math.radians(deg)
+        return [[math.cos(a), -math.sin(a), 0.0], [math.sin(a), math.cos(a), 0.0], [0.0, 0.0, 1.0]]
+    poses = configs.f32([configs.pose_from(configs.rot_y(1.0), (0.08, 0.01, 0.0)),
+                         configs.pose_from(rot_x(12.0), (0.0, 0.1, 0.05)),
+                         configs.pose_from(rot_z(90.0), (0.02, -0.03, 0.0)),
+                         configs.pose_from(rot_x(-25.0), (0.05, 0.3, 0.6))])
+    depths = configs.inv_depths(1, 60, D)
+    ki, proj = _host.psv_matrices(K, K, poses)
+    want = oracle.plane_sweep(img.numpy(), ki.numpy(), proj.numpy(), depths, Ht, Wt)
+    out = _lib.plane_sweep(img.to(dev), depths, ki, proj, Ht, Wt)
+    assert_bits(out.cpu().numpy(), want, f"C={C} D={D} band={band}")
 
 
 @pytest.mark.parametrize("C", [3, 4])

@@ -102,6 +102,32 @@ def bwd(dev, it):
     run("c4 render backward with checkpoints, 1 view", ROWS, fn, 2 * P * H * W * 16 + H * W * 12, it)
 
 
+def bwdgrp(dev, it):
+    """The backward in plane groups of 8 / 16 / 32 planes vs one group: a group's d samples (8 planes:
+    134 MB at config 4) fit the 256-MB Infinity Cache between its chain and its gather."""
+    mpi, homs, H, W, P = c4_mpi(dev)
+    g = torch.Generator(device=dev).manual_seed(1)
+    dout = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    _, ck = _lib.render_train(mpi, homs)
+    ref = None
+    for p in range(2):
+        for grp, ov in ((0, 0), (0, 1), (16, 1), (32, 0), (64, 1)):
+            with _lib.debug(bwd_group=grp, bwd_overlap=ov):
+                ws = torch.empty(_lib.load().mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+                fn = lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)  # noqa: E731
+                got = fn()
+                if ref is None:
+                    ref = got.clone()
+                same = bool(torch.equal(got.view(torch.int32), ref.view(torch.int32)))
+                ms, mn = timed(fn, it)
+                b2b = span(fn, it)
+                print(json.dumps({"exp": "c4 backward plane groups", "variant": f"group{grp}_overlap{ov}", "pass": p, "ms": round(ms, 4),
+                                  "ms_min": round(mn, 4), "ms_b2b": round(b2b, 4), "ws_GB": round(ws.numel() / 1e9, 3),
+                                  "same": same}), flush=True)
+                del ws, got
+                torch.cuda.empty_cache()
+
+
 STRIP = [("rows64x1", {"chunk_strip": 0}), ("strip8x16", {"chunk_strip": 1})]
 STRIPS = [("strip8x16", {"chunk_strip": 1}), ("strip8x8", {"chunk_strip": 2}), ("strip8x8_nt3", {"chunk_strip": 3}),
           ("strip8x16_nt3", {"chunk_strip": 4})]
@@ -256,6 +282,39 @@ def bwdg(dev, it):
                           bool(torch.equal(got.view(torch.int32), ref.view(torch.int32))), "fallback_flag": flag}))
     fn = lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)  # noqa: E731
     run("c4 render backward with checkpoints, 1 view", GATHER, fn, 2 * P * H * W * 16 + H * W * 12, it)
+
+
+def swband(dev, it):
+    """The LDS-staged sweep with one box per 4-row tile (plane_sweep_dlane_kernel, sweep_band=0) against
+    the band-walking ring kernel (plane_sweep_band_kernel, sweep_band=1): config-3 sources into 10 / 16 /
+    64 depths (4 and 5 sources, as bench.py's legs), bit-identical volumes checked first."""
+    c = configs.config3()
+    S, H, W = c["S"], c["H"], c["W"]
+    g = torch.Generator(device=dev).manual_seed(1)
+    img = torch.rand((S, H, W, 3), generator=g, device=dev)
+    K = configs.f32([c["K"]] * S)
+    ki, proj = _host.psv_matrices(K, K, configs.f32(c["poses"]))
+    ki, proj = ki.to(dev), proj.to(dev)
+    for D, Sx in ((10, 4), (16, 4), (64, 5)):
+        d = configs.f32(configs.inv_depths(1, 100, D)).to(dev)
+        out = torch.empty((Sx, H, W, D * 3), device=dev)
+        im = img[:Sx]
+        alg = Sx * H * W * 12 + Sx * D * H * W * 12
+        raw = lambda: _lib._call("mpiv_plane_sweep", im, _lib._strides(im), Sx, H, W, 3, ki, proj, d, D, H, W,  # noqa: E731
+                                 out, _lib._stream(dev))
+        vols = []
+        for b in (0, 1):
+            with _lib.debug(sweep_band=b, sweep_direct=-1):
+                out.zero_()
+                raw()
+                vols.append(out.clone())
+        print(json.dumps({"exp": "sweep band bit-exact", "D": D,
+                          "same": bool(torch.equal(vols[0].view(torch.int32), vols[1].view(torch.int32)))}), flush=True)
+        del vols
+        run(f"c3 sources ({Sx}) -> {D} planes", [("dlane", {"sweep_band": 0, "sweep_direct": -1}),
+                                                ("band", {"sweep_band": 1, "sweep_direct": -1})], raw, alg, it)
+        del out
+        torch.cuda.empty_cache()
 
 
 def sw10(dev, it):
