@@ -130,10 +130,10 @@ def main():
             cg.setdefault(k, {}).update(cs)
     launches = []
     for key in sorted(set(tg) | set(cg), key=lambda k: (k[0], k[1], k[2] or "")):
-        kern, grid, tag = key
+        kern, grid, phase = key
         e = {"kernel": kern, "grid": grid}
-        if tag is not None:
-            e["tag"] = tag
+        if phase is not None:
+            e["tag"] = phase
         d = tg.get(key)
         if d:
             e.update(calls=len(d), avg_ns=mean(d), min_ns=min(d), max_ns=max(d))
