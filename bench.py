@@ -254,6 +254,29 @@ def prof_fields(kernel: str, grid: int, alg_bytes: float, ms: float, tag: str | 
 # timing helpers
 # ---------------------------------------------------------------------------
 
+# Device time of untimed launches before each timed region.  After a host-side gap (an allocation,
+# a check with a host sync) the next ~25 ms of launches run up to 40 % slower on the box before they
+# settle (config 3: 0.88 vs 0.61 ms per launch; profiles/r05_c3_ramp.jsonl), so a few untimed
+# launches are not a warm-up; every leg now runs >= WARM_MS of back-to-back launches first.
+WARM_MS = 60.0
+
+
+def warm(fn, stream, min_ms=WARM_MS, cap=5000):
+    """Untimed back-to-back calls of fn for about min_ms of device time (the count from 2 timed
+    calls, then enqueued without a host sync); returns the number of calls."""
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    fn()
+    fn()
+    b.record(stream)
+    b.synchronize()
+    per = max(a.elapsed_time(b) / 2, 1e-3)
+    k = min(cap, int(np.ceil(min_ms / per)))
+    for _ in range(k):
+        fn()
+    return k + 2
+
+
 def event_ms(fn, n, stream, each=False):
     """Average device time of fn() over n calls, HIP events on the launch stream (each: the list)."""
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
@@ -364,8 +387,7 @@ def single_view_leg(packed, H, W, P, h_sv, dev, stream):
     """One view per launch (every texel crosses HBM once): the north-star HBM bar."""
     one = torch.empty((1, H, W, 3), device=dev)
     launch = lambda: _lib._call("mpiv_render_packed", packed, H, W, P, h_sv, 1, one, _lib._stream(dev))  # noqa: E731
-    for _ in range(50):  # ~20 ms of untimed launches: the clocks leave their idle state first
-        launch()
+    warm(launch, stream)
     mark("sv", dev)
     ms = event_ms(launch, 20, stream)
     mark("untimed", dev)
@@ -389,8 +411,7 @@ def config2_leg(dev, stream, n=20):
                                      configs.f32([c["K"]] * V), V).to(dev)
     out = torch.empty((V, H, W, 3), device=dev)
     launch = lambda: _lib._call("mpiv_render_packed", packed, H, W, P, homs, V, out, _lib._stream(dev))  # noqa: E731
-    for _ in range(3):
-        launch()
+    warm(launch, stream)
     mark("c2", dev)
     ms = event_ms(launch, n, stream)
     mark("untimed", dev)
@@ -420,8 +441,7 @@ def config3_leg(dev, stream, n=20):
     pose = configs.f32(c["poses"]).to(dev)
     depths = list(c["depths"])
     vol = mv.plane_sweep_torch(img, depths, pose, K)
-    for _ in range(3):
-        mv.plane_sweep_torch(img, depths, pose, K)
+    warm(lambda: mv.plane_sweep_torch(img, depths, pose, K), stream)
     mark("c3_dropin", dev)
     dropin_ms = span_ms(lambda: mv.plane_sweep_torch(img, depths, pose, K), n, stream)
     mark("untimed", dev)
@@ -433,11 +453,10 @@ def config3_leg(dev, stream, n=20):
                                 out, _lib._stream(dev))
     launch()
     same = bool(torch.equal(out.view(torch.int32), vol.view(torch.int32)))
-    # every timed launch counts: 3 untimed launches, then the mean of 3n back-to-back launches --
-    # the rate this write-heavy kernel sustains, including its slowdown under sustained load
-    # (round 4 quoted the best steady state after 40 untimed launches)
-    for _ in range(3):
-        launch()
+    # every timed launch counts: the warm-up (WARM_MS of untimed launches), then the mean of 3n
+    # back-to-back launches -- the rate this write-heavy kernel sustains (the mean of
+    # every timed launch, not a best case; the thirds show any drift)
+    nwarm = warm(launch, stream)
     mark("c3", dev)
     ms_each = event_ms(launch, 3 * n, stream, each=True)
     mark("untimed", dev)
@@ -453,8 +472,7 @@ def config3_leg(dev, stream, n=20):
     img10 = img[:S10]
     launch10 = lambda: _lib._call("mpiv_plane_sweep", img10, _lib._strides(img10), S10, H, W, 3, ki, proj, d10,  # noqa: E731
                                   D10, H, W, out10, _lib._stream(dev))
-    for _ in range(3):
-        launch10()
+    warm(launch10, stream)
     mark("c3_ten", dev)
     ms10 = event_ms(launch10, n, stream)
     mark("untimed", dev)
@@ -467,7 +485,7 @@ def config3_leg(dev, stream, n=20):
     del out10
     res = {"workload": "BASELINE config 3: PSV of 5 source 1024x768x3 images into 64 depth planes "
                        "(plane_sweep_torch, utils.py:452-471)",
-           "kernel_ms": round(ms, 4), "kernel_ms_def": f"mean of {3 * n} back-to-back launches after 3 untimed",
+           "kernel_ms": round(ms, 4), "kernel_ms_def": f"mean of {3 * n} back-to-back launches after {nwarm} untimed ({WARM_MS:.0f} ms)",
            "kernel_ms_first_last_third": [round(float(np.mean(ms_each[:n])), 4), round(float(np.mean(ms_each[-n:])), 4)],
            "dropin_ms": round(dropin_ms, 4),
            "Mplanepix_per_s": round(S * D * H * W / 1e6 / (ms * 1e-3), 1),
@@ -497,8 +515,7 @@ def notebook_leg(dev, stream, n=50):
     g = torch.Generator(device=dev).manual_seed(5)
     img = torch.rand((S, N, 3), generator=g, device=dev)
     psv = lambda: mv.plane_sweep_torch_one(img, depths, pose, K)  # noqa: E731
-    for _ in range(5):
-        psv()
+    warm(psv, stream)
     psv_ms = span_ms(psv, n, stream)
     ki, proj = _host.psv_matrices(K.cpu()[None], K.cpu()[None], pose.cpu()[None])
     ki, proj = ki.to(dev), proj.to(dev)
@@ -507,7 +524,7 @@ def notebook_leg(dev, stream, n=50):
     img4 = img[None]
     launch = lambda: _lib._call("mpiv_plane_sweep", img4, _lib._strides(img4), 1, S, N, 3, ki, proj, dd, P, S, N,  # noqa: E731
                                 out, _lib._stream(dev))
-    launch()
+    warm(launch, stream)
     mark("nb", dev)
     psv_kernel_ms = event_ms(launch, n, stream)
     mark("untimed", dev)
@@ -517,8 +534,7 @@ def notebook_leg(dev, stream, n=50):
     poses = pose[None]
     Kb = K[None]
     rend = lambda: mv.mpi_render_view_torch(mpi, poses, planes, Kb)  # noqa: E731
-    for _ in range(5):
-        rend()
+    warm(rend, stream)
     render_ms = span_ms(rend, n, stream)
     leaf = mpi.clone().requires_grad_(True)
     dout = torch.rand((1, S, N, 3), generator=g, device=dev)
@@ -527,8 +543,7 @@ def notebook_leg(dev, stream, n=50):
         o = mv.mpi_render_view_torch(leaf, poses, planes, Kb)
         o.backward(dout)
         leaf.grad = None
-    for _ in range(5):
-        train_step()
+    warm(train_step, stream)
     train_ms = span_ms(train_step, n, stream)
     kname, grid = _lib.route("plane_sweep", 1, S, N, 3, P, S, N)
     r_alg = P * S * N * 16 + S * N * 12
@@ -568,8 +583,7 @@ def u8_leg(dev, stream, V, homs_sv, homs_v, n=10):
     many = torch.empty((V, H, W, 3), device=dev)
     l1 = lambda: _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs_sv, 1, one, _lib._stream(dev))  # noqa: E731
     lv_u8 = lambda: _lib._call("mpiv_render_packed_u8", pk, H, W, P, homs_v, V, many, _lib._stream(dev))  # noqa: E731
-    for _ in range(50):
-        l1()
+    warm(l1, stream)
     mark("u8_sv", dev)
     ms1 = event_ms(l1, 20, stream)
     mark("untimed", dev)
@@ -584,12 +598,12 @@ def u8_leg(dev, stream, V, homs_sv, homs_v, n=10):
     convert_ms = ev0.elapsed_time(ev1) if route_float else None
     lv = (lambda: _lib._call("mpiv_render_packed", fcopy, H, W, P, homs_v, V, many, _lib._stream(dev))) \
         if route_float else lv_u8  # noqa: E731
-    lv()
+    warm(lv, stream)
     mark("u8_mv", dev)
     msv = event_ms(lv, n, stream)
     mark("untimed", dev)
     want = many.clone()
-    lv_u8()
+    warm(lv_u8, stream)
     mark("u8_kernel", dev)
     msv_u8 = event_ms(lv_u8, n, stream)
     mark("untimed", dev)
@@ -644,8 +658,7 @@ def netout_leg(dev, stream, n=20):
     out = torch.empty((1, H, W, 3), device=dev)
     launch = lambda: _lib._call("mpiv_render_net_output", pred, _lib._strides(pred), fg, _lib._strides(fg), 1,  # noqa: E731
                                 H, W, P, homs, out, _lib._stream(dev))
-    for _ in range(20):
-        launch()
+    warm(launch, stream)
     mark("netout", dev)
     ms = event_ms(launch, n, stream)
     mark("untimed", dev)
@@ -683,28 +696,37 @@ def training_leg(dev, stream, n=10):
     f_out = torch.empty((1, H, W, 3), device=dev)
     f_ck = torch.empty_like(ck)
     st = _lib._strides(mpi)
+    fwd = lambda: _lib._call("mpiv_render_train", mpi, st, 1, H, W, P, homs, f_out, f_ck,  # noqa: E731
+                             _lib._stream(dev))
+    inf = lambda: _lib._call("mpiv_render", mpi, st, 1, H, W, P, homs, f_out, _lib._stream(dev))  # noqa: E731
+    warm(fwd, stream)
     mark("train_fwd", dev)
-    fwd_ms = span_ms(lambda: _lib._call("mpiv_render_train", mpi, st, 1, H, W, P, homs, f_out, f_ck,  # noqa: E731
-                                        _lib._stream(dev)), n, stream)
+    fwd_ms = span_ms(fwd, n, stream)
+    mark("untimed", dev)
+    warm(inf, stream)
     mark("train_inf", dev)
-    inf_ms = span_ms(lambda: _lib._call("mpiv_render", mpi, st, 1, H, W, P, homs, f_out, _lib._stream(dev)),  # noqa: E731
-                     n, stream)
+    inf_ms = span_ms(inf, n, stream)
+    mark("untimed", dev)
+    warm(lambda: _lib.render(mpi, homs), stream)
     mark("train_inf_dropin", dev)
     inf_dropin_ms = event_ms(lambda: _lib.render(mpi, homs), n, stream)
     mark("untimed", dev)
     same_ck = bool(torch.equal(f_ck.view(torch.int32), ck.view(torch.int32)))
     del f_ck
     g1 = _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck)
+    warm(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck), stream)
     mark("train_bwd", dev)
     bwd_ms = span_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws, ckpt=ck), n, stream)
     mark("untimed", dev)
     g2 = _lib.render_backward(mpi, homs, dout, workspace=ws)
+    warm(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws), stream)
     mark("train_bwd_nockpt", dev)
     bwd2_ms = span_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws), n, stream)
     mark("untimed", dev)
     # the smallest workspace (plane groups, round 4): same gradient, d samples of one group resident
     ws_min = torch.empty(_lib.load().mpiv_render_backward_workspace_size_min(H, W, P), dtype=torch.uint8, device=dev)
     g3 = _lib.render_backward(mpi, homs, dout, workspace=ws_min, ckpt=ck)
+    warm(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws_min, ckpt=ck), stream)
     mark("train_bwd_minws", dev)
     bwd3_ms = span_ms(lambda: _lib.render_backward(mpi, homs, dout, workspace=ws_min, ckpt=ck), n,
                       stream)
@@ -782,7 +804,7 @@ def config5_leg(world, rank, dev, steps, warmup):
         step = lambda: parallel.render_plane_sharded(packed, hl, H, stats=xstats, pipelined=pipe)  # noqa: E731
         shard_bytes = (p1 - p0) * H * W * 16 + H * W * 16
         kname, grid = _lib.route("render_packed_ct", H, W, p1 - p0, 1)
-    launch()
+    warm(launch, stream)
     mark("c5_kernel", dev)
     kern_ms = event_ms(launch, 3, stream)
     mark("untimed", dev)

@@ -113,6 +113,12 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      group k-1's chain, two d-sample windows: measured no faster)
 //   netout_buf=0|1     render_netout_kernel's staged loads through pointers (0) or buffer resources
 //                      with 32-bit offsets (1, default where the spans fit)
+//   sweep_pf=0|1       (A/B build) mpiv_plane_sweep[_into]'s LDS-staged route: one block per tile
+//                      (plane_sweep_dlane_kernel, 0 = default) or resident blocks walking the tiles with
+//                      the next tile's box and texels prefetched (plane_sweep_pf_kernel: measured 15-22 %
+//                      slower)
+//   sweep_soa=0|1      (A/B build) mpiv_plane_sweep[_into]'s depth-per-lane kernel stages its box as
+//                      float4 texels (0 = default) or as channel planes (1: measured 4-7 % slower)
 //   bwd_margin=k       the tile gather's pixel-window margin in 1/64 pixel (default 16);
 //                      negative values make windows miss contributors, which the pair
 //                      count must catch (tests)
@@ -122,13 +128,14 @@ enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOpt
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
                 kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kOptU8Flight, kOptBwdGroup,
-                kOptNetoutGeo, kOptNetoutBuf, kOptBwdOverlap, kOptSweepBand, kNumOpts };
+                kOptNetoutGeo, kOptNetoutBuf, kOptBwdOverlap, kOptSweepBand, kOptSweepPf, kOptSweepSoa, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
                                          "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode",
-                                         "chunk_strip", "u8_flight", "bwd_group", "netout_geo", "netout_buf", "bwd_overlap", "sweep_band"};
+                                         "chunk_strip", "u8_flight", "bwd_group", "netout_geo", "netout_buf", "bwd_overlap", "sweep_band",
+                                         "sweep_pf", "sweep_soa"};
 #ifndef MPIV_CHUNK_STRIP
 #define MPIV_CHUNK_STRIP 1  // round 4: 0.506 vs 0.64 ms in place (profiles/r04j_strip*_ab.jsonl)
 #endif
@@ -136,9 +143,9 @@ const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_nat
 #define MPIV_U8_FLIGHT 0
 #endif
 const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP,
-                                    MPIV_U8_FLIGHT, 0, 0, 1, 0, 0};
+                                    MPIV_U8_FLIGHT, 0, 0, 1, 0, 0, 0, 0};
 int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP, MPIV_U8_FLIGHT, 0,
-                        0, 1, 0, 0};
+                        0, 1, 0, 0, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -161,6 +168,7 @@ bool ab_only(int o, int v) {
         case kOptBwdGather: return v == 1 || v == 2 || v == 3;
         case kOptBwdPollLimit: case kOptBwdFbBlocks: case kOptBwdFbMode: return v != 0;
         case kOptBwdOverlap: case kOptSweepBand: return v != 0;
+        case kOptSweepPf: case kOptSweepSoa: return v > 0;
         default: return false;
     }
 }
@@ -1085,6 +1093,28 @@ static SweepParams sweep_params(int B, int Hs, int Ws, int C, int D, int Ht, int
     return sp;
 }
 
+#if MPIV_AB
+// blocks of plane_sweep_pf_kernel resident at once (CUs x blocks per CU), queried once per device;
+// a dry run without a device reports MI355X's 256 CUs x 3
+static int sweep_pf_blocks() {
+    static int s_blocks[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return g_route ? 256 * 3 : 0;
+    int nb = __atomic_load_n(&s_blocks[dev], __ATOMIC_RELAXED);
+    if (nb == 0) {
+        int ncu = 0, per = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)plane_sweep_pf_kernel<3, 1>, kDLThreads, 0) !=
+                hipSuccess ||
+            ncu <= 0 || per <= 0)
+            return g_route ? 256 * 3 : 0;
+        nb = ncu * per;
+        __atomic_store_n(&s_blocks[dev], nb, __ATOMIC_RELAXED);
+    }
+    return nb;
+}
+#endif
+
 // plane_sweep_dlane_kernel on the caller's strided source (C <= 4): no padded copy
 static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4], int B, int Hs, int Ws, int C,
                           const float* ki, const float* proj, const float* depths, int D, int Ht, int Wt, float* out,
@@ -1153,17 +1183,55 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
 #undef MPIV_DIRECT
         return launched(nm);
     }
+    // persistent tiles with the next tile's box and texels prefetched (plane_sweep_pf_kernel)
+    const int opf = opt(kOptSweepPf);
+    (void)opf;
+    // (its fill reads each source image through a buffer resource: non-negative strides, a span
+    // under 2 GiB)
+    const int64_t span = ((int64_t)(Hs - 1) * st[1] + (int64_t)(Ws - 1) * st[2] + (int64_t)(C - 1) * st[3] + 1) * 4;
+    [[maybe_unused]] const bool pf_ok = st[1] >= 0 && st[2] >= 0 && st[3] >= 0 && st[1] < (1 << 28) && st[2] < (1 << 28) &&
+                       st[3] < (1 << 28) && span < kOOB - 64 && tiles * B < (1ll << 31);
+#if MPIV_AB  // measured slower than one block per tile
+    if (SLR == 4 && shrink == 0 && pf_ok && opt(kOptSweepBand) == 0 && opf > 0) {
+        const int64_t total = tiles * B;
+        const int res = sweep_pf_blocks();
+        if (res <= 0) return fail(MPIV_ERR_HIP, "%s: device query failed", nm);
+        const unsigned G = (unsigned)std::min<int64_t>(total, res);
+        if (g_route) return note_route(G, kDLThreads, "plane_sweep_pf_kernel<%d, 1>", C < 4 ? C : 4);
+#define MPIV_PF(CC)                                                                                             \
+    plane_sweep_pf_kernel<CC, 1><<<G, kDLThreads, 0, q>>>(img, st[0], (int)st[1], (int)st[2], (int)st[3], sp,    \
+                                                          rc_hs, rc_ws, ki, proj, depths, out,                    \
+                                                          out_bstride, out_pstride, (int)vec, shrink, (int)tiles, \
+                                                          (int)total, (int)span)
+        switch (C) {
+            case 1: MPIV_PF(1); break;
+            case 2: MPIV_PF(2); break;
+            case 3: MPIV_PF(3); break;
+            default: MPIV_PF(4); break;
+        }
+#undef MPIV_PF
+        return launched(nm);
+    }
+#endif
     // one pixel per lane and iteration for few depths (D = 10: 0.228 vs 0.243 ms), two above
     // (D = 64: 0.640 vs 0.652; profiles/r03_sweep_few_depths_ab.txt)
     const int pix = (SLR == 4 && D <= 16) ? 1 : kDLPix;
+    const bool soa = MPIV_AB && opt(kOptSweepSoa) > 0;
     if (g_route && !(MPIV_AB && opt(kOptSweepBand) != 0 && SLR == 4))
-        return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true, %d, %d, %d>", C < 4 ? C : 4, SLR,
-                          SLR == 4 ? kSLCap : 4096, pix);
-#define MPIV_DLRAW(CC, RR, CAP, PP)                                                                          \
-    plane_sweep_dlane_kernel<CC, true, RR, CAP, PP><<<lgrid, kDLThreads, 0, q>>>(nullptr, PadGeom{0, 0, 0, 0}, img, \
-                                                                                is, sp, rc_hs, rc_ws, ki, proj,     \
-                                                                                depths, out, out_bstride,           \
-                                                                                out_pstride, (int)vec, shrink)
+        return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true, %d, %d, %d%s>", C < 4 ? C : 4, SLR,
+                          SLR == 4 ? kSLCap : 4096, pix, soa ? ", true" : "");
+#define MPIV_DLRAW1(CC, RR, CAP, PP, SO)                                                                           \
+    plane_sweep_dlane_kernel<CC, true, RR, CAP, PP, SO><<<lgrid, kDLThreads, 0, q>>>(nullptr, PadGeom{0, 0, 0, 0}, img, \
+                                                                                    is, sp, rc_hs, rc_ws, ki, proj,     \
+                                                                                    depths, out, out_bstride,           \
+                                                                                    out_pstride, (int)vec, shrink)
+#if MPIV_AB  // channel-planar staging: measured slower
+#define MPIV_DLRAW(CC, RR, CAP, PP)         \
+    if (soa) MPIV_DLRAW1(CC, RR, CAP, PP, true); \
+    else MPIV_DLRAW1(CC, RR, CAP, PP, false)
+#else
+#define MPIV_DLRAW(CC, RR, CAP, PP) MPIV_DLRAW1(CC, RR, CAP, PP, false)
+#endif
 #define MPIV_DLRAW_C(RR, CAP, PP)                  \
     switch (C) {                                   \
         case 1: MPIV_DLRAW(1, RR, CAP, PP); break; \
@@ -1210,6 +1278,7 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
     }
 #undef MPIV_DLRAW_C
 #undef MPIV_DLRAW
+#undef MPIV_DLRAW1
     return launched(nm);
 }
 

@@ -354,6 +354,9 @@ __device__ __forceinline__ float4 net_assemble2(const NetWA& q, const NetBF& r) 
 // 1152 blocks of RPT = 1 ran in two rounds of a latency-bound per-plane loop (round 4: 0.14 ms).
 // NW waves per block (tile 64 x NW*RPT); the planes' w / a loads run DEPTH planes ahead (1: plane
 // p+1's while plane p is sampled), bg / fg one plane ahead.
+#ifndef MPIV_NET_BFONCE
+#define MPIV_NET_BFONCE 0  // timing probe only (wrong frames): bg / fg loaded for plane 0's box alone
+#endif
 template <int NW, int RPT, int DEPTH, bool BUF>
 __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __restrict__ pred,
                                                                 const float* __restrict__ fg, NetStrides ns,
@@ -520,7 +523,7 @@ __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __r
         const int4 bx = box_of(p);
         if (staged(bx)) commit(st, bx);
         __syncthreads();  // plane p's box is in LDS
-        if (p + 1 < P) {
+        if (p + 1 < P && !MPIV_NET_BFONCE) {
             const int4 bn = box_of(p + 1);
             if (staged(bn)) fetch_bf(bn);
         }

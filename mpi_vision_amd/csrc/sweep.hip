@@ -896,12 +896,11 @@ __device__ __forceinline__ f32x4 raw_texel(const float* __restrict__ t, int64_t 
 // (CONTIG is decided once per fill, outside the unrolled loop: a branch per texel kept the
 // loads from being in flight together)
 template <int C, int NT, bool CONTIG, int CAP = kSLCap>
-__device__ __forceinline__ void sweep_fill_box_raw(float4* __restrict__ s_src, const float* __restrict__ img,
-                                                   const ImgStrides& is, int Hs, int Ws, const SweepBox& bx) {
+__device__ __forceinline__ void sweep_fill_load_raw(f32x4 (&stg)[CAP / NT], const float* __restrict__ img,
+                                                    const ImgStrides& is, int Hs, int Ws, const SweepBox& bx) {
     constexpr int kFill = CAP / NT;
     const int nfp = bx.rows * bx.pitch;
     const float rp = 1.0f / (float)bx.pitch;
-    f32x4 stg[kFill];
 #pragma unroll
     for (int k = 0; k < kFill; ++k) {
         const int idx = threadIdx.x + NT * k;
@@ -913,8 +912,59 @@ __device__ __forceinline__ void sweep_fill_box_raw(float4* __restrict__ s_src, c
         const float* t = img + (in ? (int64_t)y * is.y + (int64_t)x * is.x : 0);
         stg[k] = raw_texel<C, CONTIG>(t, is.c, in);
     }
+}
+
+typedef float f32x3b __attribute__((ext_vector_type(3)));
+__device__ f32x3b llvm_raw_buffer_load_v3f32(__amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset,
+                                             int aux) __asm("llvm.amdgcn.raw.ptr.buffer.load.v3f32");
+
+// sweep_fill_load_raw through a buffer resource over one source image (r: its span, < 2 GiB):
+// texels outside the image read the out-of-range offset, whose loads return 0 -- the same values,
+// with no per-texel mask held until the data arrives.
+template <int C, int NT, bool CONTIG, int CAP = kSLCap>
+__device__ __forceinline__ void sweep_fill_load_rsrc(f32x4 (&stg)[CAP / NT], __amdgpu_buffer_rsrc_t r,
+                                                     const ImgStrides& is, int Hs, int Ws, const SweepBox& bx) {
+    constexpr int kFill = CAP / NT;
+    const int nfp = bx.rows * bx.pitch;
+    const float rp = 1.0f / (float)bx.pitch;
+    const int sy = (int)is.y * 4, sx = (int)is.x * 4, sc = (int)is.c * 4;
 #pragma unroll
-    for (int k = 0; k < kFill; ++k) *reinterpret_cast<f32x4*>(&s_src[threadIdx.x + NT * k]) = stg[k];
+    for (int k = 0; k < kFill; ++k) {
+        const int idx = threadIdx.x + NT * k;
+        int row = (int)((float)idx * rp);  // idx < 2^12: off by at most one, corrected
+        row -= row * bx.pitch > idx ? 1 : 0;
+        row += (row + 1) * bx.pitch <= idx ? 1 : 0;
+        const int x = bx.xl + idx - row * bx.pitch, y = bx.yl + row;
+        const bool in = idx < nfp && (unsigned)x < (unsigned)Ws && (unsigned)y < (unsigned)Hs;
+        const int off = in ? y * sy + x * sx : kOOB;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (CONTIG && C == 4) {
+            v = llvm_raw_buffer_load_v4f32(r, off, 0, 0);
+        } else if (CONTIG && C == 3) {
+            const f32x3b q = llvm_raw_buffer_load_v3f32(r, off, 0, 0);
+            v[0] = q[0];
+            v[1] = q[1];
+            v[2] = q[2];
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[c] = llvm_raw_buffer_load_f32(r, off, c * sc, 0);
+        }
+        stg[k] = v;
+    }
+}
+
+template <int NT, int CAP = kSLCap>
+__device__ __forceinline__ void sweep_fill_store(float4* __restrict__ s_src, const f32x4 (&stg)[CAP / NT]) {
+#pragma unroll
+    for (int k = 0; k < CAP / NT; ++k) *reinterpret_cast<f32x4*>(&s_src[threadIdx.x + NT * k]) = stg[k];
+}
+
+template <int C, int NT, bool CONTIG, int CAP = kSLCap>
+__device__ __forceinline__ void sweep_fill_box_raw(float4* __restrict__ s_src, const float* __restrict__ img,
+                                                   const ImgStrides& is, int Hs, int Ws, const SweepBox& bx) {
+    f32x4 stg[CAP / NT];
+    sweep_fill_load_raw<C, NT, CONTIG, CAP>(stg, img, is, Hs, Ws, bx);
+    sweep_fill_store<NT, CAP>(s_src, stg);
 }
 
 // issue_taps_padded + blend_taps on a RAW source: the same weights and fma chain, taps outside
@@ -944,60 +994,101 @@ __device__ __forceinline__ f32x4 raw_sample(const float* __restrict__ img, const
     return blend_taps(t);
 }
 
-// RAW: the source is the caller's strided tensor (img, is) instead of padded texels (img4, pg).
-// SLR target rows per tile, CAP staged texels: (4, 3072) by default; few depths take taller
-// tiles (more samples per staged box, abi.hip sweep_tile_rows) with a larger box.
-// PIX pixels (samples per lane) per iteration: 1 for few depths (D <= 16), 2 above.
-template <int C, bool RAW, int SLR = kSLR, int CAP = kSLCap, int PIX = kDLPix>
-__global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
-    const float4* __restrict__ img4, PadGeom pg, const float* __restrict__ img, ImgStrides is, SweepParams sp,
-    float rc_hs, float rc_ws, const float* __restrict__ ki, const float* __restrict__ proj,
-    const float* __restrict__ depths, float* __restrict__ out, int64_t out_bstride, int64_t out_pstride, int vec,
-    int shrink) {
-    static_assert(CAP % kDLThreads == 0, "the box fill writes every staging slot");
-    __shared__ __attribute__((aligned(16))) float4 s_src[CAP];
-    __shared__ SweepBox s_box;
+// A source image read through a buffer resource (plane_sweep_pf_kernel: span < 2 GiB): 32-bit byte
+// offsets, and texels outside the image read the out-of-range offset (0) instead of a masked load.
+struct RsrcImg {
+    __amdgpu_buffer_rsrc_t r;
+    int sy4, sx4, sc4;  // byte strides of a row, a pixel, a channel
+};
 
-    const int segs = (sp.Wt + kSLP - 1) / kSLP;
-    const int b = blockIdx.y;
-    const int ty = blockIdx.x / segs;
-    const int y0 = ty * SLR, x0 = (blockIdx.x - ty * segs) * kSLP;
-    const int np = min(kSLP, sp.Wt - x0), nr = min(SLR, sp.Ht - y0);
-    const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const float* k9 = ki + (int64_t)b * 9;
-    const float* m = proj + (int64_t)b * 16;
-    const __amdgpu_buffer_rsrc_t r =
-        make_rsrc(RAW ? nullptr : img4 + (int64_t)b * (pg.plane_bytes / 16), RAW ? 0 : pg.plane_bytes);
-    const float* imb = RAW ? img + (int64_t)b * is.b : nullptr;
+// raw_sample's weights, taps and blend (issue_taps_padded + blend_taps) on a RsrcImg: the same bits
+template <int C>
+__device__ __forceinline__ f32x4 rsrc_sample(const RsrcImg& ri, int Ws, int Hs, float px, float py) {
+    TapSet t;
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
+    const int cx = (int)__builtin_amdgcn_fmed3f(fx0, -2.0f, (float)Ws);
+    const int cy = (int)__builtin_amdgcn_fmed3f(fy0, -2.0f, (float)Hs);
+    auto tap = [&](int x, int y) {
+        const bool in = (unsigned)x < (unsigned)Ws && (unsigned)y < (unsigned)Hs;
+        const int off = in ? y * ri.sy4 + x * ri.sx4 : kOOB;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < C; ++c) v[c] = llvm_raw_buffer_load_f32(ri.r, off, c * ri.sc4, 0);
+        return v;
+    };
+    t.a = tap(cx, cy);
+    t.b = tap(cx + 1, cy);
+    t.c = tap(cx, cy + 1);
+    t.d = tap(cx + 1, cy + 1);
+    return blend_taps(t);
+}
 
-    if (wave == 0) {
-        float dmin, dmax, dbad;
-        sweep_depth_range(depths, sp.D, lane, dmin, dmax, dbad);
-        const SweepBox bx = sweep_tile_box(k9, m, sp, rc_hs, rc_ws, x0, y0, np, nr, dmin, dmax, dbad, shrink, lane, CAP);
-        if (lane == 0) s_box = bx;
-    }
-    __syncthreads();
-    SweepBox bx;
-    bx.xl = __builtin_amdgcn_readfirstlane(s_box.xl);
-    bx.yl = __builtin_amdgcn_readfirstlane(s_box.yl);
-    bx.rows = __builtin_amdgcn_readfirstlane(s_box.rows);
-    bx.pitch = __builtin_amdgcn_readfirstlane(s_box.pitch);
-    bx.fast = __builtin_amdgcn_readfirstlane(s_box.fast);
-    bx.zero = __builtin_amdgcn_readfirstlane(s_box.zero);
-    if (bx.zero) {  // the tile's output is all +0: store it
-        sweep_zero_tile<C, kDLThreads>(out, out_bstride, out_pstride, sp, vec, b, x0, y0, np, nr);
-        return;
-    }
-    if (bx.pitch > 0) {
-        if (RAW && is.c == 1 && C > 1)
-            sweep_fill_box_raw<C, kDLThreads, true, CAP>(s_src, imb, is, sp.Hs, sp.Ws, bx);
-        else if (RAW)
-            sweep_fill_box_raw<C, kDLThreads, false, CAP>(s_src, imb, is, sp.Hs, sp.Ws, bx);
-        else
-            sweep_fill_box<kDLThreads, CAP>(s_src, r, pg, bx);
-    }
-    __syncthreads();
+// Channel-planar staging (round 5, sweep_soa): the box as C planes of CAP floats instead of CAP
+// float4 texels.  A depth-per-lane wave's 16-lane LDS phase reads 16 samples along one epipolar
+// line (~1.4 px apart at config 3's widest baseline): as 16-B texels they fall on 16 four-bank
+// groups by column mod 16, and columns 16 apart collide (PMC r05, config 3: bank-conflict cycles
+// 3.6x the LDS instruction cycles); as 4-B words the columns spread over all 64 banks.  The NW / NE
+// (SW / SE) taps of one channel are adjacent words: one ds_read2_b32.  Same values, same blend.
+template <int C, int NT, int CAP>
+__device__ __forceinline__ void sweep_fill_store_soa(float* __restrict__ s, const f32x4 (&stg)[CAP / NT]) {
+#pragma unroll
+    for (int k = 0; k < CAP / NT; ++k)
+#pragma unroll
+        for (int c = 0; c < C; ++c) s[c * CAP + threadIdx.x + NT * k] = stg[k][c];
+}
 
+// lds_issue on the channel-planar box: the same origin test and taps (channels >= C read as 0)
+template <int C, int CAP>
+__device__ __forceinline__ bool lds_issue_soa(const float* __restrict__ tex, const LdsBox& b, float px, float py,
+                                              TapSet& t) {
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float wx = px - fx0, ex = 1.0f - wx;
+    const float wy = py - fy0, sy = 1.0f - wy;
+    t.nw = sy * ex;
+    t.ne = sy * wx;
+    t.sw = wy * ex;
+    t.se = wy * wx;
+    const float rx = fx0 - b.xl, ry = fy0 - b.yl;  // exact wherever the origin can be staged
+    const float ix = __builtin_amdgcn_fmed3f(rx, 0.0f, b.xspan);
+    const float iy = __builtin_amdgcn_fmed3f(ry, 0.0f, b.yspan);
+    const float* st = tex + (int)__builtin_fmaf(iy, (float)b.pitch, ix);  // < rows * pitch: exact
+    t.a = t.b = t.c = t.d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        t.a[c] = st[c * CAP];
+        t.b[c] = st[c * CAP + 1];
+        t.c[c] = st[c * CAP + b.pitch];
+        t.d[c] = st[c * CAP + b.pitch + 1];
+    }
+    return (__builtin_amdgcn_fmed3f(rx, b.gxl, b.gxh) == rx) & (__builtin_amdgcn_fmed3f(ry, b.gyl, b.gyh) == ry);
+}
+
+#ifndef MPIV_SW_NOSAMPLE  // timing probes of the depth-per-lane sweep (wrong volumes; never in a product build)
+#define MPIV_SW_NOSAMPLE 0
+#endif
+#ifndef MPIV_SW_NOSTORE
+#define MPIV_SW_NOSTORE 0
+#endif
+#ifndef MPIV_SW_NOFILL
+#define MPIV_SW_NOFILL 0
+#endif
+// The samples and stores of one staged tile (box bx staged in s_src when bx.pitch > 0), shared by
+// plane_sweep_dlane_kernel and plane_sweep_pf_kernel: the same arithmetic, so their volumes are
+// bit-identical.
+template <int C, bool RAW, int PIX, bool RS = false, bool SOA = false, int CAP = kSLCap>
+__device__ __forceinline__ void dlane_tile(const float4* __restrict__ s_src, const SweepBox& bx,
+                                           __amdgpu_buffer_rsrc_t r, const PadGeom& pg, const float* __restrict__ imb,
+                                           const ImgStrides& is, const SweepParams& sp, float rc_hs, float rc_ws,
+                                           const float* __restrict__ k9, const float* __restrict__ m,
+                                           const float* __restrict__ depths, float* __restrict__ out,
+                                           int64_t out_bstride, int64_t out_pstride, int vec, int b, int x0, int y0,
+                                           int np, int nr, int lane, int wave, const RsrcImg* ri = nullptr) {
     const int pitch = bx.pitch;
     const bool all_fast = bx.fast != 0;
     const LdsBox lbx = make_lds_box(bx.xl, bx.yl, bx.rows, pitch, sp.Ws, sp.Hs);
@@ -1066,11 +1157,18 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
             py[j] = unnormalize(to_grid(cy), sp.half_hs);
         }
         f32x4 s[PIX];
-        bool staged = pitch > 0;
+        bool staged = pitch > 0 && !MPIV_SW_NOSAMPLE;
+        if (MPIV_SW_NOSAMPLE) {  // timing probe: no samples, the stores write the positions
+#pragma unroll
+            for (int j = 0; j < PIX; ++j) s[j] = f32x4{px[j], py[j], 0.0f, 0.0f};
+        }
         if (staged) {  // 16-B tap reads (ds_read_b128: 4 LDS cycles, ds_read_b96 8)
             TapSet ts[PIX];
 #pragma unroll
-            for (int j = 0; j < PIX; ++j) staged = lds_issue(s_src, lbx, px[j], py[j], ts[j]) && staged;
+            for (int j = 0; j < PIX; ++j)
+                staged = (SOA ? lds_issue_soa<C, CAP>(reinterpret_cast<const float*>(s_src), lbx, px[j], py[j], ts[j])
+                              : lds_issue(s_src, lbx, px[j], py[j], ts[j])) &&
+                         staged;
 #pragma unroll
             for (int j = 0; j < PIX; ++j) s[j] = blend_taps(ts[j]);
             // the unused channels' registers stay allocated until the reads are consumed
@@ -1079,11 +1177,13 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
             for (int j = 0; j < PIX; ++j)
                 asm volatile("" ::"v"(ts[j].a), "v"(ts[j].b), "v"(ts[j].c), "v"(ts[j].d));
         }
-        if (__builtin_amdgcn_ballot_w64(!staged)) {  // wave-uniform test, then per lane
+        if (!MPIV_SW_NOSAMPLE && __builtin_amdgcn_ballot_w64(!staged)) {  // wave-uniform test, then per lane
             if (!staged) {                            // a tap origin not staged: gather from global memory
 #pragma unroll
                 for (int j = 0; j < PIX; ++j) {
-                    if (RAW) {
+                    if (RS) {
+                        s[j] = rsrc_sample<C>(*ri, sp.Ws, sp.Hs, px[j], py[j]);
+                    } else if (RAW) {
                         s[j] = raw_sample<C>(imb, is, sp.Ws, sp.Hs, px[j], py[j]);
                     } else {
                         TapSet ts;
@@ -1096,7 +1196,7 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
         }
 #pragma unroll
         for (int j = 0; j < PIX; ++j) {
-            if (live[j]) {
+            if (live[j] && (!MPIV_SW_NOSTORE || s[j][0] == -12345.0f)) {  // (probe: stores kept only nominally)
                 f32xC v;
 #pragma unroll
                 for (int c = 0; c < C; ++c) v[c] = s[j][c];
@@ -1111,6 +1211,192 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     }
     }
 }
+
+// RAW: the source is the caller's strided tensor (img, is) instead of padded texels (img4, pg).
+// SLR target rows per tile, CAP staged texels: (4, 3072) by default; few depths take taller
+// tiles (more samples per staged box, abi.hip sweep_tile_rows) with a larger box.
+// PIX pixels (samples per lane) per iteration: 1 for few depths (D <= 16), 2 above.
+template <int C, bool RAW, int SLR = kSLR, int CAP = kSLCap, int PIX = kDLPix, bool SOA = false>
+__global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
+    const float4* __restrict__ img4, PadGeom pg, const float* __restrict__ img, ImgStrides is, SweepParams sp,
+    float rc_hs, float rc_ws, const float* __restrict__ ki, const float* __restrict__ proj,
+    const float* __restrict__ depths, float* __restrict__ out, int64_t out_bstride, int64_t out_pstride, int vec,
+    int shrink) {
+    static_assert(CAP % kDLThreads == 0, "the box fill writes every staging slot");
+    static_assert(!SOA || RAW, "channel-planar staging reads RAW sources");
+    __shared__ __attribute__((aligned(16))) float4 s_src[CAP];
+    __shared__ SweepBox s_box;
+
+    const int segs = (sp.Wt + kSLP - 1) / kSLP;
+    const int b = blockIdx.y;
+    const int ty = blockIdx.x / segs;
+    const int y0 = ty * SLR, x0 = (blockIdx.x - ty * segs) * kSLP;
+    const int np = min(kSLP, sp.Wt - x0), nr = min(SLR, sp.Ht - y0);
+    const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const float* k9 = ki + (int64_t)b * 9;
+    const float* m = proj + (int64_t)b * 16;
+    const __amdgpu_buffer_rsrc_t r =
+        make_rsrc(RAW ? nullptr : img4 + (int64_t)b * (pg.plane_bytes / 16), RAW ? 0 : pg.plane_bytes);
+    const float* imb = RAW ? img + (int64_t)b * is.b : nullptr;
+
+    if (wave == 0) {
+        float dmin, dmax, dbad;
+        sweep_depth_range(depths, sp.D, lane, dmin, dmax, dbad);
+        const SweepBox bx = sweep_tile_box(k9, m, sp, rc_hs, rc_ws, x0, y0, np, nr, dmin, dmax, dbad, shrink, lane, CAP);
+        if (lane == 0) s_box = bx;
+    }
+    __syncthreads();
+    SweepBox bx;
+    bx.xl = __builtin_amdgcn_readfirstlane(s_box.xl);
+    bx.yl = __builtin_amdgcn_readfirstlane(s_box.yl);
+    bx.rows = __builtin_amdgcn_readfirstlane(s_box.rows);
+    bx.pitch = __builtin_amdgcn_readfirstlane(s_box.pitch);
+    bx.fast = __builtin_amdgcn_readfirstlane(s_box.fast);
+    bx.zero = __builtin_amdgcn_readfirstlane(s_box.zero);
+    if (bx.zero) {  // the tile's output is all +0: store it
+        sweep_zero_tile<C, kDLThreads>(out, out_bstride, out_pstride, sp, vec, b, x0, y0, np, nr);
+        return;
+    }
+    if (SOA && bx.pitch > 0) {  // channel-planar staging (RAW sources)
+        f32x4 stg[CAP / kDLThreads];
+        if (is.c == 1 && C > 1)
+            sweep_fill_load_raw<C, kDLThreads, true, CAP>(stg, imb, is, sp.Hs, sp.Ws, bx);
+        else
+            sweep_fill_load_raw<C, kDLThreads, false, CAP>(stg, imb, is, sp.Hs, sp.Ws, bx);
+        sweep_fill_store_soa<C, kDLThreads, CAP>(reinterpret_cast<float*>(s_src), stg);
+    } else if (bx.pitch > 0 && !MPIV_SW_NOFILL) {
+        if (RAW && is.c == 1 && C > 1)
+            sweep_fill_box_raw<C, kDLThreads, true, CAP>(s_src, imb, is, sp.Hs, sp.Ws, bx);
+        else if (RAW)
+            sweep_fill_box_raw<C, kDLThreads, false, CAP>(s_src, imb, is, sp.Hs, sp.Ws, bx);
+        else
+            sweep_fill_box<kDLThreads, CAP>(s_src, r, pg, bx);
+    }
+    __syncthreads();
+
+    dlane_tile<C, RAW, PIX, false, SOA, CAP>(s_src, bx, r, pg, imb, is, sp, rc_hs, rc_ws, k9, m, depths, out, out_bstride,
+                                             out_pstride, vec, b, x0, y0, np, nr, lane, wave);
+}
+
+#if MPIV_AB
+// Persistent depth-per-lane sweep with the next tile's box prefetched (round 5).  Per tile,
+// plane_sweep_dlane_kernel computes a box, stages it and only then samples: two dependent
+// latencies (the box's vertex math, the fill's loads) and two barriers before the first store.
+// With few depths that prologue is most of the kernel (PMC r05, 768x1024 sources: ~3350 of the
+// 4700 cycles a wave lives at D = 10, and ~3350 of 11900 at D = 64).  Here a block stays
+// resident (grid = the blocks that fit at once) and walks the tiles t = lb, lb + G, ... (G
+// blocks, XCD-aware: at every step an XCD holds a contiguous run of tiles); while tile t is
+// sampled, the source texels of tile t + G are already on their way into registers (issued
+// right after t's box was staged; committed to LDS after t's last read), and wave 0 computes
+// the box of tile t + 2G after its share of the samples.  The boxes, fills, samples and stores
+// are plane_sweep_dlane_kernel's (sweep_tile_box, sweep_fill_load_raw, dlane_tile): the volume
+// is bit-identical.  One pixel per lane and iteration (the prefetched fill holds 24 VGPRs).
+// Measured SLOWER (A/B build only, sweep_pf=1; profiles/r05_sweep_pf_ab.jsonl): config 3 0.71 vs
+// 0.62 ms, D = 10 0.216 vs 0.177 -- the per-tile prologue is already hidden by the 3 blocks per
+// CU of the one-tile kernel, and the persistent loop needs 100 VGPRs (4 waves per SIMD) or spills
+// at 80.
+#ifndef MPIV_PF_NOPF
+#define MPIV_PF_NOPF 0  // probe: the next tile's fill issued after this tile's samples
+#endif
+#ifndef MPIV_PF_WAVES
+#define MPIV_PF_WAVES 6  // waves per SIMD the allocator must keep (3 blocks per CU, the LDS limit); 0: free
+#endif
+template <int C, int PIX>
+__global__ __launch_bounds__(kDLThreads) __attribute__((amdgpu_waves_per_eu(MPIV_PF_WAVES > 0 ? MPIV_PF_WAVES : 1)))
+void plane_sweep_pf_kernel(
+    const float* __restrict__ img, int64_t img_bstride, int sy, int sx, int sc, SweepParams sp, float rc_hs,
+    float rc_ws, const float* __restrict__ ki, const float* __restrict__ proj, const float* __restrict__ depths,
+    float* __restrict__ out, int64_t out_bstride, int64_t out_pstride, int vec, int shrink, int ntiles, int total,
+    int span) {
+    constexpr int CAP = kSLCap, SLR = kSLR, kFill = CAP / kDLThreads;
+    __shared__ __attribute__((aligned(16))) float4 s_src[CAP];
+    __shared__ SweepBox s_box[2];
+    const int segs = (sp.Wt + kSLP - 1) / kSLP;
+    const int G = gridDim.x;
+    const int lb = xcd_logical_block(blockIdx.x, G);
+    const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (lb >= total) return;  // whole block (the grid is at most `total`); no barrier follows
+    struct TileGeo {
+        int b, x0, y0, np, nr;
+    };
+    auto geo = [&](int t) {
+        TileGeo q;
+        q.b = t / ntiles;
+        const int tile = t - q.b * ntiles;
+        const int ty = tile / segs;
+        q.y0 = ty * SLR;
+        q.x0 = (tile - ty * segs) * kSLP;
+        q.np = min(kSLP, sp.Wt - q.x0);
+        q.nr = min(SLR, sp.Ht - q.y0);
+        return q;
+    };
+    float dmin = 0.0f, dmax = 0.0f, dbad = 0.0f;
+    if (wave == 0) sweep_depth_range(depths, sp.D, lane, dmin, dmax, dbad);
+    auto box_to = [&](int t, int slot) {  // wave 0
+        const TileGeo q = geo(t);
+        const SweepBox bx = sweep_tile_box(ki + (int64_t)q.b * 9, proj + (int64_t)q.b * 16, sp, rc_hs, rc_ws, q.x0,
+                                           q.y0, q.np, q.nr, dmin, dmax, dbad, shrink, lane, CAP);
+        if (lane == 0) s_box[slot] = bx;
+    };
+    auto read_box = [&](int slot) {
+        SweepBox bx;
+        bx.xl = __builtin_amdgcn_readfirstlane(s_box[slot].xl);
+        bx.yl = __builtin_amdgcn_readfirstlane(s_box[slot].yl);
+        bx.rows = __builtin_amdgcn_readfirstlane(s_box[slot].rows);
+        bx.pitch = __builtin_amdgcn_readfirstlane(s_box[slot].pitch);
+        bx.fast = __builtin_amdgcn_readfirstlane(s_box[slot].fast);
+        bx.zero = __builtin_amdgcn_readfirstlane(s_box[slot].zero);
+        return bx;
+    };
+    const ImgStrides is{0, sy, sx, sc};
+    f32x4 stg[kFill];
+    auto fill_load = [&](const SweepBox& bx, int b) {
+        if (bx.zero || bx.pitch == 0) return;  // block-uniform
+        const __amdgpu_buffer_rsrc_t rb = make_rsrc(img + (int64_t)b * img_bstride, span);
+        if (sc == 1 && C > 1)
+            sweep_fill_load_rsrc<C, kDLThreads, true, CAP>(stg, rb, is, sp.Hs, sp.Ws, bx);
+        else
+            sweep_fill_load_rsrc<C, kDLThreads, false, CAP>(stg, rb, is, sp.Hs, sp.Ws, bx);
+    };
+    const __amdgpu_buffer_rsrc_t r0 = make_rsrc(nullptr, 0);
+    const PadGeom pg0{0, 0, 0, 0};
+    int t = lb;
+    if (wave == 0) {
+        box_to(t, 0);
+        if (t + G < total) box_to(t + G, 1);
+    }
+    __syncthreads();
+    SweepBox bx = read_box(0);
+    fill_load(bx, t / ntiles);
+    for (int i = 0;; ++i) {
+        const TileGeo q = geo(t);
+        if (!bx.zero && bx.pitch > 0) sweep_fill_store<kDLThreads, CAP>(s_src, stg);
+        __syncthreads();  // tile t staged; s_box[(i + 1) & 1] holds tile t + G's box
+        const int tn = t + G;
+        SweepBox bn;
+        if (tn < total) {  // block-uniform: the next tile's texels, in flight while t is sampled
+            bn = read_box((i + 1) & 1);
+            if (!MPIV_PF_NOPF) fill_load(bn, tn / ntiles);
+        }
+        if (bx.zero) {
+            sweep_zero_tile<C, kDLThreads>(out, out_bstride, out_pstride, sp, vec, q.b, q.x0, q.y0, q.np, q.nr);
+        } else {
+            // lane-only values re-derived per tile: hoisted out of the tile loop they would stay live
+            // across it (the allocator then spills at 6 waves per SIMD)
+            const RsrcImg ri{make_rsrc(img + (int64_t)q.b * img_bstride, span), sy * 4, sx * 4, sc * 4};
+            dlane_tile<C, true, PIX, true>(s_src, bx, r0, pg0, nullptr, is, sp, rc_hs, rc_ws, ki + (int64_t)q.b * 9,
+                                           proj + (int64_t)q.b * 16, depths, out, out_bstride, out_pstride, vec, q.b,
+                                           q.x0, q.y0, q.np, q.nr, lane, wave, &ri);
+        }
+        if (tn >= total) break;  // block-uniform; no barrier follows
+        if (MPIV_PF_NOPF) fill_load(bn, tn / ntiles);
+        if (wave == 0 && tn + G < total) box_to(tn + G, i & 1);
+        __syncthreads();  // every read of tile t's staging is done; s_box[i & 1] holds tile t + 2G's box
+        t = tn;
+        bx = bn;
+    }
+}
+#endif  // MPIV_AB
 
 // Band-walking depth-per-lane sweep (round 5).  plane_sweep_dlane_kernel stages a fresh box for
 // every 4 x 64 tile: its prologue (box from the 8 vertices, fill, two barriers) is paid per tile
