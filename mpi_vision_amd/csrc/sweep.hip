@@ -1075,6 +1075,9 @@ __device__ __forceinline__ bool lds_issue_soa(const float* __restrict__ tex, con
 #ifndef MPIV_SW_NOSTORE
 #define MPIV_SW_NOSTORE 0
 #endif
+#ifndef MPIV_SW_WAVEBOX
+#define MPIV_SW_WAVEBOX 0
+#endif
 #ifndef MPIV_SW_NOFILL
 #define MPIV_SW_NOFILL 0
 #endif
@@ -1239,6 +1242,18 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
         make_rsrc(RAW ? nullptr : img4 + (int64_t)b * (pg.plane_bytes / 16), RAW ? 0 : pg.plane_bytes);
     const float* imb = RAW ? img + (int64_t)b * is.b : nullptr;
 
+    SweepBox bx;
+    if (MPIV_SW_WAVEBOX) {  // probe: every wave derives the box itself (no barrier before the fill)
+        float dmin, dmax, dbad;
+        sweep_depth_range(depths, sp.D, lane, dmin, dmax, dbad);
+        const SweepBox b0 = sweep_tile_box(k9, m, sp, rc_hs, rc_ws, x0, y0, np, nr, dmin, dmax, dbad, shrink, lane, CAP);
+        bx.xl = __builtin_amdgcn_readfirstlane(b0.xl);
+        bx.yl = __builtin_amdgcn_readfirstlane(b0.yl);
+        bx.rows = __builtin_amdgcn_readfirstlane(b0.rows);
+        bx.pitch = __builtin_amdgcn_readfirstlane(b0.pitch);
+        bx.fast = __builtin_amdgcn_readfirstlane(b0.fast);
+        bx.zero = __builtin_amdgcn_readfirstlane(b0.zero);
+    } else {
     if (wave == 0) {
         float dmin, dmax, dbad;
         sweep_depth_range(depths, sp.D, lane, dmin, dmax, dbad);
@@ -1246,13 +1261,13 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
         if (lane == 0) s_box = bx;
     }
     __syncthreads();
-    SweepBox bx;
     bx.xl = __builtin_amdgcn_readfirstlane(s_box.xl);
     bx.yl = __builtin_amdgcn_readfirstlane(s_box.yl);
     bx.rows = __builtin_amdgcn_readfirstlane(s_box.rows);
     bx.pitch = __builtin_amdgcn_readfirstlane(s_box.pitch);
     bx.fast = __builtin_amdgcn_readfirstlane(s_box.fast);
     bx.zero = __builtin_amdgcn_readfirstlane(s_box.zero);
+    }
     if (bx.zero) {  // the tile's output is all +0: store it
         sweep_zero_tile<C, kDLThreads>(out, out_bstride, out_pstride, sp, vec, b, x0, y0, np, nr);
         return;

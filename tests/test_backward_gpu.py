@@ -92,6 +92,28 @@ def test_backward_collapsing_homography_vs_oracle(dev, bwd_mode):
     assert np.abs(want[0, :, :, 0]).max() > 1.0  # plane 0's one texel gathered the whole frame
 
 
+def test_backward_one_bucket_at_config4_size(dev):
+    """a legitimately slow fallback must complete, not time out into a NaN gradient.
+    At config 4's size (1024 x 1024) plane 0 collapses the whole frame onto one texel -- ONE
+    bucket of 2^20 pixels, which the fallback's phase 6 merge-sorts with a single block (its
+    slowest case) while every other block waits on its ticket -- and plane 1 minifies 16x.
+    The production path (tile gather refused -> fallback, wall-clock wait limit): no abort,
+    the gradient bit-exact to the oracle."""
+    g = torch.Generator().manual_seed(23)
+    H = W = 1024
+    P = 2
+    mpi = configs.synthetic_mpi(1, H, W, P, 31)
+    s = (H - 1) / (W - 1)
+    homs = torch.tensor([[[0.0, 0.0, 511.3, 0.0, 0.0, 400.6, 0.0, 0.0, 1.0],
+                          [16.0 * s, 0.0, 0.5, 0.0, 16.0 / s, 0.25, 0.0, 0.0, 1.0]]], dtype=torch.float32)
+    dout = torch.rand((1, H, W, 3), generator=g) * 2 - 1
+    want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
+    got, flag = _backward_flag(mpi.to(dev), homs, dout.to(dev), dev)
+    assert flag == 1  # the view went through the fallback
+    assert_bits(got, want, "one 2^20-pixel bucket")
+    assert np.abs(want[0, :, :, 0]).max() > 100.0  # plane 0's one texel gathered the whole frame
+
+
 def test_backward_broadcast_mpi(grad, dev, bwd_mode):
     """Broadcast MPI (stride-0 batch): per-view gradients are bit-exact to the oracle;
     their sum (torch's expand backward on the GPU) matches the reference within 1e-6."""
