@@ -104,7 +104,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      b, b + nblk, ...; diagnosis)
 //   bwd_fb_blocks=k    (A/B build) the backward fallback launches k blocks instead of the resident count
 //   netout_geo=WRD     render_netout_kernel<W, R, D>: W waves per block, R rows per work-item
-//                      (64 x W*R tiles), D planes' w / a loads in flight (e.g. 821; 0 = automatic)
+//                      (64 x W*R tiles), D planes' w / a loads in flight (e.g. 821); + 1000: two staged
+//                      boxes, one barrier per plane (1821, the default; 0 = automatic)
 //   sweep_band=0|1     (A/B build) mpiv_plane_sweep[_into]'s LDS-staged route: one box per 4-row tile
 //                      (plane_sweep_dlane_kernel, 0 = default) or bands of 8 tiles with the source rows
 //                      in an LDS ring (plane_sweep_band_kernel: measured 15-20 % slower)
@@ -1607,11 +1608,12 @@ int mpiv_assemble_mpi_backward(const float* drgba, const int64_t gs[5], const fl
 }
 
 // render_netout_kernel's geometry (netout_geo = 100 * waves + 10 * rows + depth; automatic: 821)
+// netout_geo: waves * 100 + rows * 10 + planes of w / a in flight; + 1000: the double-buffered box (DB)
 static int netout_geo() {
     const int o = opt(kOptNetoutGeo);
     switch (o) {
-        case 811: case 821: case 822: case 422: return o;
-        default: return 821;
+        case 811: case 821: case 822: case 422: case 1821: return o;
+        default: return 1821;  // round 5: double-buffered box, one barrier per plane (0.110-0.116 vs 0.115-0.122 ms)
     }
 }
 
@@ -1626,7 +1628,8 @@ int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* 
     const NetStrides s{ps[0], ps[1], ps[2], ps[3], fs[0], fs[1], fs[2], fs[3]};
     const RenderGeom g = make_geom(H, W, P);
     const int geo = netout_geo();
-    const int NW = geo / 100, R = geo / 10 % 10;
+    const int NW = geo / 100 % 10, R = geo / 10 % 10;
+    const bool db = geo >= 1000;
     const int64_t nb = (int64_t)blocks(W, kNTX) * blocks(H, NW * R) * B;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     // buffer addressing when one batch element's pred / fg spans fit a 32-bit byte offset
@@ -1638,7 +1641,9 @@ int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* 
         sb.pred_bytes = (int)pspan;
         sb.fg_bytes = (int)fspan;
     }
-    if (g_route) return note_route(nb, 64 * NW, "render_netout_kernel<%d, %d, %d, %s>", NW, R, geo % 10, buf ? "true" : "false");
+    if (g_route)
+        return note_route(nb, 64 * NW, "render_netout_kernel<%d, %d, %d, %s%s>", NW, R, geo % 10, buf ? "true" : "false",
+                          db ? ", true" : "");
     const unsigned nbu = (unsigned)nb;
     hipStream_t q = S(stream);
     switch (geo * 2 + (buf ? 1 : 0)) {
@@ -1649,6 +1654,12 @@ int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* 
         MPIV_NETOUT(8, 1, 1, 0) MPIV_NETOUT(8, 2, 1, 0) MPIV_NETOUT(8, 2, 2, 0) MPIV_NETOUT(4, 2, 2, 0)
         MPIV_NETOUT(8, 1, 1, 1) MPIV_NETOUT(8, 2, 1, 1) MPIV_NETOUT(8, 2, 2, 1) MPIV_NETOUT(4, 2, 2, 1)
 #undef MPIV_NETOUT
+        case 1821 * 2:
+            render_netout_kernel<8, 2, 1, false, true><<<nbu, 512, P * sizeof(int2), q>>>(pred, fg, sb, g, B, homs, out);
+            break;
+        case 1821 * 2 + 1:
+            render_netout_kernel<8, 2, 1, true, true><<<nbu, 512, P * sizeof(int2), q>>>(pred, fg, sb, g, B, homs, out);
+            break;
     }
     return launched(nm);
 }

@@ -354,22 +354,33 @@ __device__ __forceinline__ float4 net_assemble2(const NetWA& q, const NetBF& r) 
 // 1152 blocks of RPT = 1 ran in two rounds of a latency-bound per-plane loop (round 4: 0.14 ms).
 // NW waves per block (tile 64 x NW*RPT); the planes' w / a loads run DEPTH planes ahead (1: plane
 // p+1's while plane p is sampled), bg / fg one plane ahead.
+#ifndef MPIV_NET_EARLY
+#define MPIV_NET_EARLY 1  // DB: the next plane's loads issued before the barrier
+#endif
 #ifndef MPIV_NET_BFONCE
 #define MPIV_NET_BFONCE 0  // timing probe only (wrong frames): bg / fg loaded for plane 0's box alone
 #endif
-template <int NW, int RPT, int DEPTH, bool BUF>
+// DB (round 5): two staged boxes, plane p in buffer p & 1, so a plane needs one barrier (its box
+// staged) instead of two -- the commit of plane p+1 goes to the other buffer, which plane p-1's
+// samples finished reading before this plane's barrier.  The boxes get 100 texels per tile row
+// (1600 at 64 x 16: the widest box of config 2's camera path is ~1570) and the box table sits in
+// dynamic LDS sized by P, so 2 x 25.6 KiB keeps 3 blocks per CU.
+template <int NW, int RPT, int DEPTH, bool BUF, bool DB = false>
 __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __restrict__ pred,
                                                                 const float* __restrict__ fg, NetStrides ns,
                                                                 RenderGeom g, int V, const float* __restrict__ homs,
                                                                 float* __restrict__ out) {
     constexpr int kThreads = 64 * NW;
     constexpr int kTY = NW * RPT;
-    constexpr int kCap = 128 * kTY;  // texels per staged box: a 64 x 8 tile 1024 (its box at the swapped
-                                     // normalisation's x stretch 1.78: ~940; 64 x 16: up to ~1550)
-    constexpr int kFill = kCap / kThreads;
+    constexpr int kCap = (DB ? 100 : 128) * kTY;  // texels per staged box: a 64 x 8 tile 1024 (its box at the
+                                                  // swapped normalisation's x stretch 1.78: ~940; 64 x 16: up
+                                                  // to ~1550)
+    constexpr int kFill = (kCap + kThreads - 1) / kThreads;
     static_assert(DEPTH >= 1 && DEPTH <= 3, "planes in flight");
-    __shared__ __attribute__((aligned(16))) float4 s_tex[kCap];
-    __shared__ int2 s_box[kNMaxP];  // per plane: (x_lo, y_lo), (rows, direct) as 16-bit pairs
+    __shared__ __attribute__((aligned(16))) float4 s_tex_all[DB ? 2 * kCap : kCap];
+    extern __shared__ int2 s_box_dyn[];
+    __shared__ int2 s_box_st[DB ? 1 : kNMaxP];  // per plane: (x_lo, y_lo), (rows, direct) as 16-bit pairs
+    int2* s_box = DB ? s_box_dyn : s_box_st;
     __shared__ int s_pitch;
     const int tiles_x = (g.W + kNTX - 1) / kNTX;
     const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
@@ -460,7 +471,7 @@ __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __r
                 bf[j] = BUF ? net_load_bf_buf(rs, ns, g.H, g.W, P, bx.x + col_j[j], bx.y + row_j[j])
                             : net_load_bf(pred, fg, ns, g.H, g.W, P, v, bx.x + col_j[j], bx.y + row_j[j]);
     };
-    auto commit = [&](const NetWA (&st)[kFill], const int4& bx) {
+    auto commit = [&](const NetWA (&st)[kFill], const int4& bx, float4* s_tex) {
         const int nfp = bx.z * pitch;
 #pragma unroll
         for (int j = 0; j < kFill; ++j)
@@ -470,7 +481,7 @@ __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __r
     float cr[RPT], cg[RPT], cb[RPT];
 #pragma unroll
     for (int r = 0; r < RPT; ++r) cr[r] = cg[r] = cb[r] = -0.0f;  // plane 0 replaces it exactly (render.hip)
-    auto sample = [&](int p, const int4& bx) {
+    auto sample = [&](int p, const int4& bx, const float4* s_tex) {
         const float* hp = hv + (int64_t)p * 9;
 #pragma unroll
         for (int r = 0; r < RPT; ++r) {
@@ -521,18 +532,23 @@ __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __r
     // plane p + 1's bg / fg, in flight while plane p is sampled
     auto step = [&](int p, NetWA (&st)[kFill]) {
         const int4 bx = box_of(p);
-        if (staged(bx)) commit(st, bx);
-        __syncthreads();  // plane p's box is in LDS
-        if (p + 1 < P && !MPIV_NET_BFONCE) {
-            const int4 bn = box_of(p + 1);
-            if (staged(bn)) fetch_bf(bn);
-        }
-        if (p + DEPTH < P) {
-            const int4 bn = box_of(p + DEPTH);
-            if (staged(bn)) fetch_wa(st, p + DEPTH, bn);
-        }
-        sample(p, bx);
-        __syncthreads();  // every sample of plane p has read the box
+        float4* s_tex = s_tex_all + (DB ? (p & 1) * kCap : 0);
+        if (staged(bx)) commit(st, bx, s_tex);
+        auto fetch_next = [&]() {
+            if (p + 1 < P && !MPIV_NET_BFONCE) {
+                const int4 bn = box_of(p + 1);
+                if (staged(bn)) fetch_bf(bn);
+            }
+            if (p + DEPTH < P) {
+                const int4 bn = box_of(p + DEPTH);
+                if (staged(bn)) fetch_wa(st, p + DEPTH, bn);
+            }
+        };
+        if (DB && MPIV_NET_EARLY) fetch_next();  // the registers are free once committed: load before the barrier
+        __syncthreads();  // plane p's box is in LDS (DB: and plane p-1's samples are done with the other buffer)
+        if (!(DB && MPIV_NET_EARLY)) fetch_next();
+        sample(p, bx, s_tex);
+        if (!DB) __syncthreads();  // every sample of plane p has read the box
     };
     if (staged(box_of(0))) fetch_bf(box_of(0));
 #pragma unroll

@@ -130,7 +130,7 @@ def test_fused_net_output_render(dev):
     assert_bits(got.cpu().numpy(), want.cpu().numpy(), "fused assemble + render")
 
 
-@pytest.mark.parametrize("geo", [0, 811, 821, 822, 422, -811, -821])
+@pytest.mark.parametrize("geo", [0, 811, 821, 822, 422, 1821, -811, -821, -1821])
 @pytest.mark.parametrize("case", ["odd", "extreme", "strided", "big"])
 def test_fused_net_output_render_cases(case, geo, dev, kopts):
     """The one-kernel assembly + render (render_netout_kernel) against the two-step drop-ins

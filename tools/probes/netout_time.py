@@ -20,7 +20,7 @@ def main():
     pred = torch.rand((1, 2 * P + 3, H, W), generator=g, device=dev) * 2 - 1
     fg = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
     lib = os.path.basename(os.environ.get("MPIV_LIB", "libmpiv.so"))
-    geos = [int(x) for x in os.environ.get("GEOS", "821,822").split(",")]
+    geos = [int(x) for x in os.environ.get("GEOS", "821,1821").split(",")]
     for pose in (5, 20):
         homs = _host.render_homographies(configs.f32(c["poses"][pose:pose + 1]), configs.f32(c["depths"]),
                                          configs.f32([c["K"]]), 1).to(dev)
