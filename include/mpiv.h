@@ -50,8 +50,9 @@ const char *mpiv_build_id(void);
  * by name ("render_mv", "render_pair", "render_native_lds", "render_chunk", "render_ring",
  * "render_tile", "render_vshare", "chunk_rows", "chunk_flight", "sweep_tile", "sweep_store",
  * "sweep_dlane", "sweep_rows", "sweep_direct", "box_shrink", "bwd_fallback", "bwd_margin",
- * "bwd_gather", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode", "chunk_strip", "u8_flight", "bwd_group"; "reset" restores every default;
- * abi.hip documents the values).  Values that
+ * "bwd_gather", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode", "chunk_strip", "u8_flight", "bwd_group",
+ * "netout_geo", "netout_buf", "bwd_overlap", "sweep_band", "sweep_pf", "sweep_soa"; "reset" restores every
+ * default; abi.hip documents the values).  Values that
  * select a kernel kept only for A/B measurement return MPIV_ERR_ARG from libmpiv.so (they are
  * compiled into libmpiv_ab.so).  Process-wide; returns MPIV_ERR_ARG for an unknown name. */
 int mpiv_debug_set(const char *name, int value);
