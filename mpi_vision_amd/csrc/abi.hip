@@ -1219,8 +1219,8 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
     const int pix = (SLR == 4 && D <= 16) ? 1 : kDLPix;
     const bool soa = MPIV_AB && opt(kOptSweepSoa) > 0;
     if (g_route && !(MPIV_AB && opt(kOptSweepBand) != 0 && SLR == 4))
-        return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true, %d, %d, %d%s>", C < 4 ? C : 4, SLR,
-                          SLR == 4 ? kSLCap : 4096, pix, soa ? ", true" : "");
+        return note_route(tiles * B, kDLThreads, "plane_sweep_dlane_kernel<%d, true, %d, %d, %d, %s>", C < 4 ? C : 4, SLR,
+                          SLR == 4 ? kSLCap : 4096, pix, soa ? "true" : "false");  // (rocprof prints every argument)
 #define MPIV_DLRAW1(CC, RR, CAP, PP, SO)                                                                           \
     plane_sweep_dlane_kernel<CC, true, RR, CAP, PP, SO><<<lgrid, kDLThreads, 0, q>>>(nullptr, PadGeom{0, 0, 0, 0}, img, \
                                                                                     is, sp, rc_hs, rc_ws, ki, proj,     \
@@ -1642,8 +1642,8 @@ int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* 
         sb.fg_bytes = (int)fspan;
     }
     if (g_route)
-        return note_route(nb, 64 * NW, "render_netout_kernel<%d, %d, %d, %s%s>", NW, R, geo % 10, buf ? "true" : "false",
-                          db ? ", true" : "");
+        return note_route(nb, 64 * NW, "render_netout_kernel<%d, %d, %d, %s, %s>", NW, R, geo % 10, buf ? "true" : "false",
+                          db ? "true" : "false");
     const unsigned nbu = (unsigned)nb;
     hipStream_t q = S(stream);
     switch (geo * 2 + (buf ? 1 : 0)) {

@@ -128,7 +128,7 @@ def test_plane_sweep_routes(C):
             assert name == f"plane_sweep_px_kernel<{C}, 64>", (D, name)
             assert grid == (Wt // 256) * Ht * B * 256, (D, grid)
         else:  # one pixel per lane and iteration up to 16 depths, two above
-            assert name == f"plane_sweep_dlane_kernel<{C}, true, 4, 3072, {1 if D <= 16 else 2}>", (D, name)
+            assert name == f"plane_sweep_dlane_kernel<{C}, true, 4, 3072, {1 if D <= 16 else 2}, false>", (D, name)
     assert _lib.route("plane_sweep", B, Hs, Ws, 5, 10, Ht, Wt)[0] == "plane_sweep_kernel"
 
 

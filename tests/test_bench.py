@@ -79,7 +79,7 @@ def test_route_dry_run_names_the_launched_kernels():
     assert _lib.route("render_packed", 576, 1024, 32, 64)[0] == "render_rows_kernel<false, 9, true, false, 3>"
     # a stretched MPI in a small launch keeps the one-row kernel
     assert _lib.route("render_packed", 576, 1024, 32, 1)[0] == "render_packed_kernel<false, true>"
-    assert _lib.route("plane_sweep", 5, 768, 1024, 3, 64, 768, 1024) == ("plane_sweep_dlane_kernel<3, true, 4, 3072, 2>",
+    assert _lib.route("plane_sweep", 5, 768, 1024, 3, 64, 768, 1024) == ("plane_sweep_dlane_kernel<3, true, 4, 3072, 2, false>",
                                                                          16 * 192 * 5 * 512)
     assert _lib.route("render", 1, 1024, 1024, 128) == ("render_chunk_strip_kernel<16, 2>", 32 * 64 * 256)
     assert _lib.route("render_train", 1, 1024, 1024, 128)[0] == "render_chunk_strip_kernel<16, 2>"
