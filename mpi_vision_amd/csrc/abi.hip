@@ -87,7 +87,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      (0 = automatic: 4 for launches under 2048 blocks)
 //   chunk_strip=0|1    the in-place render at CH = 8, one row: render_chunk_kernel's 64 x 1 wave rows
 //                      (0) or render_chunk_strip_kernel's 8 x 16 strips with vertical tap reuse (1);
-//                      A/B: 2 = 8 x 8 strips, 3 = 8 x 8 with 3 rows in flight, 4 = 8 x 16 with 3
+//                      A/B: 2 = 8 x 8 strips, 3 = 8 x 8 with 3 rows in flight, 4 = 8 x 16 with 3,
+//                      5 = 8 x 16 with the homographies read through the caches (4 blocks per CU)
 //   sweep_direct=-1|0|1  mpiv_plane_sweep[_into] without LDS staging (plane_sweep_direct_kernel):
 //                      never / automatic (D <= 2) / for any D <= 64; 2|3: pixel per lane, the wave's
 //                      samples staged in LDS (plane_sweep_px_kernel, D * C <= 48; 64 / 32 pixels
@@ -236,6 +237,9 @@ int launch_chunk(int R, const float* mpi, int64_t vstride, const RenderGeom& g, 
             render_chunk_strip_kernel<8, 3><<<(unsigned)ns, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
         else if (so == 4)
             render_chunk_strip_kernel<16, 3><<<(unsigned)ns, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);
+        else if (so == 5)  // homographies read through the caches instead of LDS: a fourth block per CU
+            render_chunk_strip_kernel<16, 2><<<(unsigned)ns, 256, (size_t)chunk_slot_floats<8, 1>() * 4, q>>>(
+                mpi, vstride, g, cg, B, homs, out, ck, 0);
         else
 #endif
             render_chunk_strip_kernel<16, 2><<<(unsigned)ns, 256, lds, q>>>(mpi, vstride, g, cg, B, homs, out, ck);

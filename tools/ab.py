@@ -168,6 +168,26 @@ def strips(dev, it):
     run("c4 render backward with checkpoints, 1 view", chains, fn, 2 * P * H * W * 16 + H * W * 12, it, passes=2)
 
 
+def striph(dev, it):
+    """Round 5: render_chunk_strip_kernel<16, 2> with its homographies in LDS (3 blocks per CU) or read
+    through the caches (chunk_strip=5: a fourth block per CU); frames compared bit for bit."""
+    mpi, homs, H, W, P = c4_mpi(dev)
+    variants = [("strip_hlds", {"chunk_strip": 1}), ("strip_hglobal", {"chunk_strip": 5})]
+    out = torch.empty((1, H, W, 3), device=dev)
+    fn = lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs, out, _lib._stream(dev))  # noqa: E731
+    frames = []
+    for label, opts in variants:
+        with _lib.debug(**opts):
+            fn()
+            torch.cuda.synchronize()
+            frames.append(out.clone())
+    print(json.dumps({"exp": "striph bit identity", "frames": bool(torch.equal(frames[0].view(torch.int32),
+                                                                                frames[1].view(torch.int32)))}), flush=True)
+    for _ in range(60):
+        fn()
+    run("c4 in-place render, 1 view", variants, fn, P * H * W * 16 + H * W * 12, it, passes=3)
+
+
 def strip(dev, it):
     """Round 4: render_chunk_strip_kernel (8 x 8 strips, vertical tap reuse) vs the 64 x 1
     wave rows, in-place render and training forward; frames and checkpoints compared bit for bit."""
