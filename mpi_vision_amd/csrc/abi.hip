@@ -1191,11 +1191,12 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
     // persistent tiles with the next tile's box and texels prefetched (plane_sweep_pf_kernel)
     const int opf = opt(kOptSweepPf);
     (void)opf;
-    // (its fill reads each source image through a buffer resource: non-negative strides, a span
-    // under 2 GiB)
+    // (fills through a buffer resource over each source image: non-negative strides, a span under 2 GiB)
     const int64_t span = ((int64_t)(Hs - 1) * st[1] + (int64_t)(Ws - 1) * st[2] + (int64_t)(C - 1) * st[3] + 1) * 4;
-    [[maybe_unused]] const bool pf_ok = st[1] >= 0 && st[2] >= 0 && st[3] >= 0 && st[1] < (1 << 28) && st[2] < (1 << 28) &&
-                       st[3] < (1 << 28) && span < kOOB - 64 && tiles * B < (1ll << 31);
+    const bool rs_ok = st[1] >= 0 && st[2] >= 0 && st[3] >= 0 && st[1] < (1 << 28) && st[2] < (1 << 28) &&
+                       st[3] < (1 << 28) && span < kOOB - 64;
+    [[maybe_unused]] const bool pf_ok = rs_ok && tiles * B < (1ll << 31);
+    const int span32 = rs_ok ? (int)span : 0;  // the staged kernels' buffer-resource fill (0: masked pointer loads)
 #if MPIV_AB  // measured slower than one block per tile
     if (SLR == 4 && shrink == 0 && pf_ok && opt(kOptSweepBand) == 0 && opf > 0) {
         const int64_t total = tiles * B;
@@ -1229,7 +1230,7 @@ static int sweep_raw_into(const char* nm, const float* img, const int64_t st[4],
     plane_sweep_dlane_kernel<CC, true, RR, CAP, PP, SO><<<lgrid, kDLThreads, 0, q>>>(nullptr, PadGeom{0, 0, 0, 0}, img, \
                                                                                     is, sp, rc_hs, rc_ws, ki, proj,     \
                                                                                     depths, out, out_bstride,           \
-                                                                                    out_pstride, (int)vec, shrink)
+                                                                                    out_pstride, (int)vec, shrink, span32)
 #if MPIV_AB  // channel-planar staging: measured slower
 #define MPIV_DLRAW(CC, RR, CAP, PP)         \
     if (soa) MPIV_DLRAW1(CC, RR, CAP, PP, true); \

@@ -1224,7 +1224,7 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
     const float4* __restrict__ img4, PadGeom pg, const float* __restrict__ img, ImgStrides is, SweepParams sp,
     float rc_hs, float rc_ws, const float* __restrict__ ki, const float* __restrict__ proj,
     const float* __restrict__ depths, float* __restrict__ out, int64_t out_bstride, int64_t out_pstride, int vec,
-    int shrink) {
+    int shrink, int span = 0) {
     static_assert(CAP % kDLThreads == 0, "the box fill writes every staging slot");
     static_assert(!SOA || RAW, "channel-planar staging reads RAW sources");
     __shared__ __attribute__((aligned(16))) float4 s_src[CAP];
@@ -1279,6 +1279,17 @@ __global__ __launch_bounds__(kDLThreads) void plane_sweep_dlane_kernel(
         else
             sweep_fill_load_raw<C, kDLThreads, false, CAP>(stg, imb, is, sp.Hs, sp.Ws, bx);
         sweep_fill_store_soa<C, kDLThreads, CAP>(reinterpret_cast<float*>(s_src), stg);
+    } else if (RAW && span > 0 && bx.pitch > 0) {
+        // (round 5) the fill through a buffer resource over the source image (span: its bytes, < 2 GiB):
+        // texels off the image read the out-of-range offset (0) instead of a masked load -- the same
+        // values; D = 10 0.173 vs 0.177 ms, config 3 0.615 vs 0.626 (profiles/r05_sweep_rsfill_ab.jsonl)
+        f32x4 stg[CAP / kDLThreads];
+        const __amdgpu_buffer_rsrc_t rb = make_rsrc(imb, span);
+        if (is.c == 1 && C > 1)
+            sweep_fill_load_rsrc<C, kDLThreads, true, CAP>(stg, rb, is, sp.Hs, sp.Ws, bx);
+        else
+            sweep_fill_load_rsrc<C, kDLThreads, false, CAP>(stg, rb, is, sp.Hs, sp.Ws, bx);
+        sweep_fill_store<kDLThreads, CAP>(s_src, stg);
     } else if (bx.pitch > 0 && !MPIV_SW_NOFILL) {
         if (RAW && is.c == 1 && C > 1)
             sweep_fill_box_raw<C, kDLThreads, true, CAP>(s_src, imb, is, sp.Hs, sp.Ws, bx);
