@@ -752,7 +752,7 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
 #pragma unroll
     for (int i = 0; i < kGSI; ++i) {
         const int q = t + i * kGThreads;
-        if (q >= np) break;
+        const bool qv = q < np;  // no divergent loop exit: pixels past the pass are masked below
         const int r = (int)(((float)q + 0.5f) * rbw);
         const int yy = ra + r, xx = bx0 + (q - r * bw);
         float px, py;
@@ -762,9 +762,9 @@ __device__ __forceinline__ void gather_stage_pass(const RenderGeom& g, const Bwd
             render_pos<true>(hp, (float)xx, (float)yy, g, px, py);
         const float fx0 = floorf(px), fy0 = floorf(py);
         const float lx = fx0 - (float)(tx0 - 1), ly = fy0 - (float)(ty0 - 1);
-        const bool in = lx >= 0.0f && lx <= (float)kGTW && ly >= 0.0f && ly <= (float)kGTY;
+        const bool in = qv && lx >= 0.0f && lx <= (float)kGTW && ly >= 0.0f && ly <= (float)kGTY;
         const int code = in ? (int)ly * TB + (int)lx : -1;
-        s_code[q] = code;
+        if (qv) s_code[q] = code;
         if (in) {
             // the four bilinear weights (issue_taps_padded's products, corner order nw, ne, sw, se):
             // the texel pass reads the one of its corner instead of re-deriving it from fractions
@@ -1084,7 +1084,8 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
             for (int b = threadIdx.x; b < 2 * kGNB; b += kGThreads) s_ent[par ^ 1][b] = ~0u;  // for the next pass
             if (threadIdx.x == 0) s_ovf[par ^ 1] = 0;
             __syncthreads();
-            const bool ovf = s_ovf[par] != 0;
+            // block-uniform: a scalar branch, not an exec-mask split per texel (round 5, fewer scalar instructions)
+            const bool ovf = __builtin_amdgcn_readfirstlane(s_ovf[par]) != 0;
 #pragma unroll
             for (int r = 0; r < kGTR; ++r)
                 gather_texel_pass<MPIV_GFRAC>(g, ws, p, margin, tx, ty[r], bt[r], tin[r], ovf, s_ent[par], s_code, s_w,
