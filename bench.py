@@ -118,6 +118,15 @@ def spawn_ranks(n: int) -> int:
     return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
+# Collective timeout of the bench's process group: well under the driver's 600-s limit for the whole
+# run, and longer than LEG_DEADLINE_S, so a hung exchange is ended by the LineGuard (which still
+# prints the line) before RCCL's watchdog would tear the process down without it.
+PG_TIMEOUT_S = float(os.environ.get("MPIV_BENCH_PG_TIMEOUT", "150"))
+# Wall-clock limit of the plane-sharded (config-5) leg at world > 1 -- the only leg with a data-path
+# collective -- counted from its start to the end of the run.
+LEG_DEADLINE_S = float(os.environ.get("MPIV_BENCH_LEG_DEADLINE", "90"))
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -126,13 +135,15 @@ def dist_setup(args):
     local = 0 if os.environ.get("MPIV_BENCH_ONE_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", "0"))
     backend = None
     if world > 1:
+        import datetime
         torch.cuda.set_device(local)
         import torch.distributed as dist
         backend = os.environ.get("MPIV_BENCH_BACKEND", "nccl")
+        timeout = datetime.timedelta(seconds=PG_TIMEOUT_S)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     return world, rank, torch.device("cuda", local), backend
@@ -163,6 +174,62 @@ def barrier(world):
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
+
+
+class LineGuard:
+    """Rank 0's one JSON line, printed exactly once, even when a collective leg hangs.
+
+    The plane-sharded leg (config 5) is the only one with a data-path exchange, and the driver's
+    8-GPU node is the first place it runs over RCCL at world > 1.  `guarded()` turns an exception
+    into an error field, but a hang would keep rank 0 from ever printing the headline it has
+    already measured.  So every rank arms a timer before that leg: if the leg (and the final
+    barrier / process-group teardown after it) has not finished by the deadline, rank 0 prints
+    the line with the leg's error field and every rank leaves with os._exit (an exit, not an
+    exec: no new program starts in the GPU-initialised process)."""
+
+    def __init__(self, rank: int, out=None):
+        import threading
+        self.rank = rank
+        self.out = out or sys.stdout
+        self.lock = threading.Lock()
+        self.printed = False
+        self.timer = None
+
+    def emit(self, res: dict) -> bool:
+        """Print res as the line (rank 0 only; at most once). True if this call printed it."""
+        with self.lock:
+            if self.rank != 0 or self.printed:
+                return False
+            self.printed = True
+            self.out.write(json.dumps(res) + "\n")
+            self.out.flush()
+            return True
+
+    def arm(self, seconds: float, res: dict, leg: str):
+        """From now on, `seconds` of wall clock until the run must have ended."""
+        import threading
+
+        def expire():
+            res[leg] = {"error": f"timed out: the leg and the run's teardown did not finish within {seconds:.0f} s "
+                                 "(a hung collective); the other legs' figures are complete"}
+            self.emit(res)
+            sys.stderr.write(f"bench.py rank {self.rank}: {leg} timed out after {seconds:.0f} s, exiting\n")
+            sys.stderr.flush()
+            os._exit(0)
+        self.timer = threading.Timer(seconds, expire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def disarm(self):
+        if self.timer is not None:
+            self.timer.cancel()
+            self.timer = None
+
+
+def fault_injected(name: str, rank: int) -> bool:
+    """MPIV_BENCH_FAULT=<name>: rehearse a failure of the plane-sharded exchange on the last rank
+    (c5_hang: it stops answering; c5_raise: it raises) -- tests of LineGuard / guarded only."""
+    return os.environ.get("MPIV_BENCH_FAULT") == name and rank == int(os.environ.get("WORLD_SIZE", "1")) - 1
 
 
 # ---------------------------------------------------------------------------
@@ -609,7 +676,7 @@ def u8_leg(dev, stream, V, homs_sv, homs_v, n=10):
     mark("untimed", dev)
     same_v = bool(torch.equal(want.view(torch.int32), many.view(torch.int32)))
     del fcopy, want
-    _lib._U8_FLOAT.clear()
+    _lib.clear_u8_float_copies()
     # float packed copy of u8/255 (numpy fp32 division is IEEE) for the bit-exact self-check
     f = (pk.view(torch.uint8).cpu().numpy().reshape(P, H + 4, W + 4, 4).astype(np.float32) / np.float32(255.0))
     fpk = torch.from_numpy(f).to(dev)
@@ -808,6 +875,10 @@ def config5_leg(world, rank, dev, steps, warmup):
     mark("c5_kernel", dev)
     kern_ms = event_ms(launch, 3, stream)
     mark("untimed", dev)
+    if world > 1 and fault_injected("c5_hang", rank):
+        time.sleep(1e6)  # the peers block in the band exchange
+    if world > 1 and fault_injected("c5_raise", rank):
+        raise RuntimeError("MPIV_BENCH_FAULT=c5_raise: injected exchange failure")
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -1006,8 +1077,6 @@ def main():
     if "u8" in legs:
         u8 = guarded(u8_leg, dev, stream, V, host_homs(0, 1).to(dev), host_homs(0).to(dev))
     train = guarded(training_leg, dev, stream) if "train" in legs else None
-    # (a Python-level failure is the same on every rank, so every rank records it and goes on)
-    c5 = guarded(config5_leg, world, rank, dev, max(3, args.steps // 2), 1) if "c5" in legs else None
     ranks = {"world_size_seen": world, "backend": backend, "per_rank_kernel_ms": [round(x, 4) for x in kern_all]}
     if world > 1:
         import torch.distributed as dist
@@ -1060,15 +1129,28 @@ def main():
             "u8_texels": u8,
             "net_output_render": nout,
             "training_render_backward": train,
-            "config5_plane_sharded": c5,
+            "config5_plane_sharded": None,
         }
         if cpu_frames is not None:
             res["cpu_baseline"] = cpu_baseline(cpu_view, host_homs(0), args.cpu_seconds, cpu_frames)
-        print(json.dumps(res), flush=True)
+    else:
+        res = {}
+    # the plane-sharded leg last, under the LineGuard at world > 1: every figure above is already in
+    # `res`, so a hung exchange costs only this leg's field, never the headline
+    guard = LineGuard(rank)
+    if world > 1 and "c5" in legs:
+        guard.arm(LEG_DEADLINE_S, res, "config5_plane_sharded")
+    # (a Python-level failure is recorded by guarded(); one that only some ranks see leaves the others
+    # in the exchange, which the guard's deadline ends)
+    c5 = guarded(config5_leg, world, rank, dev, max(3, args.steps // 2), 1) if "c5" in legs else None
+    if rank == 0:
+        res["config5_plane_sharded"] = c5
+        guard.emit(res)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()
+    guard.disarm()
 
 
 if __name__ == "__main__":

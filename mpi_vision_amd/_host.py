@@ -217,9 +217,18 @@ def psv_matrices(src_intrinsics: torch.Tensor, tgt_intrinsics: torch.Tensor, pos
         proj = [[K_src, 0], [0, 0, 0, 1]] @ pose    [B, 16]
     computed on CPU in fp32 with the reference's ops (page-locked with pin=True, ready for
     an asynchronous upload)."""
-    Ks, pose = _cpu32_together(src_intrinsics, pose)
+    kt = tgt_intrinsics.detach()
+    if kt.device.type != "cpu" and kt.numel() > 0:
+        # the storage span of K_tgt rides in the same device-to-host copy (ADVICE r5) and is
+        # re-viewed on the host with the caller's strides (cpu32_like's contract)
+        span = 1 + sum((n - 1) * st for n, st in zip(kt.shape, kt.stride()))
+        Ks, pose, kflat = _cpu32_together(src_intrinsics, pose,
+                                          torch.as_strided(kt, (span,), (1,), kt.storage_offset()))
+        kt = torch.as_strided(kflat, kt.shape, kt.stride())
+    else:
+        Ks, pose = _cpu32_together(src_intrinsics, pose)
     B = pose.shape[0]
-    ki = psv_inverse(tgt_intrinsics, B)  # the caller's layout (utils.py:370)
+    ki = psv_inverse(kt, B)  # the caller's layout (utils.py:370)
     Ks = Ks.expand(B, 3, 3)
     k4 = torch.cat([Ks, torch.zeros(B, 3, 1)], dim=2)
     k4 = torch.cat([k4, torch.tensor([[[0.0, 0.0, 0.0, 1.0]]]).repeat(B, 1, 1)], dim=1)

@@ -393,6 +393,8 @@ def pack_planes_u8(view: torch.Tensor, out: torch.Tensor | None = None) -> torch
     else:
         packed = out
     _call("mpiv_pack_planes_u8", view, _strides(view), H, W, P, packed, _stream(dev))
+    if out is not None:
+        _wrote(packed)
     return packed
 
 
@@ -426,19 +428,43 @@ U8_FLOAT_MIN_VIEWS = int(os.environ.get("MPIV_U8_FLOAT_MIN_VIEWS", "32"))
 _U8_FLOAT: dict = {}
 
 
+def _wrote(t: torch.Tensor) -> None:
+    """A kernel wrote t through ctypes (an out= argument): bump its version counter as a torch
+    in-place op would, so memos keyed on it (u8_float_copy) see the new contents."""
+    torch.autograd.graph.increment_version(t)
+
+
 def u8_float_copy(packed: torch.Tensor) -> torch.Tensor:
     """The packed float copy of a packed u8 MPI, memoised per device on the tensor object, its
-    storage and version counter (a camera path converts its MPI once; an in-place edit or a new
-    MPI converts again).  One entry per device: the copy is 4x the u8 MPI (2.2 GB at config 4)."""
+    storage, version counter and the current stream (a camera path converts its MPI once; an
+    in-place edit, a refill through pack_planes_u8(out=) or a new MPI converts again; a copy is
+    only read on the stream that made it).  One entry per device: the copy is 4x the u8 MPI
+    (2.2 GB at config 4); it is dropped when the u8 MPI is freed, or by clear_u8_float_copies()."""
     dev = packed.device
-    key = (id(packed), packed.data_ptr(), packed._version, tuple(packed.shape))
+    key = (id(packed), packed.data_ptr(), packed._version, tuple(packed.shape),
+           torch.cuda.current_stream(dev).cuda_stream)
     ent = _U8_FLOAT.get(dev)
     if ent is not None and ent[0] == key and ent[1]() is packed:
         return ent[2]
     _U8_FLOAT.pop(dev, None)  # free the old copy first
     f = unpack_planes_u8(packed)
     _U8_FLOAT[dev] = (key, weakref.ref(packed), f)
+    weakref.finalize(packed, _drop_u8_float, dev, key)
     return f
+
+
+def _drop_u8_float(dev, key) -> None:
+    ent = _U8_FLOAT.get(dev)
+    if ent is not None and ent[0] == key:
+        del _U8_FLOAT[dev]
+
+
+def clear_u8_float_copies(device=None) -> None:
+    """Free the memoised float copies of u8 MPIs (all devices, or `device`'s)."""
+    if device is None:
+        _U8_FLOAT.clear()
+    else:
+        _U8_FLOAT.pop(torch.device(device), None)
 
 
 def render_packed_u8(packed: torch.Tensor, homs: torch.Tensor, out: torch.Tensor | None = None,

@@ -854,13 +854,14 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const float margin = (float)opt(kOptBwdMargin) / 64.0f;
     hipStream_t q = S(stream);
     // fallback grid: at most the blocks that fit at once, <= 4 per CU (more would only wait for
-    // tickets; fewer resident ones still complete); queried once per device (relaxed atomics:
-    // racing first calls store the same value)
+    // tickets; fewer resident ones still complete); queried once per device (racing first calls
+    // store the same values; the block count is published with release after the clock rate and
+    // read with acquire, so a thread that sees it also sees the clock -- ADVICE r5)
     static int s_fb_blocks[64] = {};
     static long long s_clock_khz[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(MPIV_ERR_HIP, "%s: hipGetDevice failed", nm);
-    int fbb = __atomic_load_n(&s_fb_blocks[dev], __ATOMIC_RELAXED);
+    int fbb = __atomic_load_n(&s_fb_blocks[dev], __ATOMIC_ACQUIRE);
     if (fbb == 0) {
         int ncu = 0, pc_t = 0, pc_f = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -875,15 +876,15 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
             khz = 100000;  // gfx9's constant 100 MHz wall clock
         __atomic_store_n(&s_clock_khz[dev], (long long)khz, __ATOMIC_RELAXED);
-        __atomic_store_n(&s_fb_blocks[dev], fbb, __ATOMIC_RELAXED);
+        __atomic_store_n(&s_fb_blocks[dev], fbb, __ATOMIC_RELEASE);
     }
     const unsigned fb_blocks = opt(kOptBwdFbBlocks) > 0 ? (unsigned)opt(kOptBwdFbBlocks) : (unsigned)fbb;
     const int pl = opt(kOptBwdPollLimit);
     // production: no poll-count limit, a 60 s wall-clock limit per wait (a poll budget
     // could expire on a slow but correct fallback); bwd_poll_limit=k (A/B, tests) adds a count limit
     const unsigned poll_limit = pl > 0 ? (unsigned)pl : pl < 0 ? 0u : ~0u;
-    const unsigned long long tick_limit =
-        60000ull * (unsigned long long)__atomic_load_n(&s_clock_khz[dev], __ATOMIC_RELAXED);
+    const long long khz_seen = __atomic_load_n(&s_clock_khz[dev], __ATOMIC_RELAXED);
+    const unsigned long long tick_limit = 60000ull * (unsigned long long)(khz_seen > 0 ? khz_seen : 100000);
     const int fb_mode = opt(kOptBwdFbMode);
     // truth, found, flag (adjacent), and the second window's set after them
     if (hipMemsetAsync(ws.truth, 0, overlap ? 2 * (2 * kCtrSlots * 8 + 256) : 2 * kCtrSlots * 8 + 256, q) != hipSuccess)

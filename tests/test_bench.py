@@ -99,3 +99,60 @@ def test_route_dry_run_u8_and_net_output():
     assert _lib.route("render_packed_u8", 1024, 1024, 128, 125)[0] == "render_u8_kernel<false, 4, true, 2>"
     name, grid = _lib.route("render_net_output", 1, 576, 1024, 32)
     assert name == "render_netout_kernel<8, 2, 1, true, true>" and grid == 576 * 512
+
+
+def test_line_guard_prints_once():
+    import io
+    buf = io.StringIO()
+    g = bench.LineGuard(0, out=buf)
+    assert g.emit({"value": 1.0}) and not g.emit({"value": 2.0})
+    assert buf.getvalue().count("\n") == 1 and '"value": 1.0' in buf.getvalue()
+    other = io.StringIO()
+    assert not bench.LineGuard(1, out=other).emit({"value": 1.0}) and other.getvalue() == ""
+
+
+_HANG_WORKER = r"""
+import os, sys, time
+sys.path.insert(0, {repo!r})
+import datetime
+import torch.distributed as dist
+import bench
+rank = int(os.environ["RANK"])
+dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=120))
+res = {{"value": 123.0, "config5_plane_sharded": None}} if rank == 0 else {{}}
+g = bench.LineGuard(rank)
+g.arm(4.0, res, "config5_plane_sharded")
+if bench.fault_injected("c5_hang", rank):
+    time.sleep(1000)          # the last rank stops answering
+dist.barrier()                # rank 0 blocks here: the exchange that never completes
+res["config5_plane_sharded"] = {{"value": 1.0}}
+g.emit(res)
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_line_guard_survives_a_hung_exchange(world, tmp_path):
+    """A rank that stops answering in the collective leg (MPIV_BENCH_FAULT=c5_hang) must not cost the
+    line: at the deadline rank 0 prints the complete line with the leg's error field and every rank
+    exits 0 (gloo, CPU; the GPU-box rehearsal runs the same through bench.py's config-5 leg)."""
+    import json
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    script = tmp_path / "w.py"
+    script.write_text(_HANG_WORKER.format(repo=REPO))
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   MPIV_BENCH_FAULT="c5_hang")
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert [p.returncode for p in procs] == [0] * world, [o[1][-500:] for o in outs]
+    lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["value"] == 123.0 and "timed out" in line["config5_plane_sharded"]["error"]
+    assert all(not any(ln.startswith("{") for ln in o[0].splitlines()) for o in outs[1:])

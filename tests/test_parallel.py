@@ -55,7 +55,7 @@ def _plane_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_plane_sharded_exchange_matches_sequential(world, tmp_path):
     sys.path.insert(0, REPO)
     from oracle import oracle
@@ -154,10 +154,13 @@ def _pipelined_worker(rank, world, port, H, W, P, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H,W,P", [(2, 37, 53, 11), (3, 37, 53, 11), (4, 3, 6, 2), (3, 2, 11, 5)])
+@pytest.mark.parametrize("world,H,W,P", [(2, 37, 53, 11), (3, 37, 53, 11), (4, 3, 6, 2), (3, 2, 11, 5),
+                                         # the driver's 8-GPU node: config 5's 2160-row frame cut into
+                                         # 8 bands of 270 rows, and a frame shorter than the world
+                                         (8, 2160, 5, 16), (8, 5, 6, 3)])
 def test_plane_sharded_pipelined_equals_one_shot(world, H, W, P, tmp_path):
     """The pipelined band exchange (SURVEY §8e "pipeline bands to overlap") on gloo at world
-    2, 3, 4 (incl. ranks with no planes and with no rows): bit-identical to the one-shot
+    2, 3, 4 and 8 (incl. ranks with no planes and with no rows): bit-identical to the one-shot
     all-to-all path, and within 1e-5 of the sequential render."""
     sys.path.insert(0, REPO)
     from oracle import oracle
@@ -263,7 +266,7 @@ def _view_gather_worker(rank, world, port, n_views, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_views", [(2, 7), (3, 7), (3, 2)])
+@pytest.mark.parametrize("world,n_views", [(2, 7), (3, 7), (3, 2), (8, 13), (8, 5)])
 def test_view_sharded_gather_uneven(world, n_views, tmp_path):
     """View sharding's final frame gather with uneven shards (incl. a rank
     holding no views): rank 0 gets every frame, in camera-path order."""

@@ -182,3 +182,35 @@ def test_u8_many_views_route_through_float_copy(large, dev):
     d = _lib.render_packed_u8(pk, homs, route_float=False)
     assert_bits(c.cpu().numpy(), d.cpu().numpy(), "after an in-place edit")
     assert not torch.equal(a, c)
+
+
+@pytest.mark.gpu
+def test_u8_float_copy_follows_out_refills_streams_and_frees(dev, large):
+    """refilling the same packed buffer through pack_planes_u8(out=) (a ctypes write,
+    invisible to torch) must not render the old MPI's memoised float copy; a copy is not served to
+    another stream; the memo entry goes when its u8 MPI is freed."""
+    u8 = _test_mpi_u8().to(dev)
+    V = 40
+    pose = torch.tensor(large["c1_pose"]).to(dev)[torch.arange(V) % 2]
+    K = torch.tensor(large["c1_K"]).to(dev)[torch.arange(V) % 2]
+    depths = torch.tensor(large["c1_depths"]).to(dev)
+    homs = _host.render_homographies(pose.cpu(), depths.cpu(), K.cpu(), V)
+    pk = _lib.pack_planes_u8(u8[0])
+    a = _lib.render_packed_u8(pk, homs, route_float=True)
+    f1 = _lib.u8_float_copy(pk)
+    other = u8[0].flip(0).contiguous()  # a different MPI of the same shape
+    _lib.pack_planes_u8(other, out=pk)
+    b = _lib.render_packed_u8(pk, homs, route_float=True)
+    assert _lib.u8_float_copy(pk) is not f1
+    assert not torch.equal(a, b)
+    assert_bits(b.cpu().numpy(), _lib.render_packed_u8(pk, homs, route_float=False).cpu().numpy(),
+                "refilled buffer: float route vs u8 kernel")
+    f2 = _lib.u8_float_copy(pk)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        f3 = _lib.u8_float_copy(pk)
+    s.synchronize()
+    assert f3 is not f2 and torch.equal(f3, f2)
+    del f1, f2, f3, pk
+    assert dev not in _lib._U8_FLOAT
+    _lib.clear_u8_float_copies()
