@@ -398,6 +398,46 @@ def hbm(alg_bytes, ms):
     return round(gbs, 1), round(gbs / HBM_PEAK_GBS, 4)
 
 
+def sampled_boxes(homs: np.ndarray, H: int, W: int) -> np.ndarray:
+    """Texel boxes [V, P, 4] (x0, x1, y0, y1, inclusive, clamped to the image) that the
+    reference's render samples for each (view, plane).  The sample position of output pixel
+    (x, y) is linear-fractional in (x, y) (utils.py:186-188: u/w, v/w, then the SWAPPED
+    normalisation x/(H-1), y/(W-1) and grid_sample's unnormalise), so while w keeps its sign
+    over the frame its extremes lie at the 4 frame corners; a plane whose w changes sign gets
+    the whole image.  The bilinear taps add one texel right and below."""
+    h = homs.reshape(homs.shape[0], -1, 3, 3).astype(np.float64)
+    xs = np.array([0.0, W - 1.0, 0.0, W - 1.0])
+    ys = np.array([0.0, 0.0, H - 1.0, H - 1.0])
+    u = h[..., 0, 0, None] * xs + h[..., 0, 1, None] * ys + h[..., 0, 2, None]
+    v = h[..., 1, 0, None] * xs + h[..., 1, 1, None] * ys + h[..., 1, 2, None]
+    w = h[..., 2, 0, None] * xs + h[..., 2, 1, None] * ys + h[..., 2, 2, None]
+    same = (np.all(w > 0, axis=-1) | np.all(w < 0, axis=-1))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        px = u / w * W / max(H - 1, 1) - 0.5
+        py = v / w * H / max(W - 1, 1) - 0.5
+    x0 = np.clip(np.floor(px.min(-1)), 0, W - 1)
+    x1 = np.clip(np.floor(px.max(-1)) + 1, 0, W - 1)
+    y0 = np.clip(np.floor(py.min(-1)), 0, H - 1)
+    y1 = np.clip(np.floor(py.max(-1)) + 1, 0, H - 1)
+    off = (px.max(-1) < -1) | (px.min(-1) > W) | (py.max(-1) < -1) | (py.min(-1) > H)
+    box = np.stack([x0, x1, y0, y1], -1)
+    box[~same] = [0, W - 1, 0, H - 1]
+    box[same & off] = [0, -1, 0, -1]  # every tap outside the image: nothing read
+    return box.astype(np.int64)
+
+
+def needed_bytes(homs: np.ndarray, H: int, W: int, union: bool = False) -> int:
+    """HBM bytes of texels the render actually samples (sampled_boxes x 16 B) + the frames
+    written (12 B per pixel per view).  union: views sharing one MPI read it once, so each
+    plane counts the bounding box of its views' boxes (an upper bound of their union)."""
+    box = sampled_boxes(homs, H, W)
+    V = box.shape[0]
+    if union:
+        box = np.stack([box[..., 0].min(0), box[..., 1].max(0), box[..., 2].min(0), box[..., 3].max(0)], -1)[None]
+    area = np.clip(box[..., 1] - box[..., 0] + 1, 0, None) * np.clip(box[..., 3] - box[..., 2] + 1, 0, None)
+    return int(area.sum()) * 16 + V * H * W * 12
+
+
 # ---------------------------------------------------------------------------
 # CPU baseline
 # ---------------------------------------------------------------------------
@@ -485,11 +525,20 @@ def config2_leg(dev, stream, n=20):
     alg = V * (P * H * W * 16 + H * W * 12)
     gbs, frac = hbm(alg, ms)
     kname, grid = _lib.route("render_packed", H, W, P, V)
+    hn = homs.cpu().numpy()
+    need_views = needed_bytes(hn, H, W)
+    need_union = needed_bytes(hn, H, W, union=True)
     res = {"workload": "BASELINE config 2: 32-plane 1024x576 MPI, 64 target views in one launch",
            "kernel_ms": round(ms, 4), "Mpix_per_s": round(V * H * W / 1e6 / (ms * 1e-3), 1),
            "baseline_bar_Mpix_s": 9160, "alg_bytes": alg, "alg_def": "V*(P*H*W*16 + H*W*12) (SURVEY §8d)",
            "alg_gbs": gbs, "alg_frac": frac,
-           "alg_frac_note": "the 64 views share one MPI through L2, so the per-view formula can exceed 1 of HBM"}
+           "alg_frac_note": "the 64 views share one MPI through L2, so the per-view formula can exceed 1 of HBM",
+           # the reference's swapped normalisation (utils.py:186-188) maps output row y to MPI row
+           # ~y*H/(W-1): a 576x1024 view samples only ~56 % of the MPI's rows
+           "needed_bytes_per_view_sum": need_views, "needed_frac_per_view_sum": hbm(need_views, ms)[1],
+           "needed_bytes_union": need_union, "needed_union_frac": hbm(need_union, ms)[1],
+           "needed_def": "texel boxes each (view, plane) samples (homographies at the frame corners; the map is "
+                         "linear-fractional) x 16 B + frames; union: one read of the views' bounding box per plane"}
     res.update(prof_fields(kname, grid, alg, ms, "c2"))
     del packed, out
     return res
@@ -738,7 +787,82 @@ def netout_leg(dev, stream, n=20):
            "reference image read, frame written", "achieved_gbs": hbm(alg, ms)[0], "frac": hbm(alg, ms)[1],
            "bound": "hbm", "equals_assemble_then_render": same}
     res.update(prof_fields(kname, grid, alg, ms, "netout"))
-    del pred, fg, out, two
+    del out, two
+    res["training"] = netout_training(dev, stream, pred, fg, c)
+    del pred, fg
+    return res
+
+
+def netout_training(dev, stream, pred0, fg0, c, n=20):
+    """The notebook losses' training step (ipynb cell 12 L7-11 / L38-42: mpi_from_net_output ->
+    mpi_render_view_torch -> backward) at config 2's size, through the drop-ins under autograd:
+    fused (mpi_render_net_output_torch: render_netout_kernel + checkpoints; the backward re-assembles
+    the MPI) against the two-step chain (assemble, training render, backward, assembly backward).
+    Same gradients bit for bit (checked); HBM bytes per step and the memory the autograd graph holds
+    between forward and backward (saved tensors + frame) beside the times."""
+    import mpi_vision_amd as mv
+    H, W, P = c["H"], c["W"], c["P"]
+    pose = configs.f32(c["poses"][5:6]).to(dev)
+    K = configs.f32([c["K"]]).to(dev)
+    planes = configs.f32(c["depths"]).to(dev)
+    dout = torch.rand((1, H, W, 3), generator=torch.Generator(device=dev).manual_seed(3), device=dev) * 2 - 1
+    pred = pred0.clone().requires_grad_(True)
+    fg = fg0.clone().requires_grad_(True)
+    dep = {"mpi_planes": torch.zeros((1, P), device=dev), "ref_img": fg}
+
+    def fused_fwd():
+        return mv.mpi_render_net_output_torch(pred, fg, pose, planes, K)
+
+    def two_fwd():
+        return mv.mpi_render_view_torch(mv.mpi_from_net_output(pred, dep), pose, planes, K)
+
+    def step(fwd):
+        pred.grad = fg.grad = None
+        fwd().backward(dout)
+
+    res = {"workload": "config-2-size training step (1024x576, 32 planes, 1 view): forward + backward through the "
+                       "drop-ins, d network output and d reference image"}
+    grads = {}
+    for name, fwd in (("fused", fused_fwd), ("two_step", two_fwd)):
+        step(fwd)
+        torch.cuda.synchronize()
+        grads[name] = (pred.grad.clone(), fg.grad.clone())
+        pred.grad = fg.grad = None
+        torch.cuda.synchronize()
+        m0 = torch.cuda.memory_allocated(dev)
+        o = fwd()
+        torch.cuda.synchronize()
+        held = torch.cuda.memory_allocated(dev) - m0
+        del o
+        warm(lambda: step(fwd), stream)
+        mark("nt_" + name, dev)
+        ms = span_ms(lambda: step(fwd), n, stream)
+        mark("untimed", dev)
+        res[name] = {"step_ms": round(ms, 4), "graph_bytes_between_fwd_and_bwd": int(held),
+                     "rocprof_kernels": prof_tag_kernels("nt_" + name, n)}
+    res["grads_bit_identical"] = bool(torch.equal(grads["fused"][0].view(torch.int32), grads["two_step"][0].view(torch.int32))
+                                      and torch.equal(grads["fused"][1].view(torch.int32),
+                                                      grads["two_step"][1].view(torch.int32)))
+    mpi = P * H * W * 16
+    net = H * W * (2 * P + 3) * 4 + H * W * 12   # prediction + reference image
+    ck = (P + 7) // 8 * H * W * 16
+    frame = H * W * 12
+    # algorithmic HBM bytes per step, kernel by kernel (render backward counted as MPI read + d MPI
+    # written + d frame read, its workspace traffic excluded, as in the training leg)
+    bwd = 2 * mpi + frame
+    asm_bwd = mpi + net + net
+    two = (net + mpi) + (mpi + ck + frame) + bwd + asm_bwd
+    fused = (net + ck + frame) + (net + mpi) + bwd + asm_bwd
+    res.update({"alg_bytes_two_step": two, "alg_bytes_fused": fused,
+                "alg_bytes_def": "assemble (pred+ref read, MPI written) + training render (MPI read, checkpoints + "
+                                 "frame written) + render backward (MPI read, d MPI written, d frame read) + assembly "
+                                 "backward (d MPI, pred + ref read, d pred + d ref written); fused: render_netout with "
+                                 "checkpoints instead of assemble + training render, the assembly moved into the "
+                                 "backward"})
+    if res["fused"]["step_ms"] and res["two_step"]["step_ms"]:
+        res["fused_over_two_step_time"] = round(res["fused"]["step_ms"] / res["two_step"]["step_ms"], 3)
+    del pred, fg, grads
+    torch.cuda.empty_cache()
     return res
 
 
@@ -891,6 +1015,8 @@ def config5_leg(world, rank, dev, steps, warmup):
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     kern_all = all_ranks(kern_ms, world, dev)
+    hn = homs[:, p0:p1].numpy()
+    shard_need = needed_bytes(hn, H, W) if world == 1 else needed_bytes(hn, H, W) + H * W * 4
     res = {"workload": "BASELINE config 5: 256-plane 4096x2160 MPI (36.2 GB), 1 pose, plane-sharded",
            "value": round(steps * H * W / 1e6 / elapsed, 2), "unit": "Mpix/s", "n_gpus": world,
            "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "scaling": "strong",
@@ -899,6 +1025,11 @@ def config5_leg(world, rank, dev, steps, warmup):
            "per_rank_shard_kernel_ms": [round(x, 3) for x in kern_all],
            "shard_alg_bytes": shard_bytes,
            "shard_hbm_frac": hbm(shard_bytes, max(kern_all))[1],
+           # the bytes the reference's mapping actually samples (utils.py:186-188: output row y reads
+           # MPI row ~y*H/(W-1), so a 4096x2160 frame touches only MPI rows ~0..1200 of each plane)
+           "shard_needed_bytes": shard_need, "shard_needed_frac": hbm(shard_need, max(kern_all))[1],
+           "needed_def": "texel boxes each plane samples (homographies at the frame corners; the map is "
+                         "linear-fractional) x 16 B + the frame / partial written",
            "parallelism": "single GPU, sequential render" if world == 1 else
            f"plane-sharded x{world}: (C,T) partials + band all-to-all + ordered combine + gather",
            "frame_sha16": sha16(frame) if rank == 0 else None}
@@ -912,6 +1043,8 @@ def config5_leg(world, rank, dev, steps, warmup):
                     "bytes_sent_per_rank": int(sent), "exchange_exposed_ms": round(step_ms - max(kern_all), 3),
                     "exchange_gbs_over_step": round(sent / (step_ms * 1e-3) / 1e9, 2)})
     res.update(prof_fields(kname, grid, shard_bytes, max(kern_all), "c5_kernel"))
+    if res.get("traffic"):
+        res["traffic_over_needed"] = round(res["traffic"] / shard_need, 3)
     del packed
     torch.cuda.empty_cache()
     return res
@@ -1093,6 +1226,11 @@ def main():
                        "H": H, "W": W, "planes": P, "views_per_gpu_per_step": V, "kernel": args.kernel,
                        "parallelism": f"view-sharded x{world} (replicas, no data-path collective)",
                        "views_per_s": round(value / (H * W / 1e6), 2), "pack_ms_once": round(pack_ms, 2),
+                       # the one-time pack folded in, amortised over the 1000-pose path: every rank packs
+                       # its replica once (in parallel), then renders its n_path / world poses
+                       "value_incl_pack": round(n_path * H * W / 1e6 / ((pack_ms + n_path / (world * V) * elapsed
+                                                                          / args.steps * 1e3) * 1e-3), 2),
+                       "value_incl_pack_def": "1000 poses x H*W / (pack_ms_once + 1000/(n_gpus*V) x ms_per_step)",
                        "build_id": _lib.load().mpiv_build_id().decode()},
             "ranks": ranks,
             "roofline": {

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 12
+#define MPIV_ABI_VERSION 13
 
 enum {
     MPIV_OK = 0,
@@ -228,6 +228,16 @@ int mpiv_assemble_mpi_packed(const float *pred, const int64_t pred_strides[4], c
 int mpiv_render_net_output(const float *pred, const int64_t pred_strides[4], const float *fg,
                            const int64_t fg_strides[4], int B, int H, int W, int P, const float *homs, float *out,
                            void *stream);
+
+/* The same kernel as the TRAINING forward of the fused path (mpi_render_net_output_torch under
+ * autograd; the reference trains through mpi_from_net_output -> mpi_render_view_torch,
+ * ipynb cell 12 L7-11 / L38-42): frames as mpiv_render_net_output, plus the composite
+ * checkpoints ckpt [B][ceil(P/8)][H][W][4] that mpiv_render_train writes for the same MPI
+ * (colour before every 8-plane chunk c >= 1; slot 0 unused) -- bit-identical to them, so
+ * mpiv_render_backward can take them for the assembled MPI.  ckpt 16-B aligned. */
+int mpiv_render_net_output_train(const float *pred, const int64_t pred_strides[4], const float *fg,
+                                 const int64_t fg_strides[4], int B, int H, int W, int P, const float *homs,
+                                 float *out, float *ckpt, void *stream);
 
 /* Backward of mpiv_assemble_mpi (the notebook trains through it, cell 12 L5-15):
  * drgba [B,H,W,P,4] (drgba_strides[5]) -> dpred [B,2P+3,H,W] contiguous and, when dfg is

@@ -75,6 +75,7 @@ _SIGS = {
     "mpiv_psv_proj_device": [_vp, _i64, _vp, _int, _vp, _vp],
     "mpiv_pack_planes_u8": [_vp, _c_i64p, _int, _int, _int, _vp, _vp],
     "mpiv_render_net_output": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp],
+    "mpiv_render_net_output_train": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp],
     "mpiv_render_packed_u8": [_vp, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_render_packed_u8_ct": [_vp, _int, _int, _int, _int, _int, _int, _vp, _int, _vp, _vp],
     "mpiv_synth_mpi_packed_u8": [ctypes.c_uint32, _int, _int, _int, _int, _vp, _vp],
@@ -85,7 +86,7 @@ _SIGS = {
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
                           "mpiv_render_backward_workspace_size_min", "mpiv_build_id", "mpiv_debug_set")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _lib = None
 _lib_ab = None
@@ -818,6 +819,60 @@ def render_net_output(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int, homs: to
     _call("mpiv_render_net_output", mpi_pred, _strides(mpi_pred), fg, _strides(fg), B, H, W, P, h, out,
           _stream(dev))
     return out
+
+
+def netout_ckpt_ok(H: int, W: int, P: int) -> bool:
+    """True when the fused training forward keeps composite checkpoints: exactly when
+    render_train() would for the assembled (contiguous) MPI -- the backward reads it in place."""
+    return H >= 2 and W >= 2 and 4 * 64 * 9 * 16 + P * 36 <= _CHUNK_LDS
+
+
+def render_net_output_train(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int, homs: torch.Tensor):
+    """The fused net-output render's training forward: (frames [B,H,W,3], checkpoints
+    [B,ceil(P/8),H,W,4]) -- the frames of render_net_output() and the checkpoints render_train()
+    writes for the assembled MPI, bit for bit (mpiv_render_net_output_train); (frames, None) where
+    render_train() keeps none."""
+    dev, B, H, W = _net_args(mpi_pred, fg, P)
+    if not netout_ckpt_ok(H, W, P):
+        return render_net_output(mpi_pred, fg, P, homs), None
+    h = _up(homs.reshape(B, P, 9), dev)
+    out = torch.empty((B, H, W, 3), device=dev, dtype=torch.float32)
+    ckpt = torch.empty((B, (P + 7) // 8, H, W, 4), device=dev, dtype=torch.float32)
+    _call("mpiv_render_net_output_train", mpi_pred, _strides(mpi_pred), fg, _strides(fg), B, H, W, P, h, out, ckpt,
+          _stream(dev))
+    return out, ckpt
+
+
+class NetOutputRenderFunction(torch.autograd.Function):
+    """Autograd node of the fused assembly + render (the training losses' two lines, ipynb cell 12
+    L7-11 / L38-42: mpi_from_net_output then mpi_render_view_torch) that never keeps the
+    [B,H,W,P,4] MPI between forward and backward.  Forward: render_netout_kernel with the
+    composite checkpoints (saves pred, ref image, checkpoints: (2P+3+3)*4 + ceil(P/8)*16 B per pixel
+    instead of the MPI's P*16 + the checkpoints).  Backward: the MPI re-assembled (assemble.hip),
+    render_backward with those checkpoints, the assembly adjoint -- the two-step chain's own
+    kernels in its order, so d pred / d ref_img are bit-identical to it and to the reference's
+    autograd (tests/golden/netout_train.npz)."""
+
+    @staticmethod
+    def forward(ctx, mpi_pred, fg, homs, P):
+        ctx.P = P
+        ctx.homs = homs
+        out, ckpt = render_net_output_train(mpi_pred, fg, P, homs)
+        ctx.save_for_backward(mpi_pred, fg, ckpt)
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dout):
+        mpi_pred, fg, ckpt = ctx.saved_tensors
+        if not (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]):
+            return None, None, None, None
+        rgba = assemble_mpi(mpi_pred, fg, ctx.P)
+        drgba = render_backward(rgba, ctx.homs, dout, ckpt=ckpt)
+        del rgba  # the re-assembled MPI lives only for the chain
+        res = assemble_mpi_backward(drgba, mpi_pred, fg, ctx.P, want_dfg=ctx.needs_input_grad[1])
+        dpred, dfg = res if ctx.needs_input_grad[1] else (res, None)
+        return (dpred if ctx.needs_input_grad[0] else None), dfg, None, None
 
 
 def assemble_mpi_backward(drgba: torch.Tensor, mpi_pred: torch.Tensor, fg: torch.Tensor, P: int,

@@ -122,4 +122,4 @@ def config5():
 PROF_TAGS = {"untimed": 1, "c4": 2, "sv": 3, "c2": 4, "c3_dropin": 5, "c3": 6, "c3_ten": 7, "nb": 8,
              "netout": 9, "u8_sv": 10, "u8_mv": 11, "u8_kernel": 12, "train_fwd": 13, "train_inf": 14,
              "train_inf_dropin": 15, "train_bwd": 16, "train_bwd_nockpt": 17, "train_bwd_minws": 18, "c5": 19,
-             "c5_kernel": 20}
+             "c5_kernel": 20, "nt_fused": 21, "nt_two_step": 22}

@@ -1623,12 +1623,15 @@ static int netout_geo() {
     }
 }
 
-// The assembly fused into the render (assemble.hip render_netout_kernel): pred/fg -> frames.
-int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* fg, const int64_t fs[4], int B, int H,
-                           int W, int P, const float* homs, float* out, void* stream) {
-    const char* nm = "mpiv_render_net_output";
+// The assembly fused into the render (assemble.hip render_netout_kernel): pred/fg -> frames
+// (and, ckpt != nullptr, the training forward's composite checkpoints).
+static int render_net_output_impl(const char* nm, const float* pred, const int64_t ps[4], const float* fg,
+                                  const int64_t fs[4], int B, int H, int W, int P, const float* homs, float* out,
+                                  float* ckpt_f, void* stream) {
+    float4* ckpt = reinterpret_cast<float4*>(ckpt_f);
     if (int rc = check_net(nm, pred, ps, fg, fs, B, H, W, P)) return rc;
     if (!homs || !out) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
+    if (ckpt && !aligned16(ckpt)) return fail(MPIV_ERR_ARG, "%s: ckpt not 16-byte aligned", nm);
     if (H < 2 || W < 2 || H >= (1 << 15) - 4 || W >= (1 << 15) - 4 || P > kNMaxP)
         return fail(MPIV_ERR_ARG, "%s: needs 2 <= H, W < 32764 and P <= %d", nm, kNMaxP);
     const NetStrides s{ps[0], ps[1], ps[2], ps[3], fs[0], fs[1], fs[2], fs[3]};
@@ -1655,19 +1658,33 @@ int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* 
     switch (geo * 2 + (buf ? 1 : 0)) {
 #define MPIV_NETOUT(A, B_, C, D)                                                                           \
     case (A * 100 + B_ * 10 + C) * 2 + D:                                                                  \
-        render_netout_kernel<A, B_, C, D><<<nbu, 64 * A, 0, q>>>(pred, fg, sb, g, B, homs, out);           \
+        render_netout_kernel<A, B_, C, D><<<nbu, 64 * A, 0, q>>>(pred, fg, sb, g, B, homs, out, ckpt);     \
         break;
         MPIV_NETOUT(8, 1, 1, 0) MPIV_NETOUT(8, 2, 1, 0) MPIV_NETOUT(8, 2, 2, 0) MPIV_NETOUT(4, 2, 2, 0)
         MPIV_NETOUT(8, 1, 1, 1) MPIV_NETOUT(8, 2, 1, 1) MPIV_NETOUT(8, 2, 2, 1) MPIV_NETOUT(4, 2, 2, 1)
 #undef MPIV_NETOUT
         case 1821 * 2:
-            render_netout_kernel<8, 2, 1, false, true><<<nbu, 512, P * sizeof(int2), q>>>(pred, fg, sb, g, B, homs, out);
+            render_netout_kernel<8, 2, 1, false, true><<<nbu, 512, P * sizeof(int2), q>>>(pred, fg, sb, g, B, homs, out,
+                                                                                           ckpt);
             break;
         case 1821 * 2 + 1:
-            render_netout_kernel<8, 2, 1, true, true><<<nbu, 512, P * sizeof(int2), q>>>(pred, fg, sb, g, B, homs, out);
+            render_netout_kernel<8, 2, 1, true, true><<<nbu, 512, P * sizeof(int2), q>>>(pred, fg, sb, g, B, homs, out,
+                                                                                          ckpt);
             break;
     }
     return launched(nm);
+}
+
+int mpiv_render_net_output(const float* pred, const int64_t ps[4], const float* fg, const int64_t fs[4], int B, int H,
+                           int W, int P, const float* homs, float* out, void* stream) {
+    return render_net_output_impl("mpiv_render_net_output", pred, ps, fg, fs, B, H, W, P, homs, out, nullptr, stream);
+}
+
+int mpiv_render_net_output_train(const float* pred, const int64_t ps[4], const float* fg, const int64_t fs[4], int B,
+                                 int H, int W, int P, const float* homs, float* out, float* ckpt, void* stream) {
+    if (!ckpt) return fail(MPIV_ERR_ARG, "mpiv_render_net_output_train: null ckpt");
+    return render_net_output_impl("mpiv_render_net_output_train", pred, ps, fg, fs, B, H, W, P, homs, out, ckpt,
+                                  stream);
 }
 
 // ---- host-side homographies (inv_homography_torch chain, utils.py:44-67) -------------

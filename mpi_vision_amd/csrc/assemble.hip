@@ -18,6 +18,11 @@
 // d rgba [B,H,W,P,4], in autograd's order where it is defined -- per plane
 // d w = (sum_c g_c*fg_c + -(sum_c g_c*bg_c)) / 2, d alpha = g_a / 2; the P background
 // contributions g_c * (1 - w_i) accumulate from the last plane to the first.
+// kZeroFlush: every d pred value ends with "+ 0.0f".  Autograd adds up the SliceBackward
+// gradients of mpi_pred's three slices (weights, alphas, bg) and the SelectBackward ones of each
+// plane, each zero-filled outside its slice, so every entry also receives +0 terms: a -0 (an
+// all-zero d rgba, i.e. a texel no output pixel samples) becomes +0; every other value is
+// unchanged (tests/golden/netout_train.npz).  d fg has no such slices and keeps its sign.
 #include "mpiv_common.hpp"
 
 namespace mpiv {
@@ -119,8 +124,8 @@ __global__ __launch_bounds__(256) void assemble_backward_kernel(const float* __r
         const float sf = (gr * f0 + gg * f1) + gb * f2;
         const float sb = (gr * b0 + gg * b1) + gb * b2;
         const float dw = sf + -sb;  // RsubBackward negates; two terms commute exactly
-        dp[(int64_t)p * npix] = dw / 2.0f;            // DivBackward
-        dp[(int64_t)(P + p) * npix] = ga / 2.0f;
+        dp[(int64_t)p * npix] = dw / 2.0f + 0.0f;     // DivBackward; + 0: see kZeroFlush
+        dp[(int64_t)(P + p) * npix] = ga / 2.0f + 0.0f;
         const float c0 = gr * om, c1 = gg * om, c2 = gb * om;
         const float e0 = gr * w, e1 = gg * w, e2 = gb * w;  // MulBackward of w * fg w.r.t. fg
         if (p == P - 1) {
@@ -131,9 +136,9 @@ __global__ __launch_bounds__(256) void assemble_backward_kernel(const float* __r
             df0 = df0 + e0; df1 = df1 + e1; df2 = df2 + e2;
         }
     }
-    dp[(int64_t)(2 * P) * npix] = db0;
-    dp[(int64_t)(2 * P + 1) * npix] = db1;
-    dp[(int64_t)(2 * P + 2) * npix] = db2;
+    dp[(int64_t)(2 * P) * npix] = db0 + 0.0f;
+    dp[(int64_t)(2 * P + 1) * npix] = db1 + 0.0f;
+    dp[(int64_t)(2 * P + 2) * npix] = db2 + 0.0f;
     if (dfg) {
         float* o = dfg + ((int64_t)b * npix + pix) * 3;
         o[0] = df0; o[1] = df1; o[2] = df2;
@@ -186,8 +191,8 @@ __global__ __launch_bounds__(kAbPix) void assemble_backward_dense_kernel(const f
             const float om = 1.0f - w;
             const float sf = (g.x * f0 + g.y * f1) + g.z * f2;
             const float sb = (g.x * b0 + g.y * b1) + g.z * b2;
-            dp[(int64_t)p * npix] = (sf + -sb) / 2.0f;
-            dp[(int64_t)(P + p) * npix] = g.w / 2.0f;
+            dp[(int64_t)p * npix] = (sf + -sb) / 2.0f + 0.0f;
+            dp[(int64_t)(P + p) * npix] = g.w / 2.0f + 0.0f;
             const float c0 = g.x * om, c1 = g.y * om, c2 = g.z * om;
             const float e0 = g.x * w, e1 = g.y * w, e2 = g.z * w;
             if (p == P - 1) {
@@ -200,9 +205,9 @@ __global__ __launch_bounds__(kAbPix) void assemble_backward_dense_kernel(const f
         }
     }
     if (!live) return;
-    dp[(int64_t)(2 * P) * npix] = db0;
-    dp[(int64_t)(2 * P + 1) * npix] = db1;
-    dp[(int64_t)(2 * P + 2) * npix] = db2;
+    dp[(int64_t)(2 * P) * npix] = db0 + 0.0f;
+    dp[(int64_t)(2 * P + 1) * npix] = db1 + 0.0f;
+    dp[(int64_t)(2 * P + 2) * npix] = db2 + 0.0f;
     if (dfg) {
         float* o = dfg + ((int64_t)b * npix + pix) * 3;
         o[0] = df0; o[1] = df1; o[2] = df2;
@@ -369,7 +374,8 @@ template <int NW, int RPT, int DEPTH, bool BUF, bool DB = false>
 __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __restrict__ pred,
                                                                 const float* __restrict__ fg, NetStrides ns,
                                                                 RenderGeom g, int V, const float* __restrict__ homs,
-                                                                float* __restrict__ out) {
+                                                                float* __restrict__ out,
+                                                                float4* __restrict__ ckpt = nullptr) {
     constexpr int kThreads = 64 * NW;
     constexpr int kTY = NW * RPT;
     constexpr int kCap = (DB ? 100 : 128) * kTY;  // texels per staged box: a 64 x 8 tile 1024 (its box at the
@@ -524,6 +530,11 @@ __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __r
                 cr[r] = over(sm[0], a, om, cr[r]);
                 cg[r] = over(sm[1], a, om, cg[r]);
                 cb[r] = over(sm[2], a, om, cb[r]);
+                // training forward: the colour before every 8-plane chunk c >= 1, render_train's
+                // [V][ceil(P/8)][H][W] checkpoints (the backward's chain rebuilds each chunk from it)
+                if (ckpt && (p & 7) == 7 && p + 1 < P)
+                    ckpt[(((int64_t)v * ((P + 7) >> 3) + ((p + 1) >> 3)) * g.H + y) * g.W + x] =
+                        make_float4(cr[r], cg[r], cb[r], 0.0f);
             }
         }
     };

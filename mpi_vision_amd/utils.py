@@ -201,11 +201,15 @@ def mpi_from_net_output(mpi_pred, dep):
 
 
 def mpi_render_net_output_torch(mpi_pred, ref_img, tgt_pose, planes, intrinsics):
-    """mpi_render_view_torch(mpi_from_net_output(mpi_pred, ...), tgt_pose, planes, intrinsics)
-    in ONE kernel (inference / viewer path, no autograd): each plane's tile footprint is
-    assembled from the network output straight into LDS and sampled there
-    (assemble.hip render_netout_kernel); no [B, H, W, P, 4] tensor and no packed MPI is
-    written.  Bit-identical to the two-step form."""
+    """mpi_render_view_torch(mpi_from_net_output(mpi_pred, {'ref_img': ref_img, ...}), tgt_pose,
+    planes, intrinsics) -- the two lines of both of the notebook's losses (ipynb cell 12 L7-11,
+    L38-42) -- in ONE kernel: each plane's tile footprint is assembled from the network output
+    straight into LDS and sampled there (assemble.hip render_netout_kernel); no [B, H, W, P, 4]
+    tensor and no packed MPI is written.  Bit-identical to the two-step form.  Differentiable
+    w.r.t. mpi_pred and ref_img when either requires grad (_lib.NetOutputRenderFunction: the
+    training forward also writes the composite checkpoints; the backward re-assembles the MPI
+    for the adjoint, so the MPI is never held between forward and backward), bit-exact to the
+    reference's autograd of the two-step form."""
     batch_size = tgt_pose.shape[0]
     n_planes = len(planes)
     depths = planes.reshape([n_planes, 1])
@@ -214,6 +218,8 @@ def mpi_render_net_output_torch(mpi_pred, ref_img, tgt_pose, planes, intrinsics)
     else:
         homs = _host.render_homographies(tgt_pose, depths.reshape(-1), intrinsics, batch_size)
     fg = ref_img.to(mpi_pred.device)
+    if torch.is_grad_enabled() and (mpi_pred.requires_grad or fg.requires_grad):
+        return _lib.NetOutputRenderFunction.apply(mpi_pred, fg, homs, n_planes)
     return _lib.render_net_output(mpi_pred, fg, n_planes, homs)
 
 

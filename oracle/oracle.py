@@ -224,6 +224,11 @@ def assemble_mpi_backward(drgba: np.ndarray, pred: np.ndarray, fg: np.ndarray, P
     for i in range(P - 2, -1, -1):
         dbg = dbg + contrib[..., i, :]
     d = np.concatenate([dw, da, dbg], axis=-1)                            # [B,H,W,2P+3]
+    # autograd sums the SliceBackward gradients of the three slices of mpi_pred (weights, alphas,
+    # bg) and the SelectBackward ones of each weight / alpha plane, each zero-filled outside its
+    # slice: every entry also receives +0 terms, which turn a -0 into +0 (x + 0 == x otherwise).
+    # Visible where d rgba is exactly 0 (texels no output pixel samples: tests/golden/netout_train.npz)
+    d = d + np.float32(0)
     return np.ascontiguousarray(np.transpose(d, (0, 3, 1, 2))).astype(np.float32)
 
 

@@ -17,7 +17,7 @@ from conftest import GOLD, assert_bits
 pytestmark = pytest.mark.gpu
 
 import mpi_vision_amd as mv  # noqa: E402
-from mpi_vision_amd import _lib, configs  # noqa: E402
+from mpi_vision_amd import _host, _lib, configs  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 CASES = ("na", "nb", "nc")
@@ -163,3 +163,79 @@ def test_fused_net_output_render_cases(case, geo, dev, kopts):
     got = mv.mpi_render_net_output_torch(pred, ref, poses, planes, K)
     torch.cuda.synchronize()
     assert_bits(got.cpu().numpy(), want.cpu().numpy(), f"fused assemble + render ({case}, geo {geo})")
+
+
+NETOUT_TRAIN = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "netout_train.npz"))
+
+
+@pytest.mark.parametrize("case", ["ta", "tb", "tc", "td"])
+@pytest.mark.parametrize("wants", ["both", "pred", "ref"])
+def test_fused_net_output_training_vs_reference(case, wants, dev):
+    """Training through the fused net-output render (the notebook's losses, ipynb cell 12 L7-11 /
+    L38-42: mpi_from_net_output then mpi_render_view_torch): frames, d network output and d
+    reference image bit-exact vs the reference's CPU autograd (tests/golden/netout_train.npz:
+    8, 12, 17 and 32 planes -- one, two and several checkpoint chunks)."""
+    g = NETOUT_TRAIN
+    pred = torch.tensor(g[case + "_pred"]).to(dev).requires_grad_(wants in ("both", "pred"))
+    ref = torch.tensor(g[case + "_ref"]).to(dev).requires_grad_(wants in ("both", "ref"))
+    pose, K, depths = (torch.tensor(g[f"{case}_{k}"]).to(dev) for k in ("pose", "K", "depths"))
+    out = mv.mpi_render_net_output_torch(pred, ref, pose, depths, K)
+    assert out.grad_fn is not None and "NetOutputRender" in type(out.grad_fn).__name__
+    out.backward(torch.tensor(g[case + "_dout"]).to(dev))
+    torch.cuda.synchronize()
+    assert_bits(out.detach().cpu().numpy(), g[case + "_out"], f"frames {case}")
+    if wants != "ref":
+        assert_bits(pred.grad.cpu().numpy(), g[case + "_dpred"], f"d pred {case}")
+    if wants != "pred":
+        assert_bits(ref.grad.cpu().numpy(), g[case + "_dref"], f"d ref_img {case}")
+
+
+@pytest.mark.parametrize("buf", [1, 0])
+@pytest.mark.parametrize("shape", [(2, 24, 40, 12), (1, 33, 47, 17), (1, 40, 64, 8), (1, 576, 1024, 32),
+                                   (2, 45, 70, 9)])
+def test_netout_train_checkpoints_equal_render_train(shape, buf, dev, kopts):
+    """The fused training forward's composite checkpoints equal mpiv_render_train's for the
+    assembled MPI (slots 1.. -- slot 0 is never written or read), and its frames the inference
+    kernel's, bit for bit; incl. a view with planes behind the camera (taps assembled directly)."""
+    B, H, W, P = shape
+    gen = torch.Generator().manual_seed(H * W + P)
+    pred = (torch.rand((B, 2 * P + 3, H, W), generator=gen) * 2 - 1).to(dev)
+    ref = (torch.rand((B, H, W, 3), generator=gen) * 2 - 1).to(dev)
+    f = configs.focal_from_fov(W)
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * B)
+    big = W == 70
+    poses = configs.f32([configs.pose_from(configs.rot_y((i + 1) * (20.0 if big else 1.2)),
+                                           ((i + 1) * (0.5 if big else 0.03), -0.02, 0.04 - (0.6 if big else 0)))
+                         for i in range(B)])
+    homs = _host.render_homographies(poses, configs.f32(mv.inv_depths(0.5 if big else 1, 100, P)), K, B).to(dev)
+    kopts(netout_buf=buf)
+    out, ck = _lib.render_net_output_train(pred, ref, P, homs)
+    inf = _lib.render_net_output(pred, ref, P, homs)
+    f2, ck2 = _lib.render_train(_lib.assemble_mpi(pred, ref, P), homs)
+    torch.cuda.synchronize()
+    assert ck is not None and ck2 is not None and ck.shape == ck2.shape
+    assert_bits(out.cpu().numpy(), inf.cpu().numpy(), "train forward frames vs inference kernel")
+    assert_bits(out.cpu().numpy(), f2.cpu().numpy(), "train forward frames vs two-step")
+    assert_bits(ck[:, 1:].cpu().numpy(), ck2[:, 1:].cpu().numpy(), "checkpoints vs render_train")
+
+
+def test_fused_net_output_training_equals_two_step_at_config2_size(dev):
+    """At config 2's size (1024x576, 32 planes) the fused training step gives the two-step
+    chain's gradients (mpi_from_net_output -> mpi_render_view_torch under autograd) bit for bit."""
+    c = configs.config2()
+    H, W, P = c["H"], c["W"], c["P"]
+    gen = torch.Generator().manual_seed(12)
+    pred0 = (torch.rand((1, 2 * P + 3, H, W), generator=gen) * 2 - 1).to(dev)
+    ref0 = (torch.rand((1, H, W, 3), generator=gen) * 2 - 1).to(dev)
+    dout = (torch.rand((1, H, W, 3), generator=gen) * 2 - 1).to(dev)
+    pose = configs.f32(c["poses"][7:8]).to(dev)
+    K = configs.f32([c["K"]]).to(dev)
+    planes = configs.f32(c["depths"]).to(dev)
+    p1, r1 = pred0.clone().requires_grad_(True), ref0.clone().requires_grad_(True)
+    mv.mpi_render_net_output_torch(p1, r1, pose, planes, K).backward(dout)
+    p2, r2 = pred0.clone().requires_grad_(True), ref0.clone().requires_grad_(True)
+    dep = {"mpi_planes": torch.zeros((1, P), device=dev), "ref_img": r2}
+    mv.mpi_render_view_torch(mv.mpi_from_net_output(p2, dep), pose, planes, K).backward(dout)
+    torch.cuda.synchronize()
+    assert_bits(p1.grad.cpu().numpy(), p2.grad.cpu().numpy(), "d pred fused vs two-step")
+    assert_bits(r1.grad.cpu().numpy(), r2.grad.cpu().numpy(), "d ref_img fused vs two-step")
