@@ -130,14 +130,15 @@ enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOpt
                 kOptRenderChunk, kOptRenderRing, kOptRenderTile, kOptBwdFallback, kOptBwdMargin, kOptSweepDlane,
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
                 kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kOptU8Flight, kOptBwdGroup,
-                kOptNetoutGeo, kOptNetoutBuf, kOptBwdOverlap, kOptSweepBand, kOptSweepPf, kOptSweepSoa, kNumOpts };
+                kOptNetoutGeo, kOptNetoutBuf, kOptBwdOverlap, kOptSweepBand, kOptSweepPf, kOptSweepSoa, kOptBwdUnfold,
+                kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
                                          "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode",
                                          "chunk_strip", "u8_flight", "bwd_group", "netout_geo", "netout_buf", "bwd_overlap", "sweep_band",
-                                         "sweep_pf", "sweep_soa"};
+                                         "sweep_pf", "sweep_soa", "bwd_unfold"};
 #ifndef MPIV_CHUNK_STRIP
 #define MPIV_CHUNK_STRIP 1  // round 4: 0.506 vs 0.64 ms in place (profiles/r04j_strip*_ab.jsonl)
 #endif
@@ -145,9 +146,9 @@ const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_nat
 #define MPIV_U8_FLIGHT 0
 #endif
 const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP,
-                                    MPIV_U8_FLIGHT, 0, 0, 1, 0, 0, 0, 0};
+                                    MPIV_U8_FLIGHT, 0, 0, 1, 0, 0, 0, 0, 0};
 int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP, MPIV_U8_FLIGHT, 0,
-                        0, 1, 0, 0, 0, 0};
+                        0, 1, 0, 0, 0, 0, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -708,10 +709,10 @@ size_t bwd_layout(int H, int W, int P, int dsp, char* base, BwdWs* ws, float4** 
     };
     char* truth = take(kCtrSlots * 8);
     char* found = take(kCtrSlots * 8);
-    char* flag = take(32);
+    char* flag = take(64);  // 16 words: [0..4] check / fallback, [8], [9] block-exit counters
     char* truth2 = take(nwin > 1 ? kCtrSlots * 8 : 0);  // the second window's counters (same carve-up)
     char* found2 = take(nwin > 1 ? kCtrSlots * 8 : 0);
-    char* flag2 = take(nwin > 1 ? 32 : 0);
+    char* flag2 = take(nwin > 1 ? 64 : 0);
     char* ds = take((size_t)nwin * dsp * hw * 16);
     char* ckpt = take(nchunk * hw * 16);
     char* inv = take((size_t)P * 12 * 4);
@@ -886,8 +887,15 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const long long khz_seen = __atomic_load_n(&s_clock_khz[dev], __ATOMIC_RELAXED);
     const unsigned long long tick_limit = 60000ull * (unsigned long long)(khz_seen > 0 ? khz_seen : 100000);
     const int fb_mode = opt(kOptBwdFbMode);
+    // Launch-folded schedule (round 6; one plane group, tile gather): per view the box kernel (the planes'
+    // inverses inside, and block 0 zeroing the counters this memset would) runs first, the pair-count
+    // check runs in the gather's last block and the NaN fill of an aborted view in the fallback's last
+    // block: 4 launches per view instead of 7 plus the memset (the notebook's 224x224 training step is
+    // launch-bound).  The other schedules keep the separate launches.
+    const bool folded = !force && G == 1 && !overlap && opt(kOptBwdUnfold) == 0 && opt(kOptBwdGather) == 0 && fb_mode != 1;
     // truth, found, flag (adjacent), and the second window's set after them
-    if (hipMemsetAsync(ws.truth, 0, overlap ? 2 * (2 * kCtrSlots * 8 + 256) : 2 * kCtrSlots * 8 + 256, q) != hipSuccess)
+    if (!folded &&
+        hipMemsetAsync(ws.truth, 0, overlap ? 2 * (2 * kCtrSlots * 8 + 256) : 2 * kCtrSlots * 8 + 256, q) != hipSuccess)
         return fail(MPIV_ERR_HIP, "%s: hipMemsetAsync failed", nm);
     if (overlap) {
         std::lock_guard<std::mutex> lk(g_aux_mu);
@@ -915,12 +923,9 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                                                                           reinterpret_cast<float*>(gbuf), ws.ckpt, h_lds);
                     ckv = ws.ckpt;
                 }
-                if (!force) {
-                    bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1),
-                                                                   ws.inv);
-                    bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x,
-                                                                                   margin, ws.box);
-                }
+                if (!force)  // the planes' inverses computed inside (one launch fewer)
+                    bwd_box_kernel<true><<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(
+                        g, hv, ws.inv, (int)ntiles, tiles_x, margin, ws.box, (double)W / (H - 1), (double)H / (W - 1));
                 for (int grp = G - 1; grp >= 0 && ok; --grp) {
                     const int k = G - 1 - grp, par = k & 1;
                     const int p_lo = grp * GP, p_hi = std::min(P, p_lo + GP);
@@ -932,7 +937,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                     chk(hipEventRecord(ax->chain[par], q));
                     chk(hipStreamWaitEvent(a, ax->chain[par], 0));
                     if (!force)
-                        bwd_gather_kernel<<<(unsigned)(ntiles * blocks(p_hi - p_lo, kGPl)), kGThreads, 0, a>>>(
+                        bwd_gather_kernel<false><<<(unsigned)(ntiles * blocks(p_hi - p_lo, kGPl)), kGThreads, 0, a>>>(
                             g, hv, wg, gv, margin, p_lo, p_hi - p_lo);
                     bwd_check_kernel<<<1, kWave, 0, a>>>(wg, force, k >= 2);
                     bwd_fallback_kernel<true><<<fb_blocks, 256, 0, a>>>(g, hv, wg, gv, poll_limit, tick_limit,
@@ -965,11 +970,9 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                                                                       ws.ckpt, h_lds);
                 ckv = ws.ckpt;
             }
-            if (!force) {
-                bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
-                bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x,
-                                                                               margin, ws.box);
-            }
+            if (!force)  // the planes' inverses computed inside (one launch fewer)
+                bwd_box_kernel<true><<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(
+                    g, hv, ws.inv, (int)ntiles, tiles_x, margin, ws.box, (double)W / (H - 1), (double)H / (W - 1));
             for (int grp = G - 1; grp >= 0; --grp) {
                 const int p_lo = grp * GP, p_hi = std::min(P, p_lo + GP);
                 BwdWs wg = ws;
@@ -977,7 +980,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                 bwd_chain_strip_kernel<8><<<blocks(W, kStripTX) * blocks(H, 8), 256, chain_lds, q>>>(
                     mv, g, cg, hv, dv, ckv, wg, h_lds, p_lo / kBwdCH, (p_hi + kBwdCH - 1) / kBwdCH, gbuf);
                 if (!force)
-                    bwd_gather_kernel<<<(unsigned)(ntiles * blocks(p_hi - p_lo, kGPl)), kGThreads, 0, q>>>(
+                    bwd_gather_kernel<false><<<(unsigned)(ntiles * blocks(p_hi - p_lo, kGPl)), kGThreads, 0, q>>>(
                         g, hv, wg, gv, margin, p_lo, p_hi - p_lo);
                 bwd_check_kernel<<<1, kWave, 0, q>>>(wg, force, grp != G - 1);
                 if (fast)
@@ -992,6 +995,10 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         }
         const int R = fast ? chunk_rows() : 1;
         const unsigned cb = blocks(W, kTileX) * blocks(H, kTileY * R);
+        if (folded)  // the boxes (and the planes' inverses) first; block 0 zeroes the counters
+            bwd_box_kernel<true><<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(
+                g, hv, ws.inv, (int)ntiles, tiles_x, margin, ws.box, (double)W / (H - 1), (double)H / (W - 1), ws,
+                v == 0 ? 2 : 1);
         if (!ck && fast && R == 1 && opt(kOptChunkStrip) == 1) {
             // no checkpoints: a strip forward pass writes them into the workspace (its frame into
             // this view's d MPI, which the gather / fallback overwrite), then the one-pass chain --
@@ -1025,16 +1032,27 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         else if (ck) MPIV_CHAIN(true, 1);
         else MPIV_CHAIN(false, 1);
 #undef MPIV_CHAIN
+        if (folded) {
+            bwd_gather_kernel<true><<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin, 0, P);
+            if (fast)
+                bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, tick_limit, fb_mode == 2, 0,
+                                                                    P, (int64_t)P * HW);
+            else
+                bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, tick_limit, fb_mode == 2, 0,
+                                                                     P, (int64_t)P * HW);
+            continue;
+        }
         if (!force) {
-            bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
 #if MPIV_AB && MPIV_GTR == 1  // one texel row per wave / staging and texel waves: measured slower
             if (opt(kOptBwdGather) == 1) {
+                bwd_inverse_kernel<<<blocks(P, 64), 64, 0, q>>>(hv, P, (double)W / (H - 1), (double)H / (W - 1), ws.inv);
                 bwd_gather_wave_kernel<<<(unsigned)gather_blocks, 256, 0, q>>>(g, hv, ws, gv, margin);
             } else
 #endif
             {
-                bwd_box_kernel<<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(g, hv, ws.inv, (int)ntiles, tiles_x,
-                                                                               margin, ws.box);
+                // the planes' inverses computed inside (bwd_plane_inverse, the same floats): one launch fewer
+                bwd_box_kernel<true><<<blocks((int64_t)P * ntiles, 256), 256, 0, q>>>(
+                    g, hv, ws.inv, (int)ntiles, tiles_x, margin, ws.box, (double)W / (H - 1), (double)H / (W - 1));
 #if MPIV_AB && MPIV_GTR == 1
                 if (opt(kOptBwdGather) == 2)
                     bwd_gather_ws_kernel<<<(unsigned)gather_blocks, 2 * kGThreads, 0, q>>>(g, hv, ws, gv, margin);
@@ -1042,7 +1060,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                     bwd_gather_dma_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin);
                 else
 #endif
-                    bwd_gather_kernel<<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin, 0, P);
+                    bwd_gather_kernel<false><<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin, 0, P);
             }
         }
         bwd_check_kernel<<<1, kWave, 0, q>>>(ws, force, 0);

@@ -576,11 +576,7 @@ __global__ __launch_bounds__(256, 1) void bwd_chain_strip_kernel(const float* __
 // F^-1 (x', y', z') of a texel point is (x, y, 1) / w, so z' > 0 exactly where the point is
 // the image of pixels in front of the camera.  Computed in double, stored as floats: the
 // windows built from it are guesses checked by the pair count.
-__global__ __launch_bounds__(64) void bwd_inverse_kernel(const float* __restrict__ homs, int P, double sx,
-                                                         double sy, float* __restrict__ inv) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P) return;
-    const float* h = homs + (int64_t)p * 9;
+__device__ __forceinline__ void bwd_plane_inverse(const float* __restrict__ h, double sx, double sy, float* o) {
     double f[9];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -599,7 +595,6 @@ __global__ __launch_bounds__(64) void bwd_inverse_kernel(const float* __restrict
     a[7] = f[1] * f[6] - f[0] * f[7];
     a[8] = f[0] * f[4] - f[1] * f[3];
     const double det = f[0] * a[0] + f[1] * a[3] + f[2] * a[6];
-    float* o = inv + (int64_t)p * 12;
     bool ok = det != 0.0 && __builtin_isfinite(det);
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
@@ -608,6 +603,13 @@ __global__ __launch_bounds__(64) void bwd_inverse_kernel(const float* __restrict
         o[k] = v;
     }
     o[9] = ok ? 1.0f : 0.0f;
+}
+
+__global__ __launch_bounds__(64) void bwd_inverse_kernel(const float* __restrict__ homs, int P, double sx,
+                                                         double sy, float* __restrict__ inv) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    bwd_plane_inverse(homs + (int64_t)p * 9, sx, sy, inv + (int64_t)p * 12);
 }
 
 // texel point (X, Y) -> output pixel point; false unless in front of the camera
@@ -633,14 +635,37 @@ __device__ __forceinline__ void pix_range(float a, float b, float e, int cl, int
 // fallback.  x0 > x1 or y0 > y1: no pixel samples the tile.
 constexpr int kGTHc = kGTY;
 constexpr int kBoxProven = 1 << 30;
+// INV (round 6): the plane's inverse computed here (bwd_plane_inverse, the same double arithmetic,
+// so the same floats) instead of read from bwd_inverse_kernel's output -- one launch fewer per
+// view; the first tile's thread of each plane stores it for the gather.
+// zero (round 6, the single-group schedule, which launches this kernel before the chain): block 0
+// also zeroes the pair counters and the flag words -- the hipMemsetAsync of the workspace's head
+// (1: per view; 2: the call's first view, with the aborted-view count).
+template <bool INV = false>
 __global__ __launch_bounds__(256) void bwd_box_kernel(RenderGeom g, const float* __restrict__ homs,
-                                                      const float* __restrict__ inv, int ntiles, int tiles_x,
-                                                      float margin, int4* __restrict__ box) {
+                                                      float* __restrict__ inv, int ntiles, int tiles_x,
+                                                      float margin, int4* __restrict__ box, double sx = 0.0,
+                                                      double sy = 0.0, BwdWs zero_ws = BwdWs{}, int zero = 0) {
+    if (zero && blockIdx.x == 0 && threadIdx.x < kCtrSlots) {
+        zero_ws.truth[threadIdx.x] = 0;
+        zero_ws.found[threadIdx.x] = 0;
+        if (threadIdx.x < 16 && (threadIdx.x != 4 || zero == 2)) zero_ws.flag[threadIdx.x] = 0;
+    }
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)g.P * ntiles) return;
     const int p = (int)(i / ntiles), tile = (int)(i - (int64_t)p * ntiles);
     const int tx0 = (tile % tiles_x) * kGTW, ty0 = (tile / tiles_x) * kGTHc;
-    const float* iv = inv + (int64_t)p * 12;
+    float iv[10];
+    if (INV) {
+        bwd_plane_inverse(homs + (int64_t)p * 9, sx, sy, iv);
+        if (tile == 0) {
+#pragma unroll
+            for (int k = 0; k < 10; ++k) inv[(int64_t)p * 12 + k] = iv[k];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) iv[k] = inv[(int64_t)p * 12 + k];
+    }
     float m[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) m[k] = iv[k];
@@ -945,6 +970,32 @@ __device__ __forceinline__ void gather_texel_pass(const RenderGeom& g, const Bwd
 // pass: one staging pass (gather_stage_pass) by all 4 waves, a barrier, one texel pass
 // (gather_texel_pass).  A texel's kGPl planes leave as one 16*kGPl-B run.
 // Planes [p_lo, p_lo + np) (a plane group of mpiv_render_backward; p_lo a multiple of kGPl).
+__device__ __forceinline__ void bwd_check_wave(BwdWs& ws, int force, int keep_abort, int l);
+
+// Workspace flag words of the launch-folded schedule (round 6): the gather's and the fallback's
+// block-exit counters (zeroed with the pair counters, reset by the last block).
+constexpr int kFlagGatherDone = 8, kFlagFallbackExit = 9;
+
+// The last block of a grid to get here (after its own global writes and atomics) returns true
+// (block-uniform); every block's earlier device-scope atomics are visible to it.
+__device__ __forceinline__ bool last_block_in(int* ctr) {
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        s_last = atomicAdd(reinterpret_cast<unsigned*>(ctr), 1u) == gridDim.x - 1;
+        if (s_last) {
+            __threadfence();
+            *ctr = 0;  // ready for the next launch
+        }
+    }
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(s_last) != 0;
+}
+
+// CHECK (round 6, the single-group schedule): the pair-count check (bwd_check_kernel's) runs in
+// the last gather block to finish instead of a launch of its own.
+template <bool CHECK = false>
 __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderGeom g, const float* __restrict__ homs, BwdWs ws,
                                                          float4* __restrict__ dmpi, float margin, int p_lo, int np) {
     __shared__ int s_code[kGCap];                    // local nw-tap bucket of the staged pixel, -1 = none
@@ -1113,6 +1164,8 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
                 }
         }
     }
+    if (CHECK && last_block_in(ws.flag + kFlagGatherDone) && threadIdx.x < kWave)
+        bwd_check_wave(ws, 0, 0, threadIdx.x);
 }
 
 #if MPIV_AB && MPIV_GTR == 1  // A/B variants of the gather (libmpiv_ab.so, one texel row per wave): measured slower, DESIGN.md §8
@@ -1647,9 +1700,10 @@ __global__ __launch_bounds__(256, MPIV_GLBW) void bwd_gather_wave_kernel(RenderG
 
 // ---- 3. check: found == truth, else the fallback runs; counters reset for the next view
 // keep_abort: a later plane group of the same view (flag[3] stays set once any group aborted)
-__global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force, int keep_abort) {
-    const int l = threadIdx.x;
-    unsigned long long t = ws.truth[l], f = ws.found[l];
+// one wave (lane l = threadIdx.x & 63): the two pair counts summed, compared and reset
+__device__ __forceinline__ void bwd_check_wave(BwdWs& ws, int force, int keep_abort, int l) {
+    unsigned long long t = __hip_atomic_load(&ws.truth[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long f = __hip_atomic_load(&ws.found[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         t += __shfl_xor(t, off);
@@ -1663,6 +1717,10 @@ __global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force, i
         ws.flag[2] = 0;
         if (!keep_abort) ws.flag[3] = 0;
     }
+}
+
+__global__ __launch_bounds__(kWave) void bwd_check_kernel(BwdWs ws, int force, int keep_abort) {
+    bwd_check_wave(ws, force, keep_abort, threadIdx.x);
 }
 
 // ---- fallback: the general bucket pipeline (runs only when flag[0] is set) -----------
@@ -2239,10 +2297,13 @@ template <bool FAST>
 // fixed != 0 (A/B diagnosis): block b takes items b, b + nblk, ... in order instead of tickets
 // (the grid-barrier schedule: needs every block resident)
 // planes [p_lo, p_hi) (a plane group of mpiv_render_backward, or all of them)
+// poison_n > 0 (round 6, the single-group schedule): bwd_poison_kernel's NaN fill of an aborted
+// view (its poison_n d MPI texels) by the last block to leave, instead of a launch of its own after
+// every view.
 __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const float* __restrict__ homs,
                                                                   BwdWs ws, float4* __restrict__ dmpi,
                                                                   unsigned poll_limit, unsigned long long tick_limit,
-                                                                  int fixed, int p_lo, int p_hi) {
+                                                                  int fixed, int p_lo, int p_hi, int64_t poison_n = 0) {
     __shared__ int s_tmp[kScanBlock];
     __shared__ int s_ticket;
     if (ws.flag[0] == 0) return;  // uniform over the grid: the tile gather was complete
@@ -2262,7 +2323,14 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
         __syncthreads();
         const int t = __builtin_amdgcn_readfirstlane(s_ticket);
         __syncthreads();  // s_ticket is rewritten by the next iteration
-        if (t < 0) return;
+        if (t < 0) {
+            if (poison_n > 0 && last_block_in(ws.flag + kFlagFallbackExit) &&
+                __hip_atomic_load(ws.flag + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                const float q = __builtin_nanf("");
+                for (int64_t i = tid; i < poison_n; i += 256) dmpi[i] = make_float4(q, q, q, q);
+            }
+            return;
+        }
         bwd_fallback_item<FAST>(g, homs, ws, dmpi, t / nblk, t % nblk, nblk, s_tmp, p_lo, p_hi);
         fallback_done(done);
     }

@@ -371,6 +371,54 @@ def test_backward_fallback_abort_is_loud(dev, kopts):
     assert_bits(got, want, "after an abort")
 
 
+@pytest.mark.parametrize("ckpt", [True, False])
+@pytest.mark.parametrize("mode", ["tile", "miss"])
+def test_backward_launch_folded_schedule(ckpt, mode, dev, kopts):
+    """Round 6: the one-group backward folds the counter memset and the planes' inverses into the
+    box kernel (launched first), the pair-count check into the gather's last block and the
+    aborted-view NaN fill into the fallback's last block (4 launches per view instead of 8).  Its
+    gradient equals the unfolded schedule's (bwd_unfold=1) and the oracle bit for bit, over 3 views
+    (counters reset between views), with and without checkpoints, with the tile gather complete and
+    with induced misses (the folded check must send each view to the fallback); flag words agree."""
+    V = 3
+    mpi, homs, dout = _medium_case(V)
+    B, H, W, P, _ = mpi.shape
+    want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
+    m, h, d = mpi.to(dev), homs.to(dev), dout.to(dev)
+    ck = _lib.render_train(m, h)[1] if ckpt else None
+    if mode == "miss":
+        kopts(bwd_margin=-96)
+    L = _lib.load()
+    res = {}
+    for unfold in (0, 1):
+        kopts(bwd_unfold=unfold)
+        ws = torch.full((L.mpiv_render_backward_workspace_size(H, W, P),), 0x5A, dtype=torch.uint8, device=dev)
+        got = _lib.render_backward(m, h, d, workspace=ws, ckpt=ck, check=True)
+        off = _lib.bwd_flag_offset(H, W, P)
+        res[unfold] = (got, ws[off:off + 20].view(torch.int32).tolist())
+        assert_bits(got, want, f"unfold={unfold} {mode}")
+    assert res[0][1][0] == res[1][1][0] == (1 if mode == "miss" else 0), (res[0][1], res[1][1])
+    assert res[0][1][3:5] == res[1][1][3:5] == [0, 0]
+
+
+def test_backward_folded_abort_is_loud(dev, kopts):
+    """The folded schedule's fallback (reached through induced misses, not forced) still poisons an
+    aborted view from its last block: NaN gradient, counted, check=True raises (A/B: forced poll
+    limit)."""
+    V = 2
+    mpi, homs, dout = _medium_case(V)
+    B, H, W, P, _ = mpi.shape
+    kopts(bwd_margin=-96, bwd_poll_limit=-1)
+    L = _lib.load()
+    ws = torch.zeros(L.mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    got = _lib.render_backward(mpi.to(dev), homs, dout.to(dev), workspace=ws, check=False)
+    assert _lib.render_backward_status(ws, H, W, P) == V
+    assert torch.isnan(got).all()
+    kopts(bwd_margin=16, bwd_poll_limit=0)
+    got = _lib.render_backward(mpi.to(dev), homs, dout.to(dev), workspace=ws, check=True)
+    assert_bits(got, oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy()), "after an abort")
+
+
 def test_backward_abort_surfaces_on_next_default_call(dev, kopts):
     """the default render_backward (check=None, the autograd path) reads the abort
     count back asynchronously -- no synchronisation -- and the next call raises; so a training
