@@ -196,6 +196,20 @@ int mpiv_render_backward(const float *mpi, const int64_t mpi_strides[5], int V, 
                          const float *homs, const float *dout, const float *ckpt, float *dmpi,
                          void *workspace, size_t workspace_bytes, void *stream);
 
+/* mpiv_render_backward that also reports an aborted view without a copy: the calling process's abort
+ * flag of the current device (mpiv_render_backward_abort_flag) is set to 1 -- a device store into a
+ * page-locked, device-mapped int, visible to the host without a copy -- when a view's bucket fallback
+ * aborted and its gradient was NaN-filled.  The caller reads and clears the flag on the host (the
+ * Python layer does so before every default backward, so a training loop fails at the latest one
+ * step after an abort, with no per-call copy, event or synchronisation). */
+int mpiv_render_backward_watched(const float *mpi, const int64_t mpi_strides[5], int V, int H, int W, int P,
+                                 const float *homs, const float *dout, const float *ckpt, float *dmpi,
+                                 void *workspace, size_t workspace_bytes, void *stream);
+
+/* The calling process's abort flag of device `device` (a page-locked int mapped into every device,
+ * fine-grained, allocated on first use).  NULL if the allocation failed or device is out of [0, 64). */
+int *mpiv_render_backward_abort_flag(int device);
+
 /* Views of the last mpiv_render_backward call on this workspace (same H, W, P) whose
  * fallback aborted -> *aborted_views.  SYNCHRONISES the stream (the one entry point that
  * does): a checker for tests and debug runs, not for the training loop. */

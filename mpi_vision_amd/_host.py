@@ -98,6 +98,20 @@ def psv_inverse(K: torch.Tensor, batch: int) -> torch.Tensor:
 _KINV_DEV: dict = {}
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _raw_stream_id(dev) -> int:
+    """The raw handle of dev's current stream (no torch Stream object built: per-call path)."""
+    if _raw_stream is not None:
+        return _raw_stream(dev.index if dev.index is not None else torch.cuda.current_device())
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _f32_on(t: torch.Tensor, dev) -> torch.Tensor:
+    return t if (t.dtype == _F32 and t.device == dev) else t.to(device=dev, dtype=_F32)
+
+
 def _kinv_device(intrinsics: torch.Tensor, batch: int, dev, sid=None, psv: bool = False) -> torch.Tensor:
     """inverse(K) [batch,3,3] on `dev` for a device-resident intrinsics tensor, memoised on
     that tensor OBJECT and its version counter (an in-place update bumps it; a new tensor
@@ -114,7 +128,7 @@ def _kinv_device(intrinsics: torch.Tensor, batch: int, dev, sid=None, psv: bool 
         ver = None
     # the stream is part of the key: the copy's memory, once evicted, is reused in the order of
     # the stream that allocated it, so each stream reads only its own copy
-    stream = torch.cuda.current_stream(dev).cuda_stream if sid is None else sid
+    stream = _raw_stream_id(dev) if sid is None else sid
     ent = _KINV_DEV.get((id(intrinsics), psv))
     if (ver is not None and ent is not None and ent[0]() is intrinsics and ent[1] == ver and ent[2] == batch
             and ent[3].device == dev and ent[4] == stream):
@@ -139,9 +153,12 @@ def render_homographies_device(pose: torch.Tensor, depths: torch.Tensor, intrins
     [B, P, 9] fp32 tensor on the pose's device."""
     from . import _lib
     dev = pose.device
-    pose_d = pose.to(dtype=_F32).contiguous()
-    d = depths.to(device=dev, dtype=_F32).reshape(-1).contiguous()
-    K = intrinsics.to(device=dev, dtype=_F32).expand(batch, 3, 3).contiguous()
+    pose_d = _f32_on(pose, dev).contiguous()
+    d = _f32_on(depths, dev).reshape(-1).contiguous()
+    K = _f32_on(intrinsics, dev)
+    if tuple(K.shape) != (batch, 3, 3):
+        K = K.expand(batch, 3, 3)
+    K = K.contiguous()
     kinv = _kinv_device(intrinsics, batch, dev)
     P = d.shape[0]
     H = torch.empty((batch, P, 9), dtype=_F32, device=dev)

@@ -60,6 +60,8 @@ _SIGS = {
     "mpiv_preprocess": [_vp, _i64, _vp, _vp],
     "mpiv_deprocess_u8": [_vp, _i64, _vp, _vp],
     "mpiv_render_backward": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp],
+    "mpiv_render_backward_watched": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t,
+                                     _vp],
     "mpiv_render_backward_status": [_vp, _int, _int, _int, ctypes.POINTER(_int), _vp],
     "mpiv_render_train": [_vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp, _vp],
     "mpiv_render_packed_census": [_vp, _int, _int, _int, _vp, _int, _vp, _vp, _vp],
@@ -85,6 +87,7 @@ _SIGS = {
                                    _vp],
 }
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
+                          "mpiv_render_backward_abort_flag",
                           "mpiv_render_backward_workspace_size_min", "mpiv_build_id", "mpiv_debug_set")
 ABI_VERSION = 13
 
@@ -154,6 +157,8 @@ def _open(path: str, check_id: bool):
     L.mpiv_render_backward_workspace_size.restype = ctypes.c_size_t
     L.mpiv_render_backward_workspace_size_min.argtypes = [_int, _int, _int]
     L.mpiv_render_backward_workspace_size_min.restype = ctypes.c_size_t
+    L.mpiv_render_backward_abort_flag.argtypes = [_int]
+    L.mpiv_render_backward_abort_flag.restype = ctypes.c_void_p
     if L.mpiv_abi_version() != ABI_VERSION:
         raise RuntimeError(f"mpi_vision_amd: {path} ABI version mismatch")
     return L
@@ -206,7 +211,8 @@ def _call(name, *args):
     stay referenced (alive) for the duration of the call, so temporaries built inline
     cannot be freed and their memory reused by a later argument's allocation."""
     L = load_ab() if name in _AB_ENTRIES else load()
-    cargs = [ctypes.c_void_p(a.data_ptr()) if isinstance(a, torch.Tensor) else a for a in args]
+    # (tensor arguments as plain ints: every pointer parameter's argtype is c_void_p)
+    cargs = [a.data_ptr() if isinstance(a, torch.Tensor) else a for a in args]
     if _ROCTX is not None:
         _ROCTX.roctxRangePushA(name.encode())
         try:
@@ -219,11 +225,15 @@ def _call(name, *args):
         raise RuntimeError(f"{name} failed ({rc}): {L.mpiv_last_error().decode()}")
 
 
+_DEBUG_GEN = 0  # bumped by every set_debug / reset_debug: memos of option-dependent values key on it
+
+
 def set_debug(**opts):
     """Select non-default kernel variants (tests and A/B tools only; mpiv_debug_set).
     Options that pick a kernel kept for A/B measurement are refused by the production
     library; then the A/B flavour takes them and runs every entry point until reset_debug()."""
-    global _override
+    global _override, _DEBUG_GEN
+    _DEBUG_GEN += 1
     L = load_main()
     need_ab = False
     for k, v in opts.items():
@@ -249,7 +259,8 @@ def set_debug(**opts):
 
 def reset_debug():
     """Every option back to its production default; entry points back on libmpiv.so."""
-    global _override
+    global _override, _DEBUG_GEN
+    _DEBUG_GEN += 1
     for L in (_lib, _lib_ab):
         if L is not None:
             L.mpiv_debug_set(b"reset", 0)
@@ -303,7 +314,14 @@ def _dev(*tensors):
     return dev
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream(dev):
+    """The current stream of dev as the hipStream_t the entry points take (the raw handle, without
+    building a torch Stream object: this runs on every launch)."""
+    if _raw_stream is not None:
+        return ctypes.c_void_p(_raw_stream(dev.index if dev.index is not None else torch.cuda.current_device()))
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
@@ -658,38 +676,43 @@ def render_backward_status(workspace: torch.Tensor, H: int, W: int, P: int) -> i
     return n.value
 
 
-class _AbortMonitor:
-    """The default (check=None) render_backward's abort count, surfaced without a synchronisation
-    (ADVICE r4): after each call the workspace's abort word is copied, stream-ordered, into a small
-    page-locked buffer and an event is recorded; the next render_backward (or
-    render_backward_raise_pending) reads every copy whose event has completed and raises if a view
-    was NaN-filled.  So an aborted fallback (never expected: render_bwd.hip) fails the training
-    loop at the latest one step later instead of silently feeding NaN gradients to the optimiser."""
+_BWD_WS: dict = {}
 
-    def __init__(self):
-        self.pending = collections.deque()
-        self.free = []
+
+def _bwd_ws_sizes(L, H: int, W: int, P: int):
+    """(minimum, fastest) workspace bytes of mpiv_render_backward for one H x W x P view, memoised."""
+    key = (L._name, H, W, P, _DEBUG_GEN)  # (the sizes follow debug options such as bwd_group)
+    v = _BWD_WS.get(key)
+    if v is None:
+        v = _BWD_WS[key] = (L.mpiv_render_backward_workspace_size_min(H, W, P),
+                            L.mpiv_render_backward_workspace_size(H, W, P))
+    return v
+
+
+class _AbortMonitor:
+    """The default (check=None) render_backward's abort report, surfaced without a synchronisation
+    (ADVICE r4): the call runs mpiv_render_backward_watched, whose NaN fill of an aborted view also
+    sets the device's page-locked, device-mapped abort flag (mpiv_render_backward_abort_flag) from the
+    device; the next default render_backward (or render_backward_raise_pending) reads the flag on the
+    host -- a memory read, no copy, event or synchronisation (round 5's stream-ordered copy and event
+    cost ~30 us per call) -- and raises.  So an aborted fallback (never expected: render_bwd.hip) fails
+    the training loop at the latest one step later instead of silently feeding NaN gradients to the
+    optimiser."""
+
+    def __init__(self, dev, L):
+        self.dev = dev
+        ptr = L.mpiv_render_backward_abort_flag(dev.index if dev.index is not None else torch.cuda.current_device())
+        if not ptr:
+            raise RuntimeError("mpiv_render_backward_abort_flag: no page-locked abort flag for " + str(dev))
+        self.flag = ctypes.cast(ptr, ctypes.POINTER(ctypes.c_int))
 
     def raise_completed(self, wait: bool = False):
-        while self.pending and (wait or self.pending[0][0].query()):
-            ev, buf, nviews = self.pending.popleft()
-            ev.synchronize()
-            n = int(buf[0])
-            self.free.append(buf)
-            if n:
-                self.pending.clear()
-                raise RuntimeError(f"mpiv_render_backward: the bucket fallback aborted on {n} of {nviews} views of an "
-                                   "earlier backward (their gradients were NaN)")
-
-    def post(self, ws: torch.Tensor, H: int, W: int, P: int, nviews: int, dev):
-        off = bwd_flag_offset(H, W, P) + 16  # flag[4]: views aborted in the call
-        buf = self.free.pop() if self.free else torch.zeros(1, dtype=torch.int32, pin_memory=True)
-        buf.copy_(ws[off:off + 4].view(torch.int32), non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        self.pending.append((ev, buf, nviews))
-        if len(self.pending) > 64:  # a caller that never lets the stream drain: bound the ring
-            self.raise_completed(wait=True)
+        if wait:
+            torch.cuda.synchronize(self.dev)
+        if self.flag[0]:
+            self.flag[0] = 0
+            raise RuntimeError("mpiv_render_backward: the bucket fallback aborted on a view of an earlier backward "
+                               "(its gradient was NaN)")
 
 
 _ABORTS: dict = {}
@@ -698,7 +721,7 @@ _ABORTS: dict = {}
 def render_backward_raise_pending(dev=None) -> None:
     """Wait for every earlier default render_backward on `dev` (all devices if None) and raise if
     any of them NaN-filled a view (the check the next call would make)."""
-    for d, mon in list(_ABORTS.items()):
+    for (d, _), mon in list(_ABORTS.items()):
         if dev is None or d == torch.device(dev):
             mon.raise_completed(wait=True)
 
@@ -724,9 +747,9 @@ def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.T
     L = load()
     # a caller's workspace of at least the minimum (plane groups, render_bwd.hip); our own: the
     # one-group size (the fastest schedule) unless MPIV_BWD_MIN_WS=1
-    need = L.mpiv_render_backward_workspace_size_min(H, W, P)
-    ws = workspace if workspace is not None else torch.empty(
-        need if BWD_MIN_WS else L.mpiv_render_backward_workspace_size(H, W, P), dtype=torch.uint8, device=dev)
+    need, full = _bwd_ws_sizes(L, H, W, P)
+    ws = workspace if workspace is not None else torch.empty(need if BWD_MIN_WS else full, dtype=torch.uint8,
+                                                             device=dev)
     if ws.dtype != torch.uint8 or not ws.is_contiguous() or ws.numel() < need or ws.device != dev:
         raise RuntimeError(f"workspace must be a contiguous uint8 tensor of >= {need} bytes on {dev}")
     grad = torch.empty((B, H, W, P, 4), device=dev, dtype=torch.float32)
@@ -735,19 +758,21 @@ def render_backward(rgba_layers: torch.Tensor, homs: torch.Tensor, dout: torch.T
     if ckpt is not None and (tuple(ckpt.shape) != (B, (P + 7) // 8, H, W, 4) or not ckpt.is_contiguous()
                              or ckpt.device != dev or ckpt.dtype != torch.float32):
         raise RuntimeError(f"ckpt must be render_train()'s contiguous [{B},{(P + 7) // 8},{H},{W},4] tensor")
-    mon = _ABORTS.get(dev) if check is None else None
-    if check is None and mon is None:
-        mon = _ABORTS.setdefault(dev, _AbortMonitor())
-    if mon is not None:
+    watch = check is None and not BWD_CHECK
+    if watch:
+        # (one flag per device and library: the A/B build, when a test selects it, has its own)
+        key = (dev, L._name)
+        mon = _ABORTS.get(key)
+        if mon is None:
+            mon = _ABORTS.setdefault(key, _AbortMonitor(dev, L))
         mon.raise_completed()  # an earlier call's abort, read without waiting
-    _call("mpiv_render_backward", src, _strides(src), B, H, W, P, h, dout, ckpt, grad, ws, ws.numel(), _stream(dev))
+    _call("mpiv_render_backward_watched" if watch else "mpiv_render_backward", src, _strides(src), B, H, W, P, h, dout,
+          ckpt, grad, ws, ws.numel(), _stream(dev))
     if BWD_CHECK if check is None else check:
         n = render_backward_status(ws, H, W, P)
         if n:
             raise RuntimeError(f"mpiv_render_backward: the bucket fallback aborted on {n} of {B} views "
                                "(their gradients are NaN)")
-    elif mon is not None:
-        mon.post(ws, H, W, P, B, dev)
     return grad
 
 

@@ -798,10 +798,41 @@ size_t mpiv_render_backward_workspace_size_min(int H, int W, int P) {
     return bwd_layout(H, W, P, bwd_group_planes(H, W, P), nullptr, nullptr);
 }
 
-int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, int W, int P, const float* homs,
-                         const float* dout, const float* ckpt, float* dmpi, void* workspace, size_t ws_bytes,
-                         void* stream) {
-    const char* nm = "mpiv_render_backward";
+// Page-locked, device-mapped abort flags, one word per device (allocated once per process, fine-grained:
+// a device store is visible to the host without a copy).  The backward's NaN fill of an aborted view sets
+// the device's word to 1; the Python layer reads and clears it on the host (_lib._AbortMonitor) -- no
+// per-call copy, event or synchronisation.
+static int* g_abort_host = nullptr;
+static int* g_abort_dev = nullptr;
+static std::once_flag g_abort_once;
+constexpr int kAbortSlots = 64;
+
+static int* abort_flags_dev() {
+    std::call_once(g_abort_once, []() {
+        void* h = nullptr;
+        if (hipHostMalloc(&h, kAbortSlots * sizeof(int), hipHostMallocMapped | hipHostMallocPortable |
+                                                              hipHostMallocCoherent) != hipSuccess || !h)
+            return;
+        std::memset(h, 0, kAbortSlots * sizeof(int));
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) return;
+        g_abort_host = static_cast<int*>(h);
+        g_abort_dev = static_cast<int*>(d);
+    });
+    return g_abort_dev;
+}
+
+int* mpiv_render_backward_abort_flag(int device) {
+    if (device < 0 || device >= kAbortSlots) return nullptr;
+    abort_flags_dev();
+    return g_abort_host ? g_abort_host + device : nullptr;
+}
+
+constexpr int64_t kFoldCheckMaxBlocks = 8192;  // gather grids up to this size run the check in their last block
+
+static int render_backward_impl(const char* nm, const float* mpi, const int64_t st[5], int V, int H, int W, int P,
+                                const float* homs, const float* dout, const float* ckpt, float* dmpi, void* workspace,
+                                size_t ws_bytes, void* stream, bool watched) {
     if (!mpi || !st || !homs || !dout || !dmpi || !workspace) return fail(MPIV_ERR_ARG, "%s: null pointer", nm);
     if (V <= 0 || H <= 0 || W <= 0 || P <= 0) return fail(MPIV_ERR_ARG, "%s: bad shape", nm);
     // in place: planes contiguous per pixel (16-B texels), every tap below the buffer range
@@ -844,6 +875,11 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
     const ChunkGeom cg{(int)(st[1] / 4), (int)(st[2] / 4), (int)rec};
     const bool fast = H >= 2 && W >= 2;
     const int64_t HW = (int64_t)H * W;
+    {
+        int d = 0;
+        int* flags = watched && hipGetDevice(&d) == hipSuccess && d >= 0 && d < kAbortSlots ? abort_flags_dev() : nullptr;
+        ws.sink = ws2.sink = flags ? flags + d : nullptr;
+    }
     const int tiles_x = (int)blocks(W, kGTW);
     const int64_t ntiles = (int64_t)tiles_x * blocks(H, kGTY);
     const int64_t gather_blocks = ntiles * blocks(P, kGPl);
@@ -945,7 +981,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                     chk(hipEventRecord(ax->done[par], a));
                 }
                 // an aborted group (never expected) leaves the view's gradient NaN, counted once
-                bwd_poison_kernel<<<256, 256, 0, a>>>(win[0].flag, gv, (int64_t)P * HW, win[1].flag, ws.flag + 4);
+                bwd_poison_kernel<<<256, 256, 0, a>>>(win[0].flag, gv, (int64_t)P * HW, win[1].flag, ws.flag + 4, ws.sink);
                 chk(hipEventRecord(ax->view, a));
             }
             chk(hipStreamWaitEvent(q, ax->view, 0));  // the caller's stream: every launch of this call
@@ -990,7 +1026,7 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
                     bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, wg, gv, poll_limit, tick_limit, fb_mode == 2, p_lo,
                                                                          p_hi);
             }
-            bwd_poison_kernel<<<256, 256, 0, q>>>(ws.flag, gv, (int64_t)P * HW);
+            bwd_poison_kernel<<<256, 256, 0, q>>>(ws.flag, gv, (int64_t)P * HW, nullptr, nullptr, ws.sink);
             continue;
         }
         const int R = fast ? chunk_rows() : 1;
@@ -1033,7 +1069,15 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         else MPIV_CHAIN(false, 1);
 #undef MPIV_CHAIN
         if (folded) {
-            bwd_gather_kernel<true><<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin, 0, P);
+            // the check in the gather's last block costs every block a wait for its stores and a barrier at
+            // its end (+2 % at config 4's 131072 blocks, profiles/r06_bwd_fold.json): small grids only, where
+            // the separate launch is what costs
+            if (gather_blocks <= kFoldCheckMaxBlocks) {
+                bwd_gather_kernel<true><<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin, 0, P);
+            } else {
+                bwd_gather_kernel<false><<<(unsigned)gather_blocks, kGThreads, 0, q>>>(g, hv, ws, gv, margin, 0, P);
+                bwd_check_kernel<<<1, kWave, 0, q>>>(ws, 0, 0);
+            }
             if (fast)
                 bwd_fallback_kernel<true><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, tick_limit, fb_mode == 2, 0,
                                                                     P, (int64_t)P * HW);
@@ -1080,9 +1124,24 @@ int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, in
         else
             bwd_fallback_kernel<false><<<fb_blocks, 256, 0, q>>>(g, hv, ws, gv, poll_limit, tick_limit, fb_mode == 2, 0, P);
         // an aborted fallback (never expected) leaves a NaN gradient, never a plausible one
-        bwd_poison_kernel<<<256, 256, 0, q>>>(ws.flag, gv, (int64_t)P * HW);
+        bwd_poison_kernel<<<256, 256, 0, q>>>(ws.flag, gv, (int64_t)P * HW, nullptr, nullptr, ws.sink);
     }
     return launched(nm);
+}
+
+int mpiv_render_backward(const float* mpi, const int64_t st[5], int V, int H, int W, int P, const float* homs,
+                         const float* dout, const float* ckpt, float* dmpi, void* workspace, size_t ws_bytes,
+                         void* stream) {
+    return render_backward_impl("mpiv_render_backward", mpi, st, V, H, W, P, homs, dout, ckpt, dmpi, workspace, ws_bytes,
+                                stream, false);
+}
+
+int mpiv_render_backward_watched(const float* mpi, const int64_t st[5], int V, int H, int W, int P, const float* homs,
+                                 const float* dout, const float* ckpt, float* dmpi, void* workspace, size_t ws_bytes,
+                                 void* stream) {
+    if (!abort_flags_dev()) return fail(MPIV_ERR_HIP, "mpiv_render_backward_watched: no page-locked abort flag");
+    return render_backward_impl("mpiv_render_backward_watched", mpi, st, V, H, W, P, homs, dout, ckpt, dmpi, workspace,
+                                ws_bytes, stream, true);
 }
 
 int mpiv_render_backward_status(const void* workspace, int H, int W, int P, int* aborted_views, void* stream) {

@@ -125,6 +125,8 @@ struct BwdWs {
     int* flag;     // [0] 1: the fallback recomputes every plane of the view; [1], [2] the fallback's
                    // ticket and completion counters; [3] 1: this view's fallback aborted (a wait
                    // outlasted its poll limit); [4] views aborted in this call (bwd_fallback_kernel)
+    int* sink = nullptr;    // the device's page-locked abort flag (mpiv_render_backward_abort_flag), set to 1
+                            // by an aborted view's NaN fill; nullptr: not mapped
     int* vcount = nullptr;  // where the fallback counts an aborted view (flag + 4; nullptr: the overlapped
                             // schedule counts views in bwd_poison_kernel instead)
     // fallback: bucket pipeline over chunks of pc planes
@@ -976,21 +978,27 @@ __device__ __forceinline__ void bwd_check_wave(BwdWs& ws, int force, int keep_ab
 // block-exit counters (zeroed with the pair counters, reset by the last block).
 constexpr int kFlagGatherDone = 8, kFlagFallbackExit = 9;
 
-// The last block of a grid to get here (after its own global writes and atomics) returns true
-// (block-uniform); every block's earlier device-scope atomics are visible to it.
-__device__ __forceinline__ bool last_block_in(int* ctr) {
-    __shared__ int s_last;
+// The last block of a grid to get here returns true (block-uniform), and the device-scope atomics
+// every block issued before it (the gather's pair counts) have been performed when it reads them with
+// device-scope atomic loads.  No release fence: on gfx950 an agent-scope release writes back the XCD's
+// L2 (the d MPI the gather just wrote), which at one fence per block cost 3x the backward (measured,
+// profiles/r06_bwd_fold.json).  Instead each wave waits until its own vector memory operations are
+// acknowledged (s_waitcnt vmcnt(0): device-scope atomics are acknowledged once performed) before the
+// block's barrier, and the counter is a relaxed device-scope atomic.  A count read too early could
+// only be smaller, which sends the view to the (bit-exact) fallback -- never a wrong gradient.
+// s_flag: an int of the caller's LDS that is free by now (no extra LDS per block).
+__device__ __forceinline__ bool last_block_in(int* ctr, int* s_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();
-        s_last = atomicAdd(reinterpret_cast<unsigned*>(ctr), 1u) == gridDim.x - 1;
-        if (s_last) {
-            __threadfence();
-            *ctr = 0;  // ready for the next launch
-        }
+        const unsigned prev = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(ctr), 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == gridDim.x - 1;
+        if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+        *s_flag = last;
     }
     __syncthreads();
-    return __builtin_amdgcn_readfirstlane(s_last) != 0;
+    return __builtin_amdgcn_readfirstlane(*s_flag) != 0;
 }
 
 // CHECK (round 6, the single-group schedule): the pair-count check (bwd_check_kernel's) runs in
@@ -1164,7 +1172,7 @@ __global__ __launch_bounds__(kGThreads, MPIV_GLB) void bwd_gather_kernel(RenderG
                 }
         }
     }
-    if (CHECK && last_block_in(ws.flag + kFlagGatherDone) && threadIdx.x < kWave)
+    if (CHECK && last_block_in(ws.flag + kFlagGatherDone, &s_ovf[0]) && threadIdx.x < kWave)
         bwd_check_wave(ws, 0, 0, threadIdx.x);
 }
 
@@ -2324,9 +2332,10 @@ __global__ __launch_bounds__(256) void bwd_fallback_kernel(RenderGeom g, const f
         const int t = __builtin_amdgcn_readfirstlane(s_ticket);
         __syncthreads();  // s_ticket is rewritten by the next iteration
         if (t < 0) {
-            if (poison_n > 0 && last_block_in(ws.flag + kFlagFallbackExit) &&
+            if (poison_n > 0 && last_block_in(ws.flag + kFlagFallbackExit, &s_ticket) &&
                 __hip_atomic_load(ws.flag + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
                 const float q = __builtin_nanf("");
+                if (tid == 0 && ws.sink) __hip_atomic_store(ws.sink, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 for (int64_t i = tid; i < poison_n; i += 256) dmpi[i] = make_float4(q, q, q, q);
             }
             return;
@@ -2376,9 +2385,10 @@ __global__ __launch_bounds__(256) void ticket_selftest_kernel(unsigned* __restri
 // whose fallbacks do not count) adds the view once
 __global__ __launch_bounds__(256) void bwd_poison_kernel(const int* __restrict__ flag, float4* __restrict__ dmpi,
                                                          int64_t n, const int* __restrict__ flag_b = nullptr,
-                                                         int* __restrict__ count = nullptr) {
+                                                         int* __restrict__ count = nullptr, int* sink = nullptr) {
     if (flag[3] == 0 && (!flag_b || flag_b[3] == 0)) return;
     if (count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(count, 1);
+    if (sink && blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(sink, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const float q = __builtin_nanf("");
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
         dmpi[i] = make_float4(q, q, q, q);

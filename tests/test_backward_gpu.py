@@ -395,10 +395,11 @@ def test_backward_launch_folded_schedule(ckpt, mode, dev, kopts):
         ws = torch.full((L.mpiv_render_backward_workspace_size(H, W, P),), 0x5A, dtype=torch.uint8, device=dev)
         got = _lib.render_backward(m, h, d, workspace=ws, ckpt=ck, check=True)
         off = _lib.bwd_flag_offset(H, W, P)
-        res[unfold] = (got, ws[off:off + 20].view(torch.int32).tolist())
+        res[unfold] = (got, ws[off:off + 40].view(torch.int32).tolist())
         assert_bits(got, want, f"unfold={unfold} {mode}")
     assert res[0][1][0] == res[1][1][0] == (1 if mode == "miss" else 0), (res[0][1], res[1][1])
     assert res[0][1][3:5] == res[1][1][3:5] == [0, 0]
+    assert res[0][1][8:10] == [0, 0]  # the block-exit counters are left at zero for the next call
 
 
 def test_backward_folded_abort_is_loud(dev, kopts):
@@ -430,7 +431,7 @@ def test_backward_abort_surfaces_on_next_default_call(dev, kopts):
     out.backward(dout.to(dev))  # aborted (forced): NaN gradient, nothing raised yet
     assert torch.isnan(leaf.grad).all()
     torch.cuda.synchronize()
-    with pytest.raises(RuntimeError, match="aborted on 2 of 2 views of an earlier backward"):
+    with pytest.raises(RuntimeError, match="aborted on a view of an earlier backward"):
         _lib.render_backward(mpi.to(dev), homs, dout.to(dev))
     # the explicit wait-and-raise form
     _lib.render_backward(mpi.to(dev), homs, dout.to(dev))
