@@ -131,14 +131,14 @@ enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOpt
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
                 kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kOptU8Flight, kOptBwdGroup,
                 kOptNetoutGeo, kOptNetoutBuf, kOptBwdOverlap, kOptSweepBand, kOptSweepPf, kOptSweepSoa, kOptBwdUnfold,
-                kNumOpts };
+                kOptNetoutFg3, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
                                          "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode",
                                          "chunk_strip", "u8_flight", "bwd_group", "netout_geo", "netout_buf", "bwd_overlap", "sweep_band",
-                                         "sweep_pf", "sweep_soa", "bwd_unfold"};
+                                         "sweep_pf", "sweep_soa", "bwd_unfold", "netout_fg3"};
 #ifndef MPIV_CHUNK_STRIP
 #define MPIV_CHUNK_STRIP 1  // round 4: 0.506 vs 0.64 ms in place (profiles/r04j_strip*_ab.jsonl)
 #endif
@@ -146,9 +146,9 @@ const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_nat
 #define MPIV_U8_FLIGHT 0
 #endif
 const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP,
-                                    MPIV_U8_FLIGHT, 0, 0, 1, 0, 0, 0, 0, 0};
+                                    MPIV_U8_FLIGHT, 0, 0, 1, 0, 0, 0, 0, 0, 1};
 int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP, MPIV_U8_FLIGHT, 0,
-                        0, 1, 0, 0, 0, 0, 0};
+                        0, 1, 0, 0, 0, 0, 0, 1};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -1727,9 +1727,14 @@ static int render_net_output_impl(const char* nm, const float* pred, const int64
         sb.pred_bytes = (int)pspan;
         sb.fg_bytes = (int)fspan;
     }
-    if (g_route)
+    // the reference image's channels contiguous: one 12-B colour load per staged texel (netout_fg3=0: three)
+    const bool fg3 = buf && db && fs[3] == 1 && opt(kOptNetoutFg3) != 0;
+    if (g_route) {
+        if (fg3)
+            return note_route(nb, 64 * NW, "render_netout_kernel<%d, %d, %d, true, true, true>", NW, R, geo % 10);
         return note_route(nb, 64 * NW, "render_netout_kernel<%d, %d, %d, %s, %s>", NW, R, geo % 10, buf ? "true" : "false",
                           db ? "true" : "false");
+    }
     const unsigned nbu = (unsigned)nb;
     hipStream_t q = S(stream);
     switch (geo * 2 + (buf ? 1 : 0)) {
@@ -1745,8 +1750,12 @@ static int render_net_output_impl(const char* nm, const float* pred, const int64
                                                                                            ckpt);
             break;
         case 1821 * 2 + 1:
-            render_netout_kernel<8, 2, 1, true, true><<<nbu, 512, P * sizeof(int2), q>>>(pred, fg, sb, g, B, homs, out,
-                                                                                          ckpt);
+            if (fg3)
+                render_netout_kernel<8, 2, 1, true, true, true><<<nbu, 512, P * sizeof(int2), q>>>(pred, fg, sb, g, B, homs,
+                                                                                                out, ckpt);
+            else
+                render_netout_kernel<8, 2, 1, true, true><<<nbu, 512, P * sizeof(int2), q>>>(pred, fg, sb, g, B, homs, out,
+                                                                                              ckpt);
             break;
     }
     return launched(nm);

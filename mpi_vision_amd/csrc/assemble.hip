@@ -331,6 +331,10 @@ __device__ __forceinline__ NetWA net_load_wa_buf(const NetRsrc& r, const NetStri
     return NetWA{llvm_raw_buffer_load_f32(r.pred, off, p * r.pc4, 0), llvm_raw_buffer_load_f32(r.pred, off, (P + p) * r.pc4, 0)};
 }
 
+// FG3 (round 6): the reference image's channels are contiguous (its [B,H,W,3] tensor as the notebook
+// holds it), so a texel's colour is ONE 12-B load instead of three 4-B loads (6 load instructions
+// per staged texel instead of 8).
+template <bool FG3 = false>
 __device__ __forceinline__ NetBF net_load_bf_buf(const NetRsrc& r, const NetStrides& s, int H, int W, int P, int tx,
                                                  int ty) {
     NetBF q;
@@ -341,9 +345,16 @@ __device__ __forceinline__ NetBF net_load_bf_buf(const NetRsrc& r, const NetStri
     q.b0 = llvm_raw_buffer_load_f32(r.pred, off, (2 * P) * r.pc4, 0);
     q.b1 = llvm_raw_buffer_load_f32(r.pred, off, (2 * P + 1) * r.pc4, 0);
     q.b2 = llvm_raw_buffer_load_f32(r.pred, off, (2 * P + 2) * r.pc4, 0);
-    q.f0 = llvm_raw_buffer_load_f32(r.fg, offf, 0, 0);
-    q.f1 = llvm_raw_buffer_load_f32(r.fg, offf, r.fc4, 0);
-    q.f2 = llvm_raw_buffer_load_f32(r.fg, offf, 2 * r.fc4, 0);
+    if (FG3) {
+        const f32x3b f = llvm_raw_buffer_load_v3f32(r.fg, offf, 0, 0);
+        q.f0 = f[0];
+        q.f1 = f[1];
+        q.f2 = f[2];
+    } else {
+        q.f0 = llvm_raw_buffer_load_f32(r.fg, offf, 0, 0);
+        q.f1 = llvm_raw_buffer_load_f32(r.fg, offf, r.fc4, 0);
+        q.f2 = llvm_raw_buffer_load_f32(r.fg, offf, 2 * r.fc4, 0);
+    }
     return q;
 }
 
@@ -370,7 +381,7 @@ __device__ __forceinline__ float4 net_assemble2(const NetWA& q, const NetBF& r) 
 // samples finished reading before this plane's barrier.  The boxes get 100 texels per tile row
 // (1600 at 64 x 16: the widest box of config 2's camera path is ~1570) and the box table sits in
 // dynamic LDS sized by P, so 2 x 25.6 KiB keeps 3 blocks per CU.
-template <int NW, int RPT, int DEPTH, bool BUF, bool DB = false>
+template <int NW, int RPT, int DEPTH, bool BUF, bool DB = false, bool FG3 = false>
 __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __restrict__ pred,
                                                                 const float* __restrict__ fg, NetStrides ns,
                                                                 RenderGeom g, int V, const float* __restrict__ homs,
@@ -474,7 +485,7 @@ __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __r
 #pragma unroll
         for (int j = 0; j < kFill; ++j)
             if (kThreads * j < nfp)
-                bf[j] = BUF ? net_load_bf_buf(rs, ns, g.H, g.W, P, bx.x + col_j[j], bx.y + row_j[j])
+                bf[j] = BUF ? net_load_bf_buf<FG3>(rs, ns, g.H, g.W, P, bx.x + col_j[j], bx.y + row_j[j])
                             : net_load_bf(pred, fg, ns, g.H, g.W, P, v, bx.x + col_j[j], bx.y + row_j[j]);
     };
     auto commit = [&](const NetWA (&st)[kFill], const int4& bx, float4* s_tex) {

@@ -98,7 +98,7 @@ def test_route_dry_run_u8_and_net_output():
                                                                   16 * 64 * 256)
     assert _lib.route("render_packed_u8", 1024, 1024, 128, 125)[0] == "render_u8_kernel<false, 4, true, 2>"
     name, grid = _lib.route("render_net_output", 1, 576, 1024, 32)
-    assert name == "render_netout_kernel<8, 2, 1, true, true>" and grid == 576 * 512
+    assert name == "render_netout_kernel<8, 2, 1, true, true, true>" and grid == 576 * 512
 
 
 def test_line_guard_prints_once():

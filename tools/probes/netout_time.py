@@ -21,6 +21,9 @@ def main():
     fg = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
     lib = os.path.basename(os.environ.get("MPIV_LIB", "libmpiv.so"))
     geos = [int(x) for x in os.environ.get("GEOS", "821,1821").split(",")]
+    # OPTS: extra debug options to A/B, "name=v;name=v" alternatives (e.g. "netout_fg3=0;netout_fg3=1")
+    alts = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in a.split(",") if kv)
+            for a in os.environ.get("OPTS", "").split(";")] or [{}]
     for pose in (5, 20):
         homs = _host.render_homographies(configs.f32(c["poses"][pose:pose + 1]), configs.f32(c["depths"]),
                                          configs.f32([c["K"]]), 1).to(dev)
@@ -29,8 +32,8 @@ def main():
         fn = lambda: _lib._call("mpiv_render_net_output", pred, _lib._strides(pred), fg, _lib._strides(fg), 1,  # noqa: E731
                                 H, W, P, homs, out, _lib._stream(dev))
         for rep in range(2):
-            for geo in geos:
-                with _lib.debug(netout_geo=geo):
+            for geo, alt in [(g_, a_) for g_ in geos for a_ in alts]:
+                with _lib.debug(netout_geo=geo, **alt):
                     for _ in range(20):
                         fn()
                     torch.cuda.synchronize()
@@ -46,7 +49,7 @@ def main():
                         ts.append(a.elapsed_time(b) / 20)
                     ts.sort()
                     same = bool(torch.equal(out.view(torch.int32), two.view(torch.int32)))
-                    print(json.dumps({"lib": lib, "pose": pose, "geo": geo, "rep": rep, "ms": round(ts[3], 4),
+                    print(json.dumps({"lib": lib, "pose": pose, "geo": geo, "opts": alt, "rep": rep, "ms": round(ts[3], 4),
                                       "min": round(ts[0], 4), "same": same}), flush=True)
 
 
