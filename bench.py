@@ -664,6 +664,34 @@ def notebook_leg(dev, stream, n=50):
     # steps, the median reported (one span can catch a garbage-collector pause; all five are listed)
     train_reps = [span_ms(train_step, n, stream) for _ in range(5)]
     train_ms = float(np.median(train_reps))
+    # the same step captured in HIP graphs (torch.cuda.make_graphed_callables): the forward and the
+    # backward each replay as one graph, so no per-step Python / autograd host work remains
+    graphed = {}
+    try:
+        class _RenderStep(torch.nn.Module):
+            def forward(self, m):
+                return mv.mpi_render_view_torch(m, poses, planes, Kb)
+        leaf.grad = None
+        mv.mpi_render_view_torch(leaf, poses, planes, Kb).backward(dout)
+        eager_grad = leaf.grad.clone()
+        leaf.grad = None
+        gfn = torch.cuda.make_graphed_callables(_RenderStep(), (leaf,))
+
+        def gstep():
+            gfn(leaf).backward(dout)
+            leaf.grad = None
+        gfn(leaf).backward(dout)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(leaf.grad.view(torch.int32), eager_grad.view(torch.int32)))
+        leaf.grad = None
+        warm(gstep, stream)
+        g_reps = [span_ms(gstep, n, stream) for _ in range(5)]
+        graphed = {"train_step_graphed_ms": round(float(np.median(g_reps)), 4),
+                   "train_step_graphed_ms_reps": [round(x, 4) for x in g_reps], "graphed_grad_bit_identical": same,
+                   "graphed_def": "the same step through torch.cuda.make_graphed_callables (HIP graphs: forward and "
+                                  "backward replayed as one graph each)"}
+    except RuntimeError as e:
+        graphed = {"train_step_graphed_error": f"{type(e).__name__}: {e}"[:300]}
     kname, grid = _lib.route("plane_sweep", 1, S, N, 3, P, S, N)
     r_alg = P * S * N * 16 + S * N * 12
     res = {"workload": "notebook shape (ipynb cell 8 L89-90): 224x224, 10 planes, bs 1",
@@ -675,6 +703,7 @@ def notebook_leg(dev, stream, n=50):
                              f"median of 5 spans of {n} back-to-back steps",
            "note": "8 MB of texels: launch-latency-bound at this size", "psv": prof_fields(kname, grid, psv_alg,
                                                                                              psv_kernel_ms, "nb")}
+    res.update(graphed)
     del mpi, leaf, out
     return res
 

@@ -130,9 +130,19 @@ def _kinv_device(intrinsics: torch.Tensor, batch: int, dev, sid=None, psv: bool 
     # the stream that allocated it, so each stream reads only its own copy
     stream = _raw_stream_id(dev) if sid is None else sid
     ent = _KINV_DEV.get((id(intrinsics), psv))
-    if (ver is not None and ent is not None and ent[0]() is intrinsics and ent[1] == ver and ent[2] == batch
-            and ent[3].device == dev and ent[4] == stream):
+    same = (ver is not None and ent is not None and ent[0]() is intrinsics and ent[1] == ver and ent[2] == batch
+            and ent[3].device == dev)
+    if same and ent[4] == stream:
         return ent[3]
+    if torch.cuda.is_current_stream_capturing():
+        # HIP-graph capture (torch.cuda.graph / make_graphed_callables): a device-to-host copy cannot be
+        # captured.  The inverse memoised during the warm-up (on another stream) is copied device to
+        # device instead -- a captured copy into the graph's own memory pool, so replays never read
+        # memory the memo may free.
+        if same:
+            return ent[3].clone()
+        raise RuntimeError("mpi_vision_amd: inverse(intrinsics) is not memoised for this tensor; run the call "
+                           "once outside the HIP-graph capture (the warm-up) first")
     if psv:
         kinv = psv_inverse(intrinsics, batch).to(dev)
     else:

@@ -511,3 +511,29 @@ def test_backward_config4_workspace_and_checkpoint_paths(dev):
     with _lib.debug(bwd_overlap=0):
         seq = _lib.render_backward(mpi, homs, dout, check=True)
     assert torch.equal(seq.view(torch.int32), one.view(torch.int32))
+
+
+class _RenderModule(torch.nn.Module):
+    def __init__(self, pose, planes, K):
+        super().__init__()
+        self.pose, self.planes, self.K = pose, planes, K
+
+    def forward(self, mpi):
+        return mv.mpi_render_view_torch(mpi, self.pose, self.planes, self.K)
+
+
+def test_training_step_captured_in_a_hip_graph(grad, dev):
+    """The drop-in's training step (forward with checkpoints + the folded backward) captured in HIP graphs
+    (torch.cuda.make_graphed_callables: every launch on the captured stream, no host synchronisation, the
+    intrinsics inverse copied device to device inside the capture) and replayed: the reference's gradient
+    bit for bit on every replay (golden 'ga')."""
+    mpi, t = _inputs(grad, "ga", dev)
+    leaf = mpi.to(dev).requires_grad_(True)
+    graphed = torch.cuda.make_graphed_callables(_RenderModule(t["pose"], t["depths"], t["K"]), (leaf,))
+    for _ in range(3):
+        leaf.grad = None
+        out = graphed(leaf)
+        out.backward(t["dout"])
+        torch.cuda.synchronize()
+        assert_bits(leaf.grad, grad["ga_grad"], "graphed training step")
+        assert_bits(out.detach(), grad["ga_out"], "graphed forward")
