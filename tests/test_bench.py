@@ -156,3 +156,40 @@ def test_line_guard_survives_a_hung_exchange(world, tmp_path):
     line = json.loads(lines[0])
     assert line["value"] == 123.0 and "timed out" in line["config5_plane_sharded"]["error"]
     assert all(not any(ln.startswith("{") for ln in o[0].splitlines()) for o in outs[1:])
+
+
+def test_sampled_boxes_cover_every_tap():
+    """bench.sampled_boxes (the needed-bytes figure of configs 2 / 5): the map from output pixel to sample
+    position is linear-fractional, so the frame corners bound it -- every tap of every pixel (computed
+    here for all pixels) lies in the box, and the box is tight to one texel."""
+    import numpy as np
+    from mpi_vision_amd import _host, configs
+    H, W, P, V = 23, 41, 6, 3
+    g = __import__("torch").Generator().manual_seed(3)
+    K = configs.f32([configs.intrinsics_matrix(40.0, 42.0, 20.0, 11.0)] * V)
+    poses = configs.f32([configs.pose_from(configs.rot_y(3.0 * (i - 1)), (0.1 * i, -0.05, 0.02 * i)) for i in range(V)])
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(1, 30, P)), K, V).numpy()
+    box = bench.sampled_boxes(homs, H, W)
+    ys, xs = np.mgrid[0:H, 0:W].astype(np.float64)
+    h = homs.reshape(V, P, 3, 3).astype(np.float64)
+    for v in range(V):
+        for p in range(P):
+            m = h[v, p]
+            u = m[0, 0] * xs + m[0, 1] * ys + m[0, 2]
+            vv = m[1, 0] * xs + m[1, 1] * ys + m[1, 2]
+            w = m[2, 0] * xs + m[2, 1] * ys + m[2, 2]
+            px = u / w * W / (H - 1) - 0.5
+            py = vv / w * H / (W - 1) - 0.5
+            x0, y0 = np.floor(px), np.floor(py)
+            tx = np.concatenate([x0.ravel(), x0.ravel() + 1])
+            ty = np.concatenate([y0.ravel(), y0.ravel() + 1])
+            inside = (tx >= 0) & (tx < W) & (ty >= 0) & (ty < H)
+            bx0, bx1, by0, by1 = box[v, p]
+            if not inside.any():
+                continue
+            assert tx[inside].min() >= bx0 and tx[inside].max() <= bx1, (v, p)
+            assert ty[inside].min() >= by0 and ty[inside].max() <= by1, (v, p)
+            assert bx0 >= tx[inside].min() - 1 and bx1 <= tx[inside].max() + 1
+    need = bench.needed_bytes(homs, H, W)
+    assert need <= V * (P * H * W * 16 + H * W * 12)
+    assert bench.needed_bytes(homs, H, W, union=True) <= need
