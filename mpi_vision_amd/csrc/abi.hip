@@ -121,6 +121,8 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      slower)
 //   sweep_soa=0|1      (A/B build) mpiv_plane_sweep[_into]'s depth-per-lane kernel stages its box as
 //                      float4 texels (0 = default) or as channel planes (1: measured 4-7 % slower)
+//   render_same=-1|0|1  render_rows_kernel's same-row tap reuse (render.hip SAME): off / automatic
+//                      (where the sample advances <= 0.8 texel rows per output row; R = 6 then) / on
 //   bwd_margin=k       the tile gather's pixel-window margin in 1/64 pixel (default 16);
 //                      negative values make windows miss contributors, which the pair
 //                      count must catch (tests)
@@ -131,14 +133,15 @@ enum DebugOpt { kOptRenderMv, kOptRenderPair, kOptNativeLds, kOptSweepTile, kOpt
                 kOptRenderVshare, kOptChunkRows, kOptSweepRows, kOptChunkFlight, kOptBwdGather, kOptSweepDirect,
                 kOptBwdPollLimit, kOptBwdFbBlocks, kOptBwdFbMode, kOptChunkStrip, kOptU8Flight, kOptBwdGroup,
                 kOptNetoutGeo, kOptNetoutBuf, kOptBwdOverlap, kOptSweepBand, kOptSweepPf, kOptSweepSoa, kOptBwdUnfold,
-                kOptNetoutFg3, kNumOpts };
+                kOptNetoutFg3, kOptRenderSame, kNumOpts };
 const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_native_lds",
                                          "sweep_tile", "sweep_store", "box_shrink", "render_chunk", "render_ring",
                                          "render_tile", "bwd_fallback", "bwd_margin", "sweep_dlane",
                                          "render_vshare", "chunk_rows", "sweep_rows", "chunk_flight", "bwd_gather",
                                          "sweep_direct", "bwd_poll_limit", "bwd_fb_blocks", "bwd_fb_mode",
                                          "chunk_strip", "u8_flight", "bwd_group", "netout_geo", "netout_buf", "bwd_overlap", "sweep_band",
-                                         "sweep_pf", "sweep_soa", "bwd_unfold", "netout_fg3"};
+                                         "sweep_pf", "sweep_soa", "bwd_unfold", "netout_fg3",
+                                         "render_same"};
 #ifndef MPIV_CHUNK_STRIP
 #define MPIV_CHUNK_STRIP 1  // round 4: 0.506 vs 0.64 ms in place (profiles/r04j_strip*_ab.jsonl)
 #endif
@@ -146,9 +149,9 @@ const char* const kOptNames[kNumOpts] = {"render_mv", "render_pair", "render_nat
 #define MPIV_U8_FLIGHT 0
 #endif
 const int kOptDefaults[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP,
-                                    MPIV_U8_FLIGHT, 0, 0, 1, 0, 0, 0, 0, 0, 1};
+                                    MPIV_U8_FLIGHT, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0};
 int g_opts[kNumOpts] = {0, 0, 1, 0, -1, 0, 0, 0, 0, 0, 16, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, MPIV_CHUNK_STRIP, MPIV_U8_FLIGHT, 0,
-                        0, 1, 0, 0, 0, 0, 0, 1};
+                        0, 1, 0, 0, 0, 0, 0, 1, 0};
 
 int opt(DebugOpt o) { return __atomic_load_n(&g_opts[o], __ATOMIC_RELAXED); }
 
@@ -375,6 +378,14 @@ int mpiv_pack_planes(const float* mpi, const int64_t st[4], int H, int W, int P,
 }
 
 // variant 0: direct gathers (render_packed_kernel, the default); 1: LDS-staged footprints
+// Same-row tap reuse (render.hip SAME): automatic where the sample advances at most 0.8 texel rows
+// per output row (the reference's swapped y / (W-1) normalisation on landscape frames: configs 2, 5);
+// render_same=-1 turns it off, 1 forces it on.
+static bool rows_same(float syr) {
+    const int o = opt(kOptRenderSame);
+    return o > 0 || (o == 0 && syr <= 0.8f);
+}
+
 static int render_packed_impl(const float* packed, int H, int W, int P, int p_begin, int p_end, int back,
                               const float* homs, int V, float* out, bool ct, int variant, void* stream) {
     const char* nm = ct ? "mpiv_render_packed_ct" : "mpiv_render_packed";
@@ -476,7 +487,11 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     //  * stretched MPIs (the reference's swapped x/(H-1), y/(W-1) normalisation: footprints
     //    stretched by W/(H-1) and H/(W-1)) only when the tiles fill the chip (>= 2048 blocks of
     //    64x32): config 5's plane shard 0.80 vs 0.87 ms one-row; config 2 at one view (288
-    //    blocks) is latency-bound (0.079 vs 0.054 ms), so the one-row kernel keeps small launches.
+    //    blocks) is latency-bound (0.079 vs 0.054 ms), so the one-row kernel keeps small launches;
+    //  * round 6: where the sample advances <= 0.8 texel rows per output row (configs 2 and 5),
+    //    same-row tap reuse with R = 6, D = 3 at every view count (profiles/r06_same_ab*.jsonl:
+    //    config-5 shard 0.655-0.67 vs 0.77-0.78 ms, config 2 at 64 views 1.95-1.96 vs 2.05, at
+    //    8 views 0.253-0.256 vs 0.26-0.27).
     const float sxr = (float)W / (float)(H > 1 ? H - 1 : 1), syr = (float)H / (float)(W > 1 ? W - 1 : 1);
     const bool square = sxr >= 0.8f && sxr <= 1.25f && syr >= 0.8f && syr <= 1.25f;
     const int rows_opt = opt(kOptRenderTile);
@@ -512,35 +527,47 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
     if (fast && (vs_opt == 3 || vs_opt == 4 || vs_opt == 5 || vs_opt == 11))
         vsd = vs_opt;
     else if (fast && vs_opt == 0 && !rows_opt && rows_auto == 8)
-        vsd = V <= 2 ? 11 : V <= 8 ? 3 : square ? 4 : 5;
+        vsd = rows_same(syr) ? 4 : V <= 2 ? 11 : V <= 8 ? 3 : square ? 4 : 5;
     if (vsd) {
         const int R = vsd == 3 ? 8 : vsd == 4 ? 6 : vsd == 5 ? 9 : 4;
         const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(H, 4 * R) * V;
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
+        // same-row tap reuse (round 6) where the sample advances less than a texel row per output row
+        const bool same = rows_same(syr);
         // the counting build (mpiv_render_packed_census) exists for the automatic choices
         if (g_route)
-            return note_route(nb, 256, "render_rows_kernel<%s, %d, true, false, %d>", ct ? "true" : "false", R,
-                              vsd == 3 || vsd == 11 ? 4 : 3);
+            return note_route(nb, 256, same ? "render_rows_kernel<%s, %d, true, false, %d, true>"
+                                            : "render_rows_kernel<%s, %d, true, false, %d>",
+                              ct ? "true" : "false", R, vsd == 3 || vsd == 11 ? 4 : 3);
         unsigned long long* cn = (g_census && !ct) ? g_census : nullptr;
         if (cn) g_census = nullptr;
-#define MPIV_VSD(R, D)                                                                                              \
-    if (ct)                                                                                                        \
-        render_rows_kernel<true, R, true, false, D><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end,    \
-                                                                                   back, homs, out);               \
-    else                                                                                                           \
-        render_rows_kernel<false, R, true, false, D><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, \
-                                                                                    homs, out)
-#define MPIV_VSDC(R, D)                                                                                                \
-    if (cn)                                                                                                           \
-        render_rows_kernel<false, R, true, true, D><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, homs, \
-                                                                                  out, cn);                           \
-    else                                                                                                              \
-        MPIV_VSD(R, D)
-        switch (vsd) {
-            case 3: MPIV_VSDC(8, 4); break;
-            case 4: MPIV_VSDC(6, 3); break;
-            case 5: MPIV_VSDC(9, 3); break;
-            default: MPIV_VSDC(4, 4); break;
+#define MPIV_VSD(R, D, SM)                                                                                            \
+    if (ct)                                                                                                          \
+        render_rows_kernel<true, R, true, false, D, SM><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end,  \
+                                                                                       back, homs, out);             \
+    else                                                                                                             \
+        render_rows_kernel<false, R, true, false, D, SM><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, \
+                                                                                        1, homs, out)
+#define MPIV_VSDC(R, D, SM)                                                                                           \
+    if (cn)                                                                                                          \
+        render_rows_kernel<false, R, true, true, D, SM><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, \
+                                                                                      homs, out, cn);                \
+    else                                                                                                             \
+        MPIV_VSD(R, D, SM)
+        if (same) {
+            switch (vsd) {
+                case 3: MPIV_VSDC(8, 4, true); break;
+                case 4: MPIV_VSDC(6, 3, true); break;
+                case 5: MPIV_VSDC(9, 3, true); break;
+                default: MPIV_VSDC(4, 4, true); break;
+            }
+        } else {
+            switch (vsd) {
+                case 3: MPIV_VSDC(8, 4, false); break;
+                case 4: MPIV_VSDC(6, 3, false); break;
+                case 5: MPIV_VSDC(9, 3, false); break;
+                default: MPIV_VSDC(4, 4, false); break;
+            }
         }
 #undef MPIV_VSDC
 #undef MPIV_VSD
@@ -647,19 +674,32 @@ int mpiv_render_packed_ct_rows(const float* packed, int H, int W, int P, int p_b
     const RenderGeom g = make_geom(H, W, P);
     const float sxr = (float)W / (float)(H - 1), syr = (float)H / (float)(W - 1);
     const bool square = sxr >= 0.8f && sxr <= 1.25f && syr >= 0.8f && syr <= 1.25f;
-    const int R = V <= 2 ? 4 : V <= 8 ? 8 : square ? 6 : 9;
+    const bool same = rows_same(syr);
+    const int R = same ? 6 : V <= 2 ? 4 : V <= 8 ? 8 : square ? 6 : 9;
     const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(y_end - y_begin, 4 * R) * V;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
-    if (g_route) return note_route(nb, 256, "render_rows_kernel<true, %d, true, false, %d>", R, R <= 8 ? 4 : 3);
+    if (g_route)
+        return note_route(nb, 256, same ? "render_rows_kernel<true, %d, true, false, %d, true>"
+                                        : "render_rows_kernel<true, %d, true, false, %d>", R,
+                          R == 4 || R == 8 ? 4 : 3);
     hipStream_t st = S(stream);
-#define MPIV_CTR(RR, DD)                                                                                            \
-    render_rows_kernel<true, RR, true, false, DD><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, \
-                                                                                homs, ct, nullptr, y_begin, y_end)
-    switch (R) {
-        case 4: MPIV_CTR(4, 4); break;
-        case 8: MPIV_CTR(8, 4); break;
-        case 6: MPIV_CTR(6, 3); break;
-        default: MPIV_CTR(9, 3); break;
+#define MPIV_CTR(RR, DD, SM)                                                                                           \
+    render_rows_kernel<true, RR, true, false, DD, SM><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, \
+                                                                                    homs, ct, nullptr, y_begin, y_end)
+    if (same) {
+        switch (R) {
+            case 4: MPIV_CTR(4, 4, true); break;
+            case 8: MPIV_CTR(8, 4, true); break;
+            case 6: MPIV_CTR(6, 3, true); break;
+            default: MPIV_CTR(9, 3, true); break;
+        }
+    } else {
+        switch (R) {
+            case 4: MPIV_CTR(4, 4, false); break;
+            case 8: MPIV_CTR(8, 4, false); break;
+            case 6: MPIV_CTR(6, 3, false); break;
+            default: MPIV_CTR(9, 3, false); break;
+        }
     }
 #undef MPIV_CTR
     return launched(nm);

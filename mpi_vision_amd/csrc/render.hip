@@ -322,19 +322,28 @@ __device__ __forceinline__ void render_rows_pixels(const float4* __restrict__ pl
 // that continue get the buffer's zero range there and take the previous row's south taps).
 // The texture path charges per wave instruction, so its work drops from 4 to ~2.5 gathers per
 // sample on a camera path; the result is bit-identical.
-template <bool CT, bool GUARD, int R, int D = 2>
+// SAME (round 6, stretched MPIs): the reference's swapped normalisation advances the sample by
+// H/(W-1) texel rows per output row -- 0.53 for config 5, 0.56 for config 2 -- so about every other
+// row's tap origin does not move at all: then all four of its taps ARE the previous row's (the same
+// memory words).  Per row and wave the south pair is gathered as before and the north pair only when
+// some lane neither stayed nor moved one row down (a lane that stayed keeps the previous row's north
+// taps): 2 gathers per row instead of 4 on most rows of a stretched frame.
+template <bool CT, bool GUARD, int R, int D = 2, bool SAME = false>
 __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__ planes, int64_t plane_stride,
                                                       const RenderGeom& g, int p_begin, int p_end, int back,
                                                       const float* __restrict__ hv, int x, int y0,
                                                       float* cr, float* cg, float* cb, float* tt,
                                                       unsigned& nvm) {
     static_assert(D != 2 || R % 2 == 0, "R must be even");
+    static_assert(!SAME || D > 2, "same-row reuse is built on the ring of rows in flight");
     struct RowTaps {
         f32x4 a, b, c, d;  // NW, NE (own, when not shared), SW, SE
         float nw, ne, sw, se;
         int off;           // byte offset of the NW tap in the padded plane
         bool sh;           // NW, NE = the previous row's SW, SE
         bool own;          // wave-uniform: some lane gathered its own north taps
+        bool same;         // SAME: all four taps = the previous row's (the origin did not move)
+        bool any_same;     // SAME, wave-uniform: some lane's origin did not move
     };
     const float fx = (float)x;
     const bool replace_first = !CT || back;
@@ -360,6 +369,21 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
         const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes);
         t.c = llvm_raw_buffer_load_v4f32(r, off, g.row, 0);
         t.d = llvm_raw_buffer_load_v4f32(r, off + 16, g.row, 0);
+        if constexpr (SAME) {
+            // the south pair stays unconditional: a wave that could skip every load of a row makes
+            // the compiler's load counting drain the whole ring before each consume (measured 30%
+            // slower); a lane whose origin stayed re-reads the previous row's south words (cached)
+            t.same = can_share && off == prev_off;
+            t.any_same = __builtin_amdgcn_ballot_w64(t.same) != 0;
+            const bool need_n = !(t.sh || t.same);
+            t.own = __builtin_amdgcn_ballot_w64(need_n) != 0;
+            nvm += t.own ? 4u : 2u;
+            if (t.own) {
+                t.a = llvm_raw_buffer_load_v4f32(r, need_n ? off : kOOB, 0, 0);
+                t.b = llvm_raw_buffer_load_v4f32(r, (need_n ? off : kOOB - 16) + 16, 0, 0);
+            }
+            return;
+        }
 #ifndef MPIV_VS_ZINIT
 #define MPIV_VS_ZINIT 0
 #endif
@@ -373,6 +397,37 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
             t.a = llvm_raw_buffer_load_v4f32(r, t.sh ? kOOB : off, 0, 0);
             t.b = llvm_raw_buffer_load_v4f32(r, (t.sh ? kOOB - 16 : off) + 16, 0, 0);
         }
+    };
+    // SAME: the previous row's effective taps (pa, pb, pc, pd) in, this row's out
+    auto consume_same = [&](const RowTaps& t, f32x4& pa, f32x4& pb, f32x4& pc, f32x4& pd, int k, bool first) {
+        f32x4 na = pc, nb = pd;  // every lane moved one row down: vertical reuse
+        const f32x4 sc_ = t.c, sd_ = t.d;
+        if (t.own || t.any_same) {
+            asm volatile("");  // keep the per-lane selects behind this wave-uniform branch
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                na[c] = t.same ? pa[c] : (t.sh ? pc[c] : t.a[c]);
+                nb[c] = t.same ? pb[c] : (t.sh ? pd[c] : t.b[c]);
+            }
+        }
+        f32x4 s;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {  // blend_taps' fma chain
+            float acc = na[c] * t.nw;
+            acc = __builtin_fmaf(nb[c], t.ne, acc);
+            acc = __builtin_fmaf(sc_[c], t.sw, acc);
+            acc = __builtin_fmaf(sd_[c], t.se, acc);
+            s[c] = acc;
+        }
+        const float a = first ? 1.0f : s[3];
+        const float om = 1.0f - a;
+        cr[k] = over(s[0], a, om, cr[k]);
+        cg[k] = over(s[1], a, om, cg[k]);
+        cb[k] = over(s[2], a, om, cb[k]);
+        if (CT) tt[k] = tt[k] * om;
+        asm volatile("" : "+v"(cr[k]), "+v"(cg[k]), "+v"(cb[k]));
+        if (CT) asm volatile("" : "+v"(tt[k]));
+        pa = na; pb = nb; pc = sc_; pd = sd_;
     };
     auto consume = [&](const RowTaps& t, const f32x4& pc, const f32x4& pd, int k, bool first) {
         f32x4 s;
@@ -411,6 +466,7 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
         if (CT) asm volatile("" : "+v"(tt[k]));
     };
     f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sd = sc;  // the previous row's south taps
+    [[maybe_unused]] f32x4 sa = sc, sb = sc;   // SAME: ... and north taps
     Hom9 h = hom(p_begin), hn = hom(p_begin + 1);
     if constexpr (D != 2) {  // D rows in flight (a ring of D tap sets; A/B)
         static_assert(R % D == 0 && D > 2, "ring depth must divide R");
@@ -431,9 +487,13 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
                     issue(p + 1, kk - R, hn, T[(kk - 1) % D].off, true, T[kk % D]);
                 asm volatile("" ::: "memory");
                 __builtin_amdgcn_sched_barrier(0);
-                consume(T[k % D], sc, sd, k, first);
-                sc = T[k % D].c;
-                sd = T[k % D].d;
+                if constexpr (SAME) {
+                    consume_same(T[k % D], sa, sb, sc, sd, k, first);
+                } else {
+                    consume(T[k % D], sc, sd, k, first);
+                    sc = T[k % D].c;
+                    sd = T[k % D].d;
+                }
             }
             h = hn;
             hn = hom(p + 2);
@@ -571,8 +631,10 @@ __global__ __launch_bounds__(256) void render_rows_lds_kernel(const float4* __re
 // instructions its waves issue (the texture path's real work, for bench.py's roofline).
 // Rows [y_lo, y_hi) of the frame (the whole frame by default; a row band of a plane-shard
 // partial, mpiv_render_packed_ct_rows: the tiles start at y_lo, rows from y_hi on are not stored).
-template <bool CT, int R, bool VS = false, bool COUNT = false, int D = 2>
-__global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restrict__ planes, int64_t plane_stride,
+// SAME with R = 6 (the automatic stretched choice) is held to 128 VGPRs, four waves per SIMD: the
+// (C, T) flavour needs 129 otherwise (config-5 shard 0.655 vs 0.667 ms; the other R spill there)
+template <bool CT, int R, bool VS = false, bool COUNT = false, int D = 2, bool SAME = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAME && R == 6 ? 4 : 1))) void render_rows_kernel(const float4* __restrict__ planes, int64_t plane_stride,
                                                           RenderGeom g, int V, int p_begin, int p_end, int back,
                                                           const float* __restrict__ homs, float* __restrict__ out,
                                                           unsigned long long* __restrict__ census = nullptr,
@@ -615,8 +677,8 @@ __global__ __launch_bounds__(256) void render_rows_kernel(const float4* __restri
     }
     unsigned nvm = 0;
     if constexpr (VS)
-        render_rows_vs_pixels<CT, false, R, D>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb,
-                                               tt, nvm);
+        render_rows_vs_pixels<CT, false, R, D, SAME>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg,
+                                                     cb, tt, nvm);
     else  // 4 gathers per issue: R per plane plus the first
         render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
     if (!VS) nvm = 4u * (unsigned)(R * (p_end - p_begin) + 1);

@@ -239,3 +239,36 @@ def test_fused_net_output_training_equals_two_step_at_config2_size(dev):
     torch.cuda.synchronize()
     assert_bits(p1.grad.cpu().numpy(), p2.grad.cpu().numpy(), "d pred fused vs two-step")
     assert_bits(r1.grad.cpu().numpy(), r2.grad.cpu().numpy(), "d ref_img fused vs two-step")
+
+
+def test_fused_net_output_training_strided_and_partial_grads(dev):
+    """Training through the fused render with a channel-strided network output (a slice of a wider
+    tensor, as a network head's output view can be) and a B = 3 batch of different MPIs: d pred and
+    d ref_img equal the two-step chain's bit for bit; a second backward through a new graph reuses nothing
+    stale."""
+    gen = torch.Generator().manual_seed(77)
+    B, H, W, P = 3, 29, 45, 11
+    wide = (torch.rand((B, 2 * P + 3 + 5, H, W), generator=gen) * 2 - 1).to(dev)
+    ref0 = (torch.rand((B, H, W, 3), generator=gen) * 2 - 1).to(dev)
+    dout = (torch.rand((B, H, W, 3), generator=gen) * 2 - 1).to(dev)
+    f = configs.focal_from_fov(W)
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * B).to(dev)
+    poses = configs.f32([configs.pose_from(configs.rot_y(2.0 * (i - 1)), (0.04 * i, -0.02, 0.05)) for i in range(B)]).to(dev)
+    planes = configs.f32(mv.inv_depths(1, 60, P)).to(dev)
+    grads = []
+    for fused in (True, False):
+        w = wide.clone().requires_grad_(True)
+        pred = w[:, 3:3 + 2 * P + 3]
+        assert not pred.is_contiguous()
+        ref = ref0.clone().requires_grad_(True)
+        if fused:
+            out = mv.mpi_render_net_output_torch(pred, ref, poses, planes, K)
+        else:
+            dep = {"mpi_planes": torch.zeros((B, P), device=dev), "ref_img": ref}
+            out = mv.mpi_render_view_torch(mv.mpi_from_net_output(pred, dep), poses, planes, K)
+        out.backward(dout)
+        torch.cuda.synchronize()
+        grads.append((w.grad.cpu().numpy(), ref.grad.cpu().numpy(), out.detach().cpu().numpy()))
+    assert_bits(grads[0][2], grads[1][2], "frames")
+    assert_bits(grads[0][0], grads[1][0], "d network output (strided slice)")
+    assert_bits(grads[0][1], grads[1][1], "d ref_img")

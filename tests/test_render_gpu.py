@@ -257,7 +257,9 @@ def _variant_env(kopts, mv):
     kernel with tile geometry k (render_ring.hip); "tile<R>": R rows per work-item
     (render_rows_kernel), "tile8vs": with vertical tap sharing."""
     if mv.startswith("vsd"):  # vertical reuse, (R, rows in flight) = (8, 4) / (6, 3) / (9, 3) / (4, 4)
-        kopts(render_vshare=int(mv[3:]))
+        # suffix "s": same-row tap reuse forced on (square frames too), "n": off (stretched frames too)
+        same = {"s": 1, "n": -1}.get(mv[-1], 0)
+        kopts(render_vshare=int(mv[3:].rstrip("sn")), render_same=same)
         return
     kopts(render_mv=1 if mv == "1" else 0, render_pair={"pair": 1, "pair1": 2}.get(mv, 0),
           render_ring=int(mv[4:]) if mv.startswith("ring") else -1,
@@ -266,6 +268,7 @@ def _variant_env(kopts, mv):
 
 
 RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile8vs", "vsd3", "vsd4", "vsd5", "vsd11",
+        "vsd3s", "vsd4s", "vsd5s", "vsd11s", "vsd4n", "vsd5n",
         "tile16",
         "tile108", "tile116", "tile132"]
 
@@ -483,3 +486,31 @@ def test_default_routing_stretched_many_views(dev):
     want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.numpy())
     got = _lib.render_packed(_lib.pack_planes(mpi[0].to(dev)), homs)
     assert_bits(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("V", [1, 8, 64])
+def test_same_row_reuse_census_and_frames(V, dev, kopts):
+    """Same-row tap reuse (render.hip SAME) on a config-2-shaped stretched frame (the sample advances
+    ~0.55 texel rows per output row): the default route's frames equal the oracle's and the frames
+    without it (render_same=-1) bit for bit, and its counting build issues fewer gathers."""
+    from mpi_vision_amd import _host
+    H, W, P = 72, 128, 6
+    mpi = configs.synthetic_mpi(1, H, W, P, 31)
+    f = configs.focal_from_fov(W)
+    poses = configs.f32(configs.sway_path(1000)[200:200 + V])
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * V)
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(1, 100, P)), K, V).to(dev)
+    packed = _lib.pack_planes(mpi[0].to(dev))
+    want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.cpu().numpy())
+    counts = {}
+    for same in (0, -1):
+        kopts(render_vshare=4, render_same=same)
+        assert_bits(_lib.render_packed(packed, homs).cpu().numpy(), want, f"render_same={same}")
+        out = torch.empty((V, H, W, 3), device=dev)
+        census = torch.zeros(1, dtype=torch.int64, device=dev)
+        _lib._call("mpiv_render_packed_census", packed, H, W, P, homs, V, out, census, _lib._stream(dev))
+        torch.cuda.synchronize()
+        assert_bits(out.cpu().numpy(), want, f"census build, render_same={same}")
+        counts[same] = int(census.item())
+    waves = V * (W // 64) * (H // 6)
+    assert waves * 2 * 6 * P <= counts[0] < counts[-1] <= waves * 4 * (6 * P + 3)

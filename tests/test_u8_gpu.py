@@ -214,3 +214,17 @@ def test_u8_float_copy_follows_out_refills_streams_and_frees(dev, large):
     del f1, f2, f3, pk
     assert dev not in _lib._U8_FLOAT
     _lib.clear_u8_float_copies()
+
+
+@pytest.mark.gpu
+def test_clear_u8_float_copies(dev):
+    """The public release of the memoised float copies: per device and all devices."""
+    u8 = _test_mpi_u8().to(dev)
+    pk = _lib.pack_planes_u8(u8[0])
+    _lib.u8_float_copy(pk)
+    assert dev in _lib._U8_FLOAT
+    _lib.clear_u8_float_copies(dev)
+    assert dev not in _lib._U8_FLOAT
+    _lib.u8_float_copy(pk)
+    _lib.clear_u8_float_copies()
+    assert not _lib._U8_FLOAT

@@ -460,6 +460,62 @@ def dflt(dev, it):
     run("c4 render backward with checkpoints, 1 view", DEF, fn, 2 * P * H * W * 16 + H * W * 12, it)
 
 
+def same(dev, it):
+    """Round 6: same-row tap reuse (render.hip SAME) on the stretched configs -- config 2 at 64 and 8
+    views, config 5's plane shard (C, T) -- against the vertical reuse alone (render_same=-1), at the
+    automatic (R, D) and the other shipped ones; frames compared bit for bit first."""
+    c = configs.config2()
+    H, W, P = c["H"], c["W"], c["P"]
+    g = torch.Generator(device=dev).manual_seed(0)
+    view = torch.rand((H, W, P, 4), generator=g, device=dev)
+    packed = _lib.pack_planes(view)
+    del view
+    V2 = len(c["poses"])
+    homs_all = _host.render_homographies(configs.f32(c["poses"]), configs.f32(c["depths"]),
+                                         configs.f32([c["K"]] * V2), V2).to(dev)
+    for V in (V2, 8):
+        homs = homs_all[:V].contiguous()
+        out = torch.empty((V, H, W, 3), device=dev)
+        fn = lambda: _lib._call("mpiv_render_packed", packed, H, W, P, homs, V, out, _lib._stream(dev))  # noqa: E731
+        vs = [("off", {"render_same": -1}), ("same", {})]
+        for r in (3, 4, 5, 11):
+            vs += [(f"off_vs{r}", {"render_same": -1, "render_vshare": r}), (f"same_vs{r}", {"render_vshare": r})]
+        frames = []
+        for label, opts in vs:
+            with _lib.debug(**opts):
+                out.zero_()
+                fn()
+                frames.append(out.clone())
+        print(json.dumps({"exp": f"same bit identity, c2 {V} views", "same": [bool(torch.equal(
+            f.view(torch.int32), frames[0].view(torch.int32))) for f in frames]}), flush=True)
+        del frames
+        run(f"c2 packed render, {V} views", vs, fn, V * (P * H * W * 16 + H * W * 12), it)
+        del out
+    del packed
+    c5c = configs.config5()
+    H, W, P = c5c["H"], c5c["W"], c5c["P"]
+    PL = P // 8
+    packed = torch.zeros(_lib.packed_shape(H, W, PL), device=dev)
+    packed[:, 2:2 + H, 2:2 + W].uniform_(generator=g)
+    homs = _host.render_homographies(configs.f32(c5c["poses"]), configs.f32(c5c["depths"]), configs.f32([c5c["K"]]),
+                                     1)[:, :PL].contiguous().to(dev)
+    ct = torch.empty((1, H, W, 4), device=dev)
+    fn = lambda: _lib.render_packed_ct(packed, homs, back=True, out=ct)  # noqa: E731
+    vs = [("off", {"render_same": -1}), ("same", {}), ("off_vs3", {"render_same": -1, "render_vshare": 3}),
+          ("same_vs3", {"render_vshare": 3}), ("off_vs4", {"render_same": -1, "render_vshare": 4}),
+          ("same_vs4", {"render_vshare": 4})]
+    frames = []
+    for label, opts in vs:
+        with _lib.debug(**opts):
+            ct.zero_()
+            fn()
+            frames.append(ct.clone())
+    print(json.dumps({"exp": "same bit identity, c5 shard", "same": [bool(torch.equal(
+        f.view(torch.int32), frames[0].view(torch.int32))) for f in frames]}), flush=True)
+    del frames
+    run(f"c5 plane shard {PL} of {P}, (C,T)", vs, fn, PL * H * W * 16 + H * W * 16, it)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
