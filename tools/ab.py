@@ -516,6 +516,57 @@ def same(dev, it):
     run(f"c5 plane shard {PL} of {P}, (C,T)", vs, fn, PL * H * W * 16 + H * W * 16, it)
 
 
+def same4(dev, it):
+    """Round 6: same-row tap reuse forced on (render_same=1) for the square config 4 (the camera path's
+    zoom makes some rows stay on their texel row): 125 and 1 views, gathers counted by the census build."""
+    c = configs.config4()
+    H, W, P = c["H"], c["W"], c["P"]
+    g = torch.Generator(device=dev).manual_seed(0)
+    view = torch.rand((H, W, P, 4), generator=g, device=dev)
+    packed = _lib.pack_planes(view)
+    del view
+    for V in (125, 1):
+        homs = _host.render_homographies(configs.f32(c["poses"][:V]), configs.f32(c["depths"]),
+                                         configs.f32([c["K"]] * V), V).to(dev)
+        out = torch.empty((V, H, W, 3), device=dev)
+        vs = [("auto", {}), ("same", {"render_same": 1})]
+        frames, counts = [], []
+        for label, opts in vs:
+            with _lib.debug(**opts):
+                census = torch.zeros(1, dtype=torch.int64, device=dev)
+                _lib._call("mpiv_render_packed_census", packed, H, W, P, homs, V, out, census, _lib._stream(dev))
+                torch.cuda.synchronize()
+                frames.append(out.clone())
+                counts.append(int(census.item()))
+        print(json.dumps({"exp": f"same4 census, c4 {V} views", "gathers": counts,
+                          "per_sample": [round(n / (V * H * W * P / 64), 4) for n in counts],
+                          "same": bool(torch.equal(frames[0].view(torch.int32), frames[1].view(torch.int32)))}),
+              flush=True)
+        del frames
+        fn = lambda: _lib._call("mpiv_render_packed", packed, H, W, P, homs, V, out, _lib._stream(dev))  # noqa: E731
+        run(f"c4 packed render, {V} views", vs, fn, V * (P * H * W * 16 + H * W * 12), max(3, it // (1 + V // 8)))
+        del out
+
+
+def same1(dev, it):
+    """Round 6: config 2 at one view per launch (288 tiles of 64 x 32: the one-row kernel by default)
+    against the same-row reuse kernel forced (render_vshare=4), and the u8 / ct variants' inputs."""
+    c = configs.config2()
+    H, W, P = c["H"], c["W"], c["P"]
+    g = torch.Generator(device=dev).manual_seed(0)
+    view = torch.rand((H, W, P, 4), generator=g, device=dev)
+    packed = _lib.pack_planes(view)
+    del view
+    for k in (0, 5, 20):
+        homs = _host.render_homographies(configs.f32(c["poses"][k:k + 1]), configs.f32(c["depths"]),
+                                         configs.f32([c["K"]]), 1).to(dev)
+        out = torch.empty((1, H, W, 3), device=dev)
+        fn = lambda: _lib._call("mpiv_render_packed", packed, H, W, P, homs, 1, out, _lib._stream(dev))  # noqa: E731
+        vs = [("one_row", {}), ("r6d3_same", {"render_vshare": 4}), ("r4d4_same", {"render_vshare": 11}),
+              ("r4d4", {"render_vshare": 11, "render_same": -1})]
+        run(f"c2 packed render, 1 view, pose {k}", vs, fn, P * H * W * 16 + H * W * 12, it)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
