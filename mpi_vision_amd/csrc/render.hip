@@ -124,6 +124,64 @@ __device__ __forceinline__ bool div2_rect_safe(const float* __restrict__ h, floa
     return ok && (pos || neg);
 }
 
+// True when every sample of the tile [x0, x1] x [y0, y1] (integer pixel coordinates) reads only
+// the packed plane's zero border: floor(px) >= W or <= -2 for every pixel (the clamped taps are
+// border columns W, W+1 or -2, -1), or the same in y -- with finite positions, so the bilinear
+// weights are finite and the sample is exactly +0.  Valid where div2_rect_safe holds for the
+// same rectangle.  The bounds are exact: u, v, w are monotone chains whose values over the
+// rectangle lie between their corner extremes (div2_rect_safe); with w of one sign, RN(u / w)
+// takes its extremes among the four (u, w) extreme pairs (the kernels' fast division equals it
+// wherever the quotient can move a position, mpiv_common.hpp div2_rn); div_const, to_grid and
+// unnormalize are monotone.  One texel of margin on top.
+// Round 6: the reference's swapped normalisation (utils.py:186-188) maps output column x to
+// texel column ~x*W/(H-1), so on a landscape MPI every column past ~H samples the border alone:
+// 44 % of a config-2 frame (1024 x 576), 47 % of config 5's (4096 x 2160).
+__device__ __forceinline__ bool tile_dead(const float* __restrict__ h, float x0, float x1, float y0, float y1,
+                                          const RenderGeom& g) {
+    float u0 = __builtin_inff(), u1 = -__builtin_inff(), v0 = u0, v1 = u1, w0 = u0, w1 = u1;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float fx = (c & 1) ? x1 : x0, fy = (c & 2) ? y1 : y0;
+        const float u = __builtin_fmaf(h[1], fy, h[0] * fx) + h[2];
+        const float v = __builtin_fmaf(h[4], fy, h[3] * fx) + h[5];
+        const float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
+        u0 = fminf(u0, u); u1 = fmaxf(u1, u);
+        v0 = fminf(v0, v); v1 = fmaxf(v1, v);
+        w0 = fminf(w0, w); w1 = fmaxf(w1, w);
+    }
+    float qu0 = __builtin_inff(), qu1 = -__builtin_inff(), qv0 = qu0, qv1 = qu1;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float w = (c & 2) ? w1 : w0;
+        const float qu = div_rn((c & 1) ? u1 : u0, w), qv = div_rn((c & 1) ? v1 : v0, w);
+        qu0 = fminf(qu0, qu); qu1 = fmaxf(qu1, qu);
+        qv0 = fminf(qv0, qv); qv1 = fmaxf(qv1, qv);
+    }
+    const float px0 = unnormalize(to_grid(div_const(qu0, g.hm1, g.rc_hm1)), g.half_w);
+    const float px1 = unnormalize(to_grid(div_const(qu1, g.hm1, g.rc_hm1)), g.half_w);
+    const float py0 = unnormalize(to_grid(div_const(qv0, g.wm1, g.rc_wm1)), g.half_h);
+    const float py1 = unnormalize(to_grid(div_const(qv1, g.wm1, g.rc_wm1)), g.half_h);
+    const float big = 0x1p100f;  // finite (|x| < inf, NaN fails) with room to spare
+    const bool finite = __builtin_fabsf(px0) < big && __builtin_fabsf(px1) < big && __builtin_fabsf(py0) < big &&
+                        __builtin_fabsf(py1) < big;
+    return finite && (px0 >= (float)(g.W + 1) || px1 < -2.0f || py0 >= (float)(g.H + 1) || py1 < -2.0f);
+}
+
+// A dead tile's pixel (tile_dead): the per-plane over-composite of zero samples, the sampling
+// kernels' own update with s = (+0, +0, +0, +0) -- no positions, no gathers.
+template <bool CT>
+__device__ __forceinline__ void composite_zero(int p_begin, int p_end, bool replace_first, float& cr, float& cg,
+                                               float& cb, float& t) {
+    for (int p = p_begin; p < p_end; ++p) {
+        const float a = (replace_first && p == p_begin) ? 1.0f : 0.0f;
+        const float om = 1.0f - a;
+        cr = over(0.0f, a, om, cr);
+        cg = over(0.0f, a, om, cg);
+        cb = over(0.0f, a, om, cb);
+        if (CT) t = t * om;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // packed plane-major layout
 // ---------------------------------------------------------------------------
@@ -234,18 +292,35 @@ __global__ __launch_bounds__(256) void render_packed_kernel(const float4* __rest
     const int y = ty0 + (threadIdx.x >> 6);
     const float* hv = homs + (int64_t)v * g.P * 9;
     // block prologue: prove the fast division for the tile, all planes at once
-    bool proven = false;
+    bool proven = false, dead = false;
     if (FAST) {
         const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
         const float y0 = (float)ty0, y1 = (float)min(ty0 + kTileY - 1, g.H - 1);
-        bool ok = true;
-        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256)
-            ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, y0, y1);
+        bool ok = true, dd = true;
+        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256) {
+            const float* hp = hv + (int64_t)p * 9;
+            const bool safe = div2_rect_safe(hp, x0, x1, y0, y1);
+            ok = ok && safe;
+            dd = dd && safe && tile_dead(hp, x0, x1, y0, y1, g);
+        }
         proven = __syncthreads_and(ok);
+        dead = __syncthreads_and(dd);
     }
     if (x >= g.W || y >= g.H) return;
     const int64_t o = ((int64_t)v * g.H + y) * g.W + x;
     float* out_px = CT ? out + o * 4 : out + o * 3;
+    if (dead) {  // every plane samples the zero border over the whole tile
+        float cr = -0.0f, cg = -0.0f, cb = -0.0f, t = 1.0f;
+        composite_zero<CT>(p_begin, p_end, !CT || back, cr, cg, cb, t);
+        if (CT) {
+            *reinterpret_cast<float4*>(out_px) = make_float4(cr, cg, cb, t);
+        } else {
+            out_px[0] = cr;
+            out_px[1] = cg;
+            out_px[2] = cb;
+        }
+        return;
+    }
     if (!FAST)
         render_packed_pixel<CT, 0>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y, out_px);
     else if (proven)
@@ -649,21 +724,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAME && R =
     const int x = tx0 + (int)(threadIdx.x & (kWave - 1));
     const int y0 = ty0 + (int)(threadIdx.x >> 6) * R;
     const float* hv = homs + (int64_t)v * g.P * 9;
-    bool ok = true;
+    bool ok = true, dd = true;
     {
         const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
         const float fy0 = (float)ty0, fy1 = (float)min(ty0 + TY - 1, g.H - 1);
-        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256)
-            ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, fy0, fy1);
+        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256) {
+            const float* hp = hv + (int64_t)p * 9;
+            const bool safe = div2_rect_safe(hp, x0, x1, fy0, fy1);
+            ok = ok && safe;
+            dd = dd && safe && tile_dead(hp, x0, x1, fy0, fy1, g);
+        }
     }
     const bool proven = __syncthreads_and(ok);
+    const bool dead = __syncthreads_and(dd);
     if (x >= g.W || y0 >= y_hi) return;  // rows past y_hi inside [y0, y0+R) are computed, not stored
     float cr[R], cg[R], cb[R], tt[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         cr[k] = -0.0f; cg[k] = -0.0f; cb[k] = -0.0f; tt[k] = 1.0f;  // render_packed_pixel: plane 0 replaces
     }
-    if (!proven) {  // rare (w near 0 over the tile): the guarded one-pixel recipe, row by row
+    if (dead) {  // every plane samples the zero border over the whole tile: no positions, no gathers
+        composite_zero<CT>(p_begin, p_end, !CT || back, cr[0], cg[0], cb[0], tt[0]);
+#pragma unroll
+        for (int k = 1; k < R; ++k) {
+            cr[k] = cr[0]; cg[k] = cg[0]; cb[k] = cb[0]; tt[k] = tt[0];
+        }
+    } else if (!proven) {  // rare (w near 0 over the tile): the guarded one-pixel recipe, row by row
         int rows = 0;
         for (int k = 0; k < R && y0 + k < y_hi; ++k, ++rows) {
             const int64_t o = ((int64_t)v * g.H + y0 + k) * g.W + x;
@@ -675,14 +761,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAME && R =
             atomicAdd(census, (unsigned long long)rows * 4ull * (unsigned long long)(p_end - p_begin + 1));
         return;
     }
-    unsigned nvm = 0;
-    if constexpr (VS)
-        render_rows_vs_pixels<CT, false, R, D, SAME>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg,
-                                                     cb, tt, nvm);
-    else  // 4 gathers per issue: R per plane plus the first
-        render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
-    if (!VS) nvm = 4u * (unsigned)(R * (p_end - p_begin) + 1);
-    if (COUNT && (threadIdx.x & (kWave - 1)) == 0) atomicAdd(census, (unsigned long long)nvm);
+    if (!dead) {
+        unsigned nvm = 0;
+        if constexpr (VS)
+            render_rows_vs_pixels<CT, false, R, D, SAME>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr,
+                                                         cg, cb, tt, nvm);
+        else  // 4 gathers per issue: R per plane plus the first
+            render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);
+        if (!VS) nvm = 4u * (unsigned)(R * (p_end - p_begin) + 1);
+        if (COUNT && (threadIdx.x & (kWave - 1)) == 0) atomicAdd(census, (unsigned long long)nvm);
+    }
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const int y = y0 + k;

@@ -427,7 +427,7 @@ def test_gather_census(vs, dev, kopts):
     4 x (R*P + 1) gathers per wave, with it between 2 and 4 per plane-sample."""
     from mpi_vision_amd import _host
     kopts(render_tile=8, render_vshare=vs)
-    H, W, P, V = 64, 128, 12, 5
+    H, W, P, V = 128, 128, 12, 5  # square: no tile samples the border alone (tile_dead)
     mpi = configs.synthetic_mpi(1, H, W, P, 4)
     f = configs.focal_from_fov(W)
     poses = configs.f32(configs.sway_path(1000)[40:40 + V])
@@ -512,5 +512,41 @@ def test_same_row_reuse_census_and_frames(V, dev, kopts):
         torch.cuda.synchronize()
         assert_bits(out.cpu().numpy(), want, f"census build, render_same={same}")
         counts[same] = int(census.item())
+    # columns past ~H sample the zero border alone (tile_dead): those waves gather nothing
     waves = V * (W // 64) * (H // 6)
-    assert waves * 2 * 6 * P <= counts[0] < counts[-1] <= waves * 4 * (6 * P + 3)
+    assert 0 < counts[0] < counts[-1] <= waves * 4 * (6 * P + 3)
+
+
+@pytest.mark.parametrize("route", ["one_row", "rows"])
+def test_dead_tiles_bit_exact(route, dev, kopts):
+    """Tiles whose every sample reads the zero border (render.hip tile_dead: on a landscape MPI the
+    reference's swapped normalisation sends every column past ~H there) take the zero-sample
+    composite without positions or gathers: frames, (C, T) partials with and without the back plane
+    and row bands equal the oracle bit for bit (signed zeros included), and the counting build shows
+    the skipped gathers."""
+    from mpi_vision_amd import _host
+    if route == "rows":
+        kopts(render_vshare=4)
+    H, W, P, V = 54, 230, 9, 4
+    mpi = configs.synthetic_mpi(1, H, W, P, 41)
+    f = configs.focal_from_fov(W)
+    poses = [configs.pose_from(configs.rot_y(0.0), (0.0, 0.0, 0.0))]
+    poses += list(configs.sway_path(1000)[600:600 + V - 2])
+    poses.append(configs.pose_from(configs.rot_y(20.0), (0.4, -0.2, 0.3)))  # planes sweep across the edge
+    poses = configs.f32(poses)
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * V)
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(1, 100, P)), K, V)
+    full = mpi.expand(V, H, W, P, 4).numpy()
+    packed = _lib.pack_planes(mpi[0].to(dev))
+    assert_bits(_lib.render_packed(packed, homs).cpu().numpy(), oracle.render(full, homs.numpy()), "frames")
+    for a, b, back in ((0, 4, True), (4, P, False), (0, P, False)):
+        ct = _lib.render_packed_ct(packed, homs, back=back, p_begin=a, p_end=b)
+        assert_bits(ct.cpu().numpy(), oracle.render_ct(full, homs.numpy(), a, b, back=back), f"ct [{a},{b}) back={back}")
+    if route == "rows":
+        hd = homs.to(dev)
+        out = torch.empty((V, H, W, 3), device=dev)
+        census = torch.zeros(1, dtype=torch.int64, device=dev)
+        _lib._call("mpiv_render_packed_census", packed, H, W, P, hd, V, out, census, _lib._stream(dev))
+        torch.cuda.synchronize()
+        waves = V * ((W + 63) // 64) * ((H + 5) // 6)
+        assert int(census.item()) < waves * 2 * 6 * P  # fewer than every wave's minimum: whole tiles skipped
