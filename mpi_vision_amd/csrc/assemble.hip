@@ -412,7 +412,7 @@ __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __r
     __syncthreads();
     // ---- footprint boxes (thread q -> plane q/4, corner q%4) + the tile's division proof
     const int cx1 = min(tx0 + kNTX - 1, g.W - 1), cy1 = min(ty0 + kTY - 1, g.H - 1);
-    bool ok_div = true;
+    bool ok_div = true, dead = true;
     for (int q0 = 0; q0 < 4 * P; q0 += kThreads) {
         const int q = q0 + (int)threadIdx.x;
         const bool live = q < 4 * P;
@@ -420,7 +420,11 @@ __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __r
         const int corner = q & 3;
         const float fx = (float)((corner & 1) ? cx1 : tx0), fy = (float)((corner & 2) ? cy1 : ty0);
         const float* h = hv + (int64_t)pl * 9;
-        if (live && corner == 0) ok_div = ok_div && div2_rect_safe(h, (float)tx0, (float)cx1, (float)ty0, (float)cy1);
+        if (live && corner == 0) {
+            const bool safe = div2_rect_safe(h, (float)tx0, (float)cx1, (float)ty0, (float)cy1);
+            ok_div = ok_div && safe;
+            dead = dead && safe && tile_dead(h, (float)tx0, (float)cx1, (float)ty0, (float)cy1, g);
+        }
         float px, py;
         render_pos<true>(h, fx, fy, g, px, py);
         float w = __builtin_fmaf(h[7], fy, h[6] * fx) + h[8];
@@ -449,6 +453,24 @@ __global__ __launch_bounds__(64 * NW) void render_netout_kernel(const float* __r
         }
     }
     const bool proven = __syncthreads_and(ok_div);
+    if (__syncthreads_and(dead)) {  // every plane samples the zero border over the whole tile (render.hip tile_dead)
+        for (int r = 0; r < RPT; ++r) {
+            const int y = ty0 + wave + NW * r;
+            if (x >= g.W || y >= g.H) continue;
+            float cr = -0.0f, cg = -0.0f, cb = -0.0f, t = 1.0f;
+            for (int p = 0; p < P; ++p) {
+                composite_zero<false>(p, p + 1, p == 0, cr, cg, cb, t);
+                if (ckpt && (p & 7) == 7 && p + 1 < P)
+                    ckpt[(((int64_t)v * ((P + 7) >> 3) + ((p + 1) >> 3)) * g.H + y) * g.W + x] =
+                        make_float4(cr, cg, cb, 0.0f);
+            }
+            const int64_t o = (((int64_t)v * g.H + y) * g.W + x) * 3;
+            out[o + 0] = cr;
+            out[o + 1] = cg;
+            out[o + 2] = cb;
+        }
+        return;
+    }
     const int pitch = s_pitch;
     auto box_of = [&](int i) {
         const int2 bb = s_box[i];

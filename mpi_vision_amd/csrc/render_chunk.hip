@@ -466,9 +466,15 @@ __global__ __launch_bounds__(256, 3) void render_chunk_strip_kernel(const float*
     const float* hs = h_lds ? hl : hv;
     const float x0 = (float)tx0, x1 = (float)min(tx0 + kStripTX - 1, g.W - 1);
     const float y0 = (float)ty0, y1 = (float)min(ty0 + SR - 1, g.H - 1);
-    bool ok = true;
-    for (int p = (int)threadIdx.x; p < g.P; p += 256) ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, y0, y1);
+    bool ok = true, dd = true;
+    for (int p = (int)threadIdx.x; p < g.P; p += 256) {
+        const float* hp = hv + (int64_t)p * 9;
+        const bool safe = div2_rect_safe(hp, x0, x1, y0, y1);
+        ok = ok && safe;
+        dd = dd && safe && tile_dead(hp, x0, x1, y0, y1, g);
+    }
     const bool proven = __syncthreads_and(ok);  // also publishes hs
+    const bool dead = __syncthreads_and(dd);
     const int sx0 = tx0 + wave * 8;
     if (sx0 >= g.W) return;  // whole wave; no barrier follows
     const float* view = mpi + (int64_t)v * view_stride;
@@ -482,7 +488,18 @@ __global__ __launch_bounds__(256, 3) void render_chunk_strip_kernel(const float*
 #pragma unroll
     for (int hh = 0; hh < SR / 8; ++hh) cr[hh] = cgr[hh] = cb[hh] = -0.0f;
     const int nhk = min(SR / 8, (g.H - y + 7) / 8);  // halves of this lane inside the frame
-    if (proven)
+    if (dead) {  // every tap of every plane is outside the image (render.hip tile_dead): zero samples
+        float r0 = -0.0f, g0 = -0.0f, b0 = -0.0f, t0 = 1.0f;
+        for (int c = 0; c * 8 < g.P; ++c) {
+            if (ck && c > 0)
+                for (int hh = 0; hh < nhk; ++hh) ck[c * HW + hh * 8 * (int64_t)g.W] = make_float4(r0, g0, b0, 0.0f);
+            composite_zero<false>(c * 8, min(c * 8 + 8, g.P), c == 0, r0, g0, b0, t0);
+        }
+#pragma unroll
+        for (int hh = 0; hh < SR / 8; ++hh) {
+            cr[hh] = r0; cgr[hh] = g0; cb[hh] = b0;
+        }
+    } else if (proven)
         render_chunk_wave_strip<false, SR, NT>(view, g, cg, hs, slot, sx0, ty0, lane, cr, cgr, cb, ck, HW,
                                                8 * (int64_t)g.W, nhk);
     else
