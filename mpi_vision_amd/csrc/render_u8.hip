@@ -303,21 +303,32 @@ __global__ __launch_bounds__(256) void render_u8_kernel(const unsigned* __restri
     const int x = tx0 + (int)(threadIdx.x & (kWave - 1));
     const int y0 = ty0 + (int)(threadIdx.x >> 6) * R;
     const float* hv = homs + (int64_t)v * g.P * 9;
-    bool ok = true;
+    bool ok = true, dd = true;
     {
         const float x0 = (float)tx0, x1 = (float)min(tx0 + kTileX - 1, g.W - 1);
         const float fy0 = (float)ty0, fy1 = (float)min(ty0 + TY - 1, g.H - 1);
-        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256)
-            ok = ok && div2_rect_safe(hv + (int64_t)p * 9, x0, x1, fy0, fy1);
+        for (int p = p_begin + (int)threadIdx.x; p < p_end; p += 256) {
+            const float* hp = hv + (int64_t)p * 9;
+            const bool safe = div2_rect_safe(hp, x0, x1, fy0, fy1);
+            ok = ok && safe;
+            dd = dd && safe && tile_dead(hp, x0, x1, fy0, fy1, g);
+        }
     }
     const bool proven = __syncthreads_and(ok);
+    const bool dead = __syncthreads_and(dd);
     if (x >= g.W || y0 >= g.H) return;  // rows past H inside [y0, y0+R) are computed, not stored
     float cr[R], cg[R], cb[R], tt[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         cr[k] = -0.0f; cg[k] = -0.0f; cb[k] = -0.0f; tt[k] = 1.0f;  // render_packed_pixel: plane 0 replaces
     }
-    if (proven) {
+    if (dead) {  // every plane samples the zero border over the whole tile (render.hip tile_dead)
+        composite_zero<CT>(p_begin, p_end, !CT || back, cr[0], cg[0], cb[0], tt[0]);
+#pragma unroll
+        for (int k = 1; k < R; ++k) {
+            cr[k] = cr[0]; cg[k] = cg[0]; cb[k] = cb[0]; tt[k] = tt[0];
+        }
+    } else if (proven) {
         if constexpr (VS)
             render_u8_vs_pixels<CT, false, R, D>(planes, plane_stride, g, ug, p_begin, p_end, back, hv, x, y0, cr, cg,
                                                  cb, tt);

@@ -567,6 +567,49 @@ def same1(dev, it):
         run(f"c2 packed render, 1 view, pose {k}", vs, fn, P * H * W * 16 + H * W * 12, it)
 
 
+def libs(dev, it):
+    """Default routes of the bench legs, for A/B across library builds (MPIV_LIB): config 4 packed at
+    1 and 125 views, u8 single view, in-place single view, the fused net-output view, config 5's shard."""
+    c = configs.config4()
+    H, W, P = c["H"], c["W"], c["P"]
+    mpi, homs1, _, _, _ = c4_mpi(dev)
+    packed = _lib.pack_planes(mpi[0])
+    out1 = torch.empty((1, H, W, 3), device=dev)
+    per_view = P * H * W * 16 + H * W * 12
+    run("c4 packed 1 view", DEF, lambda: _lib.render_packed(packed, homs1, out1), per_view, it)
+    run("c4 in-place 1 view", DEF, lambda: _lib._call("mpiv_render", mpi, _lib._strides(mpi), 1, H, W, P, homs1, out1,
+                                                      _lib._stream(dev)), per_view, it)
+    homs = _host.render_homographies(configs.f32(c["poses"][:125]), configs.f32(c["depths"]),
+                                     configs.f32([c["K"]] * 125), 125).to(dev)
+    out = torch.empty((125, H, W, 3), device=dev)
+    run("c4 packed 125 views", DEF, lambda: _lib.render_packed(packed, homs, out), 125 * per_view, 3)
+    del out, mpi
+    pk8 = _lib.synth_mpi_packed_u8(c["seed"], H, W, 0, P, dev)
+    run("u8 c4 1 view", DEF, lambda: _lib._call("mpiv_render_packed_u8", pk8, H, W, P, homs1, 1, out1,
+                                                _lib._stream(dev)), P * H * W * 4 + H * W * 12, it)
+    del pk8, packed
+    c2 = configs.config2()
+    H, W, P = c2["H"], c2["W"], c2["P"]
+    g = torch.Generator(device=dev).manual_seed(c2["seed"])
+    pred = torch.rand((1, 2 * P + 3, H, W), generator=g, device=dev) * 2 - 1
+    fg = torch.rand((1, H, W, 3), generator=g, device=dev) * 2 - 1
+    h2 = _host.render_homographies(configs.f32(c2["poses"][5:6]), configs.f32(c2["depths"]), configs.f32([c2["K"]]),
+                                   1).to(dev)
+    o2 = torch.empty((1, H, W, 3), device=dev)
+    run("netout c2 1 view", DEF, lambda: _lib._call("mpiv_render_net_output", pred, _lib._strides(pred), fg,
+                                                    _lib._strides(fg), 1, H, W, P, h2, o2, _lib._stream(dev)),
+        H * W * ((2 * P + 3) * 4 + 24), it)
+    c5c = configs.config5()
+    H, W, P = c5c["H"], c5c["W"], c5c["P"]
+    PL = P // 8
+    pk = torch.zeros(_lib.packed_shape(H, W, PL), device=dev)
+    pk[:, 2:2 + H, 2:2 + W].uniform_(generator=g)
+    h5 = _host.render_homographies(configs.f32(c5c["poses"]), configs.f32(c5c["depths"]), configs.f32([c5c["K"]]),
+                                   1)[:, :PL].contiguous().to(dev)
+    ct = torch.empty((1, H, W, 4), device=dev)
+    run("c5 shard", DEF, lambda: _lib.render_packed_ct(pk, h5, back=True, out=ct), PL * H * W * 16 + H * W * 16, it)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
