@@ -675,6 +675,10 @@ def notebook_leg(dev, stream, n=50):
         mv.mpi_render_view_torch(leaf, poses, planes, Kb).backward(dout)
         eager_grad = leaf.grad.clone()
         leaf.grad = None
+        # the leaf's AccumulateGrad node dates from the eager steps on the bench stream; the capture's
+        # warm-up runs on a side stream, which PyTorch reports as a stream mismatch (expected here)
+        if hasattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch"):
+            torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
         gfn = torch.cuda.make_graphed_callables(_RenderStep(), (leaf,))
 
         def gstep():
