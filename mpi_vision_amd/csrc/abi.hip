@@ -537,7 +537,7 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
         // the counting build (mpiv_render_packed_census) exists for the automatic choices
         if (g_route)
             return note_route(nb, 256, same ? "render_rows_kernel<%s, %d, true, false, %d, true>"
-                                            : "render_rows_kernel<%s, %d, true, false, %d>",
+                                            : "render_rows_kernel<%s, %d, true, false, %d, false>",
                               ct ? "true" : "false", R, vsd == 3 || vsd == 11 ? 4 : 3);
         unsigned long long* cn = (g_census && !ct) ? g_census : nullptr;
         if (cn) g_census = nullptr;
@@ -680,7 +680,7 @@ int mpiv_render_packed_ct_rows(const float* packed, int H, int W, int P, int p_b
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     if (g_route)
         return note_route(nb, 256, same ? "render_rows_kernel<true, %d, true, false, %d, true>"
-                                        : "render_rows_kernel<true, %d, true, false, %d>", R,
+                                        : "render_rows_kernel<true, %d, true, false, %d, false>", R,
                           R == 4 || R == 8 ? 4 : 3);
     hipStream_t st = S(stream);
 #define MPIV_CTR(RR, DD, SM)                                                                                           \
