@@ -552,17 +552,41 @@ __global__ __launch_bounds__(256, 1) void bwd_chain_strip_kernel(const float* __
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     if (h_lds)
         for (int k = threadIdx.x; k < g.P * 9; k += 256) hl[k] = homs[k];
-    bool ok = true;
+    bool ok = true, dd = true;
     {
         const float x0 = (float)tx0, x1 = (float)min(tx0 + kStripTX - 1, g.W - 1);
         const float y0 = (float)ty0, y1 = (float)min(ty0 + SR - 1, g.H - 1);
         const int p_end = min(g.P, c_hi * kBwdCH);  // the group's planes (the rows issued past it are unused)
-        for (int p = c_lo * kBwdCH + (int)threadIdx.x; p < p_end; p += 256)
-            ok = ok && div2_rect_safe(homs + (int64_t)p * 9, x0, x1, y0, y1);
+        for (int p = c_lo * kBwdCH + (int)threadIdx.x; p < p_end; p += 256) {
+            const float* hp = homs + (int64_t)p * 9;
+            const bool safe = div2_rect_safe(hp, x0, x1, y0, y1);
+            ok = ok && safe;
+            dd = dd && safe && tile_dead(hp, x0, x1, y0, y1, g);
+        }
     }
     const bool proven = __syncthreads_and(ok);  // also publishes hs
+    const bool dead = __syncthreads_and(dd);
     const int sx0 = tx0 + wave * 8;
     if (sx0 >= g.W) return;  // whole wave; no barrier follows
+    if (dead) {
+        // Round 6: no sample of the tile has an in-image tap in the group's planes (render.hip
+        // tile_dead).  Its d samples are never read -- the gather and the fallback sum the contributors
+        // of real texels only -- its pair count is 0, and g crosses every plane unchanged (sample +0:
+        // a = +0, g * 1 = g); only the hand-over to the group below remains, and where g came from
+        // gbuf (c_hi < n) it is already there.
+        const int n = (g.P + kBwdCH - 1) / kBwdCH;
+        if (c_lo > 0 && c_hi == n) {
+            const int x = sx0 + (lane & 7), y = ty0 + (lane >> 3);
+#pragma unroll
+            for (int hh = 0; hh < SR / 8; ++hh) {
+                if (x < g.W && y + 8 * hh < g.H) {
+                    const int64_t q = (int64_t)(y + 8 * hh) * g.W + x;
+                    gbuf[q] = make_float4(dout[q * 3 + 0], dout[q * 3 + 1], dout[q * 3 + 2], 0.0f);
+                }
+            }
+        }
+        return;
+    }
     f32x4* slot = slots + wave * kWave * (kBwdCH + 1);
     if (proven)
         bwd_chain_wave_strip<2, SR>(view, g, cg, hs, slot, sx0, ty0, lane, dout, ck, ws, c_lo, c_hi, gbuf);
