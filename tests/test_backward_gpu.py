@@ -537,3 +537,31 @@ def test_training_step_captured_in_a_hip_graph(grad, dev):
         torch.cuda.synchronize()
         assert_bits(leaf.grad, grad["ga_grad"], "graphed training step")
         assert_bits(out.detach(), grad["ga_out"], "graphed forward")
+
+
+@pytest.mark.parametrize("group", [0, 8])
+def test_backward_dead_tiles_vs_oracle(group, dev, bwd_mode, kopts):
+    """Tiles whose samples all fall outside the image (render_bwd.hip bwd_chain_strip_kernel, round 6:
+    on a landscape MPI the swapped normalisation sends every column past ~H there) skip the chain;
+    with a pose whose planes sweep across the frame edge a tile can be dead for one plane group and
+    live for another (the running adjoint handed down unchanged): bit-exact vs the oracle in every
+    backward mode, one group and groups of 8 planes, with and without the forward's checkpoints."""
+    H, W, P = 54, 230, 20
+    mpi = configs.synthetic_mpi(1, H, W, P, 43)
+    f = configs.focal_from_fov(W)
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)])
+    planes = configs.f32(configs.inv_depths(0.5, 60, P))
+    dout = torch.rand((1, H, W, 3), generator=torch.Generator().manual_seed(47)) * 2 - 1
+    if group:
+        kopts(bwd_group=group)
+    for pose in (configs.pose_from(configs.rot_y(0.0), (0.0, 0.0, 0.0)),
+                 configs.pose_from(configs.rot_y(14.0), (0.35, -0.1, 0.2))):
+        pose = configs.f32([pose])
+        homs = _host.render_homographies(pose, planes, K, 1)
+        want = oracle.render_backward(mpi.numpy(), homs.numpy(), dout.numpy())
+        got, _ = _backward_flag(mpi.to(dev), homs, dout.to(dev), dev)  # no checkpoints
+        assert_bits(got, want, "no checkpoints")
+        leaf = mpi.to(dev).requires_grad_(True)
+        out = mv.mpi_render_view_torch(leaf, pose.to(dev), planes.to(dev), K.to(dev))
+        out.backward(dout.to(dev))
+        assert_bits(leaf.grad.cpu().numpy(), want, "forward checkpoints")
