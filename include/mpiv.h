@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MPIV_ABI_VERSION 13
+#define MPIV_ABI_VERSION 14
 
 enum {
     MPIV_OK = 0,
@@ -226,6 +226,15 @@ int mpiv_render_backward_status(const void *workspace, int H, int W, int P, int 
  * 16-B aligned. */
 int mpiv_assemble_mpi(const float *pred, const int64_t pred_strides[4], const float *fg,
                       const int64_t fg_strides[4], int B, int H, int W, int P, float *rgba, void *stream);
+
+/* mpiv_assemble_mpi for the backward of a render of the assembled MPI (the fused net-output
+ * training's re-assembly, round 6): homs [B][P][9] are that render's homographies; texel rows
+ * no output pixel's in-image taps can read (exact bounds of the sample positions over the
+ * frame, one row of margin; every row where they cannot be proven) are left UNWRITTEN.  Only
+ * for mpiv_render_backward of those homographies. */
+int mpiv_assemble_mpi_sampled(const float *pred, const int64_t pred_strides[4], const float *fg,
+                              const int64_t fg_strides[4], int B, int H, int W, int P, const float *homs,
+                              float *rgba, void *stream);
 
 /* The same for batch element b, written straight into the render's packed layout
  * (mpiv_pack_planes: [P][H+4][W+4][4] with a zero border): assembly + pack in one

@@ -71,6 +71,7 @@ _SIGS = {
                                      _vp],
     "mpiv_assemble_mpi": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
     "mpiv_assemble_mpi_packed": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp],
+    "mpiv_assemble_mpi_sampled": [_vp, _c_i64p, _vp, _c_i64p, _int, _int, _int, _int, _vp, _vp, _vp],
     "mpiv_render_homographies": [_vp, _vp, _vp, _vp, _int, _int, _vp],
     "mpiv_render_homographies_device": [_vp, _vp, _vp, _vp, _int, _int, _vp, _vp],
     "mpiv_psv_proj": [_vp, _i64, _vp, _int, _vp],
@@ -89,7 +90,7 @@ _SIGS = {
 EXPORTS = tuple(_SIGS) + ("mpiv_abi_version", "mpiv_last_error", "mpiv_render_backward_workspace_size",
                           "mpiv_render_backward_abort_flag",
                           "mpiv_render_backward_workspace_size_min", "mpiv_build_id", "mpiv_debug_set")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _lib = None
 _lib_ab = None
@@ -821,6 +822,17 @@ def assemble_mpi(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int) -> torch.Tens
     return out
 
 
+def assemble_mpi_sampled(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int, homs: torch.Tensor) -> torch.Tensor:
+    """assemble_mpi for the backward of a render with homs [B,P,9] only: texel rows no output pixel
+    of that render can sample are left unwritten (mpiv_assemble_mpi_sampled)."""
+    dev, B, H, W = _net_args(mpi_pred, fg, P)
+    h = _up(homs.reshape(B, P, 9), dev)
+    out = torch.empty((B, H, W, P, 4), device=dev, dtype=torch.float32)
+    _call("mpiv_assemble_mpi_sampled", mpi_pred, _strides(mpi_pred), fg, _strides(fg), B, H, W, P, h, out,
+          _stream(dev))
+    return out
+
+
 def assemble_mpi_packed(mpi_pred: torch.Tensor, fg: torch.Tensor, P: int, b: int,
                         out: torch.Tensor | None = None) -> torch.Tensor:
     """Batch element b of the assembled MPI, straight into the packed layout [P,H+4,W+4,4]."""
@@ -873,7 +885,8 @@ class NetOutputRenderFunction(torch.autograd.Function):
     L7-11 / L38-42: mpi_from_net_output then mpi_render_view_torch) that never keeps the
     [B,H,W,P,4] MPI between forward and backward.  Forward: render_netout_kernel with the
     composite checkpoints (saves pred, ref image, checkpoints: (2P+3+3)*4 + ceil(P/8)*16 B per pixel
-    instead of the MPI's P*16 + the checkpoints).  Backward: the MPI re-assembled (assemble.hip),
+    instead of the MPI's P*16 + the checkpoints).  Backward: the MPI re-assembled (assemble.hip; the
+    texel rows the render samples only, mpiv_assemble_mpi_sampled),
     render_backward with those checkpoints, the assembly adjoint -- the two-step chain's own
     kernels in its order, so d pred / d ref_img are bit-identical to it and to the reference's
     autograd (tests/golden/netout_train.npz)."""
@@ -892,7 +905,8 @@ class NetOutputRenderFunction(torch.autograd.Function):
         mpi_pred, fg, ckpt = ctx.saved_tensors
         if not (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]):
             return None, None, None, None
-        rgba = assemble_mpi(mpi_pred, fg, ctx.P)
+        # only the texel rows the render samples (round 6): the chain reads no other
+        rgba = assemble_mpi_sampled(mpi_pred, fg, ctx.P, ctx.homs)
         drgba = render_backward(rgba, ctx.homs, dout, ckpt=ckpt)
         del rgba  # the re-assembled MPI lives only for the chain
         res = assemble_mpi_backward(drgba, mpi_pred, fg, ctx.P, want_dfg=ctx.needs_input_grad[1])

@@ -1697,6 +1697,25 @@ int mpiv_assemble_mpi(const float* pred, const int64_t ps[4], const float* fg, c
     return launched("mpiv_assemble_mpi");
 }
 
+// mpiv_assemble_mpi for a render's backward only (round 6, the fused net-output training's
+// re-assembly): the texel rows no output pixel of the render of `homs` ([B][P][9], the render's
+// own) can sample are left unwritten -- the chain reads in-image taps only, inside those rows.
+int mpiv_assemble_mpi_sampled(const float* pred, const int64_t ps[4], const float* fg, const int64_t fs[4], int B,
+                              int H, int W, int P, const float* homs, float* rgba, void* stream) {
+    if (int rc = check_net("mpiv_assemble_mpi_sampled", pred, ps, fg, fs, B, H, W, P)) return rc;
+    if (!rgba || !aligned16(rgba) || !homs)
+        return fail(MPIV_ERR_ARG, "mpiv_assemble_mpi_sampled: rgba / homs null or rgba not 16-byte aligned");
+    if (blocks(P, kAsmPl) > kMaxGridYZ) return fail(MPIV_ERR_ARG, "mpiv_assemble_mpi_sampled: too many planes");
+    const NetStrides s{ps[0], ps[1], ps[2], ps[3], fs[0], fs[1], fs[2], fs[3]};
+    const dim3 grid(blocks((int64_t)H * W, kAsmPix), blocks(P, kAsmPl), B);
+    // the bounds use the render's fast position recipe (H, W >= 2); smaller frames assemble every row
+    const bool rows = H >= 2 && W >= 2;
+    assemble_native_kernel<<<grid, 256, 0, S(stream)>>>(pred, fg, s, H, W, P, make_fastdiv((unsigned)W),
+                                                        reinterpret_cast<float4*>(rgba), rows ? homs : nullptr,
+                                                        rows ? make_geom(H, W, P) : RenderGeom{});
+    return launched("mpiv_assemble_mpi_sampled");
+}
+
 int mpiv_assemble_mpi_packed(const float* pred, const int64_t ps[4], const float* fg, const int64_t fs[4], int b,
                              int H, int W, int P, float* packed, void* stream) {
     if (int rc = check_net("mpiv_assemble_mpi_packed", pred, ps, fg, fs, b + 1, H, W, P)) return rc;

@@ -55,14 +55,29 @@ __device__ __forceinline__ float4 assemble_texel(const float* __restrict__ pred,
 constexpr int kAsmPix = 64;
 constexpr int kAsmPl = 16;
 
+// homs (mpiv_assemble_mpi_sampled, round 6): the render's [B][P][9] homographies; a block whose
+// pixels lie outside every row its 16 planes' samples can read (render.hip sampled_rows, over the
+// whole frame) writes nothing -- those texels of out keep whatever they held.
 __global__ __launch_bounds__(256) void assemble_native_kernel(const float* __restrict__ pred,
                                                               const float* __restrict__ fg, NetStrides s, int H,
-                                                              int W, int P, FastDiv w_div, float4* __restrict__ out) {
+                                                              int W, int P, FastDiv w_div, float4* __restrict__ out,
+                                                              const float* __restrict__ homs = nullptr,
+                                                              RenderGeom g = RenderGeom{}) {
     __shared__ float4 tile[kAsmPl][kAsmPix + 1];
     const int64_t npix = (int64_t)H * W;
     const int64_t pix0 = (int64_t)blockIdx.x * kAsmPix;
     const int p0 = blockIdx.y * kAsmPl;
     const int b = blockIdx.z;
+    if (homs) {
+        const int ylo = (int)(pix0 / W), yhi = (int)(min(pix0 + kAsmPix, npix) - 1) / W;  // the block's rows
+        bool need = false;
+        if (threadIdx.x < kAsmPl && p0 + (int)threadIdx.x < P) {
+            const int2 r = sampled_rows(homs + ((int64_t)b * P + p0 + threadIdx.x) * 9, 0.0f, (float)(W - 1), 0.0f,
+                                        (float)(H - 1), g);
+            need = r.x <= yhi && r.y >= ylo;
+        }
+        if (!__syncthreads_or(need)) return;
+    }
     for (int k = threadIdx.x; k < kAsmPix * kAsmPl; k += blockDim.x) {  // pixel fastest
         const int i = k % kAsmPix, j = k / kAsmPix;
         const int64_t pix = pix0 + i;

@@ -136,8 +136,8 @@ __device__ __forceinline__ bool div2_rect_safe(const float* __restrict__ h, floa
 // Round 6: the reference's swapped normalisation (utils.py:186-188) maps output column x to
 // texel column ~x*W/(H-1), so on a landscape MPI every column past ~H samples the border alone:
 // 44 % of a config-2 frame (1024 x 576), 47 % of config 5's (4096 x 2160).
-__device__ __forceinline__ bool tile_dead(const float* __restrict__ h, float x0, float x1, float y0, float y1,
-                                          const RenderGeom& g) {
+__device__ __forceinline__ bool sample_bounds(const float* __restrict__ h, float x0, float x1, float y0, float y1,
+                                              const RenderGeom& g, float& px0, float& px1, float& py0, float& py1) {
     float u0 = __builtin_inff(), u1 = -__builtin_inff(), v0 = u0, v1 = u1, w0 = u0, w1 = u1;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -157,14 +157,34 @@ __device__ __forceinline__ bool tile_dead(const float* __restrict__ h, float x0,
         qu0 = fminf(qu0, qu); qu1 = fmaxf(qu1, qu);
         qv0 = fminf(qv0, qv); qv1 = fmaxf(qv1, qv);
     }
-    const float px0 = unnormalize(to_grid(div_const(qu0, g.hm1, g.rc_hm1)), g.half_w);
-    const float px1 = unnormalize(to_grid(div_const(qu1, g.hm1, g.rc_hm1)), g.half_w);
-    const float py0 = unnormalize(to_grid(div_const(qv0, g.wm1, g.rc_wm1)), g.half_h);
-    const float py1 = unnormalize(to_grid(div_const(qv1, g.wm1, g.rc_wm1)), g.half_h);
+    px0 = unnormalize(to_grid(div_const(qu0, g.hm1, g.rc_hm1)), g.half_w);
+    px1 = unnormalize(to_grid(div_const(qu1, g.hm1, g.rc_hm1)), g.half_w);
+    py0 = unnormalize(to_grid(div_const(qv0, g.wm1, g.rc_wm1)), g.half_h);
+    py1 = unnormalize(to_grid(div_const(qv1, g.wm1, g.rc_wm1)), g.half_h);
     const float big = 0x1p100f;  // finite (|x| < inf, NaN fails) with room to spare
-    const bool finite = __builtin_fabsf(px0) < big && __builtin_fabsf(px1) < big && __builtin_fabsf(py0) < big &&
-                        __builtin_fabsf(py1) < big;
+    return __builtin_fabsf(px0) < big && __builtin_fabsf(px1) < big && __builtin_fabsf(py0) < big &&
+           __builtin_fabsf(py1) < big;
+}
+
+__device__ __forceinline__ bool tile_dead(const float* __restrict__ h, float x0, float x1, float y0, float y1,
+                                          const RenderGeom& g) {
+    float px0, px1, py0, py1;
+    const bool finite = sample_bounds(h, x0, x1, y0, y1, g, px0, px1, py0, py1);
     return finite && (px0 >= (float)(g.W + 1) || px1 < -2.0f || py0 >= (float)(g.H + 1) || py1 < -2.0f);
+}
+
+// The texel rows [r0, r1] (r0 > r1: none) that the in-image taps of every output pixel of
+// [x0, x1] x [y0, y1] can read for this plane: floor(py) and floor(py) + 1 over sample_bounds'
+// exact range, one row of margin each side; the whole image where the division is not provable
+// or a bound is not finite.  (mpiv_assemble_mpi_sampled: the rows the fused backward's chain reads.)
+__device__ __forceinline__ int2 sampled_rows(const float* __restrict__ h, float x0, float x1, float y0, float y1,
+                                             const RenderGeom& g) {
+    float px0, px1, py0, py1;
+    if (!div2_rect_safe(h, x0, x1, y0, y1) || !sample_bounds(h, x0, x1, y0, y1, g, px0, px1, py0, py1))
+        return make_int2(0, g.H - 1);
+    if (px0 >= (float)(g.W + 1) || px1 < -2.0f || py0 >= (float)(g.H + 1) || py1 < -2.0f) return make_int2(0, -1);
+    const int r0 = (int)floorf(fmaxf(py0, -4.0f)) - 1, r1 = (int)floorf(fminf(py1, (float)(g.H + 4))) + 2;
+    return make_int2(max(r0, 0), min(r1, g.H - 1));
 }
 
 // A dead tile's pixel (tile_dead): the per-plane over-composite of zero samples, the sampling

@@ -272,3 +272,39 @@ def test_fused_net_output_training_strided_and_partial_grads(dev):
     assert_bits(grads[0][2], grads[1][2], "frames")
     assert_bits(grads[0][0], grads[1][0], "d network output (strided slice)")
     assert_bits(grads[0][1], grads[1][1], "d ref_img")
+
+
+@pytest.mark.parametrize("shape", [(54, 230, 12), (48, 80, 20), (72, 72, 9), (33, 47, 17)])
+def test_assemble_sampled_rows_cover_every_read(shape, dev):
+    """mpiv_assemble_mpi_sampled (the fused training's re-assembly, round 6) leaves the texel rows no
+    output pixel samples unwritten: with those rows NaN-filled, the render and its backward equal the
+    ones over the whole assembly bit for bit (a NaN read anywhere would show), the written texels equal
+    mpiv_assemble_mpi's, and on a landscape MPI (the swapped normalisation samples its top rows only)
+    texels are actually skipped.  Camera-path, rotated and extreme poses (planes behind the camera:
+    bounds not provable, every row written)."""
+    H, W, P = shape
+    g = torch.Generator().manual_seed(H * W + P)
+    pred = (torch.rand((3, 2 * P + 3, H, W), generator=g) * 2 - 1).to(dev)
+    fg = (torch.rand((3, H, W, 3), generator=g) * 2 - 1).to(dev)
+    f = configs.focal_from_fov(W)
+    K = configs.f32([configs.intrinsics_matrix(f, f, W / 2.0, H / 2.0)] * 3)
+    poses = configs.f32([configs.sway_path(1000)[250],
+                         configs.pose_from(configs.rot_y(11.0), (0.3, -0.15, 0.25)),
+                         configs.pose_from(configs.rot_y(-40.0), (1.5, 0.4, -2.0))])
+    homs = _host.render_homographies(poses, configs.f32(configs.inv_depths(0.5, 50, P)), K, 3).to(dev)
+    full = _lib.assemble_mpi(pred, fg, P)
+    part = torch.full_like(full, float("nan"))
+    _lib._call("mpiv_assemble_mpi_sampled", pred, _lib._strides(pred), fg, _lib._strides(fg), 3, H, W, P, homs, part,
+               _lib._stream(dev))
+    torch.cuda.synchronize()
+    written = ~torch.isnan(part).any(dim=-1)  # [B, H, W, P]: blocks of 64 pixels x 16 planes are skipped whole
+    assert torch.equal(part[written].view(torch.int32), full[written].view(torch.int32))
+    if W > H:
+        assert not bool(written[0].all()), "a landscape MPI's unsampled rows are skipped"
+    dout = (torch.rand((3, H, W, 3), generator=g) * 2 - 1).to(dev)
+    assert_bits(_lib.render(part, homs).cpu().numpy(), _lib.render(full, homs).cpu().numpy(), "render")
+    want = _lib.render_backward(full, homs, dout, check=True)
+    assert_bits(_lib.render_backward(part, homs, dout, check=True).cpu().numpy(), want.cpu().numpy(), "backward")
+    _, ck = _lib.render_train(full, homs)
+    assert_bits(_lib.render_backward(part, homs, dout, ckpt=ck, check=True).cpu().numpy(), want.cpu().numpy(),
+                "backward with checkpoints")
