@@ -599,6 +599,13 @@ def libs(dev, it):
     run("netout c2 1 view", DEF, lambda: _lib._call("mpiv_render_net_output", pred, _lib._strides(pred), fg,
                                                     _lib._strides(fg), 1, H, W, P, h2, o2, _lib._stream(dev)),
         H * W * ((2 * P + 3) * 4 + 24), it)
+    packed2 = _lib.pack_planes(torch.rand((H, W, P, 4), generator=g, device=dev))
+    V2 = len(c2["poses"])
+    h64 = _host.render_homographies(configs.f32(c2["poses"]), configs.f32(c2["depths"]), configs.f32([c2["K"]] * V2),
+                                    V2).to(dev)
+    o64 = torch.empty((V2, H, W, 3), device=dev)
+    run("c2 packed 64 views", DEF, lambda: _lib.render_packed(packed2, h64, o64), V2 * (P * H * W * 16 + H * W * 12), it)
+    del packed2, o64
     c5c = configs.config5()
     H, W, P = c5c["H"], c5c["W"], c5c["P"]
     PL = P // 8
