@@ -121,8 +121,9 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
 //                      slower)
 //   sweep_soa=0|1      (A/B build) mpiv_plane_sweep[_into]'s depth-per-lane kernel stages its box as
 //                      float4 texels (0 = default) or as channel planes (1: measured 4-7 % slower)
-//   render_same=-1|0|1  render_rows_kernel's same-row tap reuse (render.hip SAME): off / automatic
-//                      (where the sample advances <= 0.8 texel rows per output row; R = 6 then) / on
+//   render_same=-1|0|1|2  render_rows_kernel's same-row tap reuse (render.hip SAME): off / automatic
+//                      (where the sample advances <= 0.8 texel rows per output row; R = 6 then, with
+//                      OOB for launches of <= 2 views) / on / on with OOB
 //   bwd_margin=k       the tile gather's pixel-window margin in 1/64 pixel (default 16);
 //                      negative values make windows miss contributors, which the pair
 //                      count must catch (tests)
@@ -386,6 +387,13 @@ static bool rows_same(float syr) {
     return o > 0 || (o == 0 && syr <= 0.8f);
 }
 
+// ... and its out-of-range south loads on rows where every lane stayed (render.hip OOB): automatic
+// for launches of one or two views; render_same=2 forces them, 1 keeps the plain same-row kernel.
+static bool rows_same_oob(int V) {
+    const int o = opt(kOptRenderSame);
+    return o == 2 || (o == 0 && V <= 2);
+}
+
 static int render_packed_impl(const float* packed, int H, int W, int P, int p_begin, int p_end, int back,
                               const float* homs, int V, float* out, bool ct, int variant, void* stream) {
     const char* nm = ct ? "mpiv_render_packed_ct" : "mpiv_render_packed";
@@ -534,39 +542,41 @@ static int render_packed_impl(const float* packed, int H, int W, int P, int p_be
         if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
         // same-row tap reuse (round 6) where the sample advances less than a texel row per output row
         const bool same = rows_same(syr);
+        const bool oob = same && vsd == 4 && rows_same_oob(V);  // R = 6 only
         // the counting build (mpiv_render_packed_census) exists for the automatic choices
         if (g_route)
-            return note_route(nb, 256, same ? "render_rows_kernel<%s, %d, true, false, %d, true>"
-                                            : "render_rows_kernel<%s, %d, true, false, %d, false>",
-                              ct ? "true" : "false", R, vsd == 3 || vsd == 11 ? 4 : 3);
+            return note_route(nb, 256, "render_rows_kernel<%s, %d, true, false, %d, %s, %s>", ct ? "true" : "false", R,
+                              vsd == 3 || vsd == 11 ? 4 : 3, same ? "true" : "false", oob ? "true" : "false");
         unsigned long long* cn = (g_census && !ct) ? g_census : nullptr;
         if (cn) g_census = nullptr;
-#define MPIV_VSD(R, D, SM)                                                                                            \
+#define MPIV_VSD(R, D, SM, OB)                                                                                        \
     if (ct)                                                                                                          \
-        render_rows_kernel<true, R, true, false, D, SM><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end,  \
-                                                                                       back, homs, out);             \
+        render_rows_kernel<true, R, true, false, D, SM, OB><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin,     \
+                                                                                           p_end, back, homs, out);  \
     else                                                                                                             \
-        render_rows_kernel<false, R, true, false, D, SM><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, \
-                                                                                        1, homs, out)
-#define MPIV_VSDC(R, D, SM)                                                                                           \
+        render_rows_kernel<false, R, true, false, D, SM, OB><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin,    \
+                                                                                            p_end, 1, homs, out)
+#define MPIV_VSDC(R, D, SM, OB)                                                                                       \
     if (cn)                                                                                                          \
-        render_rows_kernel<false, R, true, true, D, SM><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, 1, \
-                                                                                      homs, out, cn);                \
+        render_rows_kernel<false, R, true, true, D, SM, OB><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin,     \
+                                                                                          p_end, 1, homs, out, cn);  \
     else                                                                                                             \
-        MPIV_VSD(R, D, SM)
-        if (same) {
+        MPIV_VSD(R, D, SM, OB)
+        if (oob) {
+            MPIV_VSDC(6, 3, true, true);
+        } else if (same) {
             switch (vsd) {
-                case 3: MPIV_VSDC(8, 4, true); break;
-                case 4: MPIV_VSDC(6, 3, true); break;
-                case 5: MPIV_VSDC(9, 3, true); break;
-                default: MPIV_VSDC(4, 4, true); break;
+                case 3: MPIV_VSDC(8, 4, true, false); break;
+                case 4: MPIV_VSDC(6, 3, true, false); break;
+                case 5: MPIV_VSDC(9, 3, true, false); break;
+                default: MPIV_VSDC(4, 4, true, false); break;
             }
         } else {
             switch (vsd) {
-                case 3: MPIV_VSDC(8, 4, false); break;
-                case 4: MPIV_VSDC(6, 3, false); break;
-                case 5: MPIV_VSDC(9, 3, false); break;
-                default: MPIV_VSDC(4, 4, false); break;
+                case 3: MPIV_VSDC(8, 4, false, false); break;
+                case 4: MPIV_VSDC(6, 3, false, false); break;
+                case 5: MPIV_VSDC(9, 3, false, false); break;
+                default: MPIV_VSDC(4, 4, false, false); break;
             }
         }
 #undef MPIV_VSDC
@@ -675,18 +685,21 @@ int mpiv_render_packed_ct_rows(const float* packed, int H, int W, int P, int p_b
     const float sxr = (float)W / (float)(H - 1), syr = (float)H / (float)(W - 1);
     const bool square = sxr >= 0.8f && sxr <= 1.25f && syr >= 0.8f && syr <= 1.25f;
     const bool same = rows_same(syr);
+    const bool oob = same && rows_same_oob(V);
     const int R = same ? 6 : V <= 2 ? 4 : V <= 8 ? 8 : square ? 6 : 9;
     const int64_t nb = (int64_t)blocks(W, kTileX) * blocks(y_end - y_begin, 4 * R) * V;
     if (nb > kMaxGridX) return fail(MPIV_ERR_ARG, "%s: too many blocks", nm);
     if (g_route)
-        return note_route(nb, 256, same ? "render_rows_kernel<true, %d, true, false, %d, true>"
-                                        : "render_rows_kernel<true, %d, true, false, %d, false>", R,
-                          R == 4 || R == 8 ? 4 : 3);
+        return note_route(nb, 256, "render_rows_kernel<true, %d, true, false, %d, %s, %s>", R, R == 4 || R == 8 ? 4 : 3,
+                          same ? "true" : "false", oob ? "true" : "false");
     hipStream_t st = S(stream);
 #define MPIV_CTR(RR, DD, SM)                                                                                           \
     render_rows_kernel<true, RR, true, false, DD, SM><<<(unsigned)nb, 256, 0, st>>>(pk, ps, g, V, p_begin, p_end, back, \
                                                                                     homs, ct, nullptr, y_begin, y_end)
-    if (same) {
+    if (oob) {
+        render_rows_kernel<true, 6, true, false, 3, true, true><<<(unsigned)nb, 256, 0, st>>>(
+            pk, ps, g, V, p_begin, p_end, back, homs, ct, nullptr, y_begin, y_end);
+    } else if (same) {
         switch (R) {
             case 4: MPIV_CTR(4, 4, true); break;
             case 8: MPIV_CTR(8, 4, true); break;

@@ -423,7 +423,7 @@ __device__ __forceinline__ void render_rows_pixels(const float4* __restrict__ pl
 // memory words).  Per row and wave the south pair is gathered as before and the north pair only when
 // some lane neither stayed nor moved one row down (a lane that stayed keeps the previous row's north
 // taps): 2 gathers per row instead of 4 on most rows of a stretched frame.
-template <bool CT, bool GUARD, int R, int D = 2, bool SAME = false>
+template <bool CT, bool GUARD, int R, int D = 2, bool SAME = false, bool OOB = false>
 __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__ planes, int64_t plane_stride,
                                                       const RenderGeom& g, int p_begin, int p_end, int back,
                                                       const float* __restrict__ hv, int x, int y0,
@@ -439,6 +439,7 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
         bool own;          // wave-uniform: some lane gathered its own north taps
         bool same;         // SAME: all four taps = the previous row's (the origin did not move)
         bool any_same;     // SAME, wave-uniform: some lane's origin did not move
+        bool all_same;     // SAME + OOB, wave-uniform: every lane's origin stayed
     };
     const float fx = (float)x;
     const bool replace_first = !CT || back;
@@ -462,14 +463,20 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
         t.off = off;
         t.sh = can_share && off == prev_off + g.row;
         const __amdgpu_buffer_rsrc_t r = make_rsrc(planes + (int64_t)q * plane_stride, g.plane_bytes);
-        t.c = llvm_raw_buffer_load_v4f32(r, off, g.row, 0);
-        t.d = llvm_raw_buffer_load_v4f32(r, off + 16, g.row, 0);
         if constexpr (SAME) {
             // the south pair stays unconditional: a wave that could skip every load of a row makes
             // the compiler's load counting drain the whole ring before each consume (measured 30%
-            // slower); a lane whose origin stayed re-reads the previous row's south words (cached)
+            // slower); a lane whose origin stayed re-reads the previous row's south words (cached).
+            // OOB: where every lane stayed, the pair goes to the buffer's out-of-range offset (no
+            // memory access, the same instruction count) and the row takes the previous row's taps
+            // whole -- one- and two-view launches (config 5's shard 0.57 -> 0.53 ms; with many views
+            // the extra live state costs the fourth wave per SIMD, profiles/r06_same_oob_ab/)
             t.same = can_share && off == prev_off;
             t.any_same = __builtin_amdgcn_ballot_w64(t.same) != 0;
+            t.all_same = OOB && __builtin_amdgcn_ballot_w64(!t.same) == 0;
+            const int soff = t.all_same ? kOOB - 16 : off;
+            t.c = llvm_raw_buffer_load_v4f32(r, soff, g.row, 0);
+            t.d = llvm_raw_buffer_load_v4f32(r, soff + 16, g.row, 0);
             const bool need_n = !(t.sh || t.same);
             t.own = __builtin_amdgcn_ballot_w64(need_n) != 0;
             nvm += t.own ? 4u : 2u;
@@ -479,6 +486,8 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
             }
             return;
         }
+        t.c = llvm_raw_buffer_load_v4f32(r, off, g.row, 0);
+        t.d = llvm_raw_buffer_load_v4f32(r, off + 16, g.row, 0);
 #ifndef MPIV_VS_ZINIT
 #define MPIV_VS_ZINIT 0
 #endif
@@ -496,8 +505,10 @@ __device__ __forceinline__ void render_rows_vs_pixels(const float4* __restrict__
     // SAME: the previous row's effective taps (pa, pb, pc, pd) in, this row's out
     auto consume_same = [&](const RowTaps& t, f32x4& pa, f32x4& pb, f32x4& pc, f32x4& pd, int k, bool first) {
         f32x4 na = pc, nb = pd;  // every lane moved one row down: vertical reuse
-        const f32x4 sc_ = t.c, sd_ = t.d;
-        if (t.own || t.any_same) {
+        f32x4 sc_ = t.c, sd_ = t.d;
+        if (OOB && t.all_same) {  // every lane stayed: the previous row's four taps
+            na = pa; nb = pb; sc_ = pc; sd_ = pd;
+        } else if (t.own || t.any_same) {
             asm volatile("");  // keep the per-lane selects behind this wave-uniform branch
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -727,9 +738,10 @@ __global__ __launch_bounds__(256) void render_rows_lds_kernel(const float4* __re
 // Rows [y_lo, y_hi) of the frame (the whole frame by default; a row band of a plane-shard
 // partial, mpiv_render_packed_ct_rows: the tiles start at y_lo, rows from y_hi on are not stored).
 // SAME with R = 6 (the automatic stretched choice) is held to 128 VGPRs, four waves per SIMD: the
-// (C, T) flavour needs 129 otherwise (config-5 shard 0.655 vs 0.667 ms; the other R spill there)
-template <bool CT, int R, bool VS = false, bool COUNT = false, int D = 2, bool SAME = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAME && R == 6 ? 4 : 1))) void render_rows_kernel(const float4* __restrict__ planes, int64_t plane_stride,
+// (C, T) flavour needs 129 otherwise (config-5 shard 0.655 vs 0.667 ms; the other R spill there);
+// with OOB (135-145 VGPRs) it keeps three
+template <bool CT, int R, bool VS = false, bool COUNT = false, int D = 2, bool SAME = false, bool OOB = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAME && R == 6 && !OOB ? 4 : 1))) void render_rows_kernel(const float4* __restrict__ planes, int64_t plane_stride,
                                                           RenderGeom g, int V, int p_begin, int p_end, int back,
                                                           const float* __restrict__ homs, float* __restrict__ out,
                                                           unsigned long long* __restrict__ census = nullptr,
@@ -784,7 +796,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SAME && R =
     if (!dead) {
         unsigned nvm = 0;
         if constexpr (VS)
-            render_rows_vs_pixels<CT, false, R, D, SAME>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr,
+            render_rows_vs_pixels<CT, false, R, D, SAME, OOB>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr,
                                                          cg, cb, tt, nvm);
         else  // 4 gathers per issue: R per plane plus the first
             render_rows_pixels<CT, false, R>(planes, plane_stride, g, p_begin, p_end, back, hv, x, y0, cr, cg, cb, tt);

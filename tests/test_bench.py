@@ -73,18 +73,19 @@ def test_host_cores_report():
 
 def test_route_dry_run_names_the_launched_kernels():
     """mpiv_route reports the production kernel and grid without a GPU (no launch)."""
-    assert _lib.route("render_packed", 1024, 1024, 128, 125) == ("render_rows_kernel<false, 6, true, false, 3, false>",
+    assert _lib.route("render_packed", 1024, 1024, 128, 125) == ("render_rows_kernel<false, 6, true, false, 3, false, false>",
                                                                  16 * 43 * 125 * 256)
-    assert _lib.route("render_packed", 1024, 1024, 128, 1)[0] == "render_rows_kernel<false, 4, true, false, 4, false>"
+    assert _lib.route("render_packed", 1024, 1024, 128, 1)[0] == "render_rows_kernel<false, 4, true, false, 4, false, false>"
     # stretched frames (the swapped normalisation advances <= 0.8 texel rows per output row): same-row
-    # tap reuse, R = 6, at every view count
-    assert _lib.route("render_packed", 576, 1024, 32, 64)[0] == "render_rows_kernel<false, 6, true, false, 3, true>"
-    assert _lib.route("render_packed", 576, 1024, 32, 8)[0] == "render_rows_kernel<false, 6, true, false, 3, true>"
-    assert _lib.route("render_packed_ct", 2160, 4096, 32, 1)[0] == "render_rows_kernel<true, 6, true, false, 3, true>"
+    # tap reuse, R = 6, at every view count; one- and two-view launches also skip the south loads of rows
+    # where every lane stayed (OOB)
+    assert _lib.route("render_packed", 576, 1024, 32, 64)[0] == "render_rows_kernel<false, 6, true, false, 3, true, false>"
+    assert _lib.route("render_packed", 576, 1024, 32, 8)[0] == "render_rows_kernel<false, 6, true, false, 3, true, false>"
+    assert _lib.route("render_packed_ct", 2160, 4096, 32, 1)[0] == "render_rows_kernel<true, 6, true, false, 3, true, true>"
     assert _lib.route("render_packed_ct_rows", 2160, 4096, 32, 1, 0, 270)[0] == \
-        "render_rows_kernel<true, 6, true, false, 3, true>"
+        "render_rows_kernel<true, 6, true, false, 3, true, true>"
     assert _lib.route("render_packed_ct_rows", 1024, 1024, 32, 125, 0, 128)[0] == \
-        "render_rows_kernel<true, 6, true, false, 3, false>"
+        "render_rows_kernel<true, 6, true, false, 3, false, false>"
     # a stretched MPI in a small launch keeps the one-row kernel
     assert _lib.route("render_packed", 576, 1024, 32, 1)[0] == "render_packed_kernel<false, true>"
     assert _lib.route("plane_sweep", 5, 768, 1024, 3, 64, 768, 1024) == ("plane_sweep_dlane_kernel<3, true, 4, 3072, 2, false>",

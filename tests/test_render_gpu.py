@@ -258,8 +258,8 @@ def _variant_env(kopts, mv):
     (render_rows_kernel), "tile8vs": with vertical tap sharing."""
     if mv.startswith("vsd"):  # vertical reuse, (R, rows in flight) = (8, 4) / (6, 3) / (9, 3) / (4, 4)
         # suffix "s": same-row tap reuse forced on (square frames too), "n": off (stretched frames too)
-        same = {"s": 1, "n": -1}.get(mv[-1], 0)
-        kopts(render_vshare=int(mv[3:].rstrip("sn")), render_same=same)
+        same = {"s": 1, "n": -1, "o": 2}.get(mv[-1], 0)  # "o": with the out-of-range south loads (OOB)
+        kopts(render_vshare=int(mv[3:].rstrip("sno")), render_same=same)
         return
     kopts(render_mv=1 if mv == "1" else 0, render_pair={"pair": 1, "pair1": 2}.get(mv, 0),
           render_ring=int(mv[4:]) if mv.startswith("ring") else -1,
@@ -268,7 +268,7 @@ def _variant_env(kopts, mv):
 
 
 RING = ["ring1", "ring2", "ring3", "ring4", "ring5", "ring6", "ring7", "ring8", "tile2", "tile4", "tile8", "tile8vs", "vsd3", "vsd4", "vsd5", "vsd11",
-        "vsd3s", "vsd4s", "vsd5s", "vsd11s", "vsd4n", "vsd5n",
+        "vsd3s", "vsd4s", "vsd5s", "vsd11s", "vsd4n", "vsd5n", "vsd4o",
         "tile16",
         "tile108", "tile116", "tile132"]
 
@@ -503,7 +503,7 @@ def test_same_row_reuse_census_and_frames(V, dev, kopts):
     packed = _lib.pack_planes(mpi[0].to(dev))
     want = oracle.render(mpi.expand(V, H, W, P, 4).numpy(), homs.cpu().numpy())
     counts = {}
-    for same in (0, -1):
+    for same in (2, 1, 0, -1):  # with OOB, without, automatic (OOB at one view), off
         kopts(render_vshare=4, render_same=same)
         assert_bits(_lib.render_packed(packed, homs).cpu().numpy(), want, f"render_same={same}")
         out = torch.empty((V, H, W, 3), device=dev)
@@ -514,7 +514,8 @@ def test_same_row_reuse_census_and_frames(V, dev, kopts):
         counts[same] = int(census.item())
     # columns past ~H sample the zero border alone (tile_dead): those waves gather nothing
     waves = V * (W // 64) * (H // 6)
-    assert 0 < counts[0] < counts[-1] <= waves * 4 * (6 * P + 3)
+    assert 0 < counts[1] < counts[-1] <= waves * 4 * (6 * P + 3)
+    assert counts[2] == counts[1] and counts[0] == counts[2 if V <= 2 else 1]  # OOB loads count as issued
 
 
 @pytest.mark.parametrize("route", ["one_row", "rows"])

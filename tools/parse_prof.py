@@ -36,8 +36,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short_name(full: str) -> str:
-    """'void mpiv::render_rows_kernel<false, 6, true, false, 3, false>(HIP_vector_type...)' ->
-    'render_rows_kernel<false, 6, true, false, 3, false>'."""
+    """'void mpiv::render_rows_kernel<false, 6, true, false, 3, false, false>(HIP_vector_type...)' ->
+    'render_rows_kernel<false, 6, true, false, 3, false, false>'."""
     s = full.strip()
     if s.startswith("void "):
         s = s[5:]
