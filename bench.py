@@ -796,6 +796,20 @@ def u8_leg(dev, stream, V, homs_sv, homs_v, n=10):
                         f"launch of {V} views", "single_view": sv, "multi_view": mv_}
 
 
+def netout_needed_bytes(homs: np.ndarray, H: int, W: int) -> int:
+    """Bytes the fused net-output render of one view needs: each plane's w / a channels over its
+    sampled texel box (sampled_boxes) x 8 B, bg / reference image over the planes' bounding box x 24 B,
+    the frame written."""
+    box = sampled_boxes(homs, H, W)[0]
+    area = np.clip(box[:, 1] - box[:, 0] + 1, 0, None) * np.clip(box[:, 3] - box[:, 2] + 1, 0, None)
+    live = area > 0
+    if live.any():
+        ub = (int(box[live, 0].min()), int(box[live, 1].max()), int(box[live, 2].min()), int(box[live, 3].max()))
+    else:
+        ub = (0, -1, 0, -1)
+    return int(area.sum()) * 8 + max(ub[1] - ub[0] + 1, 0) * max(ub[3] - ub[2] + 1, 0) * 24 + H * W * 12
+
+
 def netout_leg(dev, stream, n=20):
     """The network output rendered in one kernel (notebook mpi_from_net_output, ipynb cell 10
     L79-111, fused into mpi_render_view_torch: render_netout_kernel) at config 2's size
@@ -826,11 +840,7 @@ def netout_leg(dev, stream, n=20):
     # the bytes the reference's mapping samples (VERDICT r5 #5's measure, as for configs 2 and 5): each
     # plane's w / a over its sampled box (8 B per texel), bg / ref image over the planes' bounding box
     # (24 B per texel), the frame written
-    box = sampled_boxes(homs.cpu().numpy(), H, W)[0]
-    area = np.clip(box[:, 1] - box[:, 0] + 1, 0, None) * np.clip(box[:, 3] - box[:, 2] + 1, 0, None)
-    live = area > 0
-    ub = (box[live, 0].min(), box[live, 1].max(), box[live, 2].min(), box[live, 3].max()) if live.any() else (0, -1, 0, -1)
-    need = int(area.sum()) * 8 + max(ub[1] - ub[0] + 1, 0) * max(ub[3] - ub[2] + 1, 0) * 24 + H * W * 12
+    need = netout_needed_bytes(homs.cpu().numpy(), H, W)
     res.update({"needed_bytes": need, "needed_frac": hbm(need, ms)[1],
                 "needed_def": "w / a over each plane's sampled texel box (bench.sampled_boxes) x 8 B + bg / ref image "
                               "over the planes' bounding box x 24 B + the frame written"})

@@ -12,7 +12,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 import bench  # noqa: E402
-from mpi_vision_amd import _lib  # noqa: E402
+from mpi_vision_amd import _lib, configs  # noqa: E402
 
 
 def _parse(monkeypatch, *argv):
@@ -202,3 +202,16 @@ def test_sampled_boxes_cover_every_tap():
     need = bench.needed_bytes(homs, H, W)
     assert need <= V * (P * H * W * 16 + H * W * 12)
     assert bench.needed_bytes(homs, H, W, union=True) <= need
+
+
+def test_netout_needed_bytes_is_json_ready():
+    """The net-output leg's needed-bytes figure is a plain int (the bench line is json.dumps'd) and sits
+    between the frame alone and the formula's whole prediction."""
+    import json
+    from mpi_vision_amd import _host
+    c = configs.config2()
+    H, W, P = c["H"], c["W"], c["P"]
+    homs = _host.render_homographies(configs.f32(c["poses"][5:6]), configs.f32(c["depths"]), configs.f32([c["K"]]), 1)
+    need = bench.netout_needed_bytes(homs.numpy(), H, W)
+    assert type(need) is int and json.dumps({"n": need})
+    assert H * W * 12 < need < H * W * ((2 * P + 3) * 4 + 24)
