@@ -176,6 +176,15 @@ def barrier(world):
         dist.barrier()
 
 
+def _json_scalar(o):
+    """numpy scalars (and 0-d arrays) that reach the bench line serialise as Python numbers."""
+    if isinstance(o, np.generic):
+        return o.item()
+    if isinstance(o, np.ndarray) and o.ndim == 0:
+        return o.item()
+    raise TypeError(f"Object of type {type(o).__name__} is not JSON serializable")
+
+
 class LineGuard:
     """Rank 0's one JSON line, printed exactly once, even when a collective leg hangs.
 
@@ -201,7 +210,7 @@ class LineGuard:
             if self.rank != 0 or self.printed:
                 return False
             self.printed = True
-            self.out.write(json.dumps(res) + "\n")
+            self.out.write(json.dumps(res, default=_json_scalar) + "\n")
             self.out.flush()
             return True
 

@@ -215,3 +215,12 @@ def test_netout_needed_bytes_is_json_ready():
     need = bench.netout_needed_bytes(homs.numpy(), H, W)
     assert type(need) is int and json.dumps({"n": need})
     assert H * W * 12 < need < H * W * ((2 * P + 3) * 4 + 24)
+
+
+def test_line_guard_serialises_numpy_scalars():
+    import io
+    import numpy as np
+    buf = io.StringIO()
+    g = bench.LineGuard(0, out=buf)
+    assert g.emit({"value": np.float32(1.5), "n": np.int64(3)})
+    assert '"value": 1.5' in buf.getvalue() and '"n": 3' in buf.getvalue()
